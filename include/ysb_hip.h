@@ -1,0 +1,234 @@
+/*
+ * ysb_hip.h -- C ABI of the MI355X-native YSB advertising hot path.
+ *
+ * One library (libysb_hip.so) replaces the Flink operator chain
+ *   DeserializeBolt -> EventFilterBolt -> project(ad_id, event_time)
+ *   -> RedisJoinBolt -> keyBy(campaign) -> CampaignProcessor/CampaignProcessorCommon
+ * of the reference (flink-benchmarks/src/main/java/flink/benchmark/
+ * AdvertisingTopologyNative.java:111-138) with hand-written gfx950 kernels.
+ * Every entry point below names the reference interface it stands in for.
+ *
+ * Conventions
+ *   - plain C, no exceptions cross the ABI; every call returns an int status,
+ *     0 = YSB_OK, negative = error; ysb_last_error(ctx) explains the last one.
+ *   - one ysb_ctx per Flink subtask and per GPU; calls on one ctx are not
+ *     concurrent (the reference's operators are single-threaded per subtask).
+ *   - counts are exact 64-bit integers (the reference's Window.seenCount is a
+ *     java.lang.Long, streaming-benchmark-common/.../Window.java:9).
+ */
+#ifndef YSB_HIP_H
+#define YSB_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YSB_ABI_VERSION 1
+
+/* status codes */
+#define YSB_OK            0
+#define YSB_ERR_ARG      (-1)  /* bad argument / size                      */
+#define YSB_ERR_HIP      (-2)  /* HIP runtime failure                      */
+#define YSB_ERR_STATE    (-3)  /* call not valid in the current state      */
+#define YSB_ERR_CAPACITY (-4)  /* batch, table or output buffer too small  */
+#define YSB_ERR_FORMAT   (-5)  /* malformed ad map / config                */
+#define YSB_ERR_RCCL     (-6)  /* RCCL failure                             */
+#define YSB_ERR_NOMEM    (-7)  /* host or device allocation failed         */
+#define YSB_ERR_DATA     (-8)  /* strict mode: the batch held records the
+                                  reference would have thrown on           */
+
+/* ysb_config.flags */
+#define YSB_F_TIMING       0x1u /* record HIP events around every scan launch */
+#define YSB_F_REQUIRE_IP   0x2u /* also require a string "ip_address" (the Storm/
+                                   Spark deserializers read 7 fields:
+                                   storm-benchmarks/.../AdvertisingTopology.java:56-62,
+                                   AdvertisingSpark.scala:124-134; Flink reads 6:
+                                   AdvertisingTopologyNative.java:267-272)      */
+#define YSB_F_NO_LDS_COUNT 0x4u /* disable the per-workgroup LDS window counters
+                                   (every joined view becomes a global atomic)   */
+
+typedef struct ysb_ctx ysb_ctx;
+
+typedef struct ysb_config {
+    int64_t  time_divisor_ms;    /* 10000: CampaignProcessorCommon.java:28           */
+    uint32_t n_campaigns;        /* campaign index space [0, n_campaigns)            */
+    uint32_t window_ring;        /* W: live (campaign, bucket) slots per campaign,
+                                    power of two >= 16 (the reference keeps <= 9 live
+                                    buckets: LRUHashMap(10), CampaignProcessorCommon.java:37) */
+    uint64_t max_ads;            /* capacity of the device ad -> campaign table      */
+    uint64_t max_batch_events;   /* per ysb_submit                                   */
+    uint64_t max_batch_bytes;    /* per ysb_submit, <= 4 GiB (u32 line offsets)      */
+    int64_t  ring_base_bucket;   /* first bucket of the ring; INT64_MIN = take it from
+                                    the first event of the first batch              */
+    uint64_t overflow_capacity;  /* (campaign, bucket) deltas outside the ring that
+                                    are kept exactly in a side list                  */
+    uint32_t flags;              /* YSB_F_*                                          */
+    uint32_t reserved;
+} ysb_config;
+
+/* Running totals since ysb_open / ysb_reset. */
+typedef struct ysb_stats {
+    uint64_t events;       /* lines scanned                                          */
+    uint64_t views;        /* parsed lines with event_type == "view"
+                              (EventFilterBolt, AdvertisingTopologyNative.java:434)   */
+    uint64_t joined;       /* views whose ad_id is in the map (RedisJoinBolt :464)   */
+    uint64_t join_misses;  /* views dropped on a map miss (:465-467)                 */
+    uint64_t parse_errors; /* lines org.json's JSONObject/getString would throw on
+                              (:263-272)                                             */
+    uint64_t time_errors;  /* joined views whose event_time Long.parseLong rejects
+                              (CampaignProcessorCommon.java:58)                       */
+    uint64_t out_of_ring;  /* joined views counted through the overflow side list    */
+    uint64_t overflow_dropped; /* side-list entries lost for lack of capacity (must be 0) */
+    uint64_t batches;      /* submits                                                */
+} ysb_stats;
+
+/* One (campaign, window) delta: the unit the Redis writer HINCRBYs into
+ * <windowUUID>.seen_count (AdvertisingSpark.scala:184-208,
+ * CampaignProcessorCommon.java:70-88 (commented in the fork)). */
+typedef struct ysb_count {
+    uint32_t campaign;     /* campaign index                                         */
+    uint32_t reserved;
+    int64_t  window_ms;    /* bucket * time_divisor_ms = Redis window timestamp
+                              (CampaignProcessorCommon.java:103)                      */
+    uint64_t count;
+} ysb_count;
+
+/* ---- lifecycle ---------------------------------------------------------------- */
+
+int         ysb_abi_version(void);
+void        ysb_config_default(ysb_config* cfg);
+
+/* Replaces CampaignProcessorCommon(String)/prepare() (CampaignProcessorCommon.java:30-55)
+ * and RedisJoinBolt.open() (AdvertisingTopologyNative.java:451-458). */
+int         ysb_open(ysb_ctx** out, int device, const ysb_config* cfg);
+int         ysb_close(ysb_ctx* ctx);
+/* ctx may be NULL: then the last error of a failed ysb_open on this thread. */
+const char* ysb_last_error(const ysb_ctx* ctx);
+
+/* Replaces getAdCampaignMap + RedisJoinBolt(Map) (AdvertisingTopologyNative.java:47-56,
+ * 443-448) and RedisAdCampaignCache (RedisAdCampaignCache.java:23-35): builds the
+ * GPU-resident open-addressing ad_id -> campaign table.  ad_ids[i] points at
+ * ad_id_lens[i] bytes (NULL lens = 36 each, the UUID length); a later duplicate
+ * wins, as HashMap.put does.  Keys are matched as exact byte strings (<= 56 B). */
+int         ysb_load_ad_map(ysb_ctx* ctx, const char* const* ad_ids,
+                            const uint32_t* ad_id_lens, const uint32_t* campaign_idx,
+                            uint64_t n);
+
+/* ---- batches --------------------------------------------------------------------
+ * A batch is n_events JSON lines packed back to back in `bytes`; line i spans
+ * [line_off[i], line_off[i+1]) (the last one ends at nbytes).  This replaces the
+ * per-record FlatMapFunction.flatMap calls of the chain
+ * (AdvertisingTopologyNative.java:111-119 / 122-138). */
+
+/* Library-owned pinned staging buffers for double-buffered slots 0 and 1, each
+ * max_batch_bytes / max_batch_events large.  Fill, then ysb_submit the slot. */
+int         ysb_slot_buffers(ysb_ctx* ctx, int slot, uint8_t** bytes, uint32_t** line_off);
+/* Asynchronous: H2D copy on the copy stream, kernel on the compute stream.
+ * bytes/line_off may be the slot's own buffers (zero-copy staging) or any host
+ * memory (copied into the slot first).  The caller must not touch the slot's
+ * buffers until ysb_wait(ctx, slot). */
+int         ysb_submit(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes,
+                       const uint32_t* line_off, uint64_t n_events);
+int         ysb_wait(ysb_ctx* ctx, int slot);
+/* Device-resident batch (HBM pointers, e.g. from ysb_device_alloc). Asynchronous. */
+int         ysb_submit_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes,
+                              const uint32_t* d_line_off, uint64_t n_events);
+/* Wait for every submitted batch. */
+int         ysb_sync(ysb_ctx* ctx);
+
+/* ---- results ------------------------------------------------------------------------
+ * Replaces CampaignProcessorCommon.flushWindows/writeWindow
+ * (CampaignProcessorCommon.java:41-54, 69-98): returns the nonzero
+ * (campaign, window) deltas with bucket in [bucket_lo, bucket_hi) (ring + side
+ * list), sorted by (campaign, window).  clear != 0 zeroes what was returned (a
+ * flush: the next drain reports only new deltas).  out == NULL: *n_out = rows
+ * needed.  After ysb_group_reduce_scatter the ring part covers only this rank's
+ * campaign block (every rank still reports its own side-list deltas; deltas are
+ * additive, exactly like the HINCRBY they feed). */
+int         ysb_drain(ysb_ctx* ctx, int64_t bucket_lo, int64_t bucket_hi, int clear,
+                      ysb_count* out, uint64_t cap, uint64_t* n_out);
+int         ysb_stats_get(ysb_ctx* ctx, ysb_stats* out);
+/* Zero counts, side list and stats; the ad table is kept. */
+int         ysb_reset(ysb_ctx* ctx);
+/* Bucket range currently held by the ring: [*lo, *lo + window_ring). */
+int         ysb_ring_range(ysb_ctx* ctx, int64_t* lo, uint32_t* width);
+
+/* ---- measurement -------------------------------------------------------------------- */
+/* With YSB_F_TIMING: total device time of the scan kernel launches (HIP events on
+ * the compute stream) and the number of launches since the last call (resets). */
+int         ysb_kernel_time(ysb_ctx* ctx, double* total_ms, uint64_t* launches);
+/* The compute stream (hipStream_t) for callers that want to order work with it. */
+void*       ysb_stream(ysb_ctx* ctx);
+
+/* ---- device memory helpers (so host code needs no framework for HBM buffers) ----------- */
+int         ysb_device_alloc(ysb_ctx* ctx, uint64_t bytes, void** d_ptr);
+int         ysb_device_free(ysb_ctx* ctx, void* d_ptr);
+int         ysb_memcpy_h2d(ysb_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes);
+int         ysb_memcpy_d2h(ysb_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes);
+
+/* ---- multi-GPU: replaces the keyBy(0) shuffle (AdvertisingTopologyNative.java:118) ----
+ * Events are sharded by ad_id hash across ranks; the per-rank (campaign, window)
+ * tables are summed with one RCCL reduce-scatter over xGMI, leaving rank r the
+ * owner of campaigns [r*Cp/N, (r+1)*Cp/N), Cp = n_campaigns padded to N. */
+#define YSB_UNIQUE_ID_BYTES 128
+int         ysb_group_unique_id(uint8_t uid[YSB_UNIQUE_ID_BYTES]);
+int         ysb_group_init(ysb_ctx* ctx, int rank, int nranks,
+                           const uint8_t uid[YSB_UNIQUE_ID_BYTES]);
+/* Asynchronous on the compute stream; sums the ring tables into the owner rank.
+ * Every rank's ring part is consumed (zeroed) by the call. */
+int         ysb_group_reduce_scatter(ysb_ctx* ctx);
+int         ysb_group_owned(ysb_ctx* ctx, uint32_t* campaign_lo, uint32_t* campaign_hi);
+/* Shard of an ad_id under the partitioning above (host function). */
+uint32_t    ysb_ad_shard(const char* ad_id, uint32_t len, uint32_t nranks);
+
+/* ---- synthetic input: the data/ generator's event format (core.clj:61-98, 163-181)
+ * restated as a seeded, counter-based generator with a file-dump mode.  Host and
+ * device produce byte-identical lines for the same parameters. */
+typedef struct ysb_gen_params {
+    uint64_t seed;
+    uint32_t n_campaigns;       /* 100 (core.clj:15)                                  */
+    uint32_t ads_per_campaign;  /* 10 ((partition 10 ads), core.clj:52)               */
+    int64_t  t0_ms;             /* event_time of event 0                              */
+    uint64_t events_per_sec;    /* event time advances 1000/rate ms per event;
+                                   100 reproduces catch-up mode (10 ms, core.clj:95)   */
+    uint32_t with_skew;         /* +-50 ms skew, 1e-5 late by <60 s (core.clj:166-174) */
+    uint32_t n_users;           /* 0: a fresh user/page UUID per event (core.clj:79-80);
+                                   k: draw from a pool of k (core.clj:187-188)         */
+    const uint32_t* ad_subset;  /* optional: draw ads only from these indices (shards) */
+    uint32_t n_ad_subset;
+    uint32_t reserved;
+} ysb_gen_params;
+
+void        ysb_gen_default(ysb_gen_params* p);
+/* Campaign and ad UUIDs, 36 bytes each, no separators (ad a -> campaign a / ads_per_campaign). */
+int         ysb_gen_ids(const ysb_gen_params* p, char* campaign_ids, char* ad_ids);
+/* Events [first, first+n) into out (cap bytes); line offsets relative to out. */
+int         ysb_gen_events_host(const ysb_gen_params* p, uint64_t first, uint64_t n,
+                                uint8_t* out, uint64_t cap, uint32_t* line_off,
+                                uint64_t* nbytes);
+/* Same on the device (d_out / d_line_off are HBM); synchronous. */
+int         ysb_gen_events_device(ysb_ctx* ctx, const ysb_gen_params* p, uint64_t first,
+                                  uint64_t n, uint8_t* d_out, uint64_t cap,
+                                  uint32_t* d_line_off, uint64_t* nbytes);
+/* Upper bound of one generated line in bytes. */
+uint64_t    ysb_gen_max_line_bytes(const ysb_gen_params* p);
+/* Generator truth, independent of any parsing: adds the (campaign, bucket) view
+ * counts of events [first, first+n) to a second device table ("truth") laid out
+ * like the ring; ysb_truth_compare counts ring/truth cells that differ. */
+int         ysb_truth_accumulate(ysb_ctx* ctx, const ysb_gen_params* p, uint64_t first,
+                                 uint64_t n);
+int         ysb_truth_compare(ysb_ctx* ctx, uint64_t* mismatched_cells,
+                              uint64_t* truth_total, uint64_t* ring_total);
+/* Writes the generator's files into dir: campaign-ids.txt, ad-ids.txt (core.clj:24-34),
+ * ad-to-campaign-ids.txt ({ "AD": "CAMPAIGN"} lines, core.clj:58), ad-to-campaign.csv
+ * (ad,campaign lines, AdvertisingTopologyNative.java:52) and kafka-json.txt with
+ * n_events events (core.clj:76-97). */
+int         ysb_gen_dump(const ysb_gen_params* p, uint64_t n_events, const char* dir);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YSB_HIP_H */

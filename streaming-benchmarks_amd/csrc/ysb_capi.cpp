@@ -1,0 +1,868 @@
+// ysb_capi.cpp -- the C ABI of include/ysb_hip.h: context lifecycle, the device
+// ad -> campaign table, double-buffered batch submission, result drain, the RCCL
+// group step and the host side of the synthetic generator.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/ysb_hip.h"
+#include "ysb_kernels.h"
+
+using namespace ysb;
+
+namespace ysb {
+int scan_lds_bytes();
+}
+
+struct ysb_ctx {
+    int device = 0;
+    ysb_config cfg{};
+    std::string err;
+    int cus = 256;
+    hipStream_t s_comp = nullptr, s_copy = nullptr;
+    // ad table
+    u32* d_table = nullptr;
+    u64 table_slots = 0;
+    bool table_loaded = false;
+    // counts
+    u32 c_pad = 0;                        // campaigns padded to the group size
+    unsigned long long* d_counts = nullptr;   // [c_pad][W]
+    unsigned long long* d_owned = nullptr;    // [c_pad / nranks][W] after reduce-scatter
+    unsigned long long* d_rs_tmp = nullptr;
+    i64* d_ring = nullptr;                // [lo, set]
+    i64* h_ring = nullptr;                // pinned mirror
+    hipEvent_t ev_ring = nullptr;
+    bool ring_query_pending = false;
+    bool ring_known = false;
+    i64 ring_lo = 0;
+    OvfEntry* d_ovf = nullptr;
+    u32* d_ovf_count = nullptr;
+    unsigned long long* d_stats = nullptr;
+    u64 batches = 0;
+    std::map<std::pair<u32, i64>, u64> side;   // drained side-list deltas
+    DivMagic div{};
+    u32 lds_wl = 0, lds_wl_log2 = 0;
+    // slots
+    u8* h_bytes[2] = {nullptr, nullptr};
+    u32* h_off[2] = {nullptr, nullptr};
+    u8* d_bytes[2] = {nullptr, nullptr};
+    u32* d_off[2] = {nullptr, nullptr};
+    hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_kdone[2] = {nullptr, nullptr};
+    bool slot_busy[2] = {false, false};
+    // timing
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    size_t tev_used = 0;
+    // group
+    ncclComm_t comm = nullptr;
+    int rank = 0, nranks = 1;
+    bool rs_done = false;
+    // truth
+    unsigned long long* d_truth = nullptr;
+    unsigned long long* d_truth_out = nullptr;
+    unsigned long long* d_cmp = nullptr;
+    u32* d_subset = nullptr;
+    u32 d_subset_n = 0;
+};
+
+static thread_local std::string g_open_err;
+
+static int fail(ysb_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    else g_open_err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail(ctx, YSB_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                                \
+    } while (0)
+
+static bool is_pow2(u64 x) { return x && !(x & (x - 1)); }
+static u32 log2u(u64 x) { u32 l = 0; while (((u64)1 << l) < x) ++l; return l; }
+
+extern "C" {
+
+int ysb_abi_version(void) { return YSB_ABI_VERSION; }
+
+void ysb_config_default(ysb_config* c) {
+    std::memset(c, 0, sizeof *c);
+    c->time_divisor_ms = 10000;
+    c->n_campaigns = 100;
+    c->window_ring = 1024;
+    c->max_ads = 1000;
+    c->max_batch_events = 1u << 20;
+    c->max_batch_bytes = 256ull << 20;
+    c->ring_base_bucket = INT64_MIN;
+    c->overflow_capacity = 1u << 20;
+    c->flags = 0;
+}
+
+const char* ysb_last_error(const ysb_ctx* c) { return c ? c->err.c_str() : g_open_err.c_str(); }
+
+static void destroy(ysb_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->s_comp) hipStreamSynchronize(c->s_comp);
+    if (c->s_copy) hipStreamSynchronize(c->s_copy);
+    if (c->comm) ncclCommDestroy(c->comm);
+    hipFree(c->d_table);
+    hipFree(c->d_counts);
+    hipFree(c->d_owned);
+    hipFree(c->d_rs_tmp);
+    hipFree(c->d_ring);
+    hipHostFree(c->h_ring);
+    hipFree(c->d_ovf);
+    hipFree(c->d_ovf_count);
+    hipFree(c->d_stats);
+    hipFree(c->d_truth);
+    hipFree(c->d_truth_out);
+    hipFree(c->d_cmp);
+    hipFree(c->d_subset);
+    for (int s = 0; s < 2; ++s) {
+        hipHostFree(c->h_bytes[s]);
+        hipHostFree(c->h_off[s]);
+        hipFree(c->d_bytes[s]);
+        hipFree(c->d_off[s]);
+        if (c->ev_h2d[s]) hipEventDestroy(c->ev_h2d[s]);
+        if (c->ev_kdone[s]) hipEventDestroy(c->ev_kdone[s]);
+    }
+    for (auto& p : c->tev) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+    if (c->ev_ring) hipEventDestroy(c->ev_ring);
+    if (c->s_comp) hipStreamDestroy(c->s_comp);
+    if (c->s_copy) hipStreamDestroy(c->s_copy);
+    delete c;
+}
+
+static int alloc_counts(ysb_ctx* c) {
+    const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
+    hipFree(c->d_counts);
+    c->d_counts = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_counts, cells * 8));
+    HIPCHK(c, hipMemset(c->d_counts, 0, cells * 8));
+    return YSB_OK;
+}
+
+int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
+    if (!out) return fail(nullptr, YSB_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    ysb_config cfg;
+    if (cfg_in) cfg = *cfg_in;
+    else ysb_config_default(&cfg);
+    if (cfg.time_divisor_ms < 1) return fail(nullptr, YSB_ERR_ARG, "time_divisor_ms must be >= 1");
+    if (cfg.n_campaigns == 0) return fail(nullptr, YSB_ERR_ARG, "n_campaigns must be > 0");
+    if (!is_pow2(cfg.window_ring) || cfg.window_ring < 16)
+        return fail(nullptr, YSB_ERR_ARG, "window_ring must be a power of two >= 16");
+    if (cfg.max_batch_bytes == 0 || cfg.max_batch_bytes > (4ull << 30) - 64)
+        return fail(nullptr, YSB_ERR_ARG, "max_batch_bytes must be in (0, 4 GiB)");
+    if (cfg.overflow_capacity == 0 || cfg.overflow_capacity > 0xFFFFFFFFull)
+        return fail(nullptr, YSB_ERR_ARG, "overflow_capacity must be in [1, 2^32)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(nullptr, YSB_ERR_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(nullptr, YSB_ERR_ARG, "device %d out of range (%d)", device, ndev);
+
+    ysb_ctx* c = new ysb_ctx();
+    c->device = device;
+    c->cfg = cfg;
+    c->c_pad = cfg.n_campaigns;
+    c->div = div_magic(cfg.time_divisor_ms);
+    int rc = YSB_OK;
+    auto bad = [&](int code) { g_open_err = c->err; destroy(c); return code; };
+    if (hipSetDevice(device) != hipSuccess) { fail(c, YSB_ERR_HIP, "hipSetDevice(%d) failed", device); return bad(YSB_ERR_HIP); }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking) != hipSuccess) {
+        fail(c, YSB_ERR_HIP, "stream creation failed");
+        return bad(YSB_ERR_HIP);
+    }
+    for (int s = 0; s < 2; ++s) {
+        if (hipEventCreateWithFlags(&c->ev_h2d[s], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_kdone[s], hipEventDisableTiming) != hipSuccess) {
+            fail(c, YSB_ERR_HIP, "event creation failed");
+            return bad(YSB_ERR_HIP);
+        }
+    }
+    if (hipEventCreateWithFlags(&c->ev_ring, hipEventDisableTiming) != hipSuccess) {
+        fail(c, YSB_ERR_HIP, "event creation failed");
+        return bad(YSB_ERR_HIP);
+    }
+    if ((rc = alloc_counts(c)) != YSB_OK) return bad(rc);
+    if (hipMalloc(&c->d_ring, 16) != hipSuccess || hipHostMalloc(&c->h_ring, 16) != hipSuccess ||
+        hipMalloc(&c->d_ovf, cfg.overflow_capacity * sizeof(OvfEntry)) != hipSuccess ||
+        hipMalloc(&c->d_ovf_count, 16) != hipSuccess || hipMalloc(&c->d_stats, ST_COUNT_ * 8) != hipSuccess) {
+        fail(c, YSB_ERR_NOMEM, "device allocation failed");
+        return bad(YSB_ERR_NOMEM);
+    }
+    i64 ring[2] = {0, 0};
+    if (cfg.ring_base_bucket != INT64_MIN) {
+        ring[0] = cfg.ring_base_bucket;
+        ring[1] = 1;
+        c->ring_known = true;
+        c->ring_lo = cfg.ring_base_bucket;
+    }
+    if (hipMemcpy(c->d_ring, ring, 16, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(c->d_ovf_count, 0, 16) != hipSuccess || hipMemset(c->d_stats, 0, ST_COUNT_ * 8) != hipSuccess) {
+        fail(c, YSB_ERR_HIP, "initialisation copy failed");
+        return bad(YSB_ERR_HIP);
+    }
+    // LDS window counters: WL = largest power of two with n_campaigns * WL <= LCNT_CAP
+    if (!(cfg.flags & YSB_F_NO_LDS_COUNT)) {
+        u32 wl = 0;
+        for (u32 w = 2; (u64)w * cfg.n_campaigns <= (u64)LCNT_CAP && w <= cfg.window_ring; w <<= 1) wl = w;
+        c->lds_wl = wl;
+        c->lds_wl_log2 = wl ? log2u(wl) : 0;
+    }
+    *out = c;
+    return YSB_OK;
+}
+
+int ysb_close(ysb_ctx* c) {
+    destroy(c);
+    return YSB_OK;
+}
+
+// ---- ad table -------------------------------------------------------------------------
+
+int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens, const uint32_t* campaign_idx,
+                    uint64_t n) {
+    if (!c) return YSB_ERR_ARG;
+    if (n && (!ad_ids || !campaign_idx)) return fail(c, YSB_ERR_ARG, "NULL ad map arrays");
+    u64 slots = 64;
+    while (slots < 2 * n) slots <<= 1;   // load factor <= 0.5
+    if (slots > (1ull << 31)) return fail(c, YSB_ERR_CAPACITY, "ad map too large (%llu)", (unsigned long long)n);
+    std::vector<u32> tab(slots * SLOT_WORDS, 0);
+    for (u64 s = 0; s < slots; ++s) tab[s * SLOT_WORDS + 1] = EMPTY_SLOT;
+    const u32 mask = (u32)(slots - 1);
+    for (u64 i = 0; i < n; ++i) {
+        const u32 len = lens ? lens[i] : 36u;
+        if (len > MAX_KEY_BYTES) return fail(c, YSB_ERR_FORMAT, "ad id %llu longer than %u bytes", (unsigned long long)i, MAX_KEY_BYTES);
+        if (campaign_idx[i] >= c->cfg.n_campaigns)
+            return fail(c, YSB_ERR_FORMAT, "campaign index %u >= n_campaigns %u", campaign_idx[i], c->cfg.n_campaigns);
+        if (!ad_ids[i] && len) return fail(c, YSB_ERR_ARG, "ad id %llu is NULL", (unsigned long long)i);
+        u32 kw[KEY_WORDS] = {0};
+        if (len) std::memcpy(kw, ad_ids[i], len);
+        const u32 h = key_hash(kw, len);
+        for (u64 pr = 0;; ++pr) {
+            u32* sl = &tab[(u64)((h + pr) & mask) * SLOT_WORDS];
+            if (sl[1] == EMPTY_SLOT) {
+                sl[0] = len;
+                sl[1] = campaign_idx[i];
+                std::memcpy(sl + 2, kw, sizeof kw);
+                break;
+            }
+            if (sl[0] == len && std::memcmp(sl + 2, kw, sizeof kw) == 0) {   // HashMap.put: later wins
+                sl[1] = campaign_idx[i];
+                break;
+            }
+        }
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    if (slots != c->table_slots) {
+        hipFree(c->d_table);
+        c->d_table = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_table, tab.size() * 4));
+        c->table_slots = slots;
+    }
+    HIPCHK(c, hipMemcpy(c->d_table, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+    c->table_loaded = true;
+    return YSB_OK;
+}
+
+// ---- batches ---------------------------------------------------------------------------
+
+static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_off, u64 n) {
+    ScanParams p{};
+    p.bytes = d_bytes;
+    p.nbytes = nbytes;
+    p.off = d_off;
+    p.n = n;
+    p.table = c->d_table;
+    p.table_mask = (u32)(c->table_slots - 1);
+    p.n_campaigns = c->cfg.n_campaigns;
+    p.counts = c->d_counts;
+    p.ring_w = c->cfg.window_ring;
+    p.lds_wl = c->lds_wl;
+    p.lds_wl_log2 = c->lds_wl_log2;
+    p.require_mask = (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu;
+    p.ring = c->d_ring;
+    p.div = c->div;
+    p.ovf = c->d_ovf;
+    p.ovf_count = c->d_ovf_count;
+    p.ovf_cap = (u32)c->cfg.overflow_capacity;
+    p.stats = c->d_stats;
+    p.n_tiles = (n + SCAN_TPB - 1) / SCAN_TPB;
+    const u64 resident = (u64)c->cus * 2;   // two 80 KiB workgroups per CU
+    const u64 blocks = std::max<u64>(1, std::min<u64>(p.n_tiles, resident));
+    p.tiles_per_block = (u32)((p.n_tiles + blocks - 1) / blocks);
+    return p;
+}
+
+static void poll_ring(ysb_ctx* c) {
+    if (c->ring_known || !c->ring_query_pending) return;
+    if (hipEventQuery(c->ev_ring) == hipSuccess) {
+        c->ring_query_pending = false;
+        if (c->h_ring[1]) { c->ring_known = true; c->ring_lo = c->h_ring[0]; }
+    }
+}
+
+static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_off, u64 n) {
+    if (!c->table_loaded) return fail(c, YSB_ERR_STATE, "ysb_load_ad_map has not been called");
+    if (n == 0) { c->batches++; return YSB_OK; }
+    const ScanParams p = make_params(c, d_bytes, nbytes, d_off, n);
+    poll_ring(c);
+    if (!c->ring_known) {
+        launch_ring_autobase(p, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->h_ring, c->d_ring, 16, hipMemcpyDeviceToHost, c->s_comp));
+        HIPCHK(c, hipEventRecord(c->ev_ring, c->s_comp));
+        c->ring_query_pending = true;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->cfg.flags & YSB_F_TIMING) {
+        if (c->tev_used == c->tev.size()) {
+            hipEvent_t a, b;
+            HIPCHK(c, hipEventCreate(&a));
+            HIPCHK(c, hipEventCreate(&b));
+            c->tev.emplace_back(a, b);
+        }
+        e0 = c->tev[c->tev_used].first;
+        e1 = c->tev[c->tev_used].second;
+        c->tev_used++;
+        HIPCHK(c, hipEventRecord(e0, c->s_comp));
+    }
+    launch_scan(p, c->s_comp);
+    HIPCHK(c, hipGetLastError());
+    if (e1) HIPCHK(c, hipEventRecord(e1, c->s_comp));
+    c->batches++;
+    return YSB_OK;
+}
+
+static int ensure_slots(ysb_ctx* c) {
+    if (c->h_bytes[0]) return YSB_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    for (int s = 0; s < 2; ++s) {
+        HIPCHK(c, hipHostMalloc(&c->h_bytes[s], c->cfg.max_batch_bytes + 64));
+        HIPCHK(c, hipHostMalloc(&c->h_off[s], c->cfg.max_batch_events * 4 + 64));
+        HIPCHK(c, hipMalloc(&c->d_bytes[s], c->cfg.max_batch_bytes + 64));
+        HIPCHK(c, hipMalloc(&c->d_off[s], c->cfg.max_batch_events * 4 + 64));
+    }
+    return YSB_OK;
+}
+
+int ysb_slot_buffers(ysb_ctx* c, int slot, uint8_t** bytes, uint32_t** line_off) {
+    if (!c || slot < 0 || slot > 1) return c ? fail(c, YSB_ERR_ARG, "slot must be 0 or 1") : YSB_ERR_ARG;
+    int rc = ensure_slots(c);
+    if (rc) return rc;
+    if (bytes) *bytes = c->h_bytes[slot];
+    if (line_off) *line_off = c->h_off[slot];
+    return YSB_OK;
+}
+
+int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, const uint32_t* line_off,
+               uint64_t n) {
+    if (!c) return YSB_ERR_ARG;
+    if (slot < 0 || slot > 1) return fail(c, YSB_ERR_ARG, "slot must be 0 or 1");
+    if (nbytes > c->cfg.max_batch_bytes || n > c->cfg.max_batch_events)
+        return fail(c, YSB_ERR_CAPACITY, "batch (%llu B, %llu events) exceeds max_batch_bytes/max_batch_events",
+                    (unsigned long long)nbytes, (unsigned long long)n);
+    if ((nbytes && !bytes) || (n && !line_off)) return fail(c, YSB_ERR_ARG, "NULL batch buffers");
+    int rc = ensure_slots(c);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    // the slot's previous H2D must be done before its pinned buffers are rewritten
+    HIPCHK(c, hipEventSynchronize(c->ev_h2d[slot]));
+    if (bytes != c->h_bytes[slot] && nbytes) std::memcpy(c->h_bytes[slot], bytes, nbytes);
+    if (line_off != c->h_off[slot] && n) std::memcpy(c->h_off[slot], line_off, n * 4);
+    // ... and the slot's previous kernel must be done before its device buffers are
+    HIPCHK(c, hipStreamWaitEvent(c->s_copy, c->ev_kdone[slot], 0));
+    if (nbytes) HIPCHK(c, hipMemcpyAsync(c->d_bytes[slot], c->h_bytes[slot], nbytes, hipMemcpyHostToDevice, c->s_copy));
+    if (n) HIPCHK(c, hipMemcpyAsync(c->d_off[slot], c->h_off[slot], n * 4, hipMemcpyHostToDevice, c->s_copy));
+    HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
+    HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_h2d[slot], 0));
+    rc = enqueue_scan(c, c->d_bytes[slot], nbytes, c->d_off[slot], n);
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_kdone[slot], c->s_comp));
+    return YSB_OK;
+}
+
+int ysb_wait(ysb_ctx* c, int slot) {
+    if (!c) return YSB_ERR_ARG;
+    if (slot < 0 || slot > 1) return fail(c, YSB_ERR_ARG, "slot must be 0 or 1");
+    if (!c->h_bytes[0]) return YSB_OK;
+    HIPCHK(c, hipEventSynchronize(c->ev_h2d[slot]));
+    return YSB_OK;
+}
+
+int ysb_submit_device(ysb_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const uint32_t* d_off, uint64_t n) {
+    if (!c) return YSB_ERR_ARG;
+    if (nbytes > (4ull << 30) - 64) return fail(c, YSB_ERR_CAPACITY, "device batch larger than 4 GiB (u32 offsets)");
+    if ((nbytes && !d_bytes) || (n && !d_off)) return fail(c, YSB_ERR_ARG, "NULL batch buffers");
+    if (reinterpret_cast<uintptr_t>(d_bytes) & 15) return fail(c, YSB_ERR_ARG, "d_bytes must be 16-byte aligned");
+    HIPCHK(c, hipSetDevice(c->device));
+    return enqueue_scan(c, d_bytes, nbytes, d_off, n);
+}
+
+int ysb_sync(ysb_ctx* c) {
+    if (!c) return YSB_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->s_copy));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    poll_ring(c);
+    return YSB_OK;
+}
+
+// ---- results --------------------------------------------------------------------------------
+
+static int read_ring(ysb_ctx* c) {
+    i64 r[2];
+    HIPCHK(c, hipMemcpy(r, c->d_ring, 16, hipMemcpyDeviceToHost));
+    if (r[1]) { c->ring_known = true; c->ring_lo = r[0]; }
+    c->ring_query_pending = false;
+    return YSB_OK;
+}
+
+static int pull_side_list(ysb_ctx* c) {
+    u32 cnt = 0;
+    HIPCHK(c, hipMemcpy(&cnt, c->d_ovf_count, 4, hipMemcpyDeviceToHost));
+    const u32 m = (u32)std::min<u64>(cnt, c->cfg.overflow_capacity);
+    if (m) {
+        std::vector<OvfEntry> v(m);
+        HIPCHK(c, hipMemcpy(v.data(), c->d_ovf, (u64)m * sizeof(OvfEntry), hipMemcpyDeviceToHost));
+        for (const auto& e : v) c->side[{e.campaign, e.bucket}] += e.count;
+    }
+    if (cnt) HIPCHK(c, hipMemset(c->d_ovf_count, 0, 4));
+    return YSB_OK;
+}
+
+int ysb_drain(ysb_ctx* c, int64_t blo, int64_t bhi, int clear, ysb_count* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return c ? fail(c, YSB_ERR_ARG, "n_out is NULL") : YSB_ERR_ARG;
+    int rc = ysb_sync(c);
+    if (rc) return rc;
+    if ((rc = read_ring(c))) return rc;
+    if ((rc = pull_side_list(c))) return rc;
+    const u32 W = c->cfg.window_ring;
+    const u32 C = c->cfg.n_campaigns;
+    std::map<std::pair<u32, i64>, u64> rows;
+    // side list
+    for (auto it = c->side.lower_bound({0, INT64_MIN}); it != c->side.end(); ++it)
+        if (it->first.second >= blo && it->first.second < bhi && it->second) rows[it->first] += it->second;
+    // ring: rank-local remnants for every campaign, plus the owned block after a reduce-scatter
+    std::vector<unsigned long long> loc((u64)C * W), own;
+    u32 own_lo = 0, own_hi = 0;
+    if (c->ring_known) {
+        HIPCHK(c, hipMemcpy(loc.data(), c->d_counts, loc.size() * 8, hipMemcpyDeviceToHost));
+        if (c->d_owned) {
+            const u32 per = c->c_pad / c->nranks;
+            own_lo = std::min<u32>(C, (u32)c->rank * per);
+            own_hi = std::min<u32>(C, own_lo + per);
+            own.resize((u64)per * W);
+            HIPCHK(c, hipMemcpy(own.data(), c->d_owned, own.size() * 8, hipMemcpyDeviceToHost));
+        }
+        const i64 lo = c->ring_lo;
+        auto bucket_of = [&](u32 j) { return lo + (i64)(((u64)j - (u64)lo) & (W - 1)); };
+        for (u32 cc = 0; cc < C; ++cc)
+            for (u32 j = 0; j < W; ++j) {
+                const i64 b = bucket_of(j);
+                if (b < blo || b >= bhi) continue;
+                u64 v = loc[(u64)cc * W + j];
+                if (cc >= own_lo && cc < own_hi) v += own[(u64)(cc - own_lo) * W + j];
+                if (v) rows[{cc, b}] += v;
+            }
+    }
+    *n_out = rows.size();
+    if (!out) return YSB_OK;
+    if (cap < rows.size()) return fail(c, YSB_ERR_CAPACITY, "drain needs %llu rows, cap %llu", (unsigned long long)rows.size(), (unsigned long long)cap);
+    u64 k = 0;
+    for (const auto& r : rows) {
+        out[k].campaign = r.first.first;
+        out[k].reserved = 0;
+        out[k].window_ms = r.first.second * c->cfg.time_divisor_ms;
+        out[k].count = r.second;
+        ++k;
+    }
+    if (clear) {
+        for (auto it = c->side.begin(); it != c->side.end();)
+            if (it->first.second >= blo && it->first.second < bhi) it = c->side.erase(it);
+            else ++it;
+        if (c->ring_known) {
+            const i64 lo = c->ring_lo;
+            bool dirty = false;
+            for (u32 j = 0; j < W; ++j) {
+                const i64 b = lo + (i64)(((u64)j - (u64)lo) & (W - 1));
+                if (b < blo || b >= bhi) continue;
+                dirty = true;
+                for (u32 cc = 0; cc < C; ++cc) loc[(u64)cc * W + j] = 0;
+                if (!own.empty())
+                    for (u32 cc = own_lo; cc < own_hi; ++cc) own[(u64)(cc - own_lo) * W + j] = 0;
+            }
+            if (dirty) {
+                HIPCHK(c, hipMemcpy(c->d_counts, loc.data(), loc.size() * 8, hipMemcpyHostToDevice));
+                if (!own.empty()) HIPCHK(c, hipMemcpy(c->d_owned, own.data(), own.size() * 8, hipMemcpyHostToDevice));
+            }
+        }
+    }
+    return YSB_OK;
+}
+
+int ysb_stats_get(ysb_ctx* c, ysb_stats* s) {
+    if (!c || !s) return c ? fail(c, YSB_ERR_ARG, "NULL stats") : YSB_ERR_ARG;
+    int rc = ysb_sync(c);
+    if (rc) return rc;
+    unsigned long long v[ST_COUNT_];
+    HIPCHK(c, hipMemcpy(v, c->d_stats, sizeof v, hipMemcpyDeviceToHost));
+    s->events = v[ST_EVENTS];
+    s->views = v[ST_VIEWS];
+    s->joined = v[ST_JOINED];
+    s->join_misses = v[ST_MISSES];
+    s->parse_errors = v[ST_PARSE_ERR];
+    s->time_errors = v[ST_TIME_ERR];
+    s->out_of_ring = v[ST_OUT_OF_RING];
+    s->overflow_dropped = v[ST_OVF_DROPPED];
+    s->batches = c->batches;
+    return YSB_OK;
+}
+
+int ysb_reset(ysb_ctx* c) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = ysb_sync(c);
+    if (rc) return rc;
+    const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
+    HIPCHK(c, hipMemset(c->d_counts, 0, cells * 8));
+    if (c->d_owned) HIPCHK(c, hipMemset(c->d_owned, 0, cells / c->nranks * 8));
+    if (c->d_truth) HIPCHK(c, hipMemset(c->d_truth, 0, cells * 8));
+    if (c->d_truth_out) HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
+    HIPCHK(c, hipMemset(c->d_ovf_count, 0, 16));
+    HIPCHK(c, hipMemset(c->d_stats, 0, ST_COUNT_ * 8));
+    c->side.clear();
+    c->batches = 0;
+    return YSB_OK;
+}
+
+int ysb_ring_range(ysb_ctx* c, int64_t* lo, uint32_t* width) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = ysb_sync(c);
+    if (rc) return rc;
+    if ((rc = read_ring(c))) return rc;
+    if (!c->ring_known) return fail(c, YSB_ERR_STATE, "ring base not set yet");
+    if (lo) *lo = c->ring_lo;
+    if (width) *width = c->cfg.window_ring;
+    return YSB_OK;
+}
+
+int ysb_kernel_time(ysb_ctx* c, double* total_ms, uint64_t* launches) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = ysb_sync(c);
+    if (rc) return rc;
+    double t = 0;
+    for (size_t i = 0; i < c->tev_used; ++i) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->tev[i].first, c->tev[i].second));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = c->tev_used;
+    c->tev_used = 0;
+    return YSB_OK;
+}
+
+void* ysb_stream(ysb_ctx* c) { return c ? (void*)c->s_comp : nullptr; }
+
+// ---- device memory ----------------------------------------------------------------------------
+
+int ysb_device_alloc(ysb_ctx* c, uint64_t bytes, void** p) {
+    if (!c || !p) return YSB_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMalloc(p, bytes ? bytes : 16));
+    return YSB_OK;
+}
+int ysb_device_free(ysb_ctx* c, void* p) {
+    if (!c) return YSB_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipFree(p));
+    return YSB_OK;
+}
+int ysb_memcpy_h2d(ysb_ctx* c, void* d, const void* h, uint64_t bytes) {
+    if (!c) return YSB_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
+    return YSB_OK;
+}
+int ysb_memcpy_d2h(ysb_ctx* c, void* h, const void* d, uint64_t bytes) {
+    if (!c) return YSB_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost));
+    return YSB_OK;
+}
+
+// ---- multi-GPU ---------------------------------------------------------------------------------
+
+int ysb_group_unique_id(uint8_t uid[YSB_UNIQUE_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == YSB_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return fail(nullptr, YSB_ERR_RCCL, "ncclGetUniqueId failed");
+    std::memcpy(uid, &id, sizeof id);
+    return YSB_OK;
+}
+
+int ysb_group_init(ysb_ctx* c, int rank, int nranks, const uint8_t uid[YSB_UNIQUE_ID_BYTES]) {
+    if (!c || !uid) return YSB_ERR_ARG;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(c, YSB_ERR_ARG, "bad rank %d / %d", rank, nranks);
+    if (c->comm) return fail(c, YSB_ERR_STATE, "group already initialised");
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof id);
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+    if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    c->rank = rank;
+    c->nranks = nranks;
+    // pad campaigns to a multiple of nranks; keep the current counts
+    const u32 cp = (c->cfg.n_campaigns + nranks - 1) / nranks * nranks;
+    if (cp != c->c_pad) {
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        unsigned long long* old = c->d_counts;
+        const u64 W = c->cfg.window_ring;
+        c->d_counts = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_counts, (u64)cp * W * 8));
+        HIPCHK(c, hipMemset(c->d_counts, 0, (u64)cp * W * 8));
+        HIPCHK(c, hipMemcpy(c->d_counts, old, (u64)c->c_pad * W * 8, hipMemcpyDeviceToDevice));
+        hipFree(old);
+        c->c_pad = cp;
+    }
+    const u64 per = (u64)c->c_pad / nranks * c->cfg.window_ring;
+    HIPCHK(c, hipMalloc(&c->d_owned, per * 8));
+    HIPCHK(c, hipMemset(c->d_owned, 0, per * 8));
+    HIPCHK(c, hipMalloc(&c->d_rs_tmp, per * 8));
+    return YSB_OK;
+}
+
+int ysb_group_reduce_scatter(ysb_ctx* c) {
+    if (!c) return YSB_ERR_ARG;
+    if (!c->comm) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
+    HIPCHK(c, hipSetDevice(c->device));
+    const u64 per = (u64)c->c_pad / c->nranks * c->cfg.window_ring;
+    ncclResult_t r = ncclReduceScatter(c->d_counts, c->d_rs_tmp, per, ncclUint64, ncclSum, c->comm, c->s_comp);
+    if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
+    launch_add_u64(c->d_owned, c->d_rs_tmp, per, c->s_comp);
+    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, (u64)c->c_pad * c->cfg.window_ring * 8, c->s_comp));
+    return YSB_OK;
+}
+
+int ysb_group_owned(ysb_ctx* c, uint32_t* lo, uint32_t* hi) {
+    if (!c) return YSB_ERR_ARG;
+    const u32 per = c->c_pad / c->nranks;
+    const u32 l = std::min<u32>(c->cfg.n_campaigns, (u32)c->rank * per);
+    if (lo) *lo = l;
+    if (hi) *hi = std::min<u32>(c->cfg.n_campaigns, l + per);
+    return YSB_OK;
+}
+
+uint32_t ysb_ad_shard(const char* ad_id, uint32_t len, uint32_t nranks) {
+    if (nranks <= 1) return 0;
+    u32 kw[KEY_WORDS] = {0};
+    std::memcpy(kw, ad_id, std::min<u32>(len, MAX_KEY_BYTES));
+    const u32 h = key_hash(kw, std::min<u32>(len, MAX_KEY_BYTES));
+    return (u32)(((u64)mix64(h) >> 32) * nranks >> 32);
+}
+
+// ---- generator -----------------------------------------------------------------------------------
+
+void ysb_gen_default(ysb_gen_params* p) {
+    std::memset(p, 0, sizeof *p);
+    p->seed = 42;
+    p->n_campaigns = 100;
+    p->ads_per_campaign = 10;
+    p->t0_ms = 1700000000000LL;
+    p->events_per_sec = 100000;
+    p->with_skew = 0;
+    p->n_users = 0;
+}
+
+static GenSpec spec_of(const ysb_gen_params* p, const u32* subset) {
+    GenSpec s{};
+    s.seed = p->seed;
+    s.n_campaigns = p->n_campaigns;
+    s.ads_per_campaign = p->ads_per_campaign;
+    s.t0_ms = p->t0_ms;
+    s.events_per_sec = p->events_per_sec;
+    s.with_skew = p->with_skew;
+    s.n_users = p->n_users;
+    s.subset = subset;
+    s.n_pick = subset ? p->n_ad_subset : p->n_campaigns * p->ads_per_campaign;
+    return s;
+}
+
+static bool gen_ok(const ysb_gen_params* p) {
+    return p && p->n_campaigns && p->ads_per_campaign && p->events_per_sec &&
+           (!p->ad_subset || p->n_ad_subset) && (u64)p->n_campaigns * p->ads_per_campaign < (1ull << 32);
+}
+
+int ysb_gen_ids(const ysb_gen_params* p, char* campaign_ids, char* ad_ids) {
+    if (!gen_ok(p)) return fail(nullptr, YSB_ERR_ARG, "bad generator parameters");
+    u64 hi, lo;
+    if (campaign_ids)
+        for (u32 c = 0; c < p->n_campaigns; ++c) {
+            uuid_words(stream_key(p->seed, S_CAMPAIGN), c, &hi, &lo);
+            uuid_format(hi, lo, campaign_ids + 36ull * c);
+        }
+    if (ad_ids)
+        for (u64 a = 0; a < (u64)p->n_campaigns * p->ads_per_campaign; ++a) {
+            uuid_words(stream_key(p->seed, S_AD), a, &hi, &lo);
+            uuid_format(hi, lo, ad_ids + 36ull * a);
+        }
+    return YSB_OK;
+}
+
+uint64_t ysb_gen_max_line_bytes(const ysb_gen_params*) { return (u64)LINE_FIXED + 16 + 8 + 20; }
+
+int ysb_gen_events_host(const ysb_gen_params* p, uint64_t first, uint64_t n, uint8_t* out, uint64_t cap,
+                        uint32_t* line_off, uint64_t* nbytes) {
+    if (!gen_ok(p) || (n && (!out || !line_off)) || !nbytes) return fail(nullptr, YSB_ERR_ARG, "bad generator arguments");
+    const GenSpec s = spec_of(p, p->ad_subset);
+    u64 o = 0;
+    char line[320];
+    for (u64 i = 0; i < n; ++i) {
+        const GenEvent e = gen_event(s, first + i);
+        const u32 len = gen_line_write(s, first + i, e, line);
+        if (o + len > cap) return fail(nullptr, YSB_ERR_CAPACITY, "generator output exceeds %llu bytes", (unsigned long long)cap);
+        if (o > 0xFFFFFFFFull) return fail(nullptr, YSB_ERR_CAPACITY, "batch exceeds 4 GiB (u32 offsets)");
+        line_off[i] = (u32)o;
+        std::memcpy(out + o, line, len);
+        o += len;
+    }
+    *nbytes = o;
+    return YSB_OK;
+}
+
+static int upload_subset(ysb_ctx* c, const ysb_gen_params* p, const u32** dptr) {
+    *dptr = nullptr;
+    if (!p->ad_subset) return YSB_OK;
+    if (c->d_subset_n < p->n_ad_subset) {
+        hipFree(c->d_subset);
+        c->d_subset = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_subset, (u64)p->n_ad_subset * 4));
+        c->d_subset_n = p->n_ad_subset;
+    }
+    HIPCHK(c, hipMemcpy(c->d_subset, p->ad_subset, (u64)p->n_ad_subset * 4, hipMemcpyHostToDevice));
+    *dptr = c->d_subset;
+    return YSB_OK;
+}
+
+int ysb_gen_events_device(ysb_ctx* c, const ysb_gen_params* p, uint64_t first, uint64_t n, uint8_t* d_out,
+                          uint64_t cap, uint32_t* d_off, uint64_t* nbytes) {
+    if (!c) return YSB_ERR_ARG;
+    if (!gen_ok(p) || !nbytes || (n && (!d_out || !d_off))) return fail(c, YSB_ERR_ARG, "bad generator arguments");
+    if (n > 0x7FFFFFFFull) return fail(c, YSB_ERR_ARG, "at most 2^31-1 events per call");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    const u32* dsub = nullptr;
+    int rc = upload_subset(c, p, &dsub);
+    if (rc) return rc;
+    const GenSpec s = spec_of(p, dsub);
+    hipError_t e = gen_events_device(s, first, n, d_out, std::min<u64>(cap, 0xFFFFFFFFull), d_off, nbytes, c->s_comp);
+    if (e == hipErrorInvalidValue && *nbytes > cap)
+        return fail(c, YSB_ERR_CAPACITY, "generator output %llu B exceeds cap %llu B", (unsigned long long)*nbytes, (unsigned long long)cap);
+    if (e != hipSuccess) return fail(c, YSB_ERR_HIP, "device generator: %s", hipGetErrorString(e));
+    return YSB_OK;
+}
+
+int ysb_truth_accumulate(ysb_ctx* c, const ysb_gen_params* p, uint64_t first, uint64_t n) {
+    if (!c) return YSB_ERR_ARG;
+    if (!gen_ok(p)) return fail(c, YSB_ERR_ARG, "bad generator parameters");
+    if (p->n_campaigns > c->cfg.n_campaigns) return fail(c, YSB_ERR_ARG, "generator has more campaigns than the context");
+    HIPCHK(c, hipSetDevice(c->device));
+    const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
+    if (!c->d_truth) {
+        HIPCHK(c, hipMalloc(&c->d_truth, cells * 8));
+        HIPCHK(c, hipMemset(c->d_truth, 0, cells * 8));
+        HIPCHK(c, hipMalloc(&c->d_truth_out, 8));
+        HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
+        HIPCHK(c, hipMalloc(&c->d_cmp, 32));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    int rc = read_ring(c);
+    if (rc) return rc;
+    if (!c->ring_known) return fail(c, YSB_ERR_STATE, "ring base not set (submit a batch first or set ring_base_bucket)");
+    const u32* dsub = nullptr;
+    if ((rc = upload_subset(c, p, &dsub))) return rc;
+    launch_truth(spec_of(p, dsub), first, n, c->div, c->d_truth, c->cfg.window_ring, c->d_ring, c->d_truth_out, c->s_comp);
+    HIPCHK(c, hipGetLastError());
+    return YSB_OK;
+}
+
+int ysb_truth_compare(ysb_ctx* c, uint64_t* mismatched, uint64_t* truth_total, uint64_t* ring_total) {
+    if (!c) return YSB_ERR_ARG;
+    if (!c->d_truth) return fail(c, YSB_ERR_STATE, "no truth accumulated");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemsetAsync(c->d_cmp, 0, 32, c->s_comp));
+    launch_compare(c->d_truth, c->d_counts, (u64)c->c_pad * c->cfg.window_ring, c->d_cmp, c->s_comp);
+    unsigned long long r[3], outside = 0;
+    HIPCHK(c, hipMemcpyAsync(r, c->d_cmp, 24, hipMemcpyDeviceToHost, c->s_comp));
+    HIPCHK(c, hipMemcpyAsync(&outside, c->d_truth_out, 8, hipMemcpyDeviceToHost, c->s_comp));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    if (mismatched) *mismatched = r[0];
+    if (truth_total) *truth_total = r[1] + outside;
+    if (ring_total) *ring_total = r[2];
+    return YSB_OK;
+}
+
+int ysb_gen_dump(const ysb_gen_params* p, uint64_t n_events, const char* dir) {
+    if (!gen_ok(p) || !dir) return fail(nullptr, YSB_ERR_ARG, "bad generator arguments");
+    const u64 A = (u64)p->n_campaigns * p->ads_per_campaign;
+    std::vector<char> cids(36ull * p->n_campaigns), aids(36ull * A);
+    int rc = ysb_gen_ids(p, cids.data(), aids.data());
+    if (rc) return rc;
+    auto open = [&](const char* name) {
+        std::string path = std::string(dir) + "/" + name;
+        return std::fopen(path.c_str(), "wb");
+    };
+    FILE* f = open("campaign-ids.txt");
+    if (!f) return fail(nullptr, YSB_ERR_ARG, "cannot write into %s", dir);
+    for (u32 c = 0; c < p->n_campaigns; ++c) std::fprintf(f, "%.36s\n", &cids[36ull * c]);
+    std::fclose(f);
+    f = open("ad-ids.txt");
+    if (!f) return fail(nullptr, YSB_ERR_ARG, "cannot write into %s", dir);
+    for (u64 a = 0; a < A; ++a) std::fprintf(f, "%.36s\n", &aids[36ull * a]);
+    std::fclose(f);
+    f = open("ad-to-campaign-ids.txt");   // core.clj:58
+    FILE* g = open("ad-to-campaign.csv");   // AdvertisingTopologyNative.java:52
+    if (!f || !g) return fail(nullptr, YSB_ERR_ARG, "cannot write into %s", dir);
+    for (u64 a = 0; a < A; ++a) {
+        const u64 cc = a / p->ads_per_campaign;
+        std::fprintf(f, "{ \"%.36s\": \"%.36s\"}\n", &aids[36 * a], &cids[36 * cc]);
+        std::fprintf(g, "%.36s,%.36s\n", &aids[36 * a], &cids[36 * cc]);
+    }
+    std::fclose(f);
+    std::fclose(g);
+    f = open("kafka-json.txt");   // core.clj:76-97
+    if (!f) return fail(nullptr, YSB_ERR_ARG, "cannot write into %s", dir);
+    const GenSpec s = spec_of(p, p->ad_subset);
+    std::vector<char> buf(1 << 22);
+    size_t used = 0;
+    for (u64 i = 0; i < n_events; ++i) {
+        if (used + 320 > buf.size()) { std::fwrite(buf.data(), 1, used, f); used = 0; }
+        used += gen_line_write(s, i, gen_event(s, i), buf.data() + used);
+    }
+    std::fwrite(buf.data(), 1, used, f);
+    std::fclose(f);
+    return YSB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,251 @@
+// ysb_common.h -- definitions shared by host C++ and gfx950 device code.
+//
+//  * the synthetic event generator (a seeded, counter-based restatement of the
+//    data/ Clojure generator's line format, data/src/setup/core.clj:90-96), so the
+//    host dumper and the device generator emit byte-identical lines;
+//  * the device ad -> campaign table layout and its hash;
+//  * exact int64 division by the (runtime) window divisor, as Java's
+//    Long.parseLong(t) / time_divisor (CampaignProcessorCommon.java:58).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define YSB_HD __host__ __device__ __forceinline__
+#else
+#define YSB_HD static inline
+#endif
+
+namespace ysb {
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef int64_t i64;
+
+// ---------------------------------------------------------------------------
+// Counter-based RNG (splitmix64 finaliser).  draw(stream, i) is a pure function
+// of (seed, stream, i), so any event can be generated independently -- on any
+// thread, any GPU, any host -- which is what makes the dump reproducible.
+// ---------------------------------------------------------------------------
+YSB_HD u64 mix64(u64 z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+YSB_HD u64 stream_key(u64 seed, u32 stream) {
+    return mix64(seed * 0x9E3779B97F4A7C15ULL + stream);
+}
+YSB_HD u64 draw(u64 key, u64 i) { return mix64(key + (i + 1) * 0x9E3779B97F4A7C15ULL); }
+
+enum : u32 {
+    S_CAMPAIGN = 1, S_AD = 2, S_USER = 3, S_PAGE = 4, S_CHOICE = 5, S_SKEW = 6,
+    S_USERPOOL = 7, S_PAGEPOOL = 8
+};
+
+// java.util.UUID.randomUUID() layout: version 4, IETF variant, lower-case hex,
+// 8-4-4-4-12 (core.clj:20-22).
+YSB_HD void uuid_words(u64 key, u64 k, u64* hi, u64* lo) {
+    u64 h = draw(key, 2 * k), l = draw(key, 2 * k + 1);
+    *hi = (h & ~0xF000ULL) | 0x4000ULL;
+    *lo = (l & 0x3FFFFFFFFFFFFFFFULL) | 0x8000000000000000ULL;
+}
+YSB_HD char hexdig(u32 v) { return (char)(v < 10 ? '0' + v : 'a' + (v - 10)); }
+YSB_HD void uuid_format(u64 hi, u64 lo, char* out) {
+    int o = 0;
+    for (int i = 0; i < 16; ++i) {
+        if (i == 8 || i == 12) out[o++] = '-';
+        out[o++] = hexdig((u32)(hi >> (60 - 4 * i)) & 0xF);
+    }
+    for (int i = 0; i < 16; ++i) {
+        if (i == 0 || i == 4) out[o++] = '-';
+        out[o++] = hexdig((u32)(lo >> (60 - 4 * i)) & 0xF);
+    }
+}
+
+// Generator constants (core.clj:68-69, 90-96).
+#define YSB_P0 "{\"user_id\": \""
+#define YSB_P1 "\", \"page_id\": \""
+#define YSB_P2 "\", \"ad_id\": \""
+#define YSB_P3 "\", \"ad_type\": \""
+#define YSB_P4 "\", \"event_type\": \""
+#define YSB_P5 "\", \"event_time\": \""
+#define YSB_P6 "\", \"ip_address\": \"1.2.3.4\"}"
+enum { LEN_P0 = 13, LEN_P1 = 15, LEN_P2 = 13, LEN_P3 = 15, LEN_P4 = 18, LEN_P5 = 18, LEN_P6 = 27 };
+enum { LINE_FIXED = LEN_P0 + LEN_P1 + LEN_P2 + LEN_P3 + LEN_P4 + LEN_P5 + LEN_P6 + 3 * 36 + 1 };  // 228
+
+YSB_HD const char* ad_type_str(u32 k) {
+    return k == 0 ? "banner" : k == 1 ? "modal" : k == 2 ? "sponsored-search" : k == 3 ? "mail" : "mobile";
+}
+YSB_HD u32 ad_type_len(u32 k) { return k == 0 ? 6 : k == 1 ? 5 : k == 2 ? 16 : k == 3 ? 4 : 6; }
+YSB_HD const char* event_type_str(u32 k) { return k == 0 ? "view" : k == 1 ? "click" : "purchase"; }
+YSB_HD u32 event_type_len(u32 k) { return k == 0 ? 4 : k == 1 ? 5 : 8; }
+
+// POD generator spec (host or device pointer in `subset`).
+struct GenSpec {
+    u64 seed;
+    u32 n_campaigns, ads_per_campaign;
+    i64 t0_ms;
+    u64 events_per_sec;
+    u32 with_skew, n_users;
+    const u32* subset;   // ad indices to draw from (nullptr: all)
+    u32 n_pick;          // number of ads drawn from
+    u32 pad;
+};
+
+struct GenEvent {
+    u32 ad, ad_type, event_type;
+    i64 time_ms;
+};
+
+YSB_HD GenEvent gen_event(const GenSpec& s, u64 i) {
+    GenEvent e;
+    u64 c = draw(stream_key(s.seed, S_CHOICE), i);
+    u32 idx = (u32)(((c >> 32) * (u64)s.n_pick) >> 32);   // rand-nth ads (core.clj:92)
+    e.ad = s.subset ? s.subset[idx] : idx;
+    e.ad_type = (u32)(c & 0xFFFF) % 5u;                    // rand-nth ad-types (:93)
+    e.event_type = (u32)((c >> 16) & 0xFFFF) % 3u;         // rand-nth event-types (:94)
+    i64 t = s.t0_ms + (i64)((i * 1000ULL) / s.events_per_sec);   // (+ start-time (* n 10)) (:95)
+    if (s.with_skew) {                                      // make-kafka-event-at (:166-174)
+        u64 r = draw(stream_key(s.seed, S_SKEW), i);
+        t += 50 - (i64)(r % 100);
+        if (((r >> 17) % 100000ULL) == 0) t -= (i64)((r >> 40) % 60000ULL);
+    }
+    e.time_ms = t;
+    return e;
+}
+
+YSB_HD u32 dec_len(i64 v) {
+    u64 m = v < 0 ? (u64)0 - (u64)v : (u64)v;
+    u32 n = 1;
+    while (m >= 10) { m /= 10; ++n; }
+    return n + (v < 0 ? 1u : 0u);
+}
+YSB_HD u32 dec_format(i64 v, char* out) {
+    u32 n = dec_len(v);
+    u64 m = v < 0 ? (u64)0 - (u64)v : (u64)v;
+    u32 o = n;
+    do { out[--o] = (char)('0' + (m % 10)); m /= 10; } while (m);
+    if (v < 0) out[0] = '-';
+    return n;
+}
+
+YSB_HD u32 gen_line_len(const GenEvent& e) {
+    return (u32)LINE_FIXED + ad_type_len(e.ad_type) + event_type_len(e.event_type) + dec_len(e.time_ms);
+}
+
+YSB_HD char* put_str(char* o, const char* s, u32 n) {
+    for (u32 k = 0; k < n; ++k) o[k] = s[k];
+    return o + n;
+}
+
+// One event line, exactly the str of core.clj:90-96 plus the "\n" of :97.
+YSB_HD u32 gen_line_write(const GenSpec& s, u64 i, const GenEvent& e, char* out) {
+    char* o = out;
+    u64 hi, lo;
+    o = put_str(o, YSB_P0, LEN_P0);
+    if (s.n_users == 0) uuid_words(stream_key(s.seed, S_USER), i, &hi, &lo);
+    else uuid_words(stream_key(s.seed, S_USER), draw(stream_key(s.seed, S_USERPOOL), i) % s.n_users, &hi, &lo);
+    uuid_format(hi, lo, o); o += 36;
+    o = put_str(o, YSB_P1, LEN_P1);
+    if (s.n_users == 0) uuid_words(stream_key(s.seed, S_PAGE), i, &hi, &lo);
+    else uuid_words(stream_key(s.seed, S_PAGE), draw(stream_key(s.seed, S_PAGEPOOL), i) % s.n_users, &hi, &lo);
+    uuid_format(hi, lo, o); o += 36;
+    o = put_str(o, YSB_P2, LEN_P2);
+    uuid_words(stream_key(s.seed, S_AD), e.ad, &hi, &lo);
+    uuid_format(hi, lo, o); o += 36;
+    o = put_str(o, YSB_P3, LEN_P3);
+    o = put_str(o, ad_type_str(e.ad_type), ad_type_len(e.ad_type));
+    o = put_str(o, YSB_P4, LEN_P4);
+    o = put_str(o, event_type_str(e.event_type), event_type_len(e.event_type));
+    o = put_str(o, YSB_P5, LEN_P5);
+    o += dec_format(e.time_ms, o);
+    o = put_str(o, YSB_P6, LEN_P6);
+    *o++ = '\n';
+    return (u32)(o - out);
+}
+
+// ---------------------------------------------------------------------------
+// Device ad -> campaign table: open addressing, linear probing, 64-byte slots
+// (one cache line per probe).  Slot words: [0] key length, [1] campaign index
+// (EMPTY_SLOT = free), [2..15] key bytes, zero padded.  Keys are exact byte
+// strings, i.e. HashMap<String,String>.get semantics on the ad_id string
+// (AdvertisingTopologyNative.java:464).
+// ---------------------------------------------------------------------------
+enum : u32 { SLOT_WORDS = 16, KEY_WORDS = 14, MAX_KEY_BYTES = 56, EMPTY_SLOT = 0xFFFFFFFFu };
+
+// Hash of a zero-padded key held as little-endian 32-bit words.
+YSB_HD u32 key_hash(const u32* w, u32 len) {
+    u32 h = 0x811C9DC5u ^ (len * 0x9E3779B1u);
+    u32 nw = (len + 3) >> 2;
+    for (u32 k = 0; k < nw; ++k) {
+        h = (h ^ w[k]) * 0x01000193u;
+        h ^= h >> 15;
+    }
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+
+// ---------------------------------------------------------------------------
+// Exact Java long division t / d (truncating toward zero) for a runtime d >= 1,
+// as a multiply-high: for n < 2^63, floor(n/d) = mulhi(n, M) >> s with
+// l = ceil(log2 d), M = ceil(2^(63+l) / d) < 2^64, s = l - 1 (Granlund-Montgomery).
+// INT64_MIN (|t| = 2^63) is precomputed.
+// ---------------------------------------------------------------------------
+struct DivMagic {
+    u64 M;
+    u32 s;
+    u32 is_one;
+    i64 d;
+    i64 q_min;   // INT64_MIN / d
+};
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+static inline DivMagic div_magic(i64 d) {
+    DivMagic m;
+    m.d = d;
+    m.q_min = INT64_MIN / d;
+    m.is_one = d == 1;
+    u32 l = 0;
+    while (l < 63 && ((u64)1 << l) < (u64)d) ++l;
+    if (d == 1) { m.M = 0; m.s = 0; return m; }
+    // M = ceil(2^(63+l)/d) computed with 128-bit arithmetic
+    unsigned __int128 num = (unsigned __int128)1 << (63 + l);
+    unsigned __int128 q = num / (u64)d;
+    if (num % (u64)d) q += 1;
+    m.M = (u64)q;
+    m.s = l - 1;
+    return m;
+}
+#endif
+
+YSB_HD u64 mulhi64(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (u64)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+YSB_HD i64 div_trunc(i64 t, const DivMagic& m) {
+    if (m.is_one) return t;
+    if (t == INT64_MIN) return m.q_min;
+    u64 n = t < 0 ? (u64)(-t) : (u64)t;
+    u64 q = mulhi64(n, m.M) >> m.s;
+    return t < 0 ? -(i64)q : (i64)q;
+}
+
+// Stats slots in the device stats array.
+enum : u32 {
+    ST_EVENTS = 0, ST_VIEWS, ST_JOINED, ST_MISSES, ST_PARSE_ERR, ST_TIME_ERR,
+    ST_OUT_OF_RING, ST_OVF_DROPPED, ST_COUNT_
+};
+
+struct OvfEntry {
+    u32 campaign;
+    u32 count;
+    i64 bucket;
+};
+
+}  // namespace ysb

@@ -1,0 +1,54 @@
+// ysb_kernels.h -- launch interface between the C-ABI layer (ysb_capi.cpp) and the
+// gfx950 kernels (ysb_scan.hip, ysb_gen.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "ysb_common.h"
+
+namespace ysb {
+
+// Geometry of the fused scan kernel (see DESIGN.md "Kernel 1").
+constexpr int SCAN_TPB = 256;                 // threads per workgroup = lines per tile
+constexpr int TILE_CAP = 66560;               // LDS bytes of one tile (260 B/line average)
+constexpr int TILE_CHUNKS = TILE_CAP / 16;    // 16-byte chunks per tile
+constexpr int CHUNKS_PER_THREAD = (TILE_CHUNKS + SCAN_TPB - 1) / SCAN_TPB;  // 17
+constexpr int LCNT_CAP = 1024;                // u32 per-workgroup (campaign, window) counters
+
+struct ScanParams {
+    const u8* bytes;            // batch bytes (16-byte aligned)
+    u64 nbytes;
+    const u32* off;             // n line offsets
+    u64 n;
+    const u32* table;           // ad table, SLOT_WORDS u32 per slot
+    u32 table_mask;             // slots - 1
+    u32 n_campaigns;
+    unsigned long long* counts; // [c_pad][W] u64, campaign-major
+    u32 ring_w;                 // W (power of two)
+    u32 lds_wl;                 // per-WG window slots in LDS (power of two), 0 = off
+    u32 lds_wl_log2;
+    u32 require_mask;           // required-key bit mask
+    const i64* ring;            // ring[0] = first bucket, ring[1] = 1 when set
+    DivMagic div;
+    OvfEntry* ovf;
+    u32* ovf_count;
+    u32 ovf_cap;
+    u32 tiles_per_block;
+    u64 n_tiles;
+    unsigned long long* stats;  // ST_COUNT_ u64
+};
+
+void launch_scan(const ScanParams& p, hipStream_t s);
+// Sets ring[0..1] from the first lines of a batch if ring[1] == 0.
+void launch_ring_autobase(const ScanParams& p, hipStream_t s);
+
+// Generator kernels (ysb_gen.hip).
+hipError_t gen_events_device(const GenSpec& spec, u64 first, u64 n, u8* d_out, u64 cap,
+                             u32* d_off, u64* nbytes, hipStream_t s);
+void launch_truth(const GenSpec& spec, u64 first, u64 n, const DivMagic& div,
+                  unsigned long long* truth, u32 ring_w, const i64* ring,
+                  unsigned long long* truth_outside, hipStream_t s);
+// out[0] += #cells differing, out[1] += sum(truth), out[2] += sum(counts)
+void launch_compare(const unsigned long long* a, const unsigned long long* b, u64 cells,
+                    unsigned long long* out, hipStream_t s);
+void launch_add_u64(unsigned long long* dst, const unsigned long long* src, u64 n, hipStream_t s);
+
+}  // namespace ysb

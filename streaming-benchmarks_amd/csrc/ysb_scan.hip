@@ -1,0 +1,773 @@
+// ysb_scan.hip -- Kernel 1: the fused YSB advertising hot path on gfx950.
+//
+// One pass over a batch of JSON event lines does what the reference's Flink chain
+// does per record (flink-benchmarks/.../AdvertisingTopologyNative.java:122-138,
+// storm-benchmarks/.../AdvertisingTopology.java:53-176):
+//
+//   DeserializeBolt   new JSONObject(line).getString(...)          (:263-272)
+//   EventFilterBolt   event_type.equals("view")                     (:434)
+//   project           (ad_id, event_time)                           (Storm :103-107)
+//   RedisJoinBolt     campaign = ad_campaign.get(ad_id), drop miss  (:461-474)
+//   CampaignProcessorCommon.execute
+//                     bucket = Long.parseLong(event_time) / 10000;
+//                     windows[bucket][campaign].seenCount++         (CampaignProcessorCommon.java:57-67)
+//
+// Structure (DESIGN.md "Kernel 1"): a workgroup of 256 threads walks a contiguous
+// run of 256-line tiles.  Phase A streams a tile's bytes HBM -> registers -> LDS
+// with 16-byte coalesced loads (the next tile's loads are issued before the
+// current tile is parsed, so they land under Phase B) and classifies every byte
+// once: a 1-bit-per-byte quote-candidate bitmap and a per-16-byte backslash flag.
+// Phase B gives each thread one line: a strict JSON tokenizer that jumps from
+// quote to quote through the bitmap, matches the required keys, and extracts the
+// ad_id / event_type / event_time values.  Joined views are counted into
+// per-workgroup LDS (campaign, window) counters that are flushed to the HBM ring
+// table with 64-bit atomics only when the workgroup's window moves.
+#include "ysb_kernels.h"
+
+namespace ysb {
+
+// Key ids (bit masks) of the fields DeserializeBolt reads.
+enum : u32 {
+    K_USER = 1u << 0, K_PAGE = 1u << 1, K_AD = 1u << 2, K_ADTYPE = 1u << 3,
+    K_ETYPE = 1u << 4, K_ETIME = 1u << 5, K_IP = 1u << 6
+};
+
+__host__ __device__ constexpr u32 w4(char a, char b, char c, char d) {
+    return (u32)(u8)a | ((u32)(u8)b << 8) | ((u32)(u8)c << 16) | ((u32)(u8)d << 24);
+}
+
+// ---------------------------------------------------------------------------
+// Byte sources.  Positions are ints relative to the source base.
+// ---------------------------------------------------------------------------
+struct LdsSrc {
+    const u32* d;   // tile bytes as dwords
+    const u32* q;   // quote-candidate bitmap (bit per byte)
+    __device__ __forceinline__ u32 b(int p) const { return (d[p >> 2] >> ((p & 3) << 3)) & 0xFFu; }
+    __device__ __forceinline__ u32 load4(int p) const {
+        const u32 lo = d[p >> 2], hi = d[(p >> 2) + 1];
+        return __builtin_amdgcn_alignbyte(hi, lo, (u32)(p & 3));
+    }
+    // First '"' at or after p (before e), or -1.  Valid only for lines without a
+    // backslash: then every quote ends or starts a string.
+    __device__ __forceinline__ int next_quote(int p, int e) const {
+        while (p < e) {
+            const int wi = p >> 5;
+            const u32 w = q[wi] >> (p & 31);
+            if (w) {
+                const int k = p + (int)__builtin_ctz(w);
+                if (k >= e) return -1;
+                if (b(k) == '"') return k;     // candidates may be false positives
+                p = k + 1;
+            } else {
+                p = (wi + 1) << 5;
+            }
+        }
+        return -1;
+    }
+};
+
+struct GlbSrc {  // slow path for tiles that do not fit the LDS tile
+    const u8* base;
+    u64 n;
+    __device__ __forceinline__ u32 b(int p) const { return (u64)p < n ? base[p] : 0u; }
+    __device__ __forceinline__ u32 load4(int p) const {
+        return b(p) | (b(p + 1) << 8) | (b(p + 2) << 16) | (b(p + 3) << 24);
+    }
+};
+
+struct BufSrc {  // decoded (un-escaped) strings
+    const u8* buf;
+    __device__ __forceinline__ u32 b(int p) const { return buf[p]; }
+    __device__ __forceinline__ u32 load4(int p) const {
+        return (u32)buf[p] | ((u32)buf[p + 1] << 8) | ((u32)buf[p + 2] << 16) | ((u32)buf[p + 3] << 24);
+    }
+};
+
+struct Span { int s, e; int esc; };
+
+__device__ __forceinline__ bool is_ws(u32 c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+__device__ __forceinline__ bool is_hex(u32 c) {
+    return (c - '0') < 10u || ((c | 0x20u) - 'a') < 6u;
+}
+__device__ __forceinline__ u32 hex_val(u32 c) { return (c - '0') < 10u ? c - '0' : (c | 0x20u) - 'a' + 10; }
+
+template <class S>
+__device__ __forceinline__ int skip_ws(const S& src, int p, int e) {
+    while (p < e && is_ws(src.b(p))) ++p;
+    return p;
+}
+
+// Index of the closing quote of a string whose content starts at p, or -1.
+// Escapes follow RFC 8259 (\" \\ \/ \b \f \n \r \t \uXXXX); esc is set when any
+// escape occurs.  Raw control characters are accepted (documented in DESIGN.md).
+template <bool FAST, class S>
+__device__ __forceinline__ int scan_str(const S& src, int p, int e, int& esc) {
+    if constexpr (FAST) {
+        return src.next_quote(p, e);
+    } else {
+        while (p < e) {
+            const u32 c = src.b(p);
+            if (c == '"') return p;
+            if (c == '\\') {
+                esc = 1;
+                if (p + 1 >= e) return -1;
+                const u32 x = src.b(p + 1);
+                if (x == 'u') {
+                    if (p + 5 >= e) return -1;
+                    if (!is_hex(src.b(p + 2)) || !is_hex(src.b(p + 3)) || !is_hex(src.b(p + 4)) ||
+                        !is_hex(src.b(p + 5)))
+                        return -1;
+                    p += 6;
+                } else if (x == '"' || x == '\\' || x == '/' || x == 'b' || x == 'f' || x == 'n' ||
+                           x == 'r' || x == 't') {
+                    p += 2;
+                } else {
+                    return -1;
+                }
+                continue;
+            }
+            ++p;
+        }
+        return -1;
+    }
+}
+
+// Decodes the (validated) escaped string [s, e) as UTF-8 into buf (at most cap
+// bytes written); returns the full decoded length.
+template <class S>
+__device__ __noinline__ int decode_str(const S& src, int s, int e, u8* buf, int cap) {
+    int n = 0, p = s;
+    auto put = [&](u32 c) { if (n < cap) buf[n] = (u8)c; ++n; };
+    while (p < e) {
+        const u32 c = src.b(p);
+        if (c != '\\') { put(c); ++p; continue; }
+        const u32 x = src.b(p + 1);
+        if (x == 'u') {
+            u32 cp = (hex_val(src.b(p + 2)) << 12) | (hex_val(src.b(p + 3)) << 8) |
+                     (hex_val(src.b(p + 4)) << 4) | hex_val(src.b(p + 5));
+            p += 6;
+            if (cp >= 0xD800 && cp < 0xDC00 && p + 5 < e && src.b(p) == '\\' && src.b(p + 1) == 'u') {
+                const u32 lo = (hex_val(src.b(p + 2)) << 12) | (hex_val(src.b(p + 3)) << 8) |
+                               (hex_val(src.b(p + 4)) << 4) | hex_val(src.b(p + 5));
+                if (lo >= 0xDC00 && lo < 0xE000) {
+                    cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+                    p += 6;
+                }
+            }
+            if (cp < 0x80) put(cp);
+            else if (cp < 0x800) { put(0xC0 | (cp >> 6)); put(0x80 | (cp & 0x3F)); }
+            else if (cp < 0x10000) { put(0xE0 | (cp >> 12)); put(0x80 | ((cp >> 6) & 0x3F)); put(0x80 | (cp & 0x3F)); }
+            else { put(0xF0 | (cp >> 18)); put(0x80 | ((cp >> 12) & 0x3F)); put(0x80 | ((cp >> 6) & 0x3F)); put(0x80 | (cp & 0x3F)); }
+        } else {
+            put(x == 'b' ? 8u : x == 'f' ? 12u : x == 'n' ? 10u : x == 'r' ? 13u : x == 't' ? 9u : x);
+            p += 2;
+        }
+    }
+    return n;
+}
+
+// Key id of the key string [s, s+len) (0 = a key DeserializeBolt does not read).
+template <class S>
+__device__ __forceinline__ u32 match_key_raw(const S& src, int s, int len) {
+    if (len == 5) {
+        return (src.load4(s) == w4('a', 'd', '_', 'i') && src.b(s + 4) == 'd') ? K_AD : 0u;
+    }
+    if (len == 7) {
+        const u32 a = src.load4(s), b = src.load4(s + 3);
+        if (a == w4('u', 's', 'e', 'r') && b == w4('r', '_', 'i', 'd')) return K_USER;
+        if (a == w4('p', 'a', 'g', 'e') && b == w4('e', '_', 'i', 'd')) return K_PAGE;
+        if (a == w4('a', 'd', '_', 't') && b == w4('t', 'y', 'p', 'e')) return K_ADTYPE;
+        return 0u;
+    }
+    if (len == 10) {
+        const u32 a = src.load4(s), b = src.load4(s + 4), c = src.load4(s + 6);
+        if (a == w4('e', 'v', 'e', 'n')) {
+            if (b == w4('t', '_', 't', 'y') && c == w4('t', 'y', 'p', 'e')) return K_ETYPE;
+            if (b == w4('t', '_', 't', 'i') && c == w4('t', 'i', 'm', 'e')) return K_ETIME;
+            return 0u;
+        }
+        if (a == w4('i', 'p', '_', 'a') && b == w4('d', 'd', 'r', 'e') && c == w4('r', 'e', 's', 's')) return K_IP;
+    }
+    return 0u;
+}
+
+template <class S>
+__device__ __noinline__ u32 match_key_esc(const S& src, int s, int e) {
+    u8 buf[20];
+    const int n = decode_str(src, s, e, buf, 16);
+    if (n > 12) return 0u;
+    for (int k = n; k < 20; ++k) buf[k] = 0;
+    return match_key_raw(BufSrc{buf}, 0, n);
+}
+
+// Skips a non-string value (number, literal, nested object/array); returns the
+// position after it or -1.  Not on the generator's path (every value is a string).
+template <class S>
+__device__ __noinline__ int skip_value(const S& src, int p, int e) {
+    u32 c = src.b(p);
+    if (c == 't') return (p + 3 < e && src.load4(p) == w4('t', 'r', 'u', 'e')) ? p + 4 : -1;
+    if (c == 'n') return (p + 3 < e && src.load4(p) == w4('n', 'u', 'l', 'l')) ? p + 4 : -1;
+    if (c == 'f') return (p + 4 < e && src.load4(p + 1) == w4('a', 'l', 's', 'e')) ? p + 5 : -1;
+    if (c == '-' || (c - '0') < 10u) {   // -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
+        if (c == '-') { if (++p >= e) return -1; c = src.b(p); }
+        if (c == '0') ++p;
+        else if ((c - '1') < 9u) { while (p < e && (src.b(p) - '0') < 10u) ++p; }
+        else return -1;
+        if (p < e && src.b(p) == '.') {
+            ++p; const int q = p;
+            while (p < e && (src.b(p) - '0') < 10u) ++p;
+            if (p == q) return -1;
+        }
+        if (p < e && (src.b(p) | 0x20u) == 'e') {
+            ++p;
+            if (p < e && (src.b(p) == '+' || src.b(p) == '-')) ++p;
+            const int q = p;
+            while (p < e && (src.b(p) - '0') < 10u) ++p;
+            if (p == q) return -1;
+        }
+        return p;
+    }
+    if (c == '{' || c == '[') {   // bracket matching, strings skipped (contents not validated)
+        int depth = 0;
+        while (p < e) {
+            c = src.b(p);
+            if (c == '"') {
+                int esc = 0;
+                const int q = scan_str<false>(src, p + 1, e, esc);
+                if (q < 0) return -1;
+                p = q + 1;
+                continue;
+            }
+            if (c == '{' || c == '[') ++depth;
+            else if (c == '}' || c == ']') { if (--depth == 0) return p + 1; }
+            ++p;
+        }
+        return -1;
+    }
+    return -1;
+}
+
+// Strict JSON object tokenizer for one line [s, e).  Returns false where org.json's
+// JSONObject(String) or getString(key) would throw (AdvertisingTopologyNative.java:263-272):
+// malformed JSON, a duplicate key among the recognised ones, a required key missing
+// or not a string.
+template <bool FAST, class S>
+__device__ __forceinline__ bool parse_line(const S& src, int s, int e, u32 require,
+                                           Span& ad, Span& et, Span& tm) {
+    int p = skip_ws(src, s, e);
+    if (p >= e || src.b(p) != '{') return false;
+    p = skip_ws(src, p + 1, e);
+    u32 seen = 0;
+    if (p < e && src.b(p) == '}') {
+        ++p;
+    } else {
+        while (true) {
+            if (p >= e || src.b(p) != '"') return false;
+            int kesc = 0;
+            const int ke = scan_str<FAST>(src, p + 1, e, kesc);
+            if (ke < 0) return false;
+            const u32 kid = kesc ? match_key_esc(src, p + 1, ke) : match_key_raw(src, p + 1, ke - p - 1);
+            p = ke + 1;
+            // common case ": " then the value's quote
+            if (p + 2 < e && (src.load4(p) & 0xFFFFFFu) == w4(':', ' ', '"', 0)) {
+                p += 2;
+            } else {
+                p = skip_ws(src, p, e);
+                if (p >= e || src.b(p) != ':') return false;
+                p = skip_ws(src, p + 1, e);
+                if (p >= e) return false;
+            }
+            if (src.b(p) == '"') {
+                int vesc = 0;
+                const int ve = scan_str<FAST>(src, p + 1, e, vesc);
+                if (ve < 0) return false;
+                if (kid) {
+                    if (seen & kid) return false;   // org.json: "Duplicate key"
+                    seen |= kid;
+                    const Span sp{p + 1, ve, vesc};
+                    if (kid == K_AD) ad = sp;
+                    else if (kid == K_ETYPE) et = sp;
+                    else if (kid == K_ETIME) tm = sp;
+                }
+                p = ve + 1;
+            } else {
+                const int q = skip_value(src, p, e);
+                if (q < 0) return false;
+                if (kid) {
+                    if (seen & kid) return false;
+                    seen |= kid;
+                    if (kid & require) return false;   // getString: "not a string."
+                }
+                p = q;
+            }
+            // common case ", " then the next key's quote
+            if (p + 2 < e && (src.load4(p) & 0xFFFFFFu) == w4(',', ' ', '"', 0)) {
+                p += 2;
+                continue;
+            }
+            p = skip_ws(src, p, e);
+            if (p >= e) return false;
+            const u32 c = src.b(p);
+            if (c == ',') { p = skip_ws(src, p + 1, e); continue; }
+            if (c == '}') { ++p; break; }
+            return false;
+        }
+    }
+    p = skip_ws(src, p, e);
+    return p == e && (seen & require) == require;
+}
+
+constexpr u32 VIEW = w4('v', 'i', 'e', 'w');
+
+template <class S>
+__device__ __forceinline__ bool span_is_view(const S& src, const Span& et) {
+    if (!et.esc) return et.e - et.s == 4 && src.load4(et.s) == VIEW;
+    u8 buf[12];
+    const int n = decode_str(src, et.s, et.e, buf, 8);
+    return n == 4 && buf[0] == 'v' && buf[1] == 'i' && buf[2] == 'e' && buf[3] == 'w';
+}
+
+// ad_id value -> zero-padded key words (false if longer than any table key can be).
+template <class S>
+__device__ __forceinline__ bool span_key(const S& src, const Span& ad, u32 (&kw)[KEY_WORDS], u32& klen) {
+    if (!ad.esc) {
+        const int len = ad.e - ad.s;
+        if (len > (int)MAX_KEY_BYTES) return false;
+        klen = (u32)len;
+#pragma unroll
+        for (int k = 0; k < (int)KEY_WORDS; ++k) {
+            const int r = len - 4 * k;
+            u32 w = r > 0 ? src.load4(ad.s + 4 * k) : 0u;
+            if (r > 0 && r < 4) w &= (1u << (8 * r)) - 1u;
+            kw[k] = w;
+        }
+        return true;
+    }
+    u8 buf[MAX_KEY_BYTES + 4];
+    const int n = decode_str(src, ad.s, ad.e, buf, MAX_KEY_BYTES);
+    if (n > (int)MAX_KEY_BYTES) return false;
+    klen = (u32)n;
+#pragma unroll
+    for (int k = 0; k < (int)KEY_WORDS; ++k) {
+        u32 w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (4 * k + j < n) w |= (u32)buf[4 * k + j] << (8 * j);
+        kw[k] = w;
+    }
+    return true;
+}
+
+__device__ __forceinline__ u32 key_hash_dev(const u32 (&w)[KEY_WORDS], u32 len) {
+    u32 h = 0x811C9DC5u ^ (len * 0x9E3779B1u);
+    const u32 nw = (len + 3) >> 2;
+#pragma unroll
+    for (u32 k = 0; k < KEY_WORDS; ++k) {
+        if (k < nw) {
+            h = (h ^ w[k]) * 0x01000193u;
+            h ^= h >> 15;
+        }
+    }
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+
+// RedisJoinBolt's ad_campaign.get(ad_id) (AdvertisingTopologyNative.java:464) as a
+// linear probe of the HBM/L2-resident table; -1 on a miss.
+__device__ __forceinline__ int probe(const u32* __restrict__ table, u32 mask, const u32 (&kw)[KEY_WORDS], u32 klen) {
+    u32 h = key_hash_dev(kw, klen);
+    for (u32 i = 0; i <= mask; ++i) {
+        const uint4* slot = reinterpret_cast<const uint4*>(table + (u64)((h + i) & mask) * SLOT_WORDS);
+        const uint4 s0 = slot[0];
+        if (s0.y == EMPTY_SLOT) return -1;
+        if (s0.x == klen) {
+            const uint4 s1 = slot[1], s2 = slot[2], s3 = slot[3];
+            const u32 diff = (s0.z ^ kw[0]) | (s0.w ^ kw[1]) | (s1.x ^ kw[2]) | (s1.y ^ kw[3]) |
+                             (s1.z ^ kw[4]) | (s1.w ^ kw[5]) | (s2.x ^ kw[6]) | (s2.y ^ kw[7]) |
+                             (s2.z ^ kw[8]) | (s2.w ^ kw[9]) | (s3.x ^ kw[10]) | (s3.y ^ kw[11]) |
+                             (s3.z ^ kw[12]) | (s3.w ^ kw[13]);
+            if (diff == 0) return (int)s0.y;
+        }
+    }
+    return -1;
+}
+
+// Long.parseLong(event_time) (CampaignProcessorCommon.java:58): [+-]?[0-9]+ within int64.
+template <class S>
+__device__ __forceinline__ bool parse_digits(const S& src, int p, int e, i64& out) {
+    if (p >= e) return false;
+    bool neg = false;
+    const u32 c0 = src.b(p);
+    if (c0 == '-') { neg = true; ++p; }
+    else if (c0 == '+') { ++p; }
+    if (p >= e) return false;
+    u64 acc = 0;
+    const u32 last_max = neg ? 8u : 7u;
+    for (; p < e; ++p) {
+        const u32 d = src.b(p) - '0';
+        if (d > 9u) return false;
+        if (acc >= 922337203685477580ULL) {
+            if (acc > 922337203685477580ULL || d > last_max) return false;
+        }
+        acc = acc * 10u + d;
+    }
+    out = neg ? (i64)(0 - acc) : (i64)acc;
+    return true;
+}
+
+template <class S>
+__device__ __forceinline__ bool span_long(const S& src, const Span& tm, i64& out) {
+    if (!tm.esc) return parse_digits(src, tm.s, tm.e, out);
+    u8 buf[68];
+    const int n = decode_str(src, tm.s, tm.e, buf, 64);
+    if (n > 64) return false;
+    return parse_digits(BufSrc{buf}, 0, n, out);
+}
+
+// One line end to end: returns 0 not counted, 1 counted (campaign/bucket set).
+// Per-thread tallies go to st[].
+struct Tally { u32 ev, view, join, miss, perr, terr, oor; };
+
+template <bool FAST, class S>
+__device__ __forceinline__ bool process_line(const S& src, int s, int e, const ScanParams& P,
+                                             Tally& t, u32& campaign, i64& bucket) {
+    Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
+    t.ev++;
+    if (!parse_line<FAST>(src, s, e, P.require_mask, ad, et, tm)) { t.perr++; return false; }
+    if (!span_is_view(src, et)) return false;                // EventFilterBolt
+    t.view++;
+    u32 kw[KEY_WORDS];
+    u32 klen = 0;
+    int c = -1;
+    if (span_key(src, ad, kw, klen)) c = probe(P.table, P.table_mask, kw, klen);   // RedisJoinBolt
+    if (c < 0) { t.miss++; return false; }
+    t.join++;
+    i64 tv;
+    if (!span_long(src, tm, tv)) { t.terr++; return false; }   // CampaignProcessorCommon :58
+    campaign = (u32)c;
+    bucket = div_trunc(tv, P.div);
+    return true;
+}
+
+// Adds v views to (campaign, bucket): the ring cell if the bucket is live, else the
+// exact side list.
+__device__ __forceinline__ void global_add(const ScanParams& P, i64 ring_lo, bool ring_set,
+                                           u32 c, i64 b, u32 v, Tally& t) {
+    if (ring_set) {
+        const i64 rel = b - ring_lo;
+        if (rel >= 0 && rel < (i64)P.ring_w) {
+            atomicAdd(&P.counts[(u64)c * P.ring_w + (u64)(b & (i64)(P.ring_w - 1))], (unsigned long long)v);
+            return;
+        }
+    }
+    t.oor += v;
+    const u32 idx = atomicAdd(P.ovf_count, 1u);
+    if (idx < P.ovf_cap) {
+        OvfEntry en;
+        en.campaign = c; en.count = v; en.bucket = b;
+        P.ovf[idx] = en;
+    } else {
+        atomicAdd(&P.stats[ST_OVF_DROPPED], (unsigned long long)v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LDS layout (dynamic, 16-byte aligned carve, no static __shared__)
+// ---------------------------------------------------------------------------
+constexpr int BS_WORDS = CHUNKS_PER_THREAD * SCAN_TPB / 32;              // 136
+constexpr int OFF_TILE = 0;
+constexpr int OFF_QBITS = OFF_TILE + TILE_CAP + 64;
+constexpr int OFF_BS = OFF_QBITS + TILE_CHUNKS * 2 + 16;
+constexpr int OFF_LSTART = OFF_BS + BS_WORDS * 4;
+constexpr int OFF_LCNT = OFF_LSTART + (SCAN_TPB + 4) * 4;
+constexpr int OFF_MISC = OFF_LCNT + LCNT_CAP * 4;
+constexpr int LDS_BYTES = OFF_MISC + 64;
+static_assert(OFF_QBITS % 16 == 0 && OFF_BS % 16 == 0 && OFF_LSTART % 16 == 0 && OFF_LCNT % 16 == 0 &&
+              OFF_MISC % 16 == 0, "LDS carve must stay 16-byte aligned");
+static_assert(LDS_BYTES <= 81920, "two workgroups per CU need <= 80 KiB of LDS each");
+
+struct TileInfo {
+    u64 first;
+    u32 count;
+    u32 s0;        // byte offset of the tile's first line
+    u32 delta;     // s0 - aligned base
+    u32 len;       // bytes in LDS (from the aligned base)
+    u32 e;         // end offset of the tile's last line
+    bool oversize; // does not fit TILE_CAP (or offsets are not monotone)
+    const u8* abase;
+};
+
+__device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t) {
+    TileInfo ti;
+    ti.first = t * SCAN_TPB;
+    const u64 rem = P.n - ti.first;
+    ti.count = rem < (u64)SCAN_TPB ? (u32)rem : (u32)SCAN_TPB;
+    const u32 s0 = P.off[ti.first];
+    const u64 e = (ti.first + ti.count < P.n) ? (u64)P.off[ti.first + ti.count] : P.nbytes;
+    ti.s0 = s0;
+    ti.e = (u32)e;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(P.bytes) + s0;
+    ti.abase = reinterpret_cast<const u8*>(a & ~(uintptr_t)15);
+    ti.delta = (u32)(a & 15);
+    const bool sane = (u64)s0 <= e && e <= P.nbytes;
+    const u64 len = sane ? e - s0 + ti.delta : ~0ULL;
+    ti.oversize = !sane || len > (u64)TILE_CAP;
+    ti.len = ti.oversize ? 0u : (u32)len;
+    return ti;
+}
+
+__device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const TileInfo& ti, uint4 (&pre)[CHUNKS_PER_THREAD],
+                                                 u32& my_off) {
+    const int tid = threadIdx.x;
+    const u32 nch = (ti.len + 15) >> 4;
+    const u8* end = P.bytes + P.nbytes;
+#pragma unroll
+    for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
+        const u32 k = (u32)(j * SCAN_TPB + tid);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < nch) {
+            const u8* a = ti.abase + 16u * k;
+            if (a + 16 <= end) {
+                v = *reinterpret_cast<const uint4*>(a);
+            } else {   // the batch's last partial chunk
+                u32 w[4] = {0, 0, 0, 0};
+                for (int x = 0; x < 16; ++x)
+                    if (a + x < end) w[x >> 2] |= (u32)a[x] << ((x & 3) * 8);
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+        pre[j] = v;
+    }
+    my_off = ((u32)tid < ti.count) ? P.off[ti.first + tid] : 0u;
+}
+
+// Quote-candidate nibble of one dword: bit i set if byte i may be '"'.  The
+// haszero trick can flag a byte above a true zero falsely; the tokenizer verifies
+// every candidate, so only exactness of the true positives matters.
+__device__ __forceinline__ u32 quote_nibble(u32 w) {
+    const u32 t = w ^ 0x22222222u;
+    const u32 z = (t - 0x01010101u) & ~t & 0x80808080u;
+    return (z * 0x00204081u) >> 28;
+}
+__device__ __forceinline__ u32 has_backslash(u32 w) {
+    const u32 t = w ^ 0x5C5C5C5Cu;
+    return (t - 0x01010101u) & ~t & 0x80808080u;
+}
+
+__device__ __forceinline__ i64 block_max_i64(i64 v, i64* scratch) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const i64 x = __shfl_xor(v, o, 64);
+        v = x > v ? x : v;
+    }
+    if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
+    __syncthreads();
+    i64 r = scratch[0];
+#pragma unroll
+    for (int w = 1; w < SCAN_TPB / 64; ++w) r = scratch[w] > r ? scratch[w] : r;
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ u32 wave_sum(u32 v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
+    extern __shared__ __attribute__((aligned(16))) u8 smem[];
+    u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
+    u16* q16 = reinterpret_cast<u16*>(smem + OFF_QBITS);
+    const u32* q32 = reinterpret_cast<const u32*>(smem + OFF_QBITS);
+    u32* bsb = reinterpret_cast<u32*>(smem + OFF_BS);
+    u32* lstart = reinterpret_cast<u32*>(smem + OFF_LSTART);
+    u32* lcnt = reinterpret_cast<u32*>(smem + OFF_LCNT);
+    i64* misc64 = reinterpret_cast<i64*>(smem + OFF_MISC);   // [0] lbase, [1] lset, [2..5] scratch
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const u64 t_begin = (u64)blockIdx.x * P.tiles_per_block;
+    if (t_begin >= P.n_tiles) return;
+    const u64 t_end = min(t_begin + P.tiles_per_block, P.n_tiles);
+
+    const i64 ring_lo = P.ring[0];
+    const bool ring_set = P.ring[1] != 0;
+    const u32 WL = P.lds_wl;
+    const u32 ncells = WL ? P.n_campaigns * WL : 0u;
+    for (u32 i = tid; i < ncells; i += SCAN_TPB) lcnt[i] = 0;
+    if (tid == 0) { misc64[0] = 0; misc64[1] = 0; }
+
+    Tally tl{0, 0, 0, 0, 0, 0, 0};
+    uint4 pre[CHUNKS_PER_THREAD];
+    u32 pre_off = 0;
+    TileInfo nxt = tile_info(P, t_begin);
+    issue_tile_loads(P, nxt, pre, pre_off);
+
+    const LdsSrc lsrc{tile32, q32};
+    for (u64 t = t_begin; t < t_end; ++t) {
+        const TileInfo cur = nxt;
+        const u32 my_off = pre_off;
+        // ---- Phase A: registers -> LDS, classify bytes --------------------------
+        if (!cur.oversize) {
+            const u32 nch = (cur.len + 15) >> 4;
+#pragma unroll
+            for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
+                const u32 k = (u32)(j * SCAN_TPB + tid);
+                const uint4 v = pre[j];
+                u32 bs = 0;
+                if (k < nch) {
+                    reinterpret_cast<uint4*>(tile32)[k] = v;
+                    q16[k] = (u16)(quote_nibble(v.x) | (quote_nibble(v.y) << 4) | (quote_nibble(v.z) << 8) |
+                                   (quote_nibble(v.w) << 12));
+                    bs = has_backslash(v.x) | has_backslash(v.y) | has_backslash(v.z) | has_backslash(v.w);
+                }
+                const unsigned long long m = __ballot(bs != 0);
+                if (lane == 0) {
+                    const u32 wi = (u32)(j * SCAN_TPB + wave * 64) >> 5;
+                    bsb[wi] = (u32)m;
+                    bsb[wi + 1] = (u32)(m >> 32);
+                }
+            }
+            if ((u32)tid < cur.count) lstart[tid] = my_off - cur.s0 + cur.delta;
+            if (tid == 0) lstart[cur.count] = cur.e - cur.s0 + cur.delta;
+        }
+        __syncthreads();
+        // ---- prefetch the next tile (lands while this one is parsed) -----------
+        if (t + 1 < t_end) {
+            nxt = tile_info(P, t + 1);
+            issue_tile_loads(P, nxt, pre, pre_off);
+        }
+        // ---- Phase B: one line per thread ---------------------------------------
+        bool valid = false;
+        u32 campaign = 0;
+        i64 bucket = 0;
+        if ((u32)tid < cur.count) {
+            if (!cur.oversize) {
+                const int ls = (int)lstart[tid], le = (int)lstart[tid + 1];
+                if (my_off < cur.s0 || ls > le || le > (int)cur.len) {
+                    tl.ev++; tl.perr++;
+                } else {
+                    bool slow = false;
+                    if (le > ls) {
+                        const int c0 = ls >> 4, c1 = (le - 1) >> 4;
+                        for (int wi = c0 >> 5; wi <= (c1 >> 5); ++wi) {
+                            u32 m = bsb[wi];
+                            if (wi == (c0 >> 5)) m &= ~0u << (c0 & 31);
+                            if (wi == (c1 >> 5) && (c1 & 31) != 31) m &= (2u << (c1 & 31)) - 1u;
+                            slow |= m != 0;
+                        }
+                    }
+                    if (!slow) valid = process_line<true>(lsrc, ls, le, P, tl, campaign, bucket);
+                    else valid = process_line<false>(lsrc, ls, le, P, tl, campaign, bucket);
+                }
+            } else {
+                // tile does not fit LDS: parse straight from HBM (rare; correctness path)
+                const u64 ls = my_off;
+                const u64 le = (cur.first + tid + 1 < P.n) ? (u64)P.off[cur.first + tid + 1] : P.nbytes;
+                if (ls > le || le > P.nbytes || le - ls > 0x7FFFFFFFull) {
+                    tl.ev++; tl.perr++;
+                } else {
+                    const GlbSrc gsrc{P.bytes + ls, le - ls};
+                    valid = process_line<false>(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket);
+                }
+            }
+        }
+        // ---- count: LDS window counters, flushed when the window moves ----------
+        if (WL) {
+            i64 lbase = misc64[0];
+            const bool lset = misc64[1] != 0;
+            const bool ahead = valid && (!lset || bucket >= lbase + (i64)WL);
+            if (__syncthreads_or(ahead)) {
+                const i64 mx = block_max_i64(valid ? bucket : INT64_MIN, misc64 + 2);
+                if (lset) {
+                    for (u32 i = tid; i < ncells; i += SCAN_TPB) {
+                        const u32 v = lcnt[i];
+                        if (v) {
+                            lcnt[i] = 0;
+                            global_add(P, ring_lo, ring_set, i >> P.lds_wl_log2,
+                                       lbase + (i64)(i & (WL - 1)), v, tl);
+                        }
+                    }
+                }
+                lbase = mx - (i64)(WL / 2) + 1;
+                __syncthreads();
+                if (tid == 0) { misc64[0] = lbase; misc64[1] = 1; }
+            }
+            if (valid) {
+                const i64 rel = bucket - lbase;
+                if (rel >= 0 && rel < (i64)WL) atomicAdd(&lcnt[(campaign << P.lds_wl_log2) + (u32)rel], 1u);
+                else global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+            }
+        } else if (valid) {
+            global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+        }
+        __syncthreads();
+    }
+    // ---- final flush + stats ---------------------------------------------------------
+    if (WL && misc64[1]) {
+        const i64 lbase = misc64[0];
+        for (u32 i = tid; i < ncells; i += SCAN_TPB) {
+            const u32 v = lcnt[i];
+            if (v) global_add(P, ring_lo, ring_set, i >> P.lds_wl_log2, lbase + (i64)(i & (WL - 1)), v, tl);
+        }
+    }
+    const u32 sums[7] = {wave_sum(tl.ev), wave_sum(tl.view), wave_sum(tl.join), wave_sum(tl.miss),
+                         wave_sum(tl.perr), wave_sum(tl.terr), wave_sum(tl.oor)};
+    if (lane == 0) {
+        const u32 slots[7] = {ST_EVENTS, ST_VIEWS, ST_JOINED, ST_MISSES, ST_PARSE_ERR, ST_TIME_ERR, ST_OUT_OF_RING};
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+            if (sums[k]) atomicAdd(&P.stats[slots[k]], (unsigned long long)sums[k]);
+    }
+}
+
+// Ring auto-base: the first joined view with a valid time among the first 256 lines
+// fixes the ring at min bucket - W/8 (room for out-of-order / late events).
+__global__ __launch_bounds__(SCAN_TPB) void ring_autobase_kernel(ScanParams P, i64* ring) {
+    __shared__ i64 scratch[SCAN_TPB / 64];
+    if (ring[1] != 0) return;
+    const int tid = threadIdx.x;
+    i64 b = INT64_MAX;
+    if ((u64)tid < P.n) {
+        const u64 ls = P.off[tid];
+        const u64 le = ((u64)tid + 1 < P.n) ? (u64)P.off[tid + 1] : P.nbytes;
+        if (ls <= le && le <= P.nbytes && le - ls < 0x7FFFFFFFull) {
+            Tally tl{0, 0, 0, 0, 0, 0, 0};
+            u32 c;
+            i64 bk;
+            const GlbSrc gsrc{P.bytes + ls, le - ls};
+            if (process_line<false>(gsrc, 0, (int)(le - ls), P, tl, c, bk)) b = bk;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const i64 x = __shfl_xor(b, o, 64);
+        b = x < b ? x : b;
+    }
+    if ((tid & 63) == 0) scratch[tid >> 6] = b;
+    __syncthreads();
+    if (tid == 0) {
+        i64 r = scratch[0];
+        for (int w = 1; w < SCAN_TPB / 64; ++w) r = scratch[w] < r ? scratch[w] : r;
+        if (r != INT64_MAX) {
+            ring[0] = r - (i64)(P.ring_w / 8);
+            ring[1] = 1;
+        }
+    }
+}
+
+void launch_scan(const ScanParams& p, hipStream_t s) {
+    if (p.n == 0) return;
+    const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;
+    hipLaunchKernelGGL(scan_kernel, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
+}
+
+void launch_ring_autobase(const ScanParams& p, hipStream_t s) {
+    if (p.n == 0) return;
+    hipLaunchKernelGGL(ring_autobase_kernel, dim3(1), dim3(SCAN_TPB), 0, s, p, const_cast<i64*>(p.ring));
+}
+
+int scan_lds_bytes() { return LDS_BYTES; }
+
+}  // namespace ysb

@@ -1,0 +1,9 @@
+"""ysb_amd: host-side binding of the MI355X-native YSB advertising hot path.
+
+The compute path is libysb_hip.so (HIP kernels for gfx950, C ABI in include/ysb_hip.h);
+this package only binds it.  There is no CPU fallback.
+"""
+from ._lib import LIB_PATH, YsbError, lib  # noqa: F401
+from .admap import AdCampaignMap  # noqa: F401
+from .context import YsbContext  # noqa: F401
+from .generator import AD_TYPES, EVENT_TYPES, GenParams, ad_shard, shard_ads  # noqa: F401

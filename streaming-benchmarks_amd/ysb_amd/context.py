@@ -1,0 +1,181 @@
+"""YsbContext: one device context of the GPU advertising operator.
+
+Mirrors the lifecycle of the reference operators it replaces
+(flink-benchmarks/.../AdvertisingTopologyNative.java:438-533):
+  RedisJoinBolt(Map) / open()         -> YsbContext(...) + load_ad_map(...)
+  flatMap(...) per record             -> submit(...) / submit_device(...) per batch
+  CampaignProcessorCommon.flushWindows -> drain(...)
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import INT64_MIN, YsbConfig, YsbCount, YsbStats, check, lib
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else C.c_void_p(0)
+
+
+class YsbContext:
+    def __init__(self, device=0, n_campaigns=100, time_divisor_ms=10000, window_ring=1024,
+                 max_batch_events=1 << 20, max_batch_bytes=256 << 20, ring_base_bucket=None,
+                 overflow_capacity=1 << 20, timing=False, require_ip=False, lds_count=True):
+        L = lib()
+        cfg = YsbConfig()
+        L.ysb_config_default(C.byref(cfg))
+        cfg.time_divisor_ms = time_divisor_ms
+        cfg.n_campaigns = n_campaigns
+        cfg.window_ring = window_ring
+        cfg.max_batch_events = max_batch_events
+        cfg.max_batch_bytes = max_batch_bytes
+        cfg.ring_base_bucket = INT64_MIN if ring_base_bucket is None else ring_base_bucket
+        cfg.overflow_capacity = overflow_capacity
+        cfg.flags = ((_lib.YSB_F_TIMING if timing else 0) | (_lib.YSB_F_REQUIRE_IP if require_ip else 0)
+                     | (0 if lds_count else _lib.YSB_F_NO_LDS_COUNT))
+        h = C.c_void_p()
+        check(L.ysb_open(C.byref(h), device, C.byref(cfg)), None)
+        self._h = h
+        self.cfg = cfg
+        self.device = device
+
+    # -- lifecycle ---------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ysb_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, rc):
+        return check(rc, self._h)
+
+    # -- join table --------------------------------------------------------------------
+    def load_ad_map(self, ad_ids, campaign_idx):
+        """ad_ids: sequence of str/bytes; campaign_idx: matching campaign indices."""
+        keys = [a.encode() if isinstance(a, str) else bytes(a) for a in ad_ids]
+        n = len(keys)
+        arr = (C.c_char_p * max(n, 1))(*keys)
+        lens = (C.c_uint32 * max(n, 1))(*[len(k) for k in keys])
+        camp = (C.c_uint32 * max(n, 1))(*[int(c) for c in campaign_idx])
+        self._c(lib().ysb_load_ad_map(self._h, arr, lens, camp, n))
+
+    # -- batches -----------------------------------------------------------------------
+    def slot_buffers(self, slot):
+        b, o = C.c_void_p(), C.c_void_p()
+        self._c(lib().ysb_slot_buffers(self._h, slot, C.byref(b), C.byref(o)))
+        return b.value, o.value
+
+    def submit(self, data, offsets, slot=0):
+        """Host batch (bytes / uint8 array + uint32 line offsets), double-buffered slot."""
+        buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(offsets, dtype=np.uint32)
+        self._c(lib().ysb_submit(self._h, slot, _ptr(buf), buf.size, _ptr(off), off.size))
+
+    def wait(self, slot):
+        self._c(lib().ysb_wait(self._h, slot))
+
+    def submit_device(self, d_bytes, nbytes, d_off, n):
+        self._c(lib().ysb_submit_device(self._h, C.c_void_p(d_bytes), nbytes, C.c_void_p(d_off), n))
+
+    def sync(self):
+        self._c(lib().ysb_sync(self._h))
+
+    # -- results -----------------------------------------------------------------------
+    def drain(self, bucket_lo=INT64_MIN, bucket_hi=(1 << 63) - 1, clear=False):
+        """Returns {(campaign, window_ms): count} for buckets in [bucket_lo, bucket_hi)."""
+        n = C.c_uint64()
+        self._c(lib().ysb_drain(self._h, bucket_lo, bucket_hi, 0, None, 0, C.byref(n)))
+        rows = (YsbCount * max(n.value, 1))()
+        self._c(lib().ysb_drain(self._h, bucket_lo, bucket_hi, int(clear), rows, n.value, C.byref(n)))
+        return {(rows[i].campaign, rows[i].window_ms): rows[i].count for i in range(n.value)}
+
+    def drain_buckets(self, **kw):
+        """Same as drain() keyed by (campaign, bucket) instead of window_ms."""
+        d = self.cfg.time_divisor_ms
+        return {(c, w // d): v for (c, w), v in self.drain(**kw).items()}
+
+    def stats(self):
+        s = YsbStats()
+        self._c(lib().ysb_stats_get(self._h, C.byref(s)))
+        return {n: getattr(s, n) for n, _ in YsbStats._fields_}
+
+    def reset(self):
+        self._c(lib().ysb_reset(self._h))
+
+    def ring_range(self):
+        lo, w = C.c_int64(), C.c_uint32()
+        self._c(lib().ysb_ring_range(self._h, C.byref(lo), C.byref(w)))
+        return lo.value, w.value
+
+    def kernel_time(self):
+        """(total ms, launches) of the scan kernel since the last call (needs timing=True)."""
+        t, k = C.c_double(), C.c_uint64()
+        self._c(lib().ysb_kernel_time(self._h, C.byref(t), C.byref(k)))
+        return t.value, k.value
+
+    def stream(self):
+        return lib().ysb_stream(self._h)
+
+    # -- device memory -----------------------------------------------------------------
+    def device_alloc(self, nbytes):
+        p = C.c_void_p()
+        self._c(lib().ysb_device_alloc(self._h, nbytes, C.byref(p)))
+        return p.value
+
+    def device_free(self, p):
+        self._c(lib().ysb_device_free(self._h, C.c_void_p(p)))
+
+    def h2d(self, d_dst, arr):
+        arr = np.ascontiguousarray(arr)
+        self._c(lib().ysb_memcpy_h2d(self._h, C.c_void_p(d_dst), _ptr(arr), arr.nbytes))
+
+    def d2h(self, arr, d_src):
+        self._c(lib().ysb_memcpy_d2h(self._h, _ptr(arr), C.c_void_p(d_src), arr.nbytes))
+        return arr
+
+    # -- multi-GPU ------------------------------------------------------------------------
+    @staticmethod
+    def group_unique_id() -> bytes:
+        buf = C.create_string_buffer(_lib.UNIQUE_ID_BYTES)
+        check(lib().ysb_group_unique_id(buf), None)
+        return buf.raw
+
+    def group_init(self, rank, nranks, uid: bytes):
+        self._c(lib().ysb_group_init(self._h, rank, nranks, C.create_string_buffer(uid, _lib.UNIQUE_ID_BYTES)))
+
+    def group_reduce_scatter(self):
+        self._c(lib().ysb_group_reduce_scatter(self._h))
+
+    def group_owned(self):
+        lo, hi = C.c_uint32(), C.c_uint32()
+        self._c(lib().ysb_group_owned(self._h, C.byref(lo), C.byref(hi)))
+        return lo.value, hi.value
+
+    # -- generator on this device ------------------------------------------------------------
+    def gen_events_device(self, params, first, n, d_out, cap, d_off):
+        nb = C.c_uint64()
+        self._c(lib().ysb_gen_events_device(self._h, C.byref(params.c), first, n, C.c_void_p(d_out), cap,
+                                            C.c_void_p(d_off), C.byref(nb)))
+        return nb.value
+
+    def truth_accumulate(self, params, first, n):
+        self._c(lib().ysb_truth_accumulate(self._h, C.byref(params.c), first, n))
+
+    def truth_compare(self):
+        m, t, r = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._c(lib().ysb_truth_compare(self._h, C.byref(m), C.byref(t), C.byref(r)))
+        return m.value, t.value, r.value

@@ -1,0 +1,81 @@
+"""Seeded generator of the data/ generator's event format (data/src/setup/core.clj:61-98,
+163-181), file-dump mode included.  Host generation runs in the C library (no GPU
+needed); device generation writes straight into HBM (YsbContext.gen_events_device).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import YsbGenParams, check, lib
+
+AD_TYPES = ("banner", "modal", "sponsored-search", "mail", "mobile")   # core.clj:68
+EVENT_TYPES = ("view", "click", "purchase")                            # core.clj:69
+
+
+class GenParams:
+    """Generator parameters; defaults: seed 42, 100 campaigns x 10 ads (core.clj:15,52),
+    t0 1.7e12 ms, 100,000 events per second of event time."""
+
+    def __init__(self, seed=42, n_campaigns=100, ads_per_campaign=10, t0_ms=1_700_000_000_000,
+                 events_per_sec=100_000, with_skew=False, n_users=0, ad_subset=None):
+        self.c = YsbGenParams()
+        lib().ysb_gen_default(C.byref(self.c))
+        self.c.seed = seed
+        self.c.n_campaigns = n_campaigns
+        self.c.ads_per_campaign = ads_per_campaign
+        self.c.t0_ms = t0_ms
+        self.c.events_per_sec = events_per_sec
+        self.c.with_skew = int(bool(with_skew))
+        self.c.n_users = n_users
+        self._subset = None
+        if ad_subset is not None:
+            self._subset = np.ascontiguousarray(ad_subset, dtype=np.uint32)
+            self.c.ad_subset = self._subset.ctypes.data_as(C.POINTER(C.c_uint32))
+            self.c.n_ad_subset = self._subset.size
+
+    @property
+    def n_ads(self):
+        return self.c.n_campaigns * self.c.ads_per_campaign
+
+    def ids(self):
+        """(campaign_ids, ad_ids) as lists of 36-char str; ad a -> campaign a // ads_per_campaign."""
+        cb = C.create_string_buffer(36 * self.c.n_campaigns)
+        ab = C.create_string_buffer(36 * self.n_ads)
+        check(lib().ysb_gen_ids(C.byref(self.c), cb, ab))
+        craw, araw = cb.raw.decode(), ab.raw.decode()
+        return ([craw[36 * i:36 * i + 36] for i in range(self.c.n_campaigns)],
+                [araw[36 * i:36 * i + 36] for i in range(self.n_ads)])
+
+    def ad_campaign_index(self):
+        return [a // self.c.ads_per_campaign for a in range(self.n_ads)]
+
+    def max_line_bytes(self):
+        return int(lib().ysb_gen_max_line_bytes(C.byref(self.c)))
+
+    def events_host(self, first, n):
+        """(bytes as uint8 array, uint32 line offsets) of events [first, first+n)."""
+        cap = n * self.max_line_bytes()
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        off = np.empty(max(n, 1), dtype=np.uint32)
+        nb = C.c_uint64()
+        check(lib().ysb_gen_events_host(C.byref(self.c), first, n, C.c_void_p(out.ctypes.data), cap,
+                                        C.c_void_p(off.ctypes.data), C.byref(nb)))
+        return out[:nb.value], off[:n]
+
+    def dump(self, n_events, directory):
+        check(lib().ysb_gen_dump(C.byref(self.c), n_events, str(directory).encode()))
+
+
+def ad_shard(ad_id: str, nranks: int) -> int:
+    b = ad_id.encode()
+    return int(lib().ysb_ad_shard(b, len(b), nranks))
+
+
+def shard_ads(ad_ids, nranks):
+    """Ad indices per rank under the ad_id-hash partitioning (include/ysb_hip.h ysb_ad_shard)."""
+    out = [[] for _ in range(nranks)]
+    for i, a in enumerate(ad_ids):
+        out[ad_shard(a, nranks)].append(i)
+    return out

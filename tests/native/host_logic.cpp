@@ -1,0 +1,47 @@
+// Host-side checks of the arithmetic shared with the device (ysb_common.h):
+// exact Java long division by a runtime divisor, and the ad-table hash.
+// Built and run by tests/test_capi.py with g++ (no GPU).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include "ysb_common.h"
+
+using namespace ysb;
+
+static int fails = 0;
+#define CHECK(c) do { if (!(c)) { std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); ++fails; } } while (0)
+
+int main() {
+    const i64 divisors[] = {1, 2, 3, 7, 10, 1000, 9999, 10000, 10001, 60000, 86400000, 1LL << 40,
+                            (1LL << 62) + 12345, INT64_MAX};
+    std::mt19937_64 rng(1234);
+    for (i64 d : divisors) {
+        DivMagic m = div_magic(d);
+        const i64 edge[] = {0, 1, -1, d - 1, d, d + 1, -d + 1, -d, -d - 1, INT64_MAX, INT64_MIN, INT64_MIN + 1,
+                            1700000000000LL, -1700000000000LL, 1700000009999LL};
+        for (i64 t : edge) CHECK(div_trunc(t, m) == t / d);
+        for (int k = 0; k < 200000; ++k) {
+            i64 t = (i64)rng();
+            if (k & 1) t >>= (k % 60);
+            CHECK(div_trunc(t, m) == t / d);
+        }
+    }
+    // key hash: zero padding beyond len must not matter
+    u32 a[KEY_WORDS] = {0}, b[KEY_WORDS];
+    std::memcpy(a, "0f8c1e7a-1111-4222-8333-944455556666", 36);
+    std::memcpy(b, a, sizeof a);
+    CHECK(key_hash(a, 36) == key_hash(b, 36));
+    CHECK(key_hash(a, 36) != key_hash(a, 35));
+    // generator line length == bytes written
+    GenSpec s{};
+    s.seed = 5; s.n_campaigns = 100; s.ads_per_campaign = 10; s.t0_ms = -123456789; s.events_per_sec = 3;
+    s.n_pick = 1000;
+    char line[400];
+    for (u64 i = 0; i < 5000; ++i) {
+        GenEvent e = gen_event(s, i);
+        CHECK(gen_line_len(e) == gen_line_write(s, i, e, line));
+    }
+    std::printf("%s\n", fails ? "FAILED" : "OK");
+    return fails ? 1 : 0;
+}

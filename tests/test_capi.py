@@ -1,0 +1,125 @@
+"""CPU: the C-ABI library loads, exports every symbol include/ysb_hip.h declares, its
+structs match the ctypes mirror, and the host-side arithmetic shared with the
+device is exact.  No compute calls (no GPU here)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from ysb_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ysb_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*[A-Za-z_][A-Za-z0-9_\s\*]*?\b(ysb_[a-z0-9_]+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for f in ("ysb_open", "ysb_load_ad_map", "ysb_submit", "ysb_submit_device", "ysb_drain", "ysb_stats_get",
+              "ysb_close", "ysb_group_init", "ysb_group_reduce_scatter", "ysb_last_error"):
+        assert f in fns
+    assert len(fns) >= 30
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    missing = [f for f in declared_functions() if not hasattr(L, f)]
+    assert missing == []
+
+
+def test_ctypes_signatures_cover_header():
+    assert sorted(_lib.SIGNATURES) == declared_functions()
+
+
+def test_nm_shows_extern_c_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    syms = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    assert set(declared_functions()) <= syms
+
+
+STRUCT_PROBE = r"""
+#include <stddef.h>
+#include <stdio.h>
+#include "ysb_hip.h"
+#define P(T, F) printf(#T "." #F " %zu\n", offsetof(T, F));
+int main(void) {
+  printf("ysb_config %zu\nysb_stats %zu\nysb_count %zu\nysb_gen_params %zu\n", sizeof(ysb_config),
+         sizeof(ysb_stats), sizeof(ysb_count), sizeof(ysb_gen_params));
+  P(ysb_config, flags) P(ysb_config, overflow_capacity) P(ysb_count, window_ms) P(ysb_count, count)
+  P(ysb_gen_params, ad_subset) P(ysb_gen_params, n_ad_subset) P(ysb_stats, batches)
+  return 0;
+}
+"""
+
+
+def test_struct_layouts_match_ctypes(tmp_path):
+    src = tmp_path / "probe.c"
+    src.write_text(STRUCT_PROBE)
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(ln.split() for ln in subprocess.run([str(exe)], capture_output=True, text=True).stdout.splitlines())
+    assert int(got["ysb_config"]) == C.sizeof(_lib.YsbConfig)
+    assert int(got["ysb_stats"]) == C.sizeof(_lib.YsbStats)
+    assert int(got["ysb_count"]) == C.sizeof(_lib.YsbCount)
+    assert int(got["ysb_gen_params"]) == C.sizeof(_lib.YsbGenParams)
+    assert int(got["ysb_config.flags"]) == _lib.YsbConfig.flags.offset
+    assert int(got["ysb_config.overflow_capacity"]) == _lib.YsbConfig.overflow_capacity.offset
+    assert int(got["ysb_count.window_ms"]) == _lib.YsbCount.window_ms.offset
+    assert int(got["ysb_gen_params.ad_subset"]) == _lib.YsbGenParams.ad_subset.offset
+    assert int(got["ysb_stats.batches"]) == _lib.YsbStats.batches.offset
+
+
+def test_abi_version_and_defaults():
+    L = _lib.lib()
+    assert L.ysb_abi_version() == 1
+    cfg = _lib.YsbConfig()
+    L.ysb_config_default(C.byref(cfg))
+    assert cfg.time_divisor_ms == 10000          # CampaignProcessorCommon.java:28
+    assert cfg.n_campaigns == 100                # core.clj:15
+    assert cfg.window_ring >= 16 and cfg.window_ring & (cfg.window_ring - 1) == 0
+    assert cfg.ring_base_bucket == _lib.INT64_MIN
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is present")
+def test_open_without_gpu_fails_loudly():
+    from ysb_amd import YsbContext, YsbError
+    with pytest.raises(YsbError):
+        YsbContext()
+
+
+def test_bad_config_rejected_before_device_use():
+    L = _lib.lib()
+    cfg = _lib.YsbConfig()
+    L.ysb_config_default(C.byref(cfg))
+    cfg.window_ring = 1000   # not a power of two
+    h = C.c_void_p()
+    assert L.ysb_open(C.byref(h), 0, C.byref(cfg)) == -1
+    assert b"window_ring" in L.ysb_last_error(None)
+
+
+def test_host_logic_native(tmp_path):
+    exe = tmp_path / "host_logic"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "streaming-benchmarks_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "native", "host_logic.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout
+
+
+def test_ad_shard_is_stable_and_balanced():
+    from ysb_amd import GenParams, ad_shard
+    _, aids = GenParams().ids()
+    for n in (1, 2, 4, 8):
+        counts = [0] * n
+        for a in aids:
+            s = ad_shard(a, n)
+            assert 0 <= s < n and s == ad_shard(a, n)
+            counts[s] += 1
+        assert min(counts) > 1000 / n * 0.7

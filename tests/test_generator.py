@@ -1,0 +1,129 @@
+"""CPU: the seeded generator (host side of the C library) reproduces the data/
+generator's format (core.clj:90-97) and the committed fixture byte for byte."""
+import json
+import os
+import re
+
+import pytest
+
+import golden_data as gd
+from ysb_amd import AD_TYPES, EVENT_TYPES, AdCampaignMap, GenParams, shard_ads
+
+UUID4 = re.compile(r"^[0-9a-f]{8}-[0-9a-f]{4}-4[0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}$")
+LINE = re.compile(r'^\{"user_id": "([^"]+)", "page_id": "([^"]+)", "ad_id": "([^"]+)", "ad_type": "([^"]+)", '
+                  r'"event_type": "([^"]+)", "event_time": "(-?[0-9]+)", "ip_address": "1\.2\.3\.4"\}\n$')
+
+
+def gen_from_fixture():
+    p = gd.gen_params()
+    return GenParams(seed=p["seed"], n_campaigns=p["n_campaigns"], ads_per_campaign=p["ads_per_campaign"],
+                     t0_ms=p["t0_ms"], events_per_sec=p["events_per_sec"], with_skew=p["with_skew"]), p
+
+
+def test_host_generator_matches_fixture_bytes():
+    g, p = gen_from_fixture()
+    data, off = g.events_host(0, p["n_events"])
+    raw, offs = gd.events("gen_s7")
+    assert bytes(data) == raw
+    assert list(off) == offs
+
+
+def test_ids_match_fixture():
+    g, _ = gen_from_fixture()
+    cids, aids = g.ids()
+    assert cids == gd.campaigns()
+    m = gd.ad_map()
+    assert set(aids) == set(m)
+    for i, a in enumerate(aids):   # (partition 10 ads): ad i -> campaign i // 10 (core.clj:52)
+        assert m[a] == cids[i // 10]
+        assert UUID4.match(a)
+
+
+def test_line_format_and_distribution():
+    g = GenParams(seed=3, events_per_sec=100)
+    data, off = g.events_host(0, 6000)
+    raw = bytes(data)
+    cids, aids = g.ids()
+    aset = set(aids)
+    types, ets, times = {}, {}, []
+    for i in range(len(off)):
+        ln = raw[off[i]:(off[i + 1] if i + 1 < len(off) else len(raw))].decode()
+        m = LINE.match(ln)
+        assert m, ln
+        assert UUID4.match(m.group(1)) and UUID4.match(m.group(2)) and m.group(3) in aset
+        types[m.group(4)] = types.get(m.group(4), 0) + 1
+        ets[m.group(5)] = ets.get(m.group(5), 0) + 1
+        times.append(int(m.group(6)))
+        json.loads(ln)
+    assert set(types) == set(AD_TYPES) and set(ets) == set(EVENT_TYPES)
+    assert all(abs(v - 2000) < 200 for v in ets.values())
+    # catch-up mode: 10 ms per event (core.clj:95)
+    assert times == [1_700_000_000_000 + 10 * i for i in range(6000)]
+    assert abs(len(raw) / len(off) - 254.07) < 1.0   # mean line 254.07 B
+
+
+def test_skew_semantics():
+    g = GenParams(seed=5, events_per_sec=1000, with_skew=True)
+    data, off = g.events_host(0, 200000)
+    raw = bytes(data)
+    late = 0
+    for i in range(0, len(off)):
+        s = off[i]
+        j = raw.index(b'"event_time": "', s) + 15
+        t = int(raw[j:raw.index(b'"', j)])
+        d = t - (1_700_000_000_000 + i)
+        assert -60000 - 49 <= d <= 50   # +-50 ms skew, late by < 60 s (core.clj:166-174)
+        late += d < -49
+    assert 0 <= late <= 10
+
+
+def test_first_offset_and_subsets():
+    g = GenParams(seed=9)
+    d1, o1 = g.events_host(0, 100)
+    d2, o2 = g.events_host(50, 50)
+    assert bytes(d1[o1[50]:]) == bytes(d2)
+    cids, aids = g.ids()
+    parts = shard_ads(aids, 4)
+    assert sorted(sum(parts, [])) == list(range(1000))
+    assert all(len(p) > 150 for p in parts)
+    gs = GenParams(seed=9, ad_subset=parts[2])
+    d, o = gs.events_host(0, 500)
+    raw = bytes(d)
+    allowed = {aids[i] for i in parts[2]}
+    for i in range(len(o)):
+        j = raw.index(b'"ad_id": "', o[i]) + 10
+        assert raw[j:j + 36].decode() in allowed
+
+
+def test_dump_mode(tmp_path):
+    g = GenParams(seed=21, n_campaigns=5, ads_per_campaign=10)
+    g.dump(1000, tmp_path)
+    names = sorted(os.listdir(tmp_path))
+    assert names == ["ad-ids.txt", "ad-to-campaign-ids.txt", "ad-to-campaign.csv", "campaign-ids.txt",
+                     "kafka-json.txt"]
+    cids, aids = g.ids()
+    assert (tmp_path / "campaign-ids.txt").read_text().split() == cids
+    assert (tmp_path / "ad-ids.txt").read_text().split() == aids
+    jm = AdCampaignMap.from_json_lines((tmp_path / "ad-to-campaign-ids.txt").read_bytes(), cids)
+    cm = AdCampaignMap.from_csv((tmp_path / "ad-to-campaign.csv").read_bytes(), cids)
+    assert jm.ad_to_campaign == cm.ad_to_campaign
+    assert jm.arrays() == (aids, [i // 10 for i in range(50)])
+    data, off = g.events_host(0, 1000)
+    assert (tmp_path / "kafka-json.txt").read_bytes() == bytes(data)
+
+
+def test_json_map_line_format(tmp_path):
+    g = GenParams(seed=1, n_campaigns=2, ads_per_campaign=10)
+    g.dump(0, tmp_path)
+    first = (tmp_path / "ad-to-campaign-ids.txt").read_text().splitlines()[0]
+    assert re.match(r'^\{ "[0-9a-f-]{36}": "[0-9a-f-]{36}"\}$', first)   # core.clj:58
+
+
+@pytest.mark.parametrize("rate", [1, 100, 100_000, 7_000_001])
+def test_event_time_rate(rate):
+    g = GenParams(seed=2, events_per_sec=rate)
+    data, off = g.events_host(123456, 3)
+    raw = bytes(data)
+    for k in range(3):
+        j = raw.index(b'"event_time": "', off[k]) + 15
+        assert int(raw[j:raw.index(b'"', j)]) == 1_700_000_000_000 + ((123456 + k) * 1000) // rate

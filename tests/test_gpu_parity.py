@@ -1,0 +1,185 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures and the
+CPU oracle, bit-exact on every (campaign, window) count and every counter."""
+import numpy as np
+import pytest
+
+import golden_data as gd
+from oracle import oracle
+from ysb_amd import GenParams, YsbContext, YsbError
+
+pytestmark = pytest.mark.gpu
+
+
+def make_ctx(n_campaigns=10, ads=None, **kw):
+    ctx = YsbContext(n_campaigns=n_campaigns, **kw)
+    a, c = ads if ads is not None else gd.ad_arrays()
+    ctx.load_ad_map(a, c)
+    return ctx
+
+
+def check_against(ctx, exp_rows, exp_st):
+    got = ctx.drain_buckets()
+    st = ctx.stats()
+    for k, v in exp_st.items():
+        assert st[k] == v, (k, st[k], v)
+    assert st["overflow_dropped"] == 0
+    assert got == exp_rows
+
+
+@pytest.mark.parametrize("stem,require_ip", gd.FIXTURES)
+@pytest.mark.parametrize("lds", [True, False])
+def test_fixture_host_submit(stem, require_ip, lds):
+    with make_ctx(require_ip=require_ip, lds_count=lds) as ctx:
+        raw, offs = gd.events(stem)
+        ctx.submit(raw, offs, slot=0)
+        check_against(ctx, *gd.expected(stem, require_ip))
+
+
+@pytest.mark.parametrize("stem,require_ip", gd.FIXTURES)
+def test_fixture_device_submit(stem, require_ip):
+    with make_ctx(require_ip=require_ip) as ctx:
+        raw, offs = gd.events(stem)
+        d_b = ctx.device_alloc(len(raw) + 64)
+        d_o = ctx.device_alloc(4 * len(offs) + 64)
+        ctx.h2d(d_b, np.frombuffer(raw, dtype=np.uint8))
+        ctx.h2d(d_o, np.asarray(offs, dtype=np.uint32))
+        ctx.submit_device(d_b, len(raw), d_o, len(offs))
+        check_against(ctx, *gd.expected(stem, require_ip))
+        ctx.device_free(d_b)
+        ctx.device_free(d_o)
+
+
+def split_batches(raw, offs, sizes):
+    offs = list(offs) + [len(raw)]
+    i = 0
+    for s in sizes:
+        j = min(i + s, len(offs) - 1)
+        base = offs[i]
+        yield raw[base:offs[j]], [o - base for o in offs[i:j]]
+        i = j
+    if i < len(offs) - 1:
+        base = offs[i]
+        yield raw[base:], [o - base for o in offs[i:-1]]
+
+
+def test_batches_and_slots_sum_exactly():
+    raw, offs = gd.events("gen_s7")
+    with make_ctx() as ctx:
+        for k, (b, o) in enumerate(split_batches(raw, offs, [1, 0, 7, 255, 256, 257, 300, 3])):
+            ctx.submit(b, o, slot=k & 1)
+        check_against(ctx, *gd.expected("gen_s7"))
+        assert ctx.stats()["batches"] >= 9
+
+
+def test_slot_buffers_zero_copy():
+    raw, offs = gd.events("gen_s7")
+    with make_ctx() as ctx:
+        import ctypes as C
+        for k, (b, o) in enumerate(split_batches(raw, offs, [600, 600])):
+            slot = k & 1
+            ctx.wait(slot)
+            pb, po = ctx.slot_buffers(slot)
+            C.memmove(pb, b, len(b))
+            oa = np.asarray(o, dtype=np.uint32)
+            C.memmove(po, oa.ctypes.data, oa.nbytes)
+            from ysb_amd._lib import lib
+            lib().ysb_submit(ctx._h, slot, C.c_void_p(pb), len(b), C.c_void_p(po), len(o))
+        check_against(ctx, *gd.expected("gen_s7"))
+
+
+def test_device_generator_matches_fixture_bytes():
+    p = gd.gen_params()
+    g = GenParams(seed=p["seed"], n_campaigns=p["n_campaigns"], ads_per_campaign=p["ads_per_campaign"],
+                  t0_ms=p["t0_ms"], events_per_sec=p["events_per_sec"], with_skew=p["with_skew"])
+    raw, offs = gd.events("gen_s7")
+    with make_ctx() as ctx:
+        n = p["n_events"]
+        cap = n * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n)
+        nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+        assert nb == len(raw)
+        got = ctx.d2h(np.empty(nb, dtype=np.uint8), d_b)
+        got_off = ctx.d2h(np.empty(n, dtype=np.uint32), d_o)
+        assert got.tobytes() == raw
+        assert list(got_off) == offs
+
+
+@pytest.mark.parametrize("rate,skew,ring", [(100, True, 4096), (100_000, False, 1024), (7, True, 16)])
+def test_generated_stream_vs_oracle(rate, skew, ring):
+    """2M events straight from the device generator vs the C oracle on the same bytes;
+    ring 16 forces most windows through the exact side list."""
+    g = GenParams(seed=1234, events_per_sec=rate, with_skew=skew)
+    cids, aids = g.ids()
+    camp = g.ad_campaign_index()
+    n = 2_000_000
+    with make_ctx(n_campaigns=100, ads=(aids[:950], camp[:950]), window_ring=ring,
+                  overflow_capacity=1 << 22, max_batch_bytes=1 << 30) as ctx:
+        cap = n * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n)
+        nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+        ctx.submit_device(d_b, nb, d_o, n)
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+        data = ctx.d2h(np.empty(nb, dtype=np.uint8), d_b)
+        off = ctx.d2h(np.empty(n, dtype=np.uint32), d_o)
+    rows, ost = oracle.run(oracle.AdMap(aids[:950], camp[:950]), data, off, threads=8)
+    for k, v in ost.items():
+        assert st[k] == v, (k, st[k], v)
+    assert st["join_misses"] > 0 and st["overflow_dropped"] == 0
+    assert got == rows
+
+
+def test_truth_counts_at_scale():
+    """20M generated events (5 GB): parsed counts == generator truth (no parsing)."""
+    g = GenParams(seed=77, events_per_sec=100_000)
+    n, seg = 20_000_000, 10_000_000
+    with make_ctx(n_campaigns=100, ads=(g.ids()[1], g.ad_campaign_index())) as ctx:
+        cap = seg * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * seg)
+        for first in range(0, n, seg):
+            nb = ctx.gen_events_device(g, first, seg, d_b, cap, d_o)
+            ctx.submit_device(d_b, nb, d_o, seg)
+            ctx.sync()
+            ctx.truth_accumulate(g, first, seg)
+        mism, truth, ring = ctx.truth_compare()
+        st = ctx.stats()
+    assert st["events"] == n and st["parse_errors"] == 0 and st["out_of_ring"] == 0
+    assert mism == 0 and truth == ring == st["joined"]
+
+
+def test_single_rank_group_reduce_scatter():
+    raw, offs = gd.events("gen_s7")
+    with make_ctx() as ctx:
+        ctx.group_init(0, 1, YsbContext.group_unique_id())
+        assert ctx.group_owned() == (0, 10)
+        ctx.submit(raw[:offs[700]], offs[:700])
+        ctx.group_reduce_scatter()
+        ctx.submit(raw[offs[700]:], [o - offs[700] for o in offs[700:]], slot=1)
+        check_against(ctx, *gd.expected("gen_s7"))
+
+
+def test_drain_clear_and_ranges():
+    raw, offs = gd.events("gen_s7")
+    exp, _ = gd.expected("gen_s7")
+    with make_ctx() as ctx:
+        ctx.submit(raw, offs)
+        lo, w = ctx.ring_range()
+        buckets = sorted({b for _, b in exp})
+        mid = buckets[len(buckets) // 2]
+        first = ctx.drain(bucket_hi=mid, clear=True)
+        assert {(c, t // 10000): v for (c, t), v in first.items()} == {k: v for k, v in exp.items() if k[1] < mid}
+        rest = ctx.drain_buckets()
+        assert rest == {k: v for k, v in exp.items() if k[1] >= mid}
+
+
+def test_misaligned_device_pointer_rejected():
+    with make_ctx() as ctx:
+        d = ctx.device_alloc(1024)
+        with pytest.raises(YsbError):
+            ctx.submit_device(d + 3, 100, d, 1)
+
+
+def test_submit_before_ad_map_is_an_error():
+    with YsbContext(n_campaigns=10) as ctx:
+        with pytest.raises(YsbError):
+            ctx.submit(b"{}\n", [0])
