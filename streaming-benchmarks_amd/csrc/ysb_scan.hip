@@ -35,6 +35,7 @@ enum : u32 {
 __host__ __device__ constexpr u32 w4(char a, char b, char c, char d) {
     return (u32)(u8)a | ((u32)(u8)b << 8) | ((u32)(u8)c << 16) | ((u32)(u8)d << 24);
 }
+constexpr u32 VIEW_W = w4('v', 'i', 'e', 'w');
 
 // ---------------------------------------------------------------------------
 // Byte sources.  Positions are ints relative to the source base.
@@ -317,11 +318,10 @@ __device__ __forceinline__ bool parse_line(const S& src, int s, int e, u32 requi
     return p == e && (seen & require) == require;
 }
 
-constexpr u32 VIEW = w4('v', 'i', 'e', 'w');
 
 template <class S>
 __device__ __forceinline__ bool span_is_view(const S& src, const Span& et) {
-    if (!et.esc) return et.e - et.s == 4 && src.load4(et.s) == VIEW;
+    if (!et.esc) return et.e - et.s == 4 && src.load4(et.s) == VIEW_W;
     u8 buf[12];
     const int n = decode_str(src, et.s, et.e, buf, 8);
     return n == 4 && buf[0] == 'v' && buf[1] == 'i' && buf[2] == 'e' && buf[3] == 'w';
@@ -424,9 +424,136 @@ __device__ __forceinline__ bool span_long(const S& src, const Span& tm, i64& out
     return parse_digits(BufSrc{buf}, 0, n, out);
 }
 
+// N realigned words of the source starting at byte p (N+1 aligned LDS reads, issued
+// back to back, then one v_alignbyte each).
+template <int N>
+__device__ __forceinline__ void load_span(const LdsSrc& src, int p, u32 (&w)[N]) {
+    u32 a[N + 1];
+    const int base = p >> 2;
+#pragma unroll
+    for (int k = 0; k <= N; ++k) a[k] = src.d[base + k];
+    const u32 sh = (u32)(p & 3);
+#pragma unroll
+    for (int k = 0; k < N; ++k) w[k] = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sh);
+}
+
+// Long.parseLong over <= 20 bytes held in registers.
+__device__ __forceinline__ bool parse_digits_regs(const u32 (&w)[5], int len, i64& out) {
+    if (len <= 0 || len > 20) return false;
+    const u32 c0 = w[0] & 0xFFu;
+    const bool neg = c0 == '-';
+    const int k0 = (c0 == '-' || c0 == '+') ? 1 : 0;
+    if (k0 >= len) return false;
+    u64 acc = 0;
+    bool ok = true;
+    const u32 last_max = neg ? 8u : 7u;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+        if (k >= k0 && k < len) {
+            const u32 d = ((w[k >> 2] >> ((k & 3) * 8)) & 0xFFu) - '0';
+            ok &= d <= 9u;
+            if (acc >= 922337203685477580ULL) ok &= !(acc > 922337203685477580ULL || d > last_max);
+            acc = acc * 10u + d;
+        }
+    }
+    out = neg ? (i64)(0 - acc) : (i64)acc;
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
+// Fast path: the generator's layout (core.clj:90-96) -- the seven keys in order,
+// ": " and ", " separators, string values without quotes or backslashes, the
+// three UUID values 36 bytes long.  Verified against the quote-candidate bitmap
+// (every quote at its template position, none inside a value) and byte compares of
+// every structural segment, which makes it exactly the JSON parse of such a line;
+// any other line returns false and takes the general tokenizer.  Costs ~3
+// dependent LDS round trips per line instead of one per token.
+// ---------------------------------------------------------------------------
+struct Canon {
+    u32 kw[9];     // ad_id bytes 113..148
+    bool view;
+    int tm_s, tm_e;
+};
+
+__device__ __forceinline__ bool parse_canonical(const LdsSrc& src, int s, int e, Canon& c) {
+    const int L = e - s;
+    if (L < 220 || L > 300) return false;
+    // line-relative quote-candidate bitmap, bytes 0..319
+    u32 W[11];
+    const int wb = s >> 5;
+#pragma unroll
+    for (int k = 0; k < 11; ++k) W[k] = src.q[wb + k];
+    // fixed structural bytes (line-relative): [0,13) [49,64) [100,113) [149,164) and the ad_id value
+    u32 s0[4], s1[4], s2[4], s3[4];
+    load_span(src, s + 0, s0);
+    load_span(src, s + 49, s1);
+    load_span(src, s + 100, s2);
+    load_span(src, s + 149, s3);
+    load_span(src, s + 113, c.kw);
+    const u32 sh = (u32)(s & 31);
+    u32 R[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) R[k] = __builtin_amdgcn_alignbit(W[k + 1], W[k], sh);
+    // quotes at 1, 9, 12, 49, 52, 60, 63, 100, 103, 109, 112, 149, 152, 160, 163 and nowhere else below 164
+    bool ok = R[0] == 0x00001202u && R[1] == 0x90120000u && R[2] == 0u && R[3] == 0x00012090u &&
+              R[4] == 0x01200000u && (R[5] & 0xFu) == 0x9u;
+    ok &= s0[0] == w4('{', '"', 'u', 's') && s0[1] == w4('e', 'r', '_', 'i') && s0[2] == w4('d', '"', ':', ' ') &&
+          (s0[3] & 0xFFu) == '"';
+    ok &= s1[0] == w4('"', ',', ' ', '"') && s1[1] == w4('p', 'a', 'g', 'e') && s1[2] == w4('_', 'i', 'd', '"') &&
+          (s1[3] & 0xFFFFFFu) == w4(':', ' ', '"', 0);
+    ok &= s2[0] == w4('"', ',', ' ', '"') && s2[1] == w4('a', 'd', '_', 'i') && s2[2] == w4('d', '"', ':', ' ') &&
+          (s2[3] & 0xFFu) == '"';
+    ok &= s3[0] == w4('"', ',', ' ', '"') && s3[1] == w4('a', 'd', '_', 't') && s3[2] == w4('y', 'p', 'e', '"') &&
+          (s3[3] & 0xFFFFFFu) == w4(':', ' ', '"', 0);
+    if (!ok) return false;
+    // variable tail: first quote candidate at or after p, from the registers
+    auto nextq = [&](int p) -> int {
+        int r = 1 << 20;
+#pragma unroll
+        for (int k = 9; k >= 5; --k) {
+            u32 m = R[k];
+            const int base = 32 * k;
+            if (p > base + 31) m = 0u;
+            else if (p > base) m &= ~0u << (p - base);
+            if (m) r = base + (int)__builtin_ctz(m);
+        }
+        return r;
+    };
+    const int e3 = nextq(164);          // end of ad_type
+    const int e4 = nextq(e3 + 18);      // end of event_type
+    const int e5 = nextq(e4 + 18);      // end of event_time
+    const int e6 = nextq(e5 + 18);      // end of ip_address
+    if (e6 + 2 > L) return false;
+    u32 t4[5], t5[5], t6[5], t7[1], ev[1];
+    load_span(src, s + e3, t4);
+    load_span(src, s + e4, t5);
+    load_span(src, s + e5, t6);
+    load_span(src, s + e6, t7);
+    load_span(src, s + e3 + 18, ev);
+    ok = t4[0] == w4('"', ',', ' ', '"') && t4[1] == w4('e', 'v', 'e', 'n') && t4[2] == w4('t', '_', 't', 'y') &&
+         t4[3] == w4('p', 'e', '"', ':') && (t4[4] & 0xFFFFu) == w4(' ', '"', 0, 0);
+    ok &= t5[0] == w4('"', ',', ' ', '"') && t5[1] == w4('e', 'v', 'e', 'n') && t5[2] == w4('t', '_', 't', 'i') &&
+          t5[3] == w4('m', 'e', '"', ':') && (t5[4] & 0xFFFFu) == w4(' ', '"', 0, 0);
+    ok &= t6[0] == w4('"', ',', ' ', '"') && t6[1] == w4('i', 'p', '_', 'a') && t6[2] == w4('d', 'd', 'r', 'e') &&
+          t6[3] == w4('s', 's', '"', ':') && (t6[4] & 0xFFFFu) == w4(' ', '"', 0, 0);
+    ok &= (t7[0] & 0xFFFFu) == w4('"', '}', 0, 0);
+    if (!ok) return false;
+    // trailing bytes after '}' must be JSON whitespace
+    for (int p = e6 + 2; p < L; ++p)
+        if (!is_ws(src.b(s + p))) return false;
+    c.view = (e4 - (e3 + 18) == 4) && ev[0] == VIEW_W;
+    c.tm_s = s + e4 + 18;
+    c.tm_e = s + e5;
+    return true;
+}
+
 // One line end to end: returns 0 not counted, 1 counted (campaign/bucket set).
 // Per-thread tallies go to st[].
 struct Tally { u32 ev, view, join, miss, perr, terr, oor; };
+
+// LDS lines: canonical fast path first, then the general tokenizer.
+__device__ __forceinline__ bool process_line_lds(const LdsSrc& src, int s, int e, bool slow, const ScanParams& P,
+                                                 Tally& t, u32& campaign, i64& bucket);
 
 template <bool FAST, class S>
 __device__ __forceinline__ bool process_line(const S& src, int s, int e, const ScanParams& P,
@@ -447,6 +574,38 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
     campaign = (u32)c;
     bucket = div_trunc(tv, P.div);
     return true;
+}
+
+__device__ __forceinline__ bool process_line_lds(const LdsSrc& src, int s, int e, bool slow, const ScanParams& P,
+                                                 Tally& t, u32& campaign, i64& bucket) {
+    Canon c;
+    if (!slow && parse_canonical(src, s, e, c)) {
+        t.ev++;
+        if (!c.view) return false;                                 // EventFilterBolt
+        t.view++;
+        u32 kw[KEY_WORDS];
+#pragma unroll
+        for (int k = 0; k < (int)KEY_WORDS; ++k) kw[k] = k < 9 ? c.kw[k] : 0u;
+        const int ci = probe(P.table, P.table_mask, kw, 36u);      // RedisJoinBolt
+        if (ci < 0) { t.miss++; return false; }
+        t.join++;
+        i64 tv;
+        const int len = c.tm_e - c.tm_s;
+        bool tok;
+        if (len <= 20) {
+            u32 dw[5];
+            load_span(src, c.tm_s, dw);
+            tok = parse_digits_regs(dw, len, tv);
+        } else {
+            tok = parse_digits(src, c.tm_s, c.tm_e, tv);
+        }
+        if (!tok) { t.terr++; return false; }                      // Long.parseLong
+        campaign = (u32)ci;
+        bucket = div_trunc(tv, P.div);
+        return true;
+    }
+    return slow ? process_line<false>(src, s, e, P, t, campaign, bucket)
+                : process_line<true>(src, s, e, P, t, campaign, bucket);
 }
 
 // Adds v views to (campaign, bucket): the ring cell if the bucket is live, else the
@@ -658,8 +817,7 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
                             slow |= m != 0;
                         }
                     }
-                    if (!slow) valid = process_line<true>(lsrc, ls, le, P, tl, campaign, bucket);
-                    else valid = process_line<false>(lsrc, ls, le, P, tl, campaign, bucket);
+                    valid = process_line_lds(lsrc, ls, le, slow, P, tl, campaign, bucket);
                 }
             } else {
                 // tile does not fit LDS: parse straight from HBM (rare; correctness path)
