@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -31,6 +32,9 @@ struct ysb_ctx {
     // ad table
     u32* d_table = nullptr;
     u64 table_slots = 0;
+    u32* d_ctable = nullptr;   // canonical-UUID cuckoo table
+    u64 ctable_slots = 0;
+    u64 cseed = 0;
     bool table_loaded = false;
     // counts
     u32 c_pad = 0;                        // campaigns padded to the group size
@@ -70,6 +74,11 @@ struct ysb_ctx {
     unsigned long long* d_cmp = nullptr;
     u32* d_subset = nullptr;
     u32 d_subset_n = 0;
+    u32* d_defer = nullptr;                // deferred (general-path) line indices
+    u64 defer_cap = 0;
+    u32* d_defer_ctr = nullptr;            // [count, done]
+    unsigned long long* d_dbg = nullptr;   // YSB_STAMPS diagnostic build
+    u64 dbg_words = 0;
 };
 
 static thread_local std::string g_open_err;
@@ -122,6 +131,7 @@ static void destroy(ysb_ctx* c) {
     if (c->s_copy) hipStreamSynchronize(c->s_copy);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_table);
+    hipFree(c->d_ctable);
     hipFree(c->d_counts);
     hipFree(c->d_owned);
     hipFree(c->d_rs_tmp);
@@ -134,6 +144,9 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_truth_out);
     hipFree(c->d_cmp);
     hipFree(c->d_subset);
+    hipFree(c->d_defer);
+    hipFree(c->d_defer_ctr);
+    hipFree(c->d_dbg);
     for (int s = 0; s < 2; ++s) {
         hipHostFree(c->h_bytes[s]);
         hipHostFree(c->h_off[s]);
@@ -282,6 +295,70 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         c->table_slots = slots;
     }
     HIPCHK(c, hipMemcpy(c->d_table, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+    // canonical-UUID keys also go into the two-choice cuckoo table (load <= 1/4)
+    std::vector<std::pair<std::array<u64, 3>, u32>> canon;
+    {
+        std::map<std::array<u64, 3>, size_t> where;
+        for (u64 i = 0; i < n; ++i) {
+            const u32 len = lens ? lens[i] : 36u;
+            u64 k0, k1;
+            u32 k2;
+            if (len != 36 || !uuid_pack_bytes(reinterpret_cast<const u8*>(ad_ids[i]), &k0, &k1, &k2)) continue;
+            const std::array<u64, 3> k{k0, k1, k2};
+            auto it = where.find(k);
+            if (it != where.end()) canon[it->second].second = campaign_idx[i];   // later wins
+            else { where[k] = canon.size(); canon.push_back({k, campaign_idx[i]}); }
+        }
+    }
+    u64 cslots = 64;
+    while (cslots < 4 * canon.size()) cslots <<= 1;
+    std::vector<u32> ct;
+    u64 seed = 0x5EEDC0FFEEULL;
+    for (int attempt = 0;; ++attempt) {
+        if (attempt == 16) { cslots <<= 1; attempt = 0; }
+        if (cslots > (1ull << 31)) return fail(c, YSB_ERR_CAPACITY, "cuckoo table construction failed");
+        seed = mix64(seed + (u64)attempt + cslots);
+        ct.assign(cslots * CSLOT_WORDS, 0);
+        for (u64 s = 0; s < cslots; ++s) ct[s * CSLOT_WORDS + 5] = EMPTY_SLOT;
+        const u32 cm = (u32)(cslots - 1);
+        bool ok = true;
+        for (const auto& kv : canon) {
+            u64 k0 = kv.first[0], k1 = kv.first[1];
+            u32 k2 = (u32)kv.first[2], camp = kv.second;
+            u32 a, b;
+            cuckoo_slots(cuckoo_hash(k0, k1, k2, seed), cm, &a, &b);
+            u32 pos = a;
+            int kicks = 0;
+            while (true) {
+                u32* sl = &ct[(u64)pos * CSLOT_WORDS];
+                if (sl[5] == EMPTY_SLOT) {
+                    sl[0] = (u32)k0; sl[1] = (u32)(k0 >> 32); sl[2] = (u32)k1; sl[3] = (u32)(k1 >> 32);
+                    sl[4] = k2; sl[5] = camp;
+                    break;
+                }
+                // evict the occupant to its other slot
+                const u64 o0 = sl[0] | ((u64)sl[1] << 32), o1 = sl[2] | ((u64)sl[3] << 32);
+                const u32 o2 = sl[4], oc = sl[5];
+                sl[0] = (u32)k0; sl[1] = (u32)(k0 >> 32); sl[2] = (u32)k1; sl[3] = (u32)(k1 >> 32);
+                sl[4] = k2; sl[5] = camp;
+                k0 = o0; k1 = o1; k2 = o2; camp = oc;
+                u32 oa, ob;
+                cuckoo_slots(cuckoo_hash(k0, k1, k2, seed), cm, &oa, &ob);
+                pos = (pos == oa) ? ob : oa;
+                if (++kicks > 500) { ok = false; break; }
+            }
+            if (!ok) break;
+        }
+        if (ok) break;
+    }
+    if (cslots != c->ctable_slots) {
+        hipFree(c->d_ctable);
+        c->d_ctable = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_ctable, ct.size() * 4));
+        c->ctable_slots = cslots;
+    }
+    HIPCHK(c, hipMemcpy(c->d_ctable, ct.data(), ct.size() * 4, hipMemcpyHostToDevice));
+    c->cseed = seed;
     c->table_loaded = true;
     return YSB_OK;
 }
@@ -296,6 +373,9 @@ static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u
     p.n = n;
     p.table = c->d_table;
     p.table_mask = (u32)(c->table_slots - 1);
+    p.ctable = c->d_ctable;
+    p.ctable_mask = (u32)(c->ctable_slots - 1);
+    p.cseed = c->cseed;
     p.n_campaigns = c->cfg.n_campaigns;
     p.counts = c->d_counts;
     p.ring_w = c->cfg.window_ring;
@@ -310,7 +390,8 @@ static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u
     p.stats = c->d_stats;
     p.n_tiles = (n + SCAN_TPB - 1) / SCAN_TPB;
     const u64 resident = (u64)c->cus * 2;   // two 80 KiB workgroups per CU
-    const u64 blocks = std::max<u64>(1, std::min<u64>(p.n_tiles, resident));
+    const u64 blocks = std::max<u64>(std::max<u64>(1, std::min<u64>(p.n_tiles, resident)),
+                                     (p.n_tiles + MAX_TILES_PER_BLOCK - 1) / MAX_TILES_PER_BLOCK);
     p.tiles_per_block = (u32)((p.n_tiles + blocks - 1) / blocks);
     return p;
 }
@@ -326,7 +407,33 @@ static void poll_ring(ysb_ctx* c) {
 static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_off, u64 n) {
     if (!c->table_loaded) return fail(c, YSB_ERR_STATE, "ysb_load_ad_map has not been called");
     if (n == 0) { c->batches++; return YSB_OK; }
-    const ScanParams p = make_params(c, d_bytes, nbytes, d_off, n);
+    if (n >= (1ull << 30)) return fail(c, YSB_ERR_CAPACITY, "at most 2^30-1 events per batch");
+    if (n > c->defer_cap) {   // the deferred-line list can hold every line of a batch
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        hipFree(c->d_defer);
+        c->d_defer = nullptr;
+        const u64 cap = std::max<u64>(n, 1u << 16);
+        HIPCHK(c, hipMalloc(&c->d_defer, cap * 4));
+        c->defer_cap = cap;
+    }
+    if (!c->d_defer_ctr) {
+        HIPCHK(c, hipMalloc(&c->d_defer_ctr, 16));
+        HIPCHK(c, hipMemset(c->d_defer_ctr, 0, 16));
+    }
+    ScanParams p = make_params(c, d_bytes, nbytes, d_off, n);
+    p.defer = c->d_defer;
+    p.defer_count = c->d_defer_ctr;
+    p.defer_done = c->d_defer_ctr + 1;
+    p.defer_cap = (u32)c->defer_cap;
+#ifdef YSB_STAMPS
+    const u64 words = (u64)c->cus * 2 * (SCAN_TPB / 64) * N_STAMPS;
+    if (!c->d_dbg) {
+        HIPCHK(c, hipMalloc(&c->d_dbg, words * 8));
+        HIPCHK(c, hipMemset(c->d_dbg, 0, words * 8));
+        c->dbg_words = words;
+    }
+    p.dbg = c->d_dbg;
+#endif
     poll_ring(c);
     if (!c->ring_known) {
         launch_ring_autobase(p, c->s_comp);
@@ -351,6 +458,8 @@ static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_
     launch_scan(p, c->s_comp);
     HIPCHK(c, hipGetLastError());
     if (e1) HIPCHK(c, hipEventRecord(e1, c->s_comp));
+    launch_defer(p, c->cus, c->s_comp);
+    HIPCHK(c, hipGetLastError());
     c->batches++;
     return YSB_OK;
 }
@@ -864,5 +973,19 @@ int ysb_gen_dump(const ysb_gen_params* p, uint64_t n_events, const char* dir) {
     std::fclose(f);
     return YSB_OK;
 }
+
+#ifdef YSB_STAMPS
+// Diagnostic build only: per-wave phase cycles of the scan kernel since the last call.
+int ysb_debug_stamps(ysb_ctx* c, uint64_t* out, uint64_t cap, uint64_t* n) {
+    if (!c || !n) return YSB_ERR_ARG;
+    int rc = ysb_sync(c);
+    if (rc) return rc;
+    *n = c->dbg_words;
+    if (!out || !c->d_dbg) return YSB_OK;
+    HIPCHK(c, hipMemcpy(out, c->d_dbg, std::min<u64>(cap, c->dbg_words) * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemset(c->d_dbg, 0, c->dbg_words * 8));
+    return YSB_OK;
+}
+#endif
 
 }  // extern "C"

@@ -188,6 +188,53 @@ YSB_HD u32 key_hash(const u32* w, u32 len) {
 }
 
 // ---------------------------------------------------------------------------
+// Canonical-UUID cuckoo table (the join's fast path).  A 36-byte lower-case
+// 8-4-4-4-12 UUID string (what java.util.UUID.toString() and the generator emit)
+// packs losslessly into 144 bits: its 36 characters as nibbles (dashes -> 0), 16 bits
+// per 4-character group, k0 = groups 0-3, k1 = groups 4-7, k2 = group 8.  Map keys
+// in that form go into a two-choice cuckoo table, so a lookup is exactly two slot
+// loads issued together.  Slot words: [k0 lo, k0 hi, k1 lo, k1 hi, k2, campaign, 0, 0].
+// ---------------------------------------------------------------------------
+enum : u32 { CSLOT_WORDS = 8 };
+
+YSB_HD bool uuid_pack_bytes(const u8* s, u64* k0, u64* k1, u32* k2) {
+    u32 g[9];
+    for (int i = 0; i < 9; ++i) {
+        u32 v = 0;
+        for (int j = 0; j < 4; ++j) {
+            const int pos = 4 * i + j;
+            const u32 c = s[pos];
+            u32 nib;
+            if (pos == 8 || pos == 13 || pos == 18 || pos == 23) {
+                if (c != '-') return false;
+                nib = 0;
+            } else if (c >= '0' && c <= '9') {
+                nib = c - '0';
+            } else if (c >= 'a' && c <= 'f') {
+                nib = c - 'a' + 10;
+            } else {
+                return false;
+            }
+            v = (v << 4) | nib;
+        }
+        g[i] = v;
+    }
+    *k0 = ((u64)g[0] << 48) | ((u64)g[1] << 32) | ((u64)g[2] << 16) | g[3];
+    *k1 = ((u64)g[4] << 48) | ((u64)g[5] << 32) | ((u64)g[6] << 16) | g[7];
+    *k2 = g[8];
+    return true;
+}
+
+YSB_HD u64 cuckoo_hash(u64 k0, u64 k1, u32 k2, u64 seed) {
+    return mix64(k0 ^ ((k1 << 21) | (k1 >> 43)) ^ ((u64)k2 << 40) ^ seed);
+}
+YSB_HD void cuckoo_slots(u64 h, u32 mask, u32* a, u32* b) {
+    *a = (u32)h & mask;
+    u32 x = (u32)(h >> 32) & mask;
+    *b = x == *a ? ((x + 1) & mask) : x;
+}
+
+// ---------------------------------------------------------------------------
 // Exact Java long division t / d (truncating toward zero) for a runtime d >= 1,
 // as a multiply-high: for n < 2^63, floor(n/d) = mulhi(n, M) >> s with
 // l = ceil(log2 d), M = ceil(2^(63+l) / d) < 2^64, s = l - 1 (Granlund-Montgomery).

@@ -12,14 +12,18 @@ constexpr int TILE_CAP = 66560;               // LDS bytes of one tile (260 B/li
 constexpr int TILE_CHUNKS = TILE_CAP / 16;    // 16-byte chunks per tile
 constexpr int CHUNKS_PER_THREAD = (TILE_CHUNKS + SCAN_TPB - 1) / SCAN_TPB;  // 17
 constexpr int LCNT_CAP = 1024;                // u32 per-workgroup (campaign, window) counters
+constexpr int MAX_TILES_PER_BLOCK = 128;      // tile bounds preloaded into LDS
 
 struct ScanParams {
     const u8* bytes;            // batch bytes (16-byte aligned)
     u64 nbytes;
     const u32* off;             // n line offsets
     u64 n;
-    const u32* table;           // ad table, SLOT_WORDS u32 per slot
+    const u32* table;           // ad table, SLOT_WORDS u32 per slot (every key)
     u32 table_mask;             // slots - 1
+    const u32* ctable;          // canonical-UUID cuckoo table, CSLOT_WORDS u32 per slot
+    u32 ctable_mask;
+    u64 cseed;
     u32 n_campaigns;
     unsigned long long* counts; // [c_pad][W] u64, campaign-major
     u32 ring_w;                 // W (power of two)
@@ -34,9 +38,18 @@ struct ScanParams {
     u32 tiles_per_block;
     u64 n_tiles;
     unsigned long long* stats;  // ST_COUNT_ u64
+    unsigned long long* dbg;    // diagnostic build only (YSB_STAMPS): per-wave phase cycles
+    u32* defer;                 // line indices for the general path (defer_kernel)
+    u32* defer_count;           // [0] entries, reset by defer_kernel
+    u32* defer_done;            // workgroup ticket of defer_kernel
+    u32 defer_cap;
 };
 
+constexpr int N_STAMPS = 8;     // phases timed by the YSB_STAMPS diagnostic build
+
 void launch_scan(const ScanParams& p, hipStream_t s);
+// The general-path lines the scan deferred (same stream, right after launch_scan).
+void launch_defer(const ScanParams& p, int blocks, hipStream_t s);
 // Sets ring[0..1] from the first lines of a batch if ring[1] == 0.
 void launch_ring_autobase(const ScanParams& p, hipStream_t s);
 

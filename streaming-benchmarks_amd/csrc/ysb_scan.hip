@@ -475,9 +475,12 @@ struct Canon {
     int tm_s, tm_e;
 };
 
-__device__ __forceinline__ bool parse_canonical(const LdsSrc& src, int s, int e, Canon& c) {
+__device__ __forceinline__ bool parse_canonical(const LdsSrc& src, const u32* bsb, int s, int e, Canon& c) {
     const int L = e - s;
     if (L < 220 || L > 300) return false;
+    // per-16-byte backslash flags of the line's chunks (a line <= 300 B spans <= 2 words)
+    const int c0 = s >> 4, c1 = (e - 1) >> 4;
+    const u32 b0 = bsb[c0 >> 5], b1 = bsb[c1 >> 5];
     // line-relative quote-candidate bitmap, bytes 0..319
     u32 W[11];
     const int wb = s >> 5;
@@ -497,6 +500,11 @@ __device__ __forceinline__ bool parse_canonical(const LdsSrc& src, int s, int e,
     // quotes at 1, 9, 12, 49, 52, 60, 63, 100, 103, 109, 112, 149, 152, 160, 163 and nowhere else below 164
     bool ok = R[0] == 0x00001202u && R[1] == 0x90120000u && R[2] == 0u && R[3] == 0x00012090u &&
               R[4] == 0x01200000u && (R[5] & 0xFu) == 0x9u;
+    {   // no backslash anywhere in the line (escapes take the general path)
+        const u32 lo = ~0u << (c0 & 31);
+        const u32 hi = (c1 & 31) == 31 ? ~0u : ((2u << (c1 & 31)) - 1u);
+        ok &= ((c0 >> 5) == (c1 >> 5)) ? (b0 & lo & hi) == 0u : ((b0 & lo) | (b1 & hi)) == 0u;
+    }
     ok &= s0[0] == w4('{', '"', 'u', 's') && s0[1] == w4('e', 'r', '_', 'i') && s0[2] == w4('d', '"', ':', ' ') &&
           (s0[3] & 0xFFu) == '"';
     ok &= s1[0] == w4('"', ',', ' ', '"') && s1[1] == w4('p', 'a', 'g', 'e') && s1[2] == w4('_', 'i', 'd', '"') &&
@@ -537,9 +545,11 @@ __device__ __forceinline__ bool parse_canonical(const LdsSrc& src, int s, int e,
     ok &= t6[0] == w4('"', ',', ' ', '"') && t6[1] == w4('i', 'p', '_', 'a') && t6[2] == w4('d', 'd', 'r', 'e') &&
           t6[3] == w4('s', 's', '"', ':') && (t6[4] & 0xFFFFu) == w4(' ', '"', 0, 0);
     ok &= (t7[0] & 0xFFFFu) == w4('"', '}', 0, 0);
+    // trailing bytes after '}' must be JSON whitespace (normally just the '\n')
+    if (L > e6 + 2) ok &= is_ws((t7[0] >> 16) & 0xFFu);
+    if (L > e6 + 3) ok &= is_ws(t7[0] >> 24);
     if (!ok) return false;
-    // trailing bytes after '}' must be JSON whitespace
-    for (int p = e6 + 2; p < L; ++p)
+    for (int p = e6 + 4; p < L; ++p)
         if (!is_ws(src.b(s + p))) return false;
     c.view = (e4 - (e3 + 18) == 4) && ev[0] == VIEW_W;
     c.tm_s = s + e4 + 18;
@@ -551,10 +561,7 @@ __device__ __forceinline__ bool parse_canonical(const LdsSrc& src, int s, int e,
 // Per-thread tallies go to st[].
 struct Tally { u32 ev, view, join, miss, perr, terr, oor; };
 
-// LDS lines: canonical fast path first, then the general tokenizer.
-__device__ __forceinline__ bool process_line_lds(const LdsSrc& src, int s, int e, bool slow, const ScanParams& P,
-                                                 Tally& t, u32& campaign, i64& bucket);
-
+// The general path (lines that are not in the generator's layout).
 template <bool FAST, class S>
 __device__ __forceinline__ bool process_line(const S& src, int s, int e, const ScanParams& P,
                                              Tally& t, u32& campaign, i64& bucket) {
@@ -576,36 +583,44 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
     return true;
 }
 
-__device__ __forceinline__ bool process_line_lds(const LdsSrc& src, int s, int e, bool slow, const ScanParams& P,
-                                                 Tally& t, u32& campaign, i64& bucket) {
-    Canon c;
-    if (!slow && parse_canonical(src, s, e, c)) {
-        t.ev++;
-        if (!c.view) return false;                                 // EventFilterBolt
-        t.view++;
-        u32 kw[KEY_WORDS];
-#pragma unroll
-        for (int k = 0; k < (int)KEY_WORDS; ++k) kw[k] = k < 9 ? c.kw[k] : 0u;
-        const int ci = probe(P.table, P.table_mask, kw, 36u);      // RedisJoinBolt
-        if (ci < 0) { t.miss++; return false; }
-        t.join++;
-        i64 tv;
-        const int len = c.tm_e - c.tm_s;
-        bool tok;
-        if (len <= 20) {
-            u32 dw[5];
-            load_span(src, c.tm_s, dw);
-            tok = parse_digits_regs(dw, len, tv);
-        } else {
-            tok = parse_digits(src, c.tm_s, c.tm_e, tv);
-        }
-        if (!tok) { t.terr++; return false; }                      // Long.parseLong
-        campaign = (u32)ci;
-        bucket = div_trunc(tv, P.div);
-        return true;
+// Long.parseLong of a canonical line's event_time span (LDS), then the bucket.
+__device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, int tms, int tme, const ScanParams& P, i64& bucket) {
+    i64 tv;
+    const int len = tme - tms;
+    bool ok;
+    if (len <= 20) {
+        u32 dw[5];
+        load_span(src, tms, dw);
+        ok = parse_digits_regs(dw, len, tv);
+    } else {
+        ok = parse_digits(src, tms, tme, tv);
     }
-    return slow ? process_line<false>(src, s, e, P, t, campaign, bucket)
-                : process_line<true>(src, s, e, P, t, campaign, bucket);
+    if (ok) bucket = div_trunc(tv, P.div);
+    return ok;
+}
+
+// The 36 ad_id bytes (kw[i] = bytes 4i..4i+3) -> the packed canonical key, or false if
+// they are not a lower-case 8-4-4-4-12 UUID (SWAR: 4 characters per operation).
+__device__ __forceinline__ bool pack_uuid_regs(const u32 (&kw)[9], u64& k0, u64& k1, u32& k2) {
+    bool ok = (kw[2] & 0xFFu) == '-' && ((kw[3] >> 8) & 0xFFu) == '-' && ((kw[4] >> 16) & 0xFFu) == '-' &&
+              (kw[5] >> 24) == '-';
+    u32 g[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        u32 w = kw[k];
+        if (k == 2) w = (w & 0xFFFFFF00u) | 0x30u;         // dashes decode as '0'
+        if (k == 3) w = (w & 0xFFFF00FFu) | 0x3000u;
+        if (k == 4) w = (w & 0xFF00FFFFu) | 0x300000u;
+        if (k == 5) w = (w & 0x00FFFFFFu) | 0x30000000u;
+        const u32 v = (w & 0x0F0F0F0Fu) + ((w >> 6) & 0x01010101u) * 9u;    // nibble per byte
+        const u32 m = (v + 0x76767676u) & 0x80808080u;                      // bytes >= 10
+        ok &= (v & 0x10101010u) == 0u && v + 0x30303030u + (m >> 7) * 0x27u == w;   // re-encodes to w
+        g[k] = ((v & 0xFu) << 12) | (((v >> 8) & 0xFu) << 8) | (((v >> 16) & 0xFu) << 4) | ((v >> 24) & 0xFu);
+    }
+    k0 = ((u64)g[0] << 48) | ((u64)g[1] << 32) | ((u64)g[2] << 16) | g[3];
+    k1 = ((u64)g[4] << 48) | ((u64)g[5] << 32) | ((u64)g[6] << 16) | g[7];
+    k2 = g[8];
+    return ok;
 }
 
 // Adds v views to (campaign, bucket): the ring cell if the bucket is live, else the
@@ -637,37 +652,36 @@ constexpr int BS_WORDS = CHUNKS_PER_THREAD * SCAN_TPB / 32;              // 136
 constexpr int OFF_TILE = 0;
 constexpr int OFF_QBITS = OFF_TILE + TILE_CAP + 64;
 constexpr int OFF_BS = OFF_QBITS + TILE_CHUNKS * 2 + 16;
-constexpr int OFF_LSTART = OFF_BS + BS_WORDS * 4;
-constexpr int OFF_LCNT = OFF_LSTART + (SCAN_TPB + 4) * 4;
+constexpr int OFF_LCNT = OFF_BS + BS_WORDS * 4;
 constexpr int OFF_MISC = OFF_LCNT + LCNT_CAP * 4;
-constexpr int LDS_BYTES = OFF_MISC + 64;
-static_assert(OFF_QBITS % 16 == 0 && OFF_BS % 16 == 0 && OFF_LSTART % 16 == 0 && OFF_LCNT % 16 == 0 &&
-              OFF_MISC % 16 == 0, "LDS carve must stay 16-byte aligned");
+constexpr int OFF_TB = OFF_MISC + 64;
+constexpr int LDS_BYTES = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
+static_assert(OFF_QBITS % 16 == 0 && OFF_BS % 16 == 0 && OFF_LCNT % 16 == 0 &&
+              OFF_MISC % 16 == 0 && OFF_TB % 16 == 0, "LDS carve must stay 16-byte aligned");
 static_assert(LDS_BYTES <= 81920, "two workgroups per CU need <= 80 KiB of LDS each");
 
 struct TileInfo {
     u64 first;
     u32 count;
     u32 s0;        // byte offset of the tile's first line
-    u32 delta;     // s0 - aligned base
+    u32 delta;     // s0 - 16-byte aligned base
     u32 len;       // bytes in LDS (from the aligned base)
     u32 e;         // end offset of the tile's last line
     bool oversize; // does not fit TILE_CAP (or offsets are not monotone)
-    const u8* abase;
 };
 
-__device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t) {
+// Tile bounds come from the LDS copy tb[] (loaded once per workgroup), so no HBM
+// round trip sits between two tiles.
+__device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_begin, const u32* tb) {
     TileInfo ti;
     ti.first = t * SCAN_TPB;
     const u64 rem = P.n - ti.first;
     ti.count = rem < (u64)SCAN_TPB ? (u32)rem : (u32)SCAN_TPB;
-    const u32 s0 = P.off[ti.first];
-    const u64 e = (ti.first + ti.count < P.n) ? (u64)P.off[ti.first + ti.count] : P.nbytes;
+    const u32 s0 = tb[t - t_begin];
+    const u64 e = tb[t - t_begin + 1];
     ti.s0 = s0;
     ti.e = (u32)e;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(P.bytes) + s0;
-    ti.abase = reinterpret_cast<const u8*>(a & ~(uintptr_t)15);
-    ti.delta = (u32)(a & 15);
+    ti.delta = s0 & 15u;   // P.bytes is 16-byte aligned
     const bool sane = (u64)s0 <= e && e <= P.nbytes;
     const u64 len = sane ? e - s0 + ti.delta : ~0ULL;
     ti.oversize = !sane || len > (u64)TILE_CAP;
@@ -675,29 +689,31 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t) {
     return ti;
 }
 
+// The next tile's bytes and line offsets, HBM -> registers.  Bounds-checked buffer
+// loads (out-of-range reads return 0 and never fault), always the same number per
+// lane, so later waits can count them (vmcnt) instead of draining everything.
 __device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const TileInfo& ti, uint4 (&pre)[CHUNKS_PER_THREAD],
-                                                 u32& my_off) {
+                                                 u32& my_off, u32& my_end) {
     const int tid = threadIdx.x;
     const u32 nch = (ti.len + 15) >> 4;
-    const u8* end = P.bytes + P.nbytes;
+    // A 16-byte access that straddles num_records reads as all zeros, so the range is
+    // the batch rounded up to 16 bytes: with a 16-byte aligned base, a chunk holding any
+    // batch byte never leaves the batch's last page.
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<u8*>(P.bytes), 0, (int)(u32)((P.nbytes + 15) & ~15ull), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32*>(P.off), 0, (int)(u32)(P.n * 4),
+                                                                        0x00020000);
+    const u32 base = ti.s0 - ti.delta;
 #pragma unroll
     for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
         const u32 k = (u32)(j * SCAN_TPB + tid);
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < nch) {
-            const u8* a = ti.abase + 16u * k;
-            if (a + 16 <= end) {
-                v = *reinterpret_cast<const uint4*>(a);
-            } else {   // the batch's last partial chunk
-                u32 w[4] = {0, 0, 0, 0};
-                for (int x = 0; x < 16; ++x)
-                    if (a + x < end) w[x >> 2] |= (u32)a[x] << ((x & 3) * 8);
-                v = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-        }
-        pre[j] = v;
+        const u32 o = k < nch ? base + 16u * k : 0xFFFFFFF0u;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)o, 0, 0);
+        pre[j] = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    my_off = ((u32)tid < ti.count) ? P.off[ti.first + tid] : 0u;
+    const u32 oo = (u32)tid < ti.count ? (u32)((ti.first + tid) * 4u) : 0xFFFFFFF0u;
+    my_off = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)oo, 0, 0);
+    my_end = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(oo + 4u), 0, 0);   // 0 past the batch end
 }
 
 // Quote-candidate nibble of one dword: bit i set if byte i may be '"'.  The
@@ -734,15 +750,43 @@ __device__ __forceinline__ u32 wave_sum(u32 v) {
     return v;
 }
 
+__device__ __forceinline__ void flush_tally(const ScanParams& P, const Tally& tl, int lane) {
+    const u32 sums[7] = {wave_sum(tl.ev), wave_sum(tl.view), wave_sum(tl.join), wave_sum(tl.miss),
+                         wave_sum(tl.perr), wave_sum(tl.terr), wave_sum(tl.oor)};
+    if (lane == 0) {
+        const u32 slots[7] = {ST_EVENTS, ST_VIEWS, ST_JOINED, ST_MISSES, ST_PARSE_ERR, ST_TIME_ERR, ST_OUT_OF_RING};
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+            if (sums[k]) atomicAdd(&P.stats[slots[k]], (unsigned long long)sums[k]);
+    }
+}
+
+#ifdef YSB_STAMPS
+// Diagnostic build only: wave-level s_memtime phase accounting (cdna_hip_programming.md
+// section 7, "In-kernel stamps").  The values go to P.dbg, never into results.
+#define STAMP_DECL unsigned long long st_acc[N_STAMPS] = {0}, st_last = stamp_now();
+#define STAMP(i) do { const unsigned long long n_ = stamp_now(); st_acc[i] += n_ - st_last; st_last = n_; } while (0)
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#else
+#define STAMP_DECL
+#define STAMP(i) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
     u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
     u16* q16 = reinterpret_cast<u16*>(smem + OFF_QBITS);
     const u32* q32 = reinterpret_cast<const u32*>(smem + OFF_QBITS);
     u32* bsb = reinterpret_cast<u32*>(smem + OFF_BS);
-    u32* lstart = reinterpret_cast<u32*>(smem + OFF_LSTART);
     u32* lcnt = reinterpret_cast<u32*>(smem + OFF_LCNT);
     i64* misc64 = reinterpret_cast<i64*>(smem + OFF_MISC);   // [0] lbase, [1] lset, [2..5] scratch
+    u32* tb = reinterpret_cast<u32*>(smem + OFF_TB);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -756,17 +800,27 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
     const u32 ncells = WL ? P.n_campaigns * WL : 0u;
     for (u32 i = tid; i < ncells; i += SCAN_TPB) lcnt[i] = 0;
     if (tid == 0) { misc64[0] = 0; misc64[1] = 0; }
+    // tile bounds of this workgroup's run: off[t * 256] for t in [t_begin, t_end], nbytes past the end
+    for (u32 i = tid; i <= (u32)(t_end - t_begin); i += SCAN_TPB) {
+        const u64 f = (t_begin + i) * SCAN_TPB;
+        tb[i] = f < P.n ? P.off[f] : (u32)P.nbytes;
+    }
+    __syncthreads();
 
     Tally tl{0, 0, 0, 0, 0, 0, 0};
     uint4 pre[CHUNKS_PER_THREAD];
-    u32 pre_off = 0;
-    TileInfo nxt = tile_info(P, t_begin);
-    issue_tile_loads(P, nxt, pre, pre_off);
+    u32 pre_off = 0, pre_end = 0;
+    TileInfo nxt = tile_info(P, t_begin, t_begin, tb);
+    issue_tile_loads(P, nxt, pre, pre_off, pre_end);
 
     const LdsSrc lsrc{tile32, q32};
+    const uint4* ct4 = reinterpret_cast<const uint4*>(P.ctable);
+    const uint2* ct2 = reinterpret_cast<const uint2*>(P.ctable);
+    STAMP_DECL
     for (u64 t = t_begin; t < t_end; ++t) {
         const TileInfo cur = nxt;
         const u32 my_off = pre_off;
+        const u32 my_end = (cur.first + tid + 1 < P.n) ? pre_end : (u32)P.nbytes;
         // ---- Phase A: registers -> LDS, classify bytes --------------------------
         if (!cur.oversize) {
             const u32 nch = (cur.len + 15) >> 4;
@@ -788,49 +842,86 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
                     bsb[wi + 1] = (u32)(m >> 32);
                 }
             }
-            if ((u32)tid < cur.count) lstart[tid] = my_off - cur.s0 + cur.delta;
-            if (tid == 0) lstart[cur.count] = cur.e - cur.s0 + cur.delta;
         }
+        STAMP(0);
         __syncthreads();
-        // ---- prefetch the next tile (lands while this one is parsed) -----------
-        if (t + 1 < t_end) {
-            nxt = tile_info(P, t + 1);
-            issue_tile_loads(P, nxt, pre, pre_off);
-        }
-        // ---- Phase B: one line per thread ---------------------------------------
-        bool valid = false;
-        u32 campaign = 0;
-        i64 bucket = 0;
+        STAMP(1);
+        // ---- Phase B1: canonical parse from LDS; any other line is deferred -------
+        bool pend = false, dfr = false;
+        u64 k0 = 0, k1 = 0;
+        u32 k2 = 0;
+        int tms = 0, tme = 0;
         if ((u32)tid < cur.count) {
-            if (!cur.oversize) {
-                const int ls = (int)lstart[tid], le = (int)lstart[tid + 1];
-                if (my_off < cur.s0 || ls > le || le > (int)cur.len) {
-                    tl.ev++; tl.perr++;
-                } else {
-                    bool slow = false;
-                    if (le > ls) {
-                        const int c0 = ls >> 4, c1 = (le - 1) >> 4;
-                        for (int wi = c0 >> 5; wi <= (c1 >> 5); ++wi) {
-                            u32 m = bsb[wi];
-                            if (wi == (c0 >> 5)) m &= ~0u << (c0 & 31);
-                            if (wi == (c1 >> 5) && (c1 & 31) != 31) m &= (2u << (c1 & 31)) - 1u;
-                            slow |= m != 0;
+            if (cur.oversize || my_off < cur.s0 || my_end < my_off || my_end > cur.e) {
+                dfr = true;                         // the general path re-checks and counts it
+            } else {
+                Canon cn;
+                const int ls = (int)(my_off - cur.s0 + cur.delta), le = (int)(my_end - cur.s0 + cur.delta);
+                if (parse_canonical(lsrc, bsb, ls, le, cn)) {
+                    if (cn.view && !pack_uuid_regs(cn.kw, k0, k1, k2)) {
+                        dfr = true;                 // ad_id not a canonical UUID: general table
+                    } else {
+                        tl.ev++;
+                        if (cn.view) {              // EventFilterBolt
+                            tl.view++;
+                            pend = true;
+                            tms = cn.tm_s;
+                            tme = cn.tm_e;
                         }
                     }
-                    valid = process_line_lds(lsrc, ls, le, slow, P, tl, campaign, bucket);
-                }
-            } else {
-                // tile does not fit LDS: parse straight from HBM (rare; correctness path)
-                const u64 ls = my_off;
-                const u64 le = (cur.first + tid + 1 < P.n) ? (u64)P.off[cur.first + tid + 1] : P.nbytes;
-                if (ls > le || le > P.nbytes || le - ls > 0x7FFFFFFFull) {
-                    tl.ev++; tl.perr++;
                 } else {
-                    const GlbSrc gsrc{P.bytes + ls, le - ls};
-                    valid = process_line<false>(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket);
+                    dfr = true;
                 }
             }
         }
+        // deferred lines -> list for defer_kernel (one atomic per wave)
+        {
+            const unsigned long long m = __ballot(dfr);
+            if (m) {
+                u32 base = 0;
+                if (lane == 0) base = atomicAdd(P.defer_count, (u32)__popcll(m));
+                base = __shfl(base, 0, 64);
+                if (dfr) {
+                    const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+                    if (base + r < P.defer_cap) P.defer[base + r] = (u32)(cur.first + tid);
+                }
+            }
+        }
+        // RedisJoinBolt's lookup for canonical keys: both cuckoo slots, loaded by every lane
+        // BEFORE the next tile's prefetch so that waiting for them does not wait for it.
+        u32 ia, ib;
+        cuckoo_slots(cuckoo_hash(k0, k1, k2, P.cseed), P.ctable_mask, &ia, &ib);
+        const uint4 sa = ct4[2 * (u64)ia], sb = ct4[2 * (u64)ib];
+        const uint2 ta = ct2[4 * (u64)ia + 2], tb2 = ct2[4 * (u64)ib + 2];
+        STAMP(2);
+        // ---- prefetch the next tile (lands while this one is parsed) -----------
+        // Issued on every iteration (the last one loads nothing: out-of-range buffer
+        // loads return zeros) so every path has the same count of loads in flight and
+        // the waits below stay counted.
+        if (t + 1 < t_end) nxt = tile_info(P, t + 1, t_begin, tb);
+        else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
+        issue_tile_loads(P, nxt, pre, pre_off, pre_end);
+        // ---- Phase B2: join result, event_time -> bucket --------------------------
+        bool valid = false;
+        u32 campaign = 0;
+        i64 bucket = 0;
+        if (pend) {
+            const u32 klo0 = (u32)k0, khi0 = (u32)(k0 >> 32), klo1 = (u32)k1, khi1 = (u32)(k1 >> 32);
+            int ci = -1;
+            if (sa.x == klo0 && sa.y == khi0 && sa.z == klo1 && sa.w == khi1 && ta.x == k2 && ta.y != EMPTY_SLOT)
+                ci = (int)ta.y;
+            else if (sb.x == klo0 && sb.y == khi0 && sb.z == klo1 && sb.w == khi1 && tb2.x == k2 && tb2.y != EMPTY_SLOT)
+                ci = (int)tb2.y;
+            if (ci < 0) {
+                tl.miss++;                                                  // drop (:465-467)
+            } else {
+                tl.join++;
+                campaign = (u32)ci;
+                valid = canonical_bucket(lsrc, tms, tme, P, bucket);       // Long.parseLong
+                if (!valid) tl.terr++;
+            }
+        }
+        STAMP(3);
         // ---- count: LDS window counters, flushed when the window moves ----------
         if (WL) {
             i64 lbase = misc64[0];
@@ -860,8 +951,17 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
         } else if (valid) {
             global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
         }
+        STAMP(4);
         __syncthreads();
+        STAMP(5);
     }
+#ifdef YSB_STAMPS
+    if (lane == 0) {
+        unsigned long long* o = P.dbg + ((u64)blockIdx.x * (SCAN_TPB / 64) + wave) * N_STAMPS;
+        for (int i = 0; i < 6; ++i) o[i] += st_acc[i];
+        o[6] += t_end - t_begin;
+    }
+#endif
     // ---- final flush + stats ---------------------------------------------------------
     if (WL && misc64[1]) {
         const i64 lbase = misc64[0];
@@ -870,13 +970,43 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
             if (v) global_add(P, ring_lo, ring_set, i >> P.lds_wl_log2, lbase + (i64)(i & (WL - 1)), v, tl);
         }
     }
-    const u32 sums[7] = {wave_sum(tl.ev), wave_sum(tl.view), wave_sum(tl.join), wave_sum(tl.miss),
-                         wave_sum(tl.perr), wave_sum(tl.terr), wave_sum(tl.oor)};
-    if (lane == 0) {
-        const u32 slots[7] = {ST_EVENTS, ST_VIEWS, ST_JOINED, ST_MISSES, ST_PARSE_ERR, ST_TIME_ERR, ST_OUT_OF_RING};
-#pragma unroll
-        for (int k = 0; k < 7; ++k)
-            if (sums[k]) atomicAdd(&P.stats[slots[k]], (unsigned long long)sums[k]);
+    flush_tally(P, tl, lane);
+}
+
+// Kernel 1b: the lines the fast path deferred (any layout other than the generator's,
+// escapes, non-canonical ad ids, over-size tiles, bad offsets) through the general
+// strict JSON tokenizer, straight from HBM.  Rare on generator data; exact always.
+// The last workgroup to finish resets the list for the next batch.
+__global__ __launch_bounds__(SCAN_TPB) void defer_kernel(ScanParams P) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const u32 cnt = min(*P.defer_count, P.defer_cap);
+    const i64 ring_lo = P.ring[0];
+    const bool ring_set = P.ring[1] != 0;
+    Tally tl{0, 0, 0, 0, 0, 0, 0};
+    for (u32 i = blockIdx.x * SCAN_TPB + tid; i < cnt; i += gridDim.x * SCAN_TPB) {
+        const u64 li = P.defer[i];
+        const u64 ls = P.off[li];
+        const u64 le = li + 1 < P.n ? (u64)P.off[li + 1] : P.nbytes;
+        if (ls > le || le > P.nbytes || le - ls > 0x7FFFFFFFull) {
+            tl.ev++;
+            tl.perr++;
+            continue;
+        }
+        u32 campaign;
+        i64 bucket;
+        const GlbSrc gsrc{P.bytes + ls, le - ls};
+        if (process_line<false>(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket))
+            global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+    }
+    flush_tally(P, tl, lane);
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        if (atomicAdd(P.defer_done, 1u) == gridDim.x - 1) {
+            if (*P.defer_count > P.defer_cap) atomicAdd(&P.stats[ST_PARSE_ERR], (unsigned long long)(*P.defer_count - P.defer_cap));
+            *P.defer_count = 0;
+            *P.defer_done = 0;
+        }
     }
 }
 
@@ -919,6 +1049,11 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
     const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;
     hipLaunchKernelGGL(scan_kernel, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
+}
+
+void launch_defer(const ScanParams& p, int blocks, hipStream_t s) {
+    if (p.n == 0) return;
+    hipLaunchKernelGGL(defer_kernel, dim3(blocks), dim3(SCAN_TPB), 0, s, p);
 }
 
 void launch_ring_autobase(const ScanParams& p, hipStream_t s) {

@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libysb_hip.so")
+# YSB_LIB_VARIANT=stamps selects the diagnostic build (tools/stamps.py only)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libysb_hip%s.so" % (
+    "_" + os.environ["YSB_LIB_VARIANT"] if os.environ.get("YSB_LIB_VARIANT") else ""))
 
 YSB_OK = 0
 ERRORS = {-1: "YSB_ERR_ARG", -2: "YSB_ERR_HIP", -3: "YSB_ERR_STATE", -4: "YSB_ERR_CAPACITY",
