@@ -210,7 +210,8 @@ def main():
         mism, truth, ring = ctx.truth_compare()
         st = ctx.stats()
         check = {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
-                 "parse_errors": st["parse_errors"], "out_of_ring": st["out_of_ring"]}
+                 "parse_errors": st["parse_errors"], "out_of_ring": st["out_of_ring"],
+                 "deferred_to_general_path": st["deferred"]}
         if d.world > 1:
             check["note"] = "rank-local table (before reduce-scatter) vs rank-local truth"
 

@@ -83,6 +83,7 @@ typedef struct ysb_stats {
     uint64_t out_of_ring;  /* joined views counted through the overflow side list    */
     uint64_t overflow_dropped; /* side-list entries lost for lack of capacity (must be 0) */
     uint64_t batches;      /* submits                                                */
+    uint64_t deferred;     /* lines the fast path handed to the general tokenizer    */
 } ysb_stats;
 
 /* One (campaign, window) delta: the unit the Redis writer HINCRBYs into

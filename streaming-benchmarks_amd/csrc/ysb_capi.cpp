@@ -646,6 +646,7 @@ int ysb_stats_get(ysb_ctx* c, ysb_stats* s) {
     s->out_of_ring = v[ST_OUT_OF_RING];
     s->overflow_dropped = v[ST_OVF_DROPPED];
     s->batches = c->batches;
+    s->deferred = v[ST_DEFERRED];
     return YSB_OK;
 }
 
@@ -975,6 +976,16 @@ int ysb_gen_dump(const ysb_gen_params* p, uint64_t n_events, const char* dir) {
 }
 
 #ifdef YSB_STAMPS
+// Diagnostic build only: the deferred-line list of the last batch.
+int ysb_debug_defer_list(ysb_ctx* c, uint32_t* out, uint64_t cap) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = ysb_sync(c);
+    if (rc) return rc;
+    if (!c->d_defer) return YSB_OK;
+    HIPCHK(c, hipMemcpy(out, c->d_defer, std::min<u64>(cap, c->defer_cap) * 4, hipMemcpyDeviceToHost));
+    return YSB_OK;
+}
+
 // Diagnostic build only: per-wave phase cycles of the scan kernel since the last call.
 int ysb_debug_stamps(ysb_ctx* c, uint64_t* out, uint64_t cap, uint64_t* n) {
     if (!c || !n) return YSB_ERR_ARG;

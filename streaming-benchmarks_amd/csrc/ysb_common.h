@@ -193,7 +193,8 @@ YSB_HD u32 key_hash(const u32* w, u32 len) {
 // packs losslessly into 144 bits: its 36 characters as nibbles (dashes -> 0), 16 bits
 // per 4-character group, k0 = groups 0-3, k1 = groups 4-7, k2 = group 8.  Map keys
 // in that form go into a two-choice cuckoo table, so a lookup is exactly two slot
-// loads issued together.  Slot words: [k0 lo, k0 hi, k1 lo, k1 hi, k2, campaign, 0, 0].
+// loads issued together.  Group value: character j of the group in nibble j.
+// Slot words: [k0 lo, k0 hi, k1 lo, k1 hi, k2, campaign, 0, 0].
 // ---------------------------------------------------------------------------
 enum : u32 { CSLOT_WORDS = 8 };
 
@@ -215,7 +216,7 @@ YSB_HD bool uuid_pack_bytes(const u8* s, u64* k0, u64* k1, u32* k2) {
             } else {
                 return false;
             }
-            v = (v << 4) | nib;
+            v |= nib << (4 * j);   // first character in the low nibble
         }
         g[i] = v;
     }
@@ -286,7 +287,7 @@ YSB_HD i64 div_trunc(i64 t, const DivMagic& m) {
 // Stats slots in the device stats array.
 enum : u32 {
     ST_EVENTS = 0, ST_VIEWS, ST_JOINED, ST_MISSES, ST_PARSE_ERR, ST_TIME_ERR,
-    ST_OUT_OF_RING, ST_OVF_DROPPED, ST_COUNT_
+    ST_OUT_OF_RING, ST_OVF_DROPPED, ST_DEFERRED, ST_COUNT_
 };
 
 struct OvfEntry {

@@ -469,91 +469,99 @@ __device__ __forceinline__ bool parse_digits_regs(const u32 (&w)[5], int len, i6
 // any other line returns false and takes the general tokenizer.  Costs ~3
 // dependent LDS round trips per line instead of one per token.
 // ---------------------------------------------------------------------------
-struct Canon {
+struct CanonA {   // after the first LDS batch
     u32 kw[9];     // ad_id bytes 113..148
-    bool view;
-    int tm_s, tm_e;
+    int e3, e4, e5, e6;   // closing quotes of ad_type, event_type, event_time, ip_address
 };
 
-__device__ __forceinline__ bool parse_canonical(const LdsSrc& src, const u32* bsb, int s, int e, Canon& c) {
+// Stage 1: one batch of independent LDS reads (quote bitmap, backslash flags, the
+// fixed-offset structure and the ad_id), then register-only checks and the tail's
+// quote positions.  False = not the generator's layout (deferred to the general path).
+__device__ __forceinline__ bool canon_stage1(const LdsSrc& src, int s, int e, CanonA& c) {
     const int L = e - s;
     if (L < 220 || L > 300) return false;
-    // per-16-byte backslash flags of the line's chunks (a line <= 300 B spans <= 2 words)
-    const int c0 = s >> 4, c1 = (e - 1) >> 4;
-    const u32 b0 = bsb[c0 >> 5], b1 = bsb[c1 >> 5];
-    // line-relative quote-candidate bitmap, bytes 0..319
+    // line-relative candidate bitmap ('"' or '\\'), bytes 0..319
     u32 W[11];
     const int wb = s >> 5;
 #pragma unroll
     for (int k = 0; k < 11; ++k) W[k] = src.q[wb + k];
-    // fixed structural bytes (line-relative): [0,13) [49,64) [100,113) [149,164) and the ad_id value
-    u32 s0[4], s1[4], s2[4], s3[4];
+    // fixed structural bytes (line-relative): [0,13) [49,64) and [100,164) (ad_id value inside)
+    u32 s0[4], s1[4], s23[16];
     load_span(src, s + 0, s0);
     load_span(src, s + 49, s1);
-    load_span(src, s + 100, s2);
-    load_span(src, s + 149, s3);
-    load_span(src, s + 113, c.kw);
+    load_span(src, s + 100, s23);
     const u32 sh = (u32)(s & 31);
     u32 R[10];
 #pragma unroll
     for (int k = 0; k < 10; ++k) R[k] = __builtin_amdgcn_alignbit(W[k + 1], W[k], sh);
+    // Every check XOR-accumulates into d (one VALU op each, no mask logic); d == 0 <=> all hold.
     // quotes at 1, 9, 12, 49, 52, 60, 63, 100, 103, 109, 112, 149, 152, 160, 163 and nowhere else below 164
-    bool ok = R[0] == 0x00001202u && R[1] == 0x90120000u && R[2] == 0u && R[3] == 0x00012090u &&
-              R[4] == 0x01200000u && (R[5] & 0xFu) == 0x9u;
-    {   // no backslash anywhere in the line (escapes take the general path)
-        const u32 lo = ~0u << (c0 & 31);
-        const u32 hi = (c1 & 31) == 31 ? ~0u : ((2u << (c1 & 31)) - 1u);
-        ok &= ((c0 >> 5) == (c1 >> 5)) ? (b0 & lo & hi) == 0u : ((b0 & lo) | (b1 & hi)) == 0u;
-    }
-    ok &= s0[0] == w4('{', '"', 'u', 's') && s0[1] == w4('e', 'r', '_', 'i') && s0[2] == w4('d', '"', ':', ' ') &&
-          (s0[3] & 0xFFu) == '"';
-    ok &= s1[0] == w4('"', ',', ' ', '"') && s1[1] == w4('p', 'a', 'g', 'e') && s1[2] == w4('_', 'i', 'd', '"') &&
-          (s1[3] & 0xFFFFFFu) == w4(':', ' ', '"', 0);
-    ok &= s2[0] == w4('"', ',', ' ', '"') && s2[1] == w4('a', 'd', '_', 'i') && s2[2] == w4('d', '"', ':', ' ') &&
-          (s2[3] & 0xFFu) == '"';
-    ok &= s3[0] == w4('"', ',', ' ', '"') && s3[1] == w4('a', 'd', '_', 't') && s3[2] == w4('y', 'p', 'e', '"') &&
-          (s3[3] & 0xFFFFFFu) == w4(':', ' ', '"', 0);
-    if (!ok) return false;
-    // variable tail: first quote candidate at or after p, from the registers
-    auto nextq = [&](int p) -> int {
-        int r = 1 << 20;
+    u32 d = (R[0] ^ 0x00001202u) | (R[1] ^ 0x90120000u) | R[2] | (R[3] ^ 0x00012090u) | (R[4] ^ 0x01200000u) |
+            ((R[5] & 0xFu) ^ 0x9u);
+    // A backslash anywhere breaks this template (the bitmap flags it like a quote):
+    // every byte of an accepted line is either compared below or inside a value span
+    // shown free of candidates, so escapes always take the general path.
+    d |= (s0[0] ^ w4('{', '"', 'u', 's')) | (s0[1] ^ w4('e', 'r', '_', 'i')) | (s0[2] ^ w4('d', '"', ':', ' ')) |
+         ((s0[3] & 0xFFu) ^ '"');
+    d |= (s1[0] ^ w4('"', ',', ' ', '"')) | (s1[1] ^ w4('p', 'a', 'g', 'e')) | (s1[2] ^ w4('_', 'i', 'd', '"')) |
+         ((s1[3] & 0xFFFFFFu) ^ w4(':', ' ', '"', 0));
+    // bytes 100..112: ", "ad_id": "   then the 36-byte value   then 149..163: ", "ad_type": "
+    d |= (s23[0] ^ w4('"', ',', ' ', '"')) | (s23[1] ^ w4('a', 'd', '_', 'i')) | (s23[2] ^ w4('d', '"', ':', ' ')) |
+         ((s23[3] & 0xFFu) ^ '"');
 #pragma unroll
-        for (int k = 9; k >= 5; --k) {
-            u32 m = R[k];
-            const int base = 32 * k;
-            if (p > base + 31) m = 0u;
-            else if (p > base) m &= ~0u << (p - base);
-            if (m) r = base + (int)__builtin_ctz(m);
-        }
-        return r;
+    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(s23[k + 4], s23[k + 3], 1u);   // bytes 113..148
+    d |= (__builtin_amdgcn_alignbyte(s23[13], s23[12], 1u) ^ w4('"', ',', ' ', '"')) |     // bytes 149..152
+         (__builtin_amdgcn_alignbyte(s23[14], s23[13], 1u) ^ w4('a', 'd', '_', 't')) |     // 153..156
+         (__builtin_amdgcn_alignbyte(s23[15], s23[14], 1u) ^ w4('y', 'p', 'e', '"')) |     // 157..160
+         ((s23[15] >> 8) ^ w4(':', ' ', '"', 0));                                           // 161..163
+    // variable tail: first quote candidate at or after p (160 <= p < 320), via a 64-bit window
+    auto nextq = [&](int p) -> int {
+        const int k = p >> 5;
+        const u32 lo = k == 5 ? R[5] : k == 6 ? R[6] : k == 7 ? R[7] : k == 8 ? R[8] : k == 9 ? R[9] : 0u;
+        const u32 hi = k == 5 ? R[6] : k == 6 ? R[7] : k == 7 ? R[8] : k == 8 ? R[9] : 0u;
+        const u64 w = (((u64)hi << 32) | lo) >> (p & 31);
+        return w ? p + (int)__builtin_ctzll(w) : (1 << 20);
     };
-    const int e3 = nextq(164);          // end of ad_type
-    const int e4 = nextq(e3 + 18);      // end of event_type
-    const int e5 = nextq(e4 + 18);      // end of event_time
-    const int e6 = nextq(e5 + 18);      // end of ip_address
-    if (e6 + 2 > L) return false;
+    c.e3 = nextq(164);            // end of ad_type
+    c.e4 = nextq(c.e3 + 18);      // end of event_type
+    c.e5 = nextq(c.e4 + 18);      // end of event_time
+    c.e6 = nextq(c.e5 + 18);      // end of ip_address
+    return d == 0u && c.e6 + 2 <= L;
+}
+
+struct CanonB {   // after the second LDS batch
+    bool view;
+    u32 td[5];     // event_time bytes (first 20)
+    int tlen;
+};
+
+// Stage 2: the variable tail -- the three separators, the closing "}", the event_type
+// value and the event_time digits -- in one batch of LDS reads.
+__device__ __forceinline__ bool canon_stage2(const LdsSrc& src, int s, int e, const CanonA& a, CanonB& c) {
+    const int L = e - s;
     u32 t4[5], t5[5], t6[5], t7[1], ev[1];
-    load_span(src, s + e3, t4);
-    load_span(src, s + e4, t5);
-    load_span(src, s + e5, t6);
-    load_span(src, s + e6, t7);
-    load_span(src, s + e3 + 18, ev);
-    ok = t4[0] == w4('"', ',', ' ', '"') && t4[1] == w4('e', 'v', 'e', 'n') && t4[2] == w4('t', '_', 't', 'y') &&
-         t4[3] == w4('p', 'e', '"', ':') && (t4[4] & 0xFFFFu) == w4(' ', '"', 0, 0);
-    ok &= t5[0] == w4('"', ',', ' ', '"') && t5[1] == w4('e', 'v', 'e', 'n') && t5[2] == w4('t', '_', 't', 'i') &&
-          t5[3] == w4('m', 'e', '"', ':') && (t5[4] & 0xFFFFu) == w4(' ', '"', 0, 0);
-    ok &= t6[0] == w4('"', ',', ' ', '"') && t6[1] == w4('i', 'p', '_', 'a') && t6[2] == w4('d', 'd', 'r', 'e') &&
-          t6[3] == w4('s', 's', '"', ':') && (t6[4] & 0xFFFFu) == w4(' ', '"', 0, 0);
-    ok &= (t7[0] & 0xFFFFu) == w4('"', '}', 0, 0);
+    load_span(src, s + a.e3, t4);
+    load_span(src, s + a.e4, t5);
+    load_span(src, s + a.e5, t6);
+    load_span(src, s + a.e6, t7);
+    load_span(src, s + a.e3 + 18, ev);
+    load_span(src, s + a.e4 + 18, c.td);
+    u32 d = (t4[0] ^ w4('"', ',', ' ', '"')) | (t4[1] ^ w4('e', 'v', 'e', 'n')) | (t4[2] ^ w4('t', '_', 't', 'y')) |
+            (t4[3] ^ w4('p', 'e', '"', ':')) | ((t4[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
+    d |= (t5[0] ^ w4('"', ',', ' ', '"')) | (t5[1] ^ w4('e', 'v', 'e', 'n')) | (t5[2] ^ w4('t', '_', 't', 'i')) |
+         (t5[3] ^ w4('m', 'e', '"', ':')) | ((t5[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
+    d |= (t6[0] ^ w4('"', ',', ' ', '"')) | (t6[1] ^ w4('i', 'p', '_', 'a')) | (t6[2] ^ w4('d', 'd', 'r', 'e')) |
+         (t6[3] ^ w4('s', 's', '"', ':')) | ((t6[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
+    d |= (t7[0] & 0xFFFFu) ^ w4('"', '}', 0, 0);
+    bool ok = d == 0u;
     // trailing bytes after '}' must be JSON whitespace (normally just the '\n')
-    if (L > e6 + 2) ok &= is_ws((t7[0] >> 16) & 0xFFu);
-    if (L > e6 + 3) ok &= is_ws(t7[0] >> 24);
+    if (L > a.e6 + 2) ok &= is_ws((t7[0] >> 16) & 0xFFu);
+    if (L > a.e6 + 3) ok &= is_ws(t7[0] >> 24);
     if (!ok) return false;
-    for (int p = e6 + 4; p < L; ++p)
+    for (int p = a.e6 + 4; p < L; ++p)
         if (!is_ws(src.b(s + p))) return false;
-    c.view = (e4 - (e3 + 18) == 4) && ev[0] == VIEW_W;
-    c.tm_s = s + e4 + 18;
-    c.tm_e = s + e5;
+    c.view = (a.e4 - (a.e3 + 18) == 4) && ev[0] == VIEW_W;
+    c.tlen = a.e5 - (a.e4 + 18);
     return true;
 }
 
@@ -583,17 +591,34 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
     return true;
 }
 
-// Long.parseLong of a canonical line's event_time span (LDS), then the bucket.
-__device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, int tms, int tme, const ScanParams& P, i64& bucket) {
+// Four ASCII digits (byte 0 most significant) -> 0..9999; bad != 0 if any byte is not a digit.
+__device__ __forceinline__ u32 swar_digits4(u32 w, u32& bad) {
+    const u32 dgt = w - 0x30303030u;                                        // per byte, borrow-free when valid
+    bad |= (w & 0xF0F0F0F0u) ^ 0x30303030u;                                 // high nibbles must be 3
+    bad |= (dgt + 0x76767676u) & 0x80808080u;                               // low nibbles must be <= 9
+    const u32 pr = (dgt & 0x00FF00FFu) * 10u + ((dgt >> 8) & 0x00FF00FFu); // two 2-digit halves
+    return (pr & 0xFFFFu) * 100u + (pr >> 16);
+}
+
+// Long.parseLong of a canonical line's event_time, then the bucket.  13 unsigned digits
+// (epoch milliseconds 2001..2286) take a SWAR path; any other form the general one.
+__device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, const CanonB& b, int tms, const ScanParams& P,
+                                                 i64& bucket) {
     i64 tv;
-    const int len = tme - tms;
-    bool ok;
-    if (len <= 20) {
-        u32 dw[5];
-        load_span(src, tms, dw);
-        ok = parse_digits_regs(dw, len, tv);
+    bool ok = false;
+    if (b.tlen == 13) {
+        u32 bad = 0;
+        const u32 g0 = swar_digits4(b.td[0], bad), g1 = swar_digits4(b.td[1], bad), g2 = swar_digits4(b.td[2], bad);
+        const u32 d12 = (b.td[3] & 0xFFu) - '0';
+        bad |= d12 > 9u;
+        tv = (i64)(((u64)(g0 * 10000u + g1) * 10000u + g2) * 10u + d12);
+        ok = bad == 0u;
+    }
+    if (ok) {
+    } else if (b.tlen <= 20) {   // signs, other lengths, errors: the general digit loop decides
+        ok = parse_digits_regs(b.td, b.tlen, tv);
     } else {
-        ok = parse_digits(src, tms, tme, tv);
+        ok = parse_digits(src, tms, tms + b.tlen, tv);
     }
     if (ok) bucket = div_trunc(tv, P.div);
     return ok;
@@ -602,8 +627,8 @@ __device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, int tms, int
 // The 36 ad_id bytes (kw[i] = bytes 4i..4i+3) -> the packed canonical key, or false if
 // they are not a lower-case 8-4-4-4-12 UUID (SWAR: 4 characters per operation).
 __device__ __forceinline__ bool pack_uuid_regs(const u32 (&kw)[9], u64& k0, u64& k1, u32& k2) {
-    bool ok = (kw[2] & 0xFFu) == '-' && ((kw[3] >> 8) & 0xFFu) == '-' && ((kw[4] >> 16) & 0xFFu) == '-' &&
-              (kw[5] >> 24) == '-';
+    u32 bad = ((kw[2] & 0xFFu) ^ '-') | (((kw[3] >> 8) & 0xFFu) ^ '-') | (((kw[4] >> 16) & 0xFFu) ^ '-') |
+              ((kw[5] >> 24) ^ '-');
     u32 g[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
@@ -614,13 +639,14 @@ __device__ __forceinline__ bool pack_uuid_regs(const u32 (&kw)[9], u64& k0, u64&
         if (k == 5) w = (w & 0x00FFFFFFu) | 0x30000000u;
         const u32 v = (w & 0x0F0F0F0Fu) + ((w >> 6) & 0x01010101u) * 9u;    // nibble per byte
         const u32 m = (v + 0x76767676u) & 0x80808080u;                      // bytes >= 10
-        ok &= (v & 0x10101010u) == 0u && v + 0x30303030u + (m >> 7) * 0x27u == w;   // re-encodes to w
-        g[k] = ((v & 0xFu) << 12) | (((v >> 8) & 0xFu) << 8) | (((v >> 16) & 0xFu) << 4) | ((v >> 24) & 0xFu);
+        bad |= (v & 0x10101010u) | ((v + 0x30303030u + (m >> 7) * 0x27u) ^ w);   // must re-encode to w
+        const u32 x = v | (v >> 4);                                         // n0|n1<<4 in byte 0, n2|n3<<4 in byte 2
+        g[k] = (x & 0xFFu) | ((x >> 8) & 0xFF00u);
     }
     k0 = ((u64)g[0] << 48) | ((u64)g[1] << 32) | ((u64)g[2] << 16) | g[3];
     k1 = ((u64)g[4] << 48) | ((u64)g[5] << 32) | ((u64)g[6] << 16) | g[7];
     k2 = g[8];
-    return ok;
+    return bad == 0u;
 }
 
 // Adds v views to (campaign, bucket): the ring cell if the bucket is live, else the
@@ -648,15 +674,13 @@ __device__ __forceinline__ void global_add(const ScanParams& P, i64 ring_lo, boo
 // ---------------------------------------------------------------------------
 // LDS layout (dynamic, 16-byte aligned carve, no static __shared__)
 // ---------------------------------------------------------------------------
-constexpr int BS_WORDS = CHUNKS_PER_THREAD * SCAN_TPB / 32;              // 136
 constexpr int OFF_TILE = 0;
 constexpr int OFF_QBITS = OFF_TILE + TILE_CAP + 64;
-constexpr int OFF_BS = OFF_QBITS + TILE_CHUNKS * 2 + 16;
-constexpr int OFF_LCNT = OFF_BS + BS_WORDS * 4;
+constexpr int OFF_LCNT = OFF_QBITS + TILE_CHUNKS * 2 + 16;
 constexpr int OFF_MISC = OFF_LCNT + LCNT_CAP * 4;
 constexpr int OFF_TB = OFF_MISC + 64;
 constexpr int LDS_BYTES = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
-static_assert(OFF_QBITS % 16 == 0 && OFF_BS % 16 == 0 && OFF_LCNT % 16 == 0 &&
+static_assert(OFF_QBITS % 16 == 0 && OFF_LCNT % 16 == 0 &&
               OFF_MISC % 16 == 0 && OFF_TB % 16 == 0, "LDS carve must stay 16-byte aligned");
 static_assert(LDS_BYTES <= 81920, "two workgroups per CU need <= 80 KiB of LDS each");
 
@@ -677,8 +701,11 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_
     ti.first = t * SCAN_TPB;
     const u64 rem = P.n - ti.first;
     ti.count = rem < (u64)SCAN_TPB ? (u32)rem : (u32)SCAN_TPB;
-    const u32 s0 = tb[t - t_begin];
-    const u64 e = tb[t - t_begin + 1];
+    // wave-uniform by construction; readfirstlane lets the compiler keep them (and the
+    // buffer descriptors built from them) in SGPRs (no waterfall loops)
+    // (readfirstlane returns int: keep it unsigned before widening, offsets reach 4 GiB)
+    const u32 s0 = (u32)__builtin_amdgcn_readfirstlane(tb[t - t_begin]);
+    const u64 e = (u32)__builtin_amdgcn_readfirstlane(tb[t - t_begin + 1]);
     ti.s0 = s0;
     ti.e = (u32)e;
     ti.delta = s0 & 15u;   // P.bytes is 16-byte aligned
@@ -690,43 +717,45 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_
 }
 
 // The next tile's bytes and line offsets, HBM -> registers.  Bounds-checked buffer
-// loads (out-of-range reads return 0 and never fault), always the same number per
-// lane, so later waits can count them (vmcnt) instead of draining everything.
+// loads through per-tile descriptors (base = the tile, num_records = its length, so
+// chunks past the tile read zeros and never fault); per-lane offsets are
+// loop-invariant, so issuing costs no VALU.  Always the same number of loads per lane,
+// so later waits can count them (vmcnt) instead of draining everything.
 __device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const TileInfo& ti, uint4 (&pre)[CHUNKS_PER_THREAD],
                                                  u32& my_off, u32& my_end) {
     const int tid = threadIdx.x;
-    const u32 nch = (ti.len + 15) >> 4;
-    // A 16-byte access that straddles num_records reads as all zeros, so the range is
-    // the batch rounded up to 16 bytes: with a 16-byte aligned base, a chunk holding any
-    // batch byte never leaves the batch's last page.
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<u8*>(P.bytes), 0, (int)(u32)((P.nbytes + 15) & ~15ull), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32*>(P.off), 0, (int)(u32)(P.n * 4),
-                                                                        0x00020000);
-    const u32 base = ti.s0 - ti.delta;
+    const u8* tbase = P.bytes + (ti.s0 - ti.delta);
+    // A 16-byte access that straddles num_records reads as all zeros, so the range is the
+    // tile rounded up to 16 bytes: with a 16-byte aligned base, a chunk holding any batch
+    // byte never leaves the batch's last page.
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(tbase), 0, (int)((ti.len + 15u) & ~15u), 0x00020000);
 #pragma unroll
     for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
-        const u32 k = (u32)(j * SCAN_TPB + tid);
-        const u32 o = k < nch ? base + 16u * k : 0xFFFFFFF0u;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)o, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, 16 * (j * SCAN_TPB + tid), 0, 0);
         pre[j] = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    const u32 oo = (u32)tid < ti.count ? (u32)((ti.first + tid) * 4u) : 0xFFFFFFF0u;
-    my_off = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)oo, 0, 0);
-    my_end = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(oo + 4u), 0, 0);   // 0 past the batch end
+    const u64 left = P.n - min(ti.first, P.n);
+    const u32 nrec = (u32)min<u64>((u64)ti.count + 1u, left) * 4u;   // my_end of the tile's last line included
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<u32*>(P.off + min(ti.first, P.n)), 0, (int)nrec, 0x00020000);
+    my_off = __builtin_amdgcn_raw_buffer_load_b32(ro, 4 * tid, 0, 0);
+    my_end = __builtin_amdgcn_raw_buffer_load_b32(ro, 4 * tid + 4, 0, 0);   // 0 past the batch end
 }
 
-// Quote-candidate nibble of one dword: bit i set if byte i may be '"'.  The
-// haszero trick can flag a byte above a true zero falsely; the tokenizer verifies
-// every candidate, so only exactness of the true positives matters.
-__device__ __forceinline__ u32 quote_nibble(u32 w) {
-    const u32 t = w ^ 0x22222222u;
-    const u32 z = (t - 0x01010101u) & ~t & 0x80808080u;
-    return (z * 0x00204081u) >> 28;
+// Candidate flags of one dword at bits 28..31 (bit 28+i: byte i may be '"' or '\\').
+// The has-zero trick can flag a byte just above a true hit falsely; the parser
+// verifies every candidate it relies on, so only exactness of the true hits matters.
+// Packing uses the full-rate 24-bit multiply (bits 7/15/23 -> 28/29/30) plus bit 31.
+__device__ __forceinline__ u32 cand_flags_hi(u32 w) {
+    const u32 tq = w ^ 0x22222222u, tb = w ^ 0x5C5C5C5Cu;
+    const u32 z = (((tq - 0x01010101u) & ~tq) | ((tb - 0x01010101u) & ~tb)) & 0x80808080u;
+    return __umul24(z, 0x00204081u) | (z & 0x80000000u);
 }
-__device__ __forceinline__ u32 has_backslash(u32 w) {
-    const u32 t = w ^ 0x5C5C5C5Cu;
-    return (t - 0x01010101u) & ~t & 0x80808080u;
+// 16 flags of a 16-byte chunk, bit i = byte i.
+__device__ __forceinline__ u32 cand_mask16(const uint4& v) {
+    return (cand_flags_hi(v.x) >> 28) | ((cand_flags_hi(v.y) >> 28) << 4) | ((cand_flags_hi(v.z) >> 28) << 8) |
+           ((cand_flags_hi(v.w) >> 28) << 12);
 }
 
 __device__ __forceinline__ i64 block_max_i64(i64 v, i64* scratch) {
@@ -783,7 +812,6 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
     u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
     u16* q16 = reinterpret_cast<u16*>(smem + OFF_QBITS);
     const u32* q32 = reinterpret_cast<const u32*>(smem + OFF_QBITS);
-    u32* bsb = reinterpret_cast<u32*>(smem + OFF_BS);
     u32* lcnt = reinterpret_cast<u32*>(smem + OFF_LCNT);
     i64* misc64 = reinterpret_cast<i64*>(smem + OFF_MISC);   // [0] lbase, [1] lset, [2..5] scratch
     u32* tb = reinterpret_cast<u32*>(smem + OFF_TB);
@@ -821,25 +849,20 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
         const TileInfo cur = nxt;
         const u32 my_off = pre_off;
         const u32 my_end = (cur.first + tid + 1 < P.n) ? pre_end : (u32)P.nbytes;
+#ifdef YSB_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: separate the prefetch wait
+        STAMP(6);
+#endif
         // ---- Phase A: registers -> LDS, classify bytes --------------------------
+        // Chunks past the tile hold zeros (bounds-checked loads), so they are written
+        // unconditionally; only the last round is cut at TILE_CHUNKS (a whole wave).
         if (!cur.oversize) {
-            const u32 nch = (cur.len + 15) >> 4;
 #pragma unroll
             for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
                 const u32 k = (u32)(j * SCAN_TPB + tid);
-                const uint4 v = pre[j];
-                u32 bs = 0;
-                if (k < nch) {
-                    reinterpret_cast<uint4*>(tile32)[k] = v;
-                    q16[k] = (u16)(quote_nibble(v.x) | (quote_nibble(v.y) << 4) | (quote_nibble(v.z) << 8) |
-                                   (quote_nibble(v.w) << 12));
-                    bs = has_backslash(v.x) | has_backslash(v.y) | has_backslash(v.z) | has_backslash(v.w);
-                }
-                const unsigned long long m = __ballot(bs != 0);
-                if (lane == 0) {
-                    const u32 wi = (u32)(j * SCAN_TPB + wave * 64) >> 5;
-                    bsb[wi] = (u32)m;
-                    bsb[wi + 1] = (u32)(m >> 32);
+                if (j * SCAN_TPB + SCAN_TPB <= TILE_CHUNKS || k < (u32)TILE_CHUNKS) {
+                    reinterpret_cast<uint4*>(tile32)[k] = pre[j];
+                    q16[k] = (u16)cand_mask16(pre[j]);
                 }
             }
         }
@@ -847,31 +870,38 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
         __syncthreads();
         STAMP(1);
         // ---- Phase B1: canonical parse from LDS; any other line is deferred -------
-        bool pend = false, dfr = false;
+        bool ok1 = false;
+        int ls = 0, le = 0;
+        CanonA ca;
         u64 k0 = 0, k1 = 0;
         u32 k2 = 0;
-        int tms = 0, tme = 0;
+        bool packed = false;
+        if ((u32)tid < cur.count && !cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
+            ls = (int)(my_off - cur.s0 + cur.delta);
+            le = (int)(my_end - cur.s0 + cur.delta);
+            ok1 = canon_stage1(lsrc, ls, le, ca);
+            if (ok1) packed = pack_uuid_regs(ca.kw, k0, k1, k2);   // speculative: views only need it
+        }
+        // RedisJoinBolt's lookup (canonical keys): both cuckoo slots, issued now so their
+        // latency hides under the second LDS batch, and before the next tile's prefetch so
+        // waiting for them never waits for it.
+        u32 ia, ib;
+        cuckoo_slots(cuckoo_hash(k0, k1, k2, P.cseed), P.ctable_mask, &ia, &ib);
+        const uint4 sa = ct4[2 * (u64)ia], sb = ct4[2 * (u64)ib];
+        const uint2 ta = ct2[4 * (u64)ia + 2], tb2 = ct2[4 * (u64)ib + 2];
+        bool pend = false, dfr = false, tok = false;
+        i64 bucket = 0;
         if ((u32)tid < cur.count) {
-            if (cur.oversize || my_off < cur.s0 || my_end < my_off || my_end > cur.e) {
-                dfr = true;                         // the general path re-checks and counts it
-            } else {
-                Canon cn;
-                const int ls = (int)(my_off - cur.s0 + cur.delta), le = (int)(my_end - cur.s0 + cur.delta);
-                if (parse_canonical(lsrc, bsb, ls, le, cn)) {
-                    if (cn.view && !pack_uuid_regs(cn.kw, k0, k1, k2)) {
-                        dfr = true;                 // ad_id not a canonical UUID: general table
-                    } else {
-                        tl.ev++;
-                        if (cn.view) {              // EventFilterBolt
-                            tl.view++;
-                            pend = true;
-                            tms = cn.tm_s;
-                            tme = cn.tm_e;
-                        }
-                    }
-                } else {
-                    dfr = true;
+            CanonB cb;
+            if (ok1 && canon_stage2(lsrc, ls, le, ca, cb) && (packed || !cb.view)) {
+                tl.ev++;
+                if (cb.view) {                                             // EventFilterBolt
+                    tl.view++;
+                    pend = true;
+                    tok = canonical_bucket(lsrc, cb, ls + ca.e4 + 18, P, bucket);   // Long.parseLong
                 }
+            } else {
+                dfr = true;   // bad offsets, other layouts, escapes, non-canonical ad ids, over-size tiles
             }
         }
         // deferred lines -> list for defer_kernel (one atomic per wave)
@@ -879,7 +909,10 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
             const unsigned long long m = __ballot(dfr);
             if (m) {
                 u32 base = 0;
-                if (lane == 0) base = atomicAdd(P.defer_count, (u32)__popcll(m));
+                if (lane == 0) {
+                    base = atomicAdd(P.defer_count, (u32)__popcll(m));
+                    atomicAdd(&P.stats[ST_DEFERRED], (unsigned long long)__popcll(m));
+                }
                 base = __shfl(base, 0, 64);
                 if (dfr) {
                     const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
@@ -887,12 +920,6 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
                 }
             }
         }
-        // RedisJoinBolt's lookup for canonical keys: both cuckoo slots, loaded by every lane
-        // BEFORE the next tile's prefetch so that waiting for them does not wait for it.
-        u32 ia, ib;
-        cuckoo_slots(cuckoo_hash(k0, k1, k2, P.cseed), P.ctable_mask, &ia, &ib);
-        const uint4 sa = ct4[2 * (u64)ia], sb = ct4[2 * (u64)ib];
-        const uint2 ta = ct2[4 * (u64)ia + 2], tb2 = ct2[4 * (u64)ib + 2];
         STAMP(2);
         // ---- prefetch the next tile (lands while this one is parsed) -----------
         // Issued on every iteration (the last one loads nothing: out-of-range buffer
@@ -901,10 +928,9 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
         if (t + 1 < t_end) nxt = tile_info(P, t + 1, t_begin, tb);
         else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
         issue_tile_loads(P, nxt, pre, pre_off, pre_end);
-        // ---- Phase B2: join result, event_time -> bucket --------------------------
+        // ---- Phase B2: join result ------------------------------------------------
         bool valid = false;
         u32 campaign = 0;
-        i64 bucket = 0;
         if (pend) {
             const u32 klo0 = (u32)k0, khi0 = (u32)(k0 >> 32), klo1 = (u32)k1, khi1 = (u32)(k1 >> 32);
             int ci = -1;
@@ -917,8 +943,8 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
             } else {
                 tl.join++;
                 campaign = (u32)ci;
-                valid = canonical_bucket(lsrc, tms, tme, P, bucket);       // Long.parseLong
-                if (!valid) tl.terr++;
+                valid = tok;
+                if (!tok) tl.terr++;
             }
         }
         STAMP(3);
@@ -958,8 +984,8 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
 #ifdef YSB_STAMPS
     if (lane == 0) {
         unsigned long long* o = P.dbg + ((u64)blockIdx.x * (SCAN_TPB / 64) + wave) * N_STAMPS;
-        for (int i = 0; i < 6; ++i) o[i] += st_acc[i];
-        o[6] += t_end - t_begin;
+        for (int i = 0; i < 7; ++i) o[i] += st_acc[i];
+        o[7] += t_end - t_begin;
     }
 #endif
     // ---- final flush + stats ---------------------------------------------------------

@@ -34,7 +34,7 @@ class YsbConfig(C.Structure):
 
 class YsbStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("events", "views", "joined", "join_misses", "parse_errors",
-                                          "time_errors", "out_of_ring", "overflow_dropped", "batches")]
+                                          "time_errors", "out_of_ring", "overflow_dropped", "batches", "deferred")]
 
 
 class YsbCount(C.Structure):

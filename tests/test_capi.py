@@ -54,7 +54,7 @@ int main(void) {
   printf("ysb_config %zu\nysb_stats %zu\nysb_count %zu\nysb_gen_params %zu\n", sizeof(ysb_config),
          sizeof(ysb_stats), sizeof(ysb_count), sizeof(ysb_gen_params));
   P(ysb_config, flags) P(ysb_config, overflow_capacity) P(ysb_count, window_ms) P(ysb_count, count)
-  P(ysb_gen_params, ad_subset) P(ysb_gen_params, n_ad_subset) P(ysb_stats, batches)
+  P(ysb_gen_params, ad_subset) P(ysb_gen_params, n_ad_subset) P(ysb_stats, batches) P(ysb_stats, deferred)
   return 0;
 }
 """
@@ -75,6 +75,7 @@ def test_struct_layouts_match_ctypes(tmp_path):
     assert int(got["ysb_count.window_ms"]) == _lib.YsbCount.window_ms.offset
     assert int(got["ysb_gen_params.ad_subset"]) == _lib.YsbGenParams.ad_subset.offset
     assert int(got["ysb_stats.batches"]) == _lib.YsbStats.batches.offset
+    assert int(got["ysb_stats.deferred"]) == _lib.YsbStats.deferred.offset
 
 
 def test_abi_version_and_defaults():

@@ -126,13 +126,15 @@ def test_generated_stream_vs_oracle(rate, skew, ring):
     for k, v in ost.items():
         assert st[k] == v, (k, st[k], v)
     assert st["join_misses"] > 0 and st["overflow_dropped"] == 0
+    assert st["deferred"] == 0          # generator lines all take the fast path
     assert got == rows
 
 
 def test_truth_counts_at_scale():
-    """20M generated events (5 GB): parsed counts == generator truth (no parsing)."""
+    """30M generated events in 15M-event (3.8 GB) batches -- byte offsets past 2^31 --:
+    parsed counts == generator truth (no parsing), and every line on the fast path."""
     g = GenParams(seed=77, events_per_sec=100_000)
-    n, seg = 20_000_000, 10_000_000
+    n, seg = 30_000_000, 15_000_000
     with make_ctx(n_campaigns=100, ads=(g.ids()[1], g.ad_campaign_index())) as ctx:
         cap = seg * g.max_line_bytes()
         d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * seg)
@@ -144,6 +146,7 @@ def test_truth_counts_at_scale():
         mism, truth, ring = ctx.truth_compare()
         st = ctx.stats()
     assert st["events"] == n and st["parse_errors"] == 0 and st["out_of_ring"] == 0
+    assert st["deferred"] == 0
     assert mism == 0 and truth == ring == st["joined"]
 
 

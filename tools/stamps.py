@@ -18,8 +18,8 @@ import numpy as np  # noqa: E402
 from ysb_amd import GenParams, YsbContext  # noqa: E402
 from ysb_amd._lib import lib  # noqa: E402
 
-PHASES = ["A: regs->LDS + classify (incl. prefetch wait)", "barrier after A", "B1: canonical parse + probe issue",
-          "prefetch issue + B2 (probe wait, time)", "count", "end barrier"]
+PHASES = ["A: regs->LDS + classify", "barrier after A", "B1: canonical parse, probe issue, defer",
+          "prefetch issue + B2 (probe wait)", "count", "end barrier", "wait for the prefetched tile"]
 
 
 def main():
@@ -41,9 +41,9 @@ def main():
         buf = np.zeros(cnt.value, dtype=np.uint64)
         L.ysb_debug_stamps(ctx._h, buf.ctypes.data, buf.size, C.byref(cnt))
         w = buf.reshape(-1, 8)
-        w = w[w[:, 6] > 0]
-        tot = w[:, :6].sum(axis=0).astype(float)
-        tiles = w[:, 6].sum()
+        w = w[w[:, 7] > 0]
+        tot = w[:, :7].sum(axis=0).astype(float)
+        tiles = w[:, 7].sum()
         print("rep %d: %d waves, %.0f tiles/wave; cycles per tile per wave:" % (rep, len(w), tiles / len(w)))
         for i, name in enumerate(PHASES):
             print("   %-48s %8.0f  %5.1f%%" % (name, tot[i] / tiles, 100 * tot[i] / tot.sum()))
