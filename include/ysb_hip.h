@@ -49,6 +49,10 @@ extern "C" {
                                    AdvertisingTopologyNative.java:267-272)      */
 #define YSB_F_NO_LDS_COUNT 0x4u /* disable the per-workgroup LDS window counters
                                    (every joined view becomes a global atomic)   */
+#define YSB_F_SPARSE_FAST_JOIN 0x8u /* test hook: leave every other 36-byte key out of
+                                   the fast-path cuckoo table, as a failed cuckoo
+                                   placement would; its misses then take the
+                                   general path (results unchanged)              */
 
 typedef struct ysb_ctx ysb_ctx;
 

@@ -32,9 +32,10 @@ struct ysb_ctx {
     // ad table
     u32* d_table = nullptr;
     u64 table_slots = 0;
-    u32* d_ctable = nullptr;   // canonical-UUID cuckoo table
+    u32* d_ctable = nullptr;   // 36-byte-key cuckoo table
     u64 ctable_slots = 0;
-    u64 cseed = 0;
+    CuckooSeed cseed{};
+    bool ctable_partial = false;
     bool table_loaded = false;
     // counts
     u32 c_pad = 0;                        // campaigns padded to the group size
@@ -295,61 +296,77 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         c->table_slots = slots;
     }
     HIPCHK(c, hipMemcpy(c->d_table, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
-    // canonical-UUID keys also go into the two-choice cuckoo table (load <= 1/4)
-    std::vector<std::pair<std::array<u64, 3>, u32>> canon;
+    // every 36-byte key also goes into the two-choice cuckoo table (load <= 1/4)
+    typedef std::array<u32, CKEY_WORDS> Key36;
+    std::vector<std::pair<Key36, u32>> keys36;
     {
-        std::map<std::array<u64, 3>, size_t> where;
+        std::map<Key36, size_t> where;
         for (u64 i = 0; i < n; ++i) {
             const u32 len = lens ? lens[i] : 36u;
-            u64 k0, k1;
-            u32 k2;
-            if (len != 36 || !uuid_pack_bytes(reinterpret_cast<const u8*>(ad_ids[i]), &k0, &k1, &k2)) continue;
-            const std::array<u64, 3> k{k0, k1, k2};
+            if (len != 36) continue;
+            Key36 k;
+            std::memcpy(k.data(), ad_ids[i], 36);
             auto it = where.find(k);
-            if (it != where.end()) canon[it->second].second = campaign_idx[i];   // later wins
-            else { where[k] = canon.size(); canon.push_back({k, campaign_idx[i]}); }
+            if (it != where.end()) keys36[it->second].second = campaign_idx[i];   // later wins
+            else { where[k] = keys36.size(); keys36.push_back({k, campaign_idx[i]}); }
         }
     }
+    bool partial = false;
+    if (c->cfg.flags & YSB_F_SPARSE_FAST_JOIN) {
+        for (size_t i = 0; 2 * i + 1 < keys36.size(); ++i) keys36[i] = keys36[2 * i + 1];
+        keys36.resize(keys36.size() / 2);
+        partial = true;
+    }
     u64 cslots = 64;
-    while (cslots < 4 * canon.size()) cslots <<= 1;
+    while (cslots < 4 * keys36.size()) cslots <<= 1;
     std::vector<u32> ct;
+    CuckooSeed cs{};
     u64 seed = 0x5EEDC0FFEEULL;
     for (int attempt = 0;; ++attempt) {
         if (attempt == 16) { cslots <<= 1; attempt = 0; }
-        if (cslots > (1ull << 31)) return fail(c, YSB_ERR_CAPACITY, "cuckoo table construction failed");
+        if (cslots > (1ull << 26)) {
+            // No placement found (a key family the hash cannot separate): keep the
+            // table without the keys that did not fit; the scan defers its misses to
+            // the general path, so the join stays exact.
+            cslots = 1ull << 26;
+            partial = true;
+        }
         seed = mix64(seed + (u64)attempt + cslots);
+        cs = cuckoo_seed(seed);
         ct.assign(cslots * CSLOT_WORDS, 0);
-        for (u64 s = 0; s < cslots; ++s) ct[s * CSLOT_WORDS + 5] = EMPTY_SLOT;
+        for (u64 s = 0; s < cslots; ++s) ct[s * CSLOT_WORDS + CSLOT_CAMP] = EMPTY_SLOT;
         const u32 cm = (u32)(cslots - 1);
         bool ok = true;
-        for (const auto& kv : canon) {
-            u64 k0 = kv.first[0], k1 = kv.first[1];
-            u32 k2 = (u32)kv.first[2], camp = kv.second;
+        for (const auto& kv : keys36) {
+            Key36 k = kv.first;
+            u32 camp = kv.second;
             u32 a, b;
-            cuckoo_slots(cuckoo_hash(k0, k1, k2, seed), cm, &a, &b);
+            cuckoo_slots36(k.data(), cs, cm, &a, &b);
             u32 pos = a;
             int kicks = 0;
             while (true) {
                 u32* sl = &ct[(u64)pos * CSLOT_WORDS];
-                if (sl[5] == EMPTY_SLOT) {
-                    sl[0] = (u32)k0; sl[1] = (u32)(k0 >> 32); sl[2] = (u32)k1; sl[3] = (u32)(k1 >> 32);
-                    sl[4] = k2; sl[5] = camp;
+                if (sl[CSLOT_CAMP] == EMPTY_SLOT) {
+                    std::memcpy(sl, k.data(), 36);
+                    sl[CSLOT_CAMP] = camp;
                     break;
                 }
                 // evict the occupant to its other slot
-                const u64 o0 = sl[0] | ((u64)sl[1] << 32), o1 = sl[2] | ((u64)sl[3] << 32);
-                const u32 o2 = sl[4], oc = sl[5];
-                sl[0] = (u32)k0; sl[1] = (u32)(k0 >> 32); sl[2] = (u32)k1; sl[3] = (u32)(k1 >> 32);
-                sl[4] = k2; sl[5] = camp;
-                k0 = o0; k1 = o1; k2 = o2; camp = oc;
+                Key36 ok_;
+                std::memcpy(ok_.data(), sl, 36);
+                const u32 oc = sl[CSLOT_CAMP];
+                std::memcpy(sl, k.data(), 36);
+                sl[CSLOT_CAMP] = camp;
+                k = ok_;
+                camp = oc;
                 u32 oa, ob;
-                cuckoo_slots(cuckoo_hash(k0, k1, k2, seed), cm, &oa, &ob);
+                cuckoo_slots36(k.data(), cs, cm, &oa, &ob);
                 pos = (pos == oa) ? ob : oa;
                 if (++kicks > 500) { ok = false; break; }
             }
-            if (!ok) break;
+            if (!ok && !partial) break;   // partial: the homeless key is simply left out
         }
-        if (ok) break;
+        if (ok || partial) break;
     }
     if (cslots != c->ctable_slots) {
         hipFree(c->d_ctable);
@@ -358,7 +375,8 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         c->ctable_slots = cslots;
     }
     HIPCHK(c, hipMemcpy(c->d_ctable, ct.data(), ct.size() * 4, hipMemcpyHostToDevice));
-    c->cseed = seed;
+    c->cseed = cs;
+    c->ctable_partial = partial;
     c->table_loaded = true;
     return YSB_OK;
 }
@@ -376,6 +394,7 @@ static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u
     p.ctable = c->d_ctable;
     p.ctable_mask = (u32)(c->ctable_slots - 1);
     p.cseed = c->cseed;
+    p.ctable_partial = c->ctable_partial ? 1u : 0u;
     p.n_campaigns = c->cfg.n_campaigns;
     p.counts = c->d_counts;
     p.ring_w = c->cfg.window_ring;

@@ -188,52 +188,59 @@ YSB_HD u32 key_hash(const u32* w, u32 len) {
 }
 
 // ---------------------------------------------------------------------------
-// Canonical-UUID cuckoo table (the join's fast path).  A 36-byte lower-case
-// 8-4-4-4-12 UUID string (what java.util.UUID.toString() and the generator emit)
-// packs losslessly into 144 bits: its 36 characters as nibbles (dashes -> 0), 16 bits
-// per 4-character group, k0 = groups 0-3, k1 = groups 4-7, k2 = group 8.  Map keys
-// in that form go into a two-choice cuckoo table, so a lookup is exactly two slot
-// loads issued together.  Group value: character j of the group in nibble j.
-// Slot words: [k0 lo, k0 hi, k1 lo, k1 hi, k2, campaign, 0, 0].
+// 36-byte-key cuckoo table (the join's fast path).  Every map key of exactly 36
+// bytes (the UUID strings core.clj:31-32 and java.util.UUID.toString() produce, but
+// any 36 bytes) sits in one of its two slots, so a lookup is exactly two slot loads
+// issued together and a raw 9-word compare -- no decoding, no key validation.
+// Slot words: [key bytes 0..35 as 9 little-endian u32, campaign (EMPTY_SLOT = free),
+// 0, 0] = 48 bytes, three 16-byte loads.
+// The slot hash folds the words with per-seed additive salts (the carries make a
+// colliding key family seed-dependent, so a failed build is cured by a new seed),
+// then avalanches: x = XOR rotl(w_k + s_k, R_k), y = SUM (w_k ^ s'_k).
 // ---------------------------------------------------------------------------
-enum : u32 { CSLOT_WORDS = 8 };
+enum : u32 { CSLOT_WORDS = 12, CKEY_WORDS = 9, CSLOT_CAMP = 9 };
 
-YSB_HD bool uuid_pack_bytes(const u8* s, u64* k0, u64* k1, u32* k2) {
-    u32 g[9];
-    for (int i = 0; i < 9; ++i) {
-        u32 v = 0;
-        for (int j = 0; j < 4; ++j) {
-            const int pos = 4 * i + j;
-            const u32 c = s[pos];
-            u32 nib;
-            if (pos == 8 || pos == 13 || pos == 18 || pos == 23) {
-                if (c != '-') return false;
-                nib = 0;
-            } else if (c >= '0' && c <= '9') {
-                nib = c - '0';
-            } else if (c >= 'a' && c <= 'f') {
-                nib = c - 'a' + 10;
-            } else {
-                return false;
-            }
-            v |= nib << (4 * j);   // first character in the low nibble
-        }
-        g[i] = v;
+struct CuckooSeed {
+    u32 s[CKEY_WORDS];   // additive salts of the XOR fold
+    u32 t[CKEY_WORDS];   // XOR salts of the sum fold
+    u32 fa, fb;          // finaliser salts
+};
+
+YSB_HD u32 rotl32(u32 x, u32 r) { return (x << r) | (x >> (32u - r)); }   // 1 <= r <= 31
+YSB_HD u32 fmix32(u32 h) {
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+
+YSB_HD void cuckoo_slots36(const u32* w, const CuckooSeed& cs, u32 mask, u32* a, u32* b) {
+    const u32 R[CKEY_WORDS] = {1, 6, 11, 16, 21, 26, 31, 4, 9};
+    u32 x = 0, y = 0;
+#pragma unroll
+    for (u32 k = 0; k < CKEY_WORDS; ++k) {
+        x ^= rotl32(w[k] + cs.s[k], R[k]);
+        y += w[k] ^ cs.t[k];
     }
-    *k0 = ((u64)g[0] << 48) | ((u64)g[1] << 32) | ((u64)g[2] << 16) | g[3];
-    *k1 = ((u64)g[4] << 48) | ((u64)g[5] << 32) | ((u64)g[6] << 16) | g[7];
-    *k2 = g[8];
-    return true;
+    const u32 ha = fmix32(x ^ cs.fa);
+    const u32 hb = fmix32(y ^ cs.fb ^ rotl32(x, 16));
+    *a = ha & mask;
+    const u32 bb = hb & mask;
+    *b = bb == *a ? ((bb + 1) & mask) : bb;
 }
 
-YSB_HD u64 cuckoo_hash(u64 k0, u64 k1, u32 k2, u64 seed) {
-    return mix64(k0 ^ ((k1 << 21) | (k1 >> 43)) ^ ((u64)k2 << 40) ^ seed);
+#if !defined(__HIP_DEVICE_COMPILE__)
+static inline CuckooSeed cuckoo_seed(u64 seed) {
+    CuckooSeed cs;
+    for (u32 k = 0; k < CKEY_WORDS; ++k) {
+        const u64 r = mix64(seed + 2 * k + 1);
+        cs.s[k] = (u32)r;
+        cs.t[k] = (u32)(r >> 32);
+    }
+    const u64 f = mix64(seed ^ 0xF1F1F1F1F1F1F1F1ULL);
+    cs.fa = (u32)f;
+    cs.fb = (u32)(f >> 32);
+    return cs;
 }
-YSB_HD void cuckoo_slots(u64 h, u32 mask, u32* a, u32* b) {
-    *a = (u32)h & mask;
-    u32 x = (u32)(h >> 32) & mask;
-    *b = x == *a ? ((x + 1) & mask) : x;
-}
+#endif
 
 // ---------------------------------------------------------------------------
 // Exact Java long division t / d (truncating toward zero) for a runtime d >= 1,

@@ -21,9 +21,10 @@ struct ScanParams {
     u64 n;
     const u32* table;           // ad table, SLOT_WORDS u32 per slot (every key)
     u32 table_mask;             // slots - 1
-    const u32* ctable;          // canonical-UUID cuckoo table, CSLOT_WORDS u32 per slot
+    const u32* ctable;          // 36-byte-key cuckoo table, CSLOT_WORDS u32 per slot
     u32 ctable_mask;
-    u64 cseed;
+    u32 ctable_partial;         // 1: some 36-byte key missed the cuckoo build (misses defer)
+    CuckooSeed cseed;
     u32 n_campaigns;
     unsigned long long* counts; // [c_pad][W] u64, campaign-major
     u32 ring_w;                 // W (power of two)

@@ -624,31 +624,6 @@ __device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, const CanonB
     return ok;
 }
 
-// The 36 ad_id bytes (kw[i] = bytes 4i..4i+3) -> the packed canonical key, or false if
-// they are not a lower-case 8-4-4-4-12 UUID (SWAR: 4 characters per operation).
-__device__ __forceinline__ bool pack_uuid_regs(const u32 (&kw)[9], u64& k0, u64& k1, u32& k2) {
-    u32 bad = ((kw[2] & 0xFFu) ^ '-') | (((kw[3] >> 8) & 0xFFu) ^ '-') | (((kw[4] >> 16) & 0xFFu) ^ '-') |
-              ((kw[5] >> 24) ^ '-');
-    u32 g[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        u32 w = kw[k];
-        if (k == 2) w = (w & 0xFFFFFF00u) | 0x30u;         // dashes decode as '0'
-        if (k == 3) w = (w & 0xFFFF00FFu) | 0x3000u;
-        if (k == 4) w = (w & 0xFF00FFFFu) | 0x300000u;
-        if (k == 5) w = (w & 0x00FFFFFFu) | 0x30000000u;
-        const u32 v = (w & 0x0F0F0F0Fu) + ((w >> 6) & 0x01010101u) * 9u;    // nibble per byte
-        const u32 m = (v + 0x76767676u) & 0x80808080u;                      // bytes >= 10
-        bad |= (v & 0x10101010u) | ((v + 0x30303030u + (m >> 7) * 0x27u) ^ w);   // must re-encode to w
-        const u32 x = v | (v >> 4);                                         // n0|n1<<4 in byte 0, n2|n3<<4 in byte 2
-        g[k] = (x & 0xFFu) | ((x >> 8) & 0xFF00u);
-    }
-    k0 = ((u64)g[0] << 48) | ((u64)g[1] << 32) | ((u64)g[2] << 16) | g[3];
-    k1 = ((u64)g[4] << 48) | ((u64)g[5] << 32) | ((u64)g[6] << 16) | g[7];
-    k2 = g[8];
-    return bad == 0u;
-}
-
 // Adds v views to (campaign, bucket): the ring cell if the bucket is live, else the
 // exact side list.
 __device__ __forceinline__ void global_add(const ScanParams& P, i64 ring_lo, bool ring_set,
@@ -758,21 +733,6 @@ __device__ __forceinline__ u32 cand_mask16(const uint4& v) {
            ((cand_flags_hi(v.w) >> 28) << 12);
 }
 
-__device__ __forceinline__ i64 block_max_i64(i64 v, i64* scratch) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const i64 x = __shfl_xor(v, o, 64);
-        v = x > v ? x : v;
-    }
-    if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
-    __syncthreads();
-    i64 r = scratch[0];
-#pragma unroll
-    for (int w = 1; w < SCAN_TPB / 64; ++w) r = scratch[w] > r ? scratch[w] : r;
-    __syncthreads();
-    return r;
-}
-
 __device__ __forceinline__ u32 wave_sum(u32 v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -787,6 +747,34 @@ __device__ __forceinline__ void flush_tally(const ScanParams& P, const Tally& tl
 #pragma unroll
         for (int k = 0; k < 7; ++k)
             if (sums[k]) atomicAdd(&P.stats[slots[k]], (unsigned long long)sums[k]);
+    }
+}
+
+// Appends the flagged lines of the wave to the deferred list (one atomic per wave).
+__device__ __forceinline__ void defer_append(const ScanParams& P, bool dfr, u64 line, int lane) {
+    const unsigned long long m = __ballot(dfr);
+    if (!m) return;
+    u32 base = 0;
+    if (lane == 0) {
+        base = atomicAdd(P.defer_count, (u32)__popcll(m));
+        atomicAdd(&P.stats[ST_DEFERRED], (unsigned long long)__popcll(m));
+    }
+    base = __shfl(base, 0, 64);
+    if (dfr) {
+        const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+        if (base + r < P.defer_cap) P.defer[base + r] = (u32)line;
+    }
+}
+
+// LDS window counters: flush every non-zero cell of the window at lbase to the ring.
+__device__ __forceinline__ void flush_window(const ScanParams& P, u32* lcnt, u32 ncells, u32 WL, i64 lbase,
+                                             i64 ring_lo, bool ring_set, Tally& tl) {
+    for (u32 i = threadIdx.x; i < ncells; i += SCAN_TPB) {
+        const u32 v = lcnt[i];
+        if (v) {
+            lcnt[i] = 0;
+            global_add(P, ring_lo, ring_set, i >> P.lds_wl_log2, lbase + (i64)(i & (WL - 1)), v, tl);
+        }
     }
 }
 
@@ -817,7 +805,7 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
     u32* tb = reinterpret_cast<u32*>(smem + OFF_TB);
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63;
     const u64 t_begin = (u64)blockIdx.x * P.tiles_per_block;
     if (t_begin >= P.n_tiles) return;
     const u64 t_end = min(t_begin + P.tiles_per_block, P.n_tiles);
@@ -827,7 +815,9 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
     const u32 WL = P.lds_wl;
     const u32 ncells = WL ? P.n_campaigns * WL : 0u;
     for (u32 i = tid; i < ncells; i += SCAN_TPB) lcnt[i] = 0;
-    if (tid == 0) { misc64[0] = 0; misc64[1] = 0; }
+    // rebase requests of the LDS window (double-buffered by tile parity): the largest
+    // bucket that fell ahead of the window, INT64_MIN = none
+    if (tid < 2) misc64[tid] = INT64_MIN;
     // tile bounds of this workgroup's run: off[t * 256] for t in [t_begin, t_end], nbytes past the end
     for (u32 i = tid; i <= (u32)(t_end - t_begin); i += SCAN_TPB) {
         const u64 f = (t_begin + i) * SCAN_TPB;
@@ -840,10 +830,12 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
     u32 pre_off = 0, pre_end = 0;
     TileInfo nxt = tile_info(P, t_begin, t_begin, tb);
     issue_tile_loads(P, nxt, pre, pre_off, pre_end);
+    // The LDS window's base, identical in every thread (each applies the same requests).
+    i64 lbase = 0;
+    bool lset = false;
 
     const LdsSrc lsrc{tile32, q32};
     const uint4* ct4 = reinterpret_cast<const uint4*>(P.ctable);
-    const uint2* ct2 = reinterpret_cast<const uint2*>(P.ctable);
     STAMP_DECL
     for (u64 t = t_begin; t < t_end; ++t) {
         const TileInfo cur = nxt;
@@ -866,34 +858,44 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
                 }
             }
         }
+        // The previous tile asked to move the LDS window: flush it (its counts are all
+        // in, the end barrier saw to that) and re-centre, before this tile counts.
+        const int par = (int)(t & 1);
+        if (WL) {
+            const i64 req = misc64[par ^ 1];
+            if (req != INT64_MIN) {
+                if (lset) flush_window(P, lcnt, ncells, WL, lbase, ring_lo, ring_set, tl);
+                lbase = req - (i64)(WL / 2) + 1;
+                lset = true;
+            }
+        }
         STAMP(0);
         __syncthreads();
+        if (tid == 0) misc64[par ^ 1] = INT64_MIN;   // every thread has read it
         STAMP(1);
         // ---- Phase B1: canonical parse from LDS; any other line is deferred -------
         bool ok1 = false;
         int ls = 0, le = 0;
         CanonA ca;
-        u64 k0 = 0, k1 = 0;
-        u32 k2 = 0;
-        bool packed = false;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) ca.kw[k] = 0u;
         if ((u32)tid < cur.count && !cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             ok1 = canon_stage1(lsrc, ls, le, ca);
-            if (ok1) packed = pack_uuid_regs(ca.kw, k0, k1, k2);   // speculative: views only need it
         }
-        // RedisJoinBolt's lookup (canonical keys): both cuckoo slots, issued now so their
-        // latency hides under the second LDS batch, and before the next tile's prefetch so
-        // waiting for them never waits for it.
+        // RedisJoinBolt's lookup (36-byte keys): both cuckoo slots, issued now so their
+        // latency hides under the second LDS batch, and before the next tile's prefetch
+        // so waiting for them never waits for it.  Speculative: only views use them.
         u32 ia, ib;
-        cuckoo_slots(cuckoo_hash(k0, k1, k2, P.cseed), P.ctable_mask, &ia, &ib);
-        const uint4 sa = ct4[2 * (u64)ia], sb = ct4[2 * (u64)ib];
-        const uint2 ta = ct2[4 * (u64)ia + 2], tb2 = ct2[4 * (u64)ib + 2];
+        cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
+        const uint4 a0 = ct4[3 * (u64)ia], a1 = ct4[3 * (u64)ia + 1], a2 = ct4[3 * (u64)ia + 2];
+        const uint4 b0 = ct4[3 * (u64)ib], b1 = ct4[3 * (u64)ib + 1], b2 = ct4[3 * (u64)ib + 2];
         bool pend = false, dfr = false, tok = false;
         i64 bucket = 0;
         if ((u32)tid < cur.count) {
             CanonB cb;
-            if (ok1 && canon_stage2(lsrc, ls, le, ca, cb) && (packed || !cb.view)) {
+            if (ok1 && canon_stage2(lsrc, ls, le, ca, cb)) {
                 tl.ev++;
                 if (cb.view) {                                             // EventFilterBolt
                     tl.view++;
@@ -901,25 +903,10 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
                     tok = canonical_bucket(lsrc, cb, ls + ca.e4 + 18, P, bucket);   // Long.parseLong
                 }
             } else {
-                dfr = true;   // bad offsets, other layouts, escapes, non-canonical ad ids, over-size tiles
+                dfr = true;   // bad offsets, other layouts, escapes, over-size tiles
             }
         }
-        // deferred lines -> list for defer_kernel (one atomic per wave)
-        {
-            const unsigned long long m = __ballot(dfr);
-            if (m) {
-                u32 base = 0;
-                if (lane == 0) {
-                    base = atomicAdd(P.defer_count, (u32)__popcll(m));
-                    atomicAdd(&P.stats[ST_DEFERRED], (unsigned long long)__popcll(m));
-                }
-                base = __shfl(base, 0, 64);
-                if (dfr) {
-                    const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
-                    if (base + r < P.defer_cap) P.defer[base + r] = (u32)(cur.first + tid);
-                }
-            }
-        }
+        defer_append(P, dfr, cur.first + tid, lane);
         STAMP(2);
         // ---- prefetch the next tile (lands while this one is parsed) -----------
         // Issued on every iteration (the last one loads nothing: out-of-range buffer
@@ -929,50 +916,42 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
         else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
         issue_tile_loads(P, nxt, pre, pre_off, pre_end);
         // ---- Phase B2: join result ------------------------------------------------
-        bool valid = false;
+        bool valid = false, dfr2 = false;
         u32 campaign = 0;
         if (pend) {
-            const u32 klo0 = (u32)k0, khi0 = (u32)(k0 >> 32), klo1 = (u32)k1, khi1 = (u32)(k1 >> 32);
-            int ci = -1;
-            if (sa.x == klo0 && sa.y == khi0 && sa.z == klo1 && sa.w == khi1 && ta.x == k2 && ta.y != EMPTY_SLOT)
-                ci = (int)ta.y;
-            else if (sb.x == klo0 && sb.y == khi0 && sb.z == klo1 && sb.w == khi1 && tb2.x == k2 && tb2.y != EMPTY_SLOT)
-                ci = (int)tb2.y;
-            if (ci < 0) {
-                tl.miss++;                                                  // drop (:465-467)
+            const u32* k = ca.kw;
+            const u32 da = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
+                           (a1.y ^ k[5]) | (a1.z ^ k[6]) | (a1.w ^ k[7]) | (a2.x ^ k[8]);
+            const u32 db = (b0.x ^ k[0]) | (b0.y ^ k[1]) | (b0.z ^ k[2]) | (b0.w ^ k[3]) | (b1.x ^ k[4]) |
+                           (b1.y ^ k[5]) | (b1.z ^ k[6]) | (b1.w ^ k[7]) | (b2.x ^ k[8]);
+            const u32 ci = (da == 0u && a2.y != EMPTY_SLOT) ? a2.y : (db == 0u ? b2.y : EMPTY_SLOT);
+            if (ci == EMPTY_SLOT) {
+                if (P.ctable_partial) {   // the key may be one the cuckoo build left out
+                    dfr2 = true;
+                    tl.ev--;
+                    tl.view--;
+                } else {
+                    tl.miss++;                                              // drop (:465-467)
+                }
             } else {
                 tl.join++;
-                campaign = (u32)ci;
+                campaign = ci;
                 valid = tok;
                 if (!tok) tl.terr++;
             }
         }
+        if (P.ctable_partial) defer_append(P, dfr2, cur.first + tid, lane);
         STAMP(3);
-        // ---- count: LDS window counters, flushed when the window moves ----------
+        // ---- count: LDS window counters; events outside go straight to the ring -----
         if (WL) {
-            i64 lbase = misc64[0];
-            const bool lset = misc64[1] != 0;
-            const bool ahead = valid && (!lset || bucket >= lbase + (i64)WL);
-            if (__syncthreads_or(ahead)) {
-                const i64 mx = block_max_i64(valid ? bucket : INT64_MIN, misc64 + 2);
-                if (lset) {
-                    for (u32 i = tid; i < ncells; i += SCAN_TPB) {
-                        const u32 v = lcnt[i];
-                        if (v) {
-                            lcnt[i] = 0;
-                            global_add(P, ring_lo, ring_set, i >> P.lds_wl_log2,
-                                       lbase + (i64)(i & (WL - 1)), v, tl);
-                        }
-                    }
-                }
-                lbase = mx - (i64)(WL / 2) + 1;
-                __syncthreads();
-                if (tid == 0) { misc64[0] = lbase; misc64[1] = 1; }
-            }
             if (valid) {
                 const i64 rel = bucket - lbase;
-                if (rel >= 0 && rel < (i64)WL) atomicAdd(&lcnt[(campaign << P.lds_wl_log2) + (u32)rel], 1u);
-                else global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+                if (lset && rel >= 0 && rel < (i64)WL) {
+                    atomicAdd(&lcnt[(campaign << P.lds_wl_log2) + (u32)rel], 1u);
+                } else {
+                    global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+                    if (!lset || rel >= (i64)WL) atomicMax(reinterpret_cast<long long*>(&misc64[par]), (long long)bucket);
+                }
             }
         } else if (valid) {
             global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
@@ -983,19 +962,13 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
     }
 #ifdef YSB_STAMPS
     if (lane == 0) {
-        unsigned long long* o = P.dbg + ((u64)blockIdx.x * (SCAN_TPB / 64) + wave) * N_STAMPS;
+        unsigned long long* o = P.dbg + ((u64)blockIdx.x * (SCAN_TPB / 64) + (threadIdx.x >> 6)) * N_STAMPS;
         for (int i = 0; i < 7; ++i) o[i] += st_acc[i];
         o[7] += t_end - t_begin;
     }
 #endif
     // ---- final flush + stats ---------------------------------------------------------
-    if (WL && misc64[1]) {
-        const i64 lbase = misc64[0];
-        for (u32 i = tid; i < ncells; i += SCAN_TPB) {
-            const u32 v = lcnt[i];
-            if (v) global_add(P, ring_lo, ring_set, i >> P.lds_wl_log2, lbase + (i64)(i & (WL - 1)), v, tl);
-        }
-    }
+    if (WL && lset) flush_window(P, lcnt, ncells, WL, lbase, ring_lo, ring_set, tl);
     flush_tally(P, tl, lane);
 }
 

@@ -21,6 +21,7 @@ ERRORS = {-1: "YSB_ERR_ARG", -2: "YSB_ERR_HIP", -3: "YSB_ERR_STATE", -4: "YSB_ER
 YSB_F_TIMING = 0x1
 YSB_F_REQUIRE_IP = 0x2
 YSB_F_NO_LDS_COUNT = 0x4
+YSB_F_SPARSE_FAST_JOIN = 0x8
 INT64_MIN = -(1 << 63)
 UNIQUE_ID_BYTES = 128
 

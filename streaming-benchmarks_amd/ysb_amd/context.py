@@ -23,7 +23,8 @@ def _ptr(a):
 class YsbContext:
     def __init__(self, device=0, n_campaigns=100, time_divisor_ms=10000, window_ring=1024,
                  max_batch_events=1 << 20, max_batch_bytes=256 << 20, ring_base_bucket=None,
-                 overflow_capacity=1 << 20, timing=False, require_ip=False, lds_count=True):
+                 overflow_capacity=1 << 20, timing=False, require_ip=False, lds_count=True,
+                 sparse_fast_join=False):
         L = lib()
         cfg = YsbConfig()
         L.ysb_config_default(C.byref(cfg))
@@ -35,7 +36,8 @@ class YsbContext:
         cfg.ring_base_bucket = INT64_MIN if ring_base_bucket is None else ring_base_bucket
         cfg.overflow_capacity = overflow_capacity
         cfg.flags = ((_lib.YSB_F_TIMING if timing else 0) | (_lib.YSB_F_REQUIRE_IP if require_ip else 0)
-                     | (0 if lds_count else _lib.YSB_F_NO_LDS_COUNT))
+                     | (0 if lds_count else _lib.YSB_F_NO_LDS_COUNT)
+                     | (_lib.YSB_F_SPARSE_FAST_JOIN if sparse_fast_join else 0))
         h = C.c_void_p()
         check(L.ysb_open(C.byref(h), device, C.byref(cfg)), None)
         self._h = h

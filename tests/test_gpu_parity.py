@@ -130,6 +130,38 @@ def test_generated_stream_vs_oracle(rate, skew, ring):
     assert got == rows
 
 
+def test_sparse_fast_join_defers_misses_exactly():
+    """Half the 36-byte keys left out of the fast-path cuckoo table (as a failed
+    placement would): their views take the general path, counts unchanged."""
+    g = GenParams(seed=99, events_per_sec=1000, with_skew=True)
+    cids, aids = g.ids()
+    camp = g.ad_campaign_index()
+    n = 500_000
+    with make_ctx(n_campaigns=100, ads=(aids[:900], camp[:900]), sparse_fast_join=True,
+                  max_batch_bytes=1 << 28) as ctx:
+        cap = n * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n)
+        nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+        ctx.submit_device(d_b, nb, d_o, n)
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+        data = ctx.d2h(np.empty(nb, dtype=np.uint8), d_b)
+        off = ctx.d2h(np.empty(n, dtype=np.uint32), d_o)
+    rows, ost = oracle.run(oracle.AdMap(aids[:900], camp[:900]), data, off, threads=8)
+    for k, v in ost.items():
+        assert st[k] == v, (k, st[k], v)
+    assert st["deferred"] > 0 and st["join_misses"] > 0
+    assert got == rows
+
+
+@pytest.mark.parametrize("stem,require_ip", gd.FIXTURES)
+def test_fixture_sparse_fast_join(stem, require_ip):
+    with make_ctx(require_ip=require_ip, sparse_fast_join=True) as ctx:
+        raw, offs = gd.events(stem)
+        ctx.submit(raw, offs, slot=0)
+        check_against(ctx, *gd.expected(stem, require_ip))
+
+
 def test_truth_counts_at_scale():
     """30M generated events in 15M-event (3.8 GB) batches -- byte offsets past 2^31 --:
     parsed counts == generator truth (no parsing), and every line on the fast path."""
