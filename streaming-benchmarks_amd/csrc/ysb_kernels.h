@@ -7,12 +7,17 @@
 namespace ysb {
 
 // Geometry of the fused scan kernel (see DESIGN.md "Kernel 1").
-constexpr int SCAN_TPB = 256;                 // threads per workgroup = lines per tile
-constexpr int TILE_CAP = 66560;               // LDS bytes of one tile (260 B/line average)
+// One wave per workgroup: no intra-workgroup barrier ever waits for a slower wave,
+// and the two waves of a SIMD drift into different phases (one classifying while the
+// other parses), which hides each other's LDS latency.
+constexpr int SCAN_TPB = 64;                  // threads per scan workgroup = lines per tile
+constexpr int SCAN_WG_PER_CU = 8;             // resident scan workgroups per CU (LDS-bound)
+constexpr int TILE_CAP = SCAN_TPB * 260;      // LDS bytes of one tile (260 B/line average)
 constexpr int TILE_CHUNKS = TILE_CAP / 16;    // 16-byte chunks per tile
 constexpr int CHUNKS_PER_THREAD = (TILE_CHUNKS + SCAN_TPB - 1) / SCAN_TPB;  // 17
-constexpr int LCNT_CAP = 1024;                // u32 per-workgroup (campaign, window) counters
+constexpr int LCNT_CAP = 256;                 // u32 per-workgroup (campaign, window) counters
 constexpr int MAX_TILES_PER_BLOCK = 128;      // tile bounds preloaded into LDS
+constexpr int AUX_TPB = 256;                  // threads per workgroup of the other kernels
 
 struct ScanParams {
     const u8* bytes;            // batch bytes (16-byte aligned)

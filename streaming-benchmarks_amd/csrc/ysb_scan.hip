@@ -657,7 +657,7 @@ constexpr int OFF_TB = OFF_MISC + 64;
 constexpr int LDS_BYTES = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
 static_assert(OFF_QBITS % 16 == 0 && OFF_LCNT % 16 == 0 &&
               OFF_MISC % 16 == 0 && OFF_TB % 16 == 0, "LDS carve must stay 16-byte aligned");
-static_assert(LDS_BYTES <= 81920, "two workgroups per CU need <= 80 KiB of LDS each");
+static_assert(LDS_BYTES <= 163840 / SCAN_WG_PER_CU, "SCAN_WG_PER_CU workgroups must fit one CU's 160 KiB of LDS");
 
 struct TileInfo {
     u64 first;
@@ -795,7 +795,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #define STAMP(i) do { } while (0)
 #endif
 
-__global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
+__global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(ScanParams P) {
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
     u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
     u16* q16 = reinterpret_cast<u16*>(smem + OFF_QBITS);
@@ -976,13 +976,13 @@ __global__ __launch_bounds__(SCAN_TPB, 2) void scan_kernel(ScanParams P) {
 // escapes, non-canonical ad ids, over-size tiles, bad offsets) through the general
 // strict JSON tokenizer, straight from HBM.  Rare on generator data; exact always.
 // The last workgroup to finish resets the list for the next batch.
-__global__ __launch_bounds__(SCAN_TPB) void defer_kernel(ScanParams P) {
+__global__ __launch_bounds__(AUX_TPB) void defer_kernel(ScanParams P) {
     const int tid = threadIdx.x, lane = tid & 63;
     const u32 cnt = min(*P.defer_count, P.defer_cap);
     const i64 ring_lo = P.ring[0];
     const bool ring_set = P.ring[1] != 0;
     Tally tl{0, 0, 0, 0, 0, 0, 0};
-    for (u32 i = blockIdx.x * SCAN_TPB + tid; i < cnt; i += gridDim.x * SCAN_TPB) {
+    for (u32 i = blockIdx.x * AUX_TPB + tid; i < cnt; i += gridDim.x * AUX_TPB) {
         const u64 li = P.defer[i];
         const u64 ls = P.off[li];
         const u64 le = li + 1 < P.n ? (u64)P.off[li + 1] : P.nbytes;
@@ -1011,8 +1011,8 @@ __global__ __launch_bounds__(SCAN_TPB) void defer_kernel(ScanParams P) {
 
 // Ring auto-base: the first joined view with a valid time among the first 256 lines
 // fixes the ring at min bucket - W/8 (room for out-of-order / late events).
-__global__ __launch_bounds__(SCAN_TPB) void ring_autobase_kernel(ScanParams P, i64* ring) {
-    __shared__ i64 scratch[SCAN_TPB / 64];
+__global__ __launch_bounds__(AUX_TPB) void ring_autobase_kernel(ScanParams P, i64* ring) {
+    __shared__ i64 scratch[AUX_TPB / 64];
     if (ring[1] != 0) return;
     const int tid = threadIdx.x;
     i64 b = INT64_MAX;
@@ -1036,7 +1036,7 @@ __global__ __launch_bounds__(SCAN_TPB) void ring_autobase_kernel(ScanParams P, i
     __syncthreads();
     if (tid == 0) {
         i64 r = scratch[0];
-        for (int w = 1; w < SCAN_TPB / 64; ++w) r = scratch[w] < r ? scratch[w] : r;
+        for (int w = 1; w < AUX_TPB / 64; ++w) r = scratch[w] < r ? scratch[w] : r;
         if (r != INT64_MAX) {
             ring[0] = r - (i64)(P.ring_w / 8);
             ring[1] = 1;
@@ -1052,12 +1052,12 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
 
 void launch_defer(const ScanParams& p, int blocks, hipStream_t s) {
     if (p.n == 0) return;
-    hipLaunchKernelGGL(defer_kernel, dim3(blocks), dim3(SCAN_TPB), 0, s, p);
+    hipLaunchKernelGGL(defer_kernel, dim3(blocks), dim3(AUX_TPB), 0, s, p);
 }
 
 void launch_ring_autobase(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
-    hipLaunchKernelGGL(ring_autobase_kernel, dim3(1), dim3(SCAN_TPB), 0, s, p, const_cast<i64*>(p.ring));
+    hipLaunchKernelGGL(ring_autobase_kernel, dim3(1), dim3(AUX_TPB), 0, s, p, const_cast<i64*>(p.ring));
 }
 
 int scan_lds_bytes() { return LDS_BYTES; }

@@ -13,7 +13,7 @@ case "$1" in
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.json" ;;
   pmc)
     name=$2; shift 2
-    timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/pmc_$name" -o run -- python3 $BENCH > "$OUT/pmc_$name.json" ;;
+    timeout -k 10 150 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/pmc_$name" -o run -- python3 $BENCH > "$OUT/pmc_$name.json" ;;
   list)
     timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 ;;
 esac
