@@ -884,26 +884,32 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
             le = (int)(my_end - cur.s0 + cur.delta);
             ok1 = canon_stage1(lsrc, ls, le, ca);
         }
-        // RedisJoinBolt's lookup (36-byte keys): both cuckoo slots, issued now so their
-        // latency hides under the second LDS batch, and before the next tile's prefetch
-        // so waiting for them never waits for it.  Speculative: only views use them.
-        u32 ia, ib;
-        cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
-        const uint4 a0 = ct4[3 * (u64)ia], a1 = ct4[3 * (u64)ia + 1], a2 = ct4[3 * (u64)ia + 2];
-        const uint4 b0 = ct4[3 * (u64)ib], b1 = ct4[3 * (u64)ib + 1], b2 = ct4[3 * (u64)ib + 2];
         bool pend = false, dfr = false, tok = false;
         i64 bucket = 0;
+        CanonB cb;
+        cb.view = false;
+        bool ok2 = false;
         if ((u32)tid < cur.count) {
-            CanonB cb;
-            if (ok1 && canon_stage2(lsrc, ls, le, ca, cb)) {
-                tl.ev++;
-                if (cb.view) {                                             // EventFilterBolt
-                    tl.view++;
-                    pend = true;
-                    tok = canonical_bucket(lsrc, cb, ls + ca.e4 + 18, P, bucket);   // Long.parseLong
-                }
-            } else {
-                dfr = true;   // bad offsets, other layouts, escapes, over-size tiles
+            ok2 = ok1 && canon_stage2(lsrc, ls, le, ca, cb);
+            dfr = !ok2;   // bad offsets, other layouts, escapes, over-size tiles
+        }
+        pend = ok2 && cb.view;                                             // EventFilterBolt
+        // RedisJoinBolt's lookup (36-byte keys): both cuckoo slots, views only (a third
+        // of the lanes: scattered loads cost address-unit time per lane), issued before
+        // the time parse and the next tile's prefetch so their latency hides under both
+        // and waiting for them never waits for the prefetch.
+        uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, a2 = a0, b0 = a0, b1 = a0, b2 = a0;
+        if (pend) {
+            u32 ia, ib;
+            cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
+            a0 = ct4[3 * (u64)ia]; a1 = ct4[3 * (u64)ia + 1]; a2 = ct4[3 * (u64)ia + 2];
+            b0 = ct4[3 * (u64)ib]; b1 = ct4[3 * (u64)ib + 1]; b2 = ct4[3 * (u64)ib + 2];
+        }
+        if (ok2) {
+            tl.ev++;
+            if (pend) {
+                tl.view++;
+                tok = canonical_bucket(lsrc, cb, ls + ca.e4 + 18, P, bucket);   // Long.parseLong
             }
         }
         defer_append(P, dfr, cur.first + tid, lane);
