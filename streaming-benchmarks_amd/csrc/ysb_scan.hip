@@ -691,6 +691,10 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_
     return ti;
 }
 
+// Cache policy of the once-read batch stream: nontemporal (aux 2), so it does not
+// displace the join table from L2 (MI355X_MICROARCH.md, row nt-weights).
+constexpr int AUX_NT = 2;
+
 // The next tile's bytes and line offsets, HBM -> registers.  Bounds-checked buffer
 // loads through per-tile descriptors (base = the tile, num_records = its length, so
 // chunks past the tile read zeros and never fault); per-lane offsets are
@@ -707,7 +711,7 @@ __device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const Tile
         __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(tbase), 0, (int)((ti.len + 15u) & ~15u), 0x00020000);
 #pragma unroll
     for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, 16 * (j * SCAN_TPB + tid), 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, 16 * (j * SCAN_TPB + tid), 0, AUX_NT);
         pre[j] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     const u64 left = P.n - min(ti.first, P.n);
