@@ -42,28 +42,10 @@ constexpr u32 VIEW_W = w4('v', 'i', 'e', 'w');
 // ---------------------------------------------------------------------------
 struct LdsSrc {
     const u32* d;   // tile bytes as dwords
-    const u32* q;   // quote-candidate bitmap (bit per byte)
     __device__ __forceinline__ u32 b(int p) const { return (d[p >> 2] >> ((p & 3) << 3)) & 0xFFu; }
     __device__ __forceinline__ u32 load4(int p) const {
         const u32 lo = d[p >> 2], hi = d[(p >> 2) + 1];
         return __builtin_amdgcn_alignbyte(hi, lo, (u32)(p & 3));
-    }
-    // First '"' at or after p (before e), or -1.  Valid only for lines without a
-    // backslash: then every quote ends or starts a string.
-    __device__ __forceinline__ int next_quote(int p, int e) const {
-        while (p < e) {
-            const int wi = p >> 5;
-            const u32 w = q[wi] >> (p & 31);
-            if (w) {
-                const int k = p + (int)__builtin_ctz(w);
-                if (k >= e) return -1;
-                if (b(k) == '"') return k;     // candidates may be false positives
-                p = k + 1;
-            } else {
-                p = (wi + 1) << 5;
-            }
-        }
-        return -1;
     }
 };
 
@@ -101,11 +83,9 @@ __device__ __forceinline__ int skip_ws(const S& src, int p, int e) {
 // Index of the closing quote of a string whose content starts at p, or -1.
 // Escapes follow RFC 8259 (\" \\ \/ \b \f \n \r \t \uXXXX); esc is set when any
 // escape occurs.  Raw control characters are accepted (documented in DESIGN.md).
-template <bool FAST, class S>
+template <class S>
 __device__ __forceinline__ int scan_str(const S& src, int p, int e, int& esc) {
-    if constexpr (FAST) {
-        return src.next_quote(p, e);
-    } else {
+    {
         while (p < e) {
             const u32 c = src.b(p);
             if (c == '"') return p;
@@ -234,7 +214,7 @@ __device__ __noinline__ int skip_value(const S& src, int p, int e) {
             c = src.b(p);
             if (c == '"') {
                 int esc = 0;
-                const int q = scan_str<false>(src, p + 1, e, esc);
+                const int q = scan_str(src, p + 1, e, esc);
                 if (q < 0) return -1;
                 p = q + 1;
                 continue;
@@ -252,7 +232,7 @@ __device__ __noinline__ int skip_value(const S& src, int p, int e) {
 // JSONObject(String) or getString(key) would throw (AdvertisingTopologyNative.java:263-272):
 // malformed JSON, a duplicate key among the recognised ones, a required key missing
 // or not a string.
-template <bool FAST, class S>
+template <class S>
 __device__ __forceinline__ bool parse_line(const S& src, int s, int e, u32 require,
                                            Span& ad, Span& et, Span& tm) {
     int p = skip_ws(src, s, e);
@@ -265,7 +245,7 @@ __device__ __forceinline__ bool parse_line(const S& src, int s, int e, u32 requi
         while (true) {
             if (p >= e || src.b(p) != '"') return false;
             int kesc = 0;
-            const int ke = scan_str<FAST>(src, p + 1, e, kesc);
+            const int ke = scan_str(src, p + 1, e, kesc);
             if (ke < 0) return false;
             const u32 kid = kesc ? match_key_esc(src, p + 1, ke) : match_key_raw(src, p + 1, ke - p - 1);
             p = ke + 1;
@@ -280,7 +260,7 @@ __device__ __forceinline__ bool parse_line(const S& src, int s, int e, u32 requi
             }
             if (src.b(p) == '"') {
                 int vesc = 0;
-                const int ve = scan_str<FAST>(src, p + 1, e, vesc);
+                const int ve = scan_str(src, p + 1, e, vesc);
                 if (ve < 0) return false;
                 if (kid) {
                     if (seen & kid) return false;   // org.json: "Duplicate key"
@@ -463,63 +443,96 @@ __device__ __forceinline__ bool parse_digits_regs(const u32 (&w)[5], int len, i6
 // ---------------------------------------------------------------------------
 // Fast path: the generator's layout (core.clj:90-96) -- the seven keys in order,
 // ": " and ", " separators, string values without quotes or backslashes, the
-// three UUID values 36 bytes long.  Verified against the quote-candidate bitmap
-// (every quote at its template position, none inside a value) and byte compares of
-// every structural segment, which makes it exactly the JSON parse of such a line;
-// any other line returns false and takes the general tokenizer.  Costs ~3
-// dependent LDS round trips per line instead of one per token.
+// three UUID values 36 bytes long.  Every structural byte is compared, every value
+// byte is shown free of '"' and '\\', and the variable tail's quotes are located
+// exactly, which makes it exactly the JSON parse of such a line; any other line
+// returns false and takes the general tokenizer.  Two dependent LDS batches per line.
 // ---------------------------------------------------------------------------
+
+// Per byte, bit 7 set if the byte may be '"' or '\\' (SWAR has-zero of w ^ '"' and
+// w ^ '\\').  Superset: a byte just above a true hit can be flagged falsely, never
+// missed, and every candidate the parser relies on is verified by a compare.
+__device__ __forceinline__ u32 cand_z(u32 w) {
+    const u32 tq = w ^ 0x22222222u, tb = w ^ 0x5C5C5C5Cu;
+    return (((tq - 0x01010101u) & ~tq) | ((tb - 0x01010101u) & ~tb)) & 0x80808080u;
+}
+// The same flags packed to bits 0..3 (bit i = byte i), via the full-rate 24-bit
+// multiply (bits 7/15/23 -> 28/29/30) plus bit 31.
+__device__ __forceinline__ u32 cand_nib(u32 w) {
+    const u32 z = cand_z(w);
+    return (__umul24(z, 0x00204081u) | (z & 0x80000000u)) >> 28;
+}
+
+// The line's first 164 bytes: structural bytes (compared) and the three UUID values
+// (scanned for candidates), as 41 little-endian words.
+constexpr int PREFIX_WORDS = 41;
+constexpr int TAIL_WORDS = 28;                  // raw dwords scanned for the tail's quotes
+constexpr int MAX_CANON_LEN = 164 + 4 * TAIL_WORDS - 3;   // 273: longest line the fast path takes
+struct PrefixTpl {
+    u32 e[PREFIX_WORDS];   // expected structural bytes
+    u32 m[PREFIX_WORDS];   // 0xFF per structural byte
+    u32 v[PREFIX_WORDS];   // 0x80 per value byte
+};
+constexpr PrefixTpl make_prefix_tpl() {
+    PrefixTpl t{};
+    const char* parts[4] = {YSB_P0, YSB_P1, YSB_P2, YSB_P3};
+    int pos = 0;
+    for (int k = 0; k < 4; ++k) {
+        for (const char* q = parts[k]; *q; ++q, ++pos) {
+            t.e[pos >> 2] |= (u32)(u8)*q << (8 * (pos & 3));
+            t.m[pos >> 2] |= 0xFFu << (8 * (pos & 3));
+        }
+        if (k < 3)
+            for (int j = 0; j < 36; ++j, ++pos) t.v[pos >> 2] |= 0x80u << (8 * (pos & 3));
+    }
+    return t;
+}
+
 struct CanonA {   // after the first LDS batch
     u32 kw[9];     // ad_id bytes 113..148
     int e3, e4, e5, e6;   // closing quotes of ad_type, event_type, event_time, ip_address
 };
 
-// Stage 1: one batch of independent LDS reads (quote bitmap, backslash flags, the
-// fixed-offset structure and the ad_id), then register-only checks and the tail's
-// quote positions.  False = not the generator's layout (deferred to the general path).
+// Stage 1: one batch of independent LDS reads -- the line's first 276 bytes as raw
+// dwords -- then register-only checks: the prefix template, the UUID values free of
+// candidates, and the tail's quote positions from a candidate bitmap of the raw tail
+// dwords.  False = not the generator's layout (deferred to the general path).
 __device__ __forceinline__ bool canon_stage1(const LdsSrc& src, int s, int e, CanonA& c) {
+    constexpr PrefixTpl T = make_prefix_tpl();
+    static_assert(T.e[0] == ('{' | ('"' << 8) | ('u' << 16) | ('s' << 24)), "prefix template");
     const int L = e - s;
-    if (L < 220 || L > 300) return false;
-    // line-relative candidate bitmap ('"' or '\\'), bytes 0..319
-    u32 W[11];
-    const int wb = s >> 5;
+    if (L < 220 || L > MAX_CANON_LEN) return false;
+    const int a = s >> 2;
+    const u32 sb = (u32)(s & 3);
+    u32 P[PREFIX_WORDS + 1];
 #pragma unroll
-    for (int k = 0; k < 11; ++k) W[k] = src.q[wb + k];
-    // fixed structural bytes (line-relative): [0,13) [49,64) and [100,164) (ad_id value inside)
-    u32 s0[4], s1[4], s23[16];
-    load_span(src, s + 0, s0);
-    load_span(src, s + 49, s1);
-    load_span(src, s + 100, s23);
-    const u32 sh = (u32)(s & 31);
-    u32 R[10];
+    for (int k = 0; k <= PREFIX_WORDS; ++k) P[k] = src.d[a + k];
+    u32 R[TAIL_WORDS];   // raw dwords from line offset 164 - sb (4-byte aligned)
 #pragma unroll
-    for (int k = 0; k < 10; ++k) R[k] = __builtin_amdgcn_alignbit(W[k + 1], W[k], sh);
-    // Every check XOR-accumulates into d (one VALU op each, no mask logic); d == 0 <=> all hold.
-    // quotes at 1, 9, 12, 49, 52, 60, 63, 100, 103, 109, 112, 149, 152, 160, 163 and nowhere else below 164
-    u32 d = (R[0] ^ 0x00001202u) | (R[1] ^ 0x90120000u) | R[2] | (R[3] ^ 0x00012090u) | (R[4] ^ 0x01200000u) |
-            ((R[5] & 0xFu) ^ 0x9u);
-    // A backslash anywhere breaks this template (the bitmap flags it like a quote):
-    // every byte of an accepted line is either compared below or inside a value span
-    // shown free of candidates, so escapes always take the general path.
-    d |= (s0[0] ^ w4('{', '"', 'u', 's')) | (s0[1] ^ w4('e', 'r', '_', 'i')) | (s0[2] ^ w4('d', '"', ':', ' ')) |
-         ((s0[3] & 0xFFu) ^ '"');
-    d |= (s1[0] ^ w4('"', ',', ' ', '"')) | (s1[1] ^ w4('p', 'a', 'g', 'e')) | (s1[2] ^ w4('_', 'i', 'd', '"')) |
-         ((s1[3] & 0xFFFFFFu) ^ w4(':', ' ', '"', 0));
-    // bytes 100..112: ", "ad_id": "   then the 36-byte value   then 149..163: ", "ad_type": "
-    d |= (s23[0] ^ w4('"', ',', ' ', '"')) | (s23[1] ^ w4('a', 'd', '_', 'i')) | (s23[2] ^ w4('d', '"', ':', ' ')) |
-         ((s23[3] & 0xFFu) ^ '"');
+    for (int k = 0; k < TAIL_WORDS; ++k) R[k] = k == 0 ? P[PREFIX_WORDS] : src.d[a + PREFIX_WORDS + k];
+    // prefix: XOR-accumulated compares and candidate flags; d == 0 <=> all hold
+    u32 d = 0, W[PREFIX_WORDS];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(s23[k + 4], s23[k + 3], 1u);   // bytes 113..148
-    d |= (__builtin_amdgcn_alignbyte(s23[13], s23[12], 1u) ^ w4('"', ',', ' ', '"')) |     // bytes 149..152
-         (__builtin_amdgcn_alignbyte(s23[14], s23[13], 1u) ^ w4('a', 'd', '_', 't')) |     // 153..156
-         (__builtin_amdgcn_alignbyte(s23[15], s23[14], 1u) ^ w4('y', 'p', 'e', '"')) |     // 157..160
-         ((s23[15] >> 8) ^ w4(':', ' ', '"', 0));                                           // 161..163
-    // variable tail: first quote candidate at or after p (160 <= p < 320), via a 64-bit window
+    for (int j = 0; j < PREFIX_WORDS; ++j) {
+        W[j] = __builtin_amdgcn_alignbyte(P[j + 1], P[j], sb);   // line bytes 4j..4j+3
+        if (T.m[j] == 0xFFFFFFFFu) d |= W[j] ^ T.e[j];
+        else if (T.m[j] != 0u) d |= (W[j] ^ T.e[j]) & T.m[j];
+        if (T.v[j] != 0u) d |= cand_z(W[j]) & T.v[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(W[29 + k], W[28 + k], 1u);   // bytes 113..148
+    // tail: candidate bitmap, bit i = line byte 164 - sb + i
+    u32 B[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < TAIL_WORDS; ++k) B[k >> 3] |= cand_nib(R[k]) << (4 * (k & 7));
+    const int tb0 = 164 - (int)sb;
+    // first candidate at or after line offset p (164 <= p), via a 64-bit window
     auto nextq = [&](int p) -> int {
-        const int k = p >> 5;
-        const u32 lo = k == 5 ? R[5] : k == 6 ? R[6] : k == 7 ? R[7] : k == 8 ? R[8] : k == 9 ? R[9] : 0u;
-        const u32 hi = k == 5 ? R[6] : k == 6 ? R[7] : k == 7 ? R[8] : k == 8 ? R[9] : 0u;
-        const u64 w = (((u64)hi << 32) | lo) >> (p & 31);
+        const int q = p - tb0;
+        const int k = q >> 5;
+        const u32 lo = k == 0 ? B[0] : k == 1 ? B[1] : k == 2 ? B[2] : k == 3 ? B[3] : 0u;
+        const u32 hi = k == 0 ? B[1] : k == 1 ? B[2] : k == 2 ? B[3] : 0u;
+        const u64 w = (((u64)hi << 32) | lo) >> (q & 31);
         return w ? p + (int)__builtin_ctzll(w) : (1 << 20);
     };
     c.e3 = nextq(164);            // end of ad_type
@@ -570,12 +583,12 @@ __device__ __forceinline__ bool canon_stage2(const LdsSrc& src, int s, int e, co
 struct Tally { u32 ev, view, join, miss, perr, terr, oor; };
 
 // The general path (lines that are not in the generator's layout).
-template <bool FAST, class S>
+template <class S>
 __device__ __forceinline__ bool process_line(const S& src, int s, int e, const ScanParams& P,
                                              Tally& t, u32& campaign, i64& bucket) {
     Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
     t.ev++;
-    if (!parse_line<FAST>(src, s, e, P.require_mask, ad, et, tm)) { t.perr++; return false; }
+    if (!parse_line(src, s, e, P.require_mask, ad, et, tm)) { t.perr++; return false; }
     if (!span_is_view(src, et)) return false;                // EventFilterBolt
     t.view++;
     u32 kw[KEY_WORDS];
@@ -650,12 +663,12 @@ __device__ __forceinline__ void global_add(const ScanParams& P, i64 ring_lo, boo
 // LDS layout (dynamic, 16-byte aligned carve, no static __shared__)
 // ---------------------------------------------------------------------------
 constexpr int OFF_TILE = 0;
-constexpr int OFF_QBITS = OFF_TILE + TILE_CAP + 64;
-constexpr int OFF_LCNT = OFF_QBITS + TILE_CHUNKS * 2 + 16;
+// 64 bytes of slack after the tile: stage 1 reads up to 276 bytes from a line start
+constexpr int OFF_LCNT = OFF_TILE + TILE_CAP + 64;
 constexpr int OFF_MISC = OFF_LCNT + LCNT_CAP * 4;
 constexpr int OFF_TB = OFF_MISC + 64;
 constexpr int LDS_BYTES = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
-static_assert(OFF_QBITS % 16 == 0 && OFF_LCNT % 16 == 0 &&
+static_assert(OFF_LCNT % 16 == 0 &&
               OFF_MISC % 16 == 0 && OFF_TB % 16 == 0, "LDS carve must stay 16-byte aligned");
 static_assert(LDS_BYTES <= 163840 / SCAN_WG_PER_CU, "SCAN_WG_PER_CU workgroups must fit one CU's 160 KiB of LDS");
 
@@ -720,21 +733,6 @@ __device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const Tile
         __builtin_amdgcn_make_buffer_rsrc(const_cast<u32*>(P.off + min(ti.first, P.n)), 0, (int)nrec, 0x00020000);
     my_off = __builtin_amdgcn_raw_buffer_load_b32(ro, 4 * tid, 0, 0);
     my_end = __builtin_amdgcn_raw_buffer_load_b32(ro, 4 * tid + 4, 0, 0);   // 0 past the batch end
-}
-
-// Candidate flags of one dword at bits 28..31 (bit 28+i: byte i may be '"' or '\\').
-// The has-zero trick can flag a byte just above a true hit falsely; the parser
-// verifies every candidate it relies on, so only exactness of the true hits matters.
-// Packing uses the full-rate 24-bit multiply (bits 7/15/23 -> 28/29/30) plus bit 31.
-__device__ __forceinline__ u32 cand_flags_hi(u32 w) {
-    const u32 tq = w ^ 0x22222222u, tb = w ^ 0x5C5C5C5Cu;
-    const u32 z = (((tq - 0x01010101u) & ~tq) | ((tb - 0x01010101u) & ~tb)) & 0x80808080u;
-    return __umul24(z, 0x00204081u) | (z & 0x80000000u);
-}
-// 16 flags of a 16-byte chunk, bit i = byte i.
-__device__ __forceinline__ u32 cand_mask16(const uint4& v) {
-    return (cand_flags_hi(v.x) >> 28) | ((cand_flags_hi(v.y) >> 28) << 4) | ((cand_flags_hi(v.z) >> 28) << 8) |
-           ((cand_flags_hi(v.w) >> 28) << 12);
 }
 
 __device__ __forceinline__ u32 wave_sum(u32 v) {
@@ -802,8 +800,6 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(ScanParams P) {
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
     u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
-    u16* q16 = reinterpret_cast<u16*>(smem + OFF_QBITS);
-    const u32* q32 = reinterpret_cast<const u32*>(smem + OFF_QBITS);
     u32* lcnt = reinterpret_cast<u32*>(smem + OFF_LCNT);
     i64* misc64 = reinterpret_cast<i64*>(smem + OFF_MISC);   // [0] lbase, [1] lset, [2..5] scratch
     u32* tb = reinterpret_cast<u32*>(smem + OFF_TB);
@@ -838,7 +834,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
     i64 lbase = 0;
     bool lset = false;
 
-    const LdsSrc lsrc{tile32, q32};
+    const LdsSrc lsrc{tile32};
     const uint4* ct4 = reinterpret_cast<const uint4*>(P.ctable);
     STAMP_DECL
     for (u64 t = t_begin; t < t_end; ++t) {
@@ -849,7 +845,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: separate the prefetch wait
         STAMP(6);
 #endif
-        // ---- Phase A: registers -> LDS, classify bytes --------------------------
+        // ---- Phase A: registers -> LDS -----------------------------------------------
         // Chunks past the tile hold zeros (bounds-checked loads), so they are written
         // unconditionally; only the last round is cut at TILE_CHUNKS (a whole wave).
         if (!cur.oversize) {
@@ -858,7 +854,6 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
                 const u32 k = (u32)(j * SCAN_TPB + tid);
                 if (j * SCAN_TPB + SCAN_TPB <= TILE_CHUNKS || k < (u32)TILE_CHUNKS) {
                     reinterpret_cast<uint4*>(tile32)[k] = pre[j];
-                    q16[k] = (u16)cand_mask16(pre[j]);
                 }
             }
         }
@@ -877,6 +872,13 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         __syncthreads();
         if (tid == 0) misc64[par ^ 1] = INT64_MIN;   // every thread has read it
         STAMP(1);
+#ifdef YSB_DIAG_A_ONLY
+        if (t + 1 < t_end) nxt = tile_info(P, t + 1, t_begin, tb);
+        else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
+        issue_tile_loads(P, nxt, pre, pre_off, pre_end);
+        __syncthreads();
+        continue;
+#endif
         // ---- Phase B1: canonical parse from LDS; any other line is deferred -------
         bool ok1 = false;
         int ls = 0, le = 0;
@@ -1004,7 +1006,7 @@ __global__ __launch_bounds__(AUX_TPB) void defer_kernel(ScanParams P) {
         u32 campaign;
         i64 bucket;
         const GlbSrc gsrc{P.bytes + ls, le - ls};
-        if (process_line<false>(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket))
+        if (process_line(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket))
             global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
     }
     flush_tally(P, tl, lane);
@@ -1034,7 +1036,7 @@ __global__ __launch_bounds__(AUX_TPB) void ring_autobase_kernel(ScanParams P, i6
             u32 c;
             i64 bk;
             const GlbSrc gsrc{P.bytes + ls, le - ls};
-            if (process_line<false>(gsrc, 0, (int)(le - ls), P, tl, c, bk)) b = bk;
+            if (process_line(gsrc, 0, (int)(le - ls), P, tl, c, bk)) b = bk;
         }
     }
 #pragma unroll
