@@ -76,6 +76,14 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def sum(self, v):
+        if not self.dist:
+            return v
+        import torch
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return int(t.item())
+
     def bcast_bytes(self, b):
         if not self.dist:
             return b
@@ -138,7 +146,7 @@ def main():
     camp = base.ad_campaign_index()
     if d.world > 1:
         subset = shard_ads(aids, d.world)[d.rank]
-        g = GenParams(seed=42 + 1_000_003 * d.rank, n_campaigns=100, ads_per_campaign=10,
+        g = GenParams(seed=42, event_stream=1 + d.rank, n_campaigns=100, ads_per_campaign=10,
                       events_per_sec=args.rate, ad_subset=subset)
     else:
         g = base
@@ -209,11 +217,13 @@ def main():
         ctx.sync()
         mism, truth, ring = ctx.truth_compare()
         st = ctx.stats()
-        check = {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
-                 "parse_errors": st["parse_errors"], "out_of_ring": st["out_of_ring"],
-                 "deferred_to_general_path": st["deferred"]}
+        vals = [mism, truth, ring, st["parse_errors"], st["out_of_ring"], st["deferred"], st["join_misses"]]
+        vals = [int(d.sum(v)) for v in vals]   # over all ranks
+        check = {"truth_mismatched_cells": vals[0], "truth_views": vals[1], "counted_views": vals[2],
+                 "parse_errors": vals[3], "out_of_ring": vals[4], "deferred_to_general_path": vals[5],
+                 "join_misses": vals[6]}
         if d.world > 1:
-            check["note"] = "rank-local table (before reduce-scatter) vs rank-local truth"
+            check["note"] = "sum over ranks of rank-local table (before reduce-scatter) vs rank-local truth"
 
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu:

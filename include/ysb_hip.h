@@ -188,6 +188,19 @@ int         ysb_group_reduce_scatter(ysb_ctx* ctx);
 int         ysb_group_owned(ysb_ctx* ctx, uint32_t* campaign_lo, uint32_t* campaign_hi);
 /* Shard of an ad_id under the partitioning above (host function). */
 uint32_t    ysb_ad_shard(const char* ad_id, uint32_t len, uint32_t nranks);
+/* Campaign block [*lo, *hi) that rank `rank` of `nranks` owns after
+ * ysb_group_reduce_scatter (host function, no context needed; ysb_group_owned of an
+ * initialised context reports the same block).  Replaces the key -> subtask mapping of
+ * Flink's keyBy(0) hash partitioner (AdvertisingTopologyNative.java:118-119). */
+int         ysb_group_block(uint32_t n_campaigns, int rank, int nranks, uint32_t* lo, uint32_t* hi);
+/* Host router for batches that are not pre-sharded: out_shard[i] = ysb_ad_shard of the
+ * raw bytes of line i's top-level "ad_id" string (generator lines: bytes 113..148;
+ * other layouts: a key scan); lines without one go to shard 0.  shard_counts (nranks
+ * entries, may be NULL) receives the lines per shard.  Any deterministic routing is
+ * exact because every rank loads the whole ad map; this one balances by ad. */
+int         ysb_route_lines(const uint8_t* bytes, uint64_t nbytes, const uint32_t* line_off,
+                            uint64_t n, uint32_t nranks, uint32_t* out_shard,
+                            uint64_t* shard_counts);
 
 /* ---- synthetic input: the data/ generator's event format (core.clj:61-98, 163-181)
  * restated as a seeded, counter-based generator with a file-dump mode.  Host and
@@ -204,7 +217,9 @@ typedef struct ysb_gen_params {
                                    k: draw from a pool of k (core.clj:187-188)         */
     const uint32_t* ad_subset;  /* optional: draw ads only from these indices (shards) */
     uint32_t n_ad_subset;
-    uint32_t reserved;
+    uint32_t event_stream;      /* 0: the single-stream generator; k > 0: an independent
+                                   event stream over the SAME campaign/ad ids (one per
+                                   rank of a sharded run); ids depend on seed only     */
 } ysb_gen_params;
 
 void        ysb_gen_default(ysb_gen_params* p);
@@ -232,6 +247,11 @@ int         ysb_truth_compare(ysb_ctx* ctx, uint64_t* mismatched_cells,
  * (ad,campaign lines, AdvertisingTopologyNative.java:52) and kafka-json.txt with
  * n_events events (core.clj:76-97). */
 int         ysb_gen_dump(const ysb_gen_params* p, uint64_t n_events, const char* dir);
+/* Sharded file-dump mode (config 4's pre-sharded replay files): the id and map files
+ * as ysb_gen_dump, and events [0, n_events) split by ysb_route_lines into
+ * kafka-json.<r>.txt for r in [0, nranks). */
+int         ysb_gen_dump_shards(const ysb_gen_params* p, uint64_t n_events, const char* dir,
+                                uint32_t nranks);
 
 #ifdef __cplusplus
 }

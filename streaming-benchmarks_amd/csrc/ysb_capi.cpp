@@ -42,6 +42,7 @@ struct ysb_ctx {
     unsigned long long* d_counts = nullptr;   // [c_pad][W]
     unsigned long long* d_owned = nullptr;    // [c_pad / nranks][W] after reduce-scatter
     unsigned long long* d_rs_tmp = nullptr;
+    bool ring_agreed = false;                 // ranks' ring bases checked equal
     i64* d_ring = nullptr;                // [lo, set]
     i64* h_ring = nullptr;                // pinned mirror
     hipEvent_t ev_ring = nullptr;
@@ -786,6 +787,31 @@ int ysb_group_reduce_scatter(ysb_ctx* c) {
     if (!c) return YSB_ERR_ARG;
     if (!c->comm) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
     HIPCHK(c, hipSetDevice(c->device));
+    if (!c->ring_agreed) {
+        // The tables are summed cell by cell (cell = bucket mod W): every rank's ring must
+        // start at the same bucket.  Checked once, on the first exchange (one small
+        // all-reduce of {lo, -lo, set} with max).
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        int rc = read_ring(c);
+        if (rc) return rc;
+        // every rank takes the same decision from the reduced values (no rank may skip
+        // the collective the others enter): {max lo, -min lo, max set, -min set}
+        i64 h[4] = {c->ring_known ? c->ring_lo : INT64_MIN + 1, c->ring_known ? -c->ring_lo : INT64_MIN + 1,
+                    c->ring_known ? 1 : 0, c->ring_known ? -1 : 0};
+        i64* d = nullptr;
+        HIPCHK(c, hipMalloc(&d, sizeof h));
+        HIPCHK(c, hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice));
+        ncclResult_t r = ncclAllReduce(d, d, 4, ncclInt64, ncclMax, c->comm, c->s_comp);
+        hipError_t e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->s_comp);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->s_comp);
+        hipFree(d);
+        if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+        if (e != hipSuccess) return fail(c, YSB_ERR_HIP, "%s", hipGetErrorString(e));
+        const bool any = h[2] != 0, all = h[3] == -1;
+        if (any && (!all || h[0] != -h[1]))
+            return fail(c, YSB_ERR_STATE, "ranks hold different ring bases (set ysb_config.ring_base_bucket)");
+        c->ring_agreed = any;
+    }
     const u64 per = (u64)c->c_pad / c->nranks * c->cfg.window_ring;
     ncclResult_t r = ncclReduceScatter(c->d_counts, c->d_rs_tmp, per, ncclUint64, ncclSum, c->comm, c->s_comp);
     if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
@@ -827,6 +853,8 @@ void ysb_gen_default(ysb_gen_params* p) {
 static GenSpec spec_of(const ysb_gen_params* p, const u32* subset) {
     GenSpec s{};
     s.seed = p->seed;
+    // stream 0 keeps the single-stream byte format of the committed fixtures
+    s.ev_seed = p->event_stream ? mix64(p->seed ^ (0xD1B54A32D192ED03ULL * p->event_stream)) : p->seed;
     s.n_campaigns = p->n_campaigns;
     s.ads_per_campaign = p->ads_per_campaign;
     s.t0_ms = p->t0_ms;

@@ -84,7 +84,8 @@ YSB_HD u32 event_type_len(u32 k) { return k == 0 ? 4 : k == 1 ? 5 : 8; }
 
 // POD generator spec (host or device pointer in `subset`).
 struct GenSpec {
-    u64 seed;
+    u64 seed;            // ids (campaigns, ads): shared by every rank
+    u64 ev_seed;         // per-event draws: seed, or seed mixed with the event stream
     u32 n_campaigns, ads_per_campaign;
     i64 t0_ms;
     u64 events_per_sec;
@@ -101,14 +102,14 @@ struct GenEvent {
 
 YSB_HD GenEvent gen_event(const GenSpec& s, u64 i) {
     GenEvent e;
-    u64 c = draw(stream_key(s.seed, S_CHOICE), i);
+    u64 c = draw(stream_key(s.ev_seed, S_CHOICE), i);
     u32 idx = (u32)(((c >> 32) * (u64)s.n_pick) >> 32);   // rand-nth ads (core.clj:92)
     e.ad = s.subset ? s.subset[idx] : idx;
     e.ad_type = (u32)(c & 0xFFFF) % 5u;                    // rand-nth ad-types (:93)
     e.event_type = (u32)((c >> 16) & 0xFFFF) % 3u;         // rand-nth event-types (:94)
     i64 t = s.t0_ms + (i64)((i * 1000ULL) / s.events_per_sec);   // (+ start-time (* n 10)) (:95)
     if (s.with_skew) {                                      // make-kafka-event-at (:166-174)
-        u64 r = draw(stream_key(s.seed, S_SKEW), i);
+        u64 r = draw(stream_key(s.ev_seed, S_SKEW), i);
         t += 50 - (i64)(r % 100);
         if (((r >> 17) % 100000ULL) == 0) t -= (i64)((r >> 40) % 60000ULL);
     }
@@ -145,12 +146,12 @@ YSB_HD u32 gen_line_write(const GenSpec& s, u64 i, const GenEvent& e, char* out)
     char* o = out;
     u64 hi, lo;
     o = put_str(o, YSB_P0, LEN_P0);
-    if (s.n_users == 0) uuid_words(stream_key(s.seed, S_USER), i, &hi, &lo);
-    else uuid_words(stream_key(s.seed, S_USER), draw(stream_key(s.seed, S_USERPOOL), i) % s.n_users, &hi, &lo);
+    if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
+    else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);
     uuid_format(hi, lo, o); o += 36;
     o = put_str(o, YSB_P1, LEN_P1);
-    if (s.n_users == 0) uuid_words(stream_key(s.seed, S_PAGE), i, &hi, &lo);
-    else uuid_words(stream_key(s.seed, S_PAGE), draw(stream_key(s.seed, S_PAGEPOOL), i) % s.n_users, &hi, &lo);
+    if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_PAGE), i, &hi, &lo);
+    else uuid_words(stream_key(s.ev_seed, S_PAGE), draw(stream_key(s.ev_seed, S_PAGEPOOL), i) % s.n_users, &hi, &lo);
     uuid_format(hi, lo, o); o += 36;
     o = put_str(o, YSB_P2, LEN_P2);
     uuid_words(stream_key(s.seed, S_AD), e.ad, &hi, &lo);

@@ -1,0 +1,173 @@
+// ysb_host.cpp -- host-only parts of the C ABI (no HIP calls, usable without a GPU):
+// the multi-GPU partitioning that replaces Flink's keyBy(0) shuffle
+// (flink-benchmarks/.../AdvertisingTopologyNative.java:118) and the sharded file-dump
+// mode of the generator.
+//
+//   ysb_group_block      campaign block a rank owns after ysb_group_reduce_scatter
+//   ysb_route_lines      per-line ad_id shard of a host batch (host router)
+//   ysb_gen_dump_shards  kafka-json.<r>.txt per shard (config 4's pre-sharded files)
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ysb_hip.h"
+#include "ysb_common.h"
+
+using namespace ysb;
+
+namespace {
+
+bool is_ws(u8 c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+// End of the string whose content starts at p (index of its closing quote), or -1.
+long scan_string(const u8* s, long p, long e) {
+    while (p < e) {
+        if (s[p] == '"') return p;
+        if (s[p] == '\\') p += 2;
+        else ++p;
+    }
+    return -1;
+}
+
+// Skips one non-string JSON value (number, literal, nested object/array); -1 if malformed.
+long skip_value(const u8* s, long p, long e) {
+    if (p >= e) return -1;
+    if (s[p] == '{' || s[p] == '[') {
+        int depth = 0;
+        while (p < e) {
+            const u8 c = s[p];
+            if (c == '"') {
+                const long q = scan_string(s, p + 1, e);
+                if (q < 0) return -1;
+                p = q + 1;
+                continue;
+            }
+            if (c == '{' || c == '[') ++depth;
+            else if ((c == '}' || c == ']') && --depth == 0) return p + 1;
+            ++p;
+        }
+        return -1;
+    }
+    while (p < e && s[p] != ',' && s[p] != '}' && !is_ws(s[p])) ++p;
+    return p;
+}
+
+}  // namespace
+
+// Raw bytes of the top-level "ad_id" string value of one line (escapes are not decoded:
+// routing only balances load, every rank holds the whole ad map).  Generator lines
+// (data/src/setup/core.clj:90-96) have it at byte 113; other layouts take a small
+// key scan.  Returns false when the line has no string ad_id.
+static bool find_ad_id(const u8* s, long n, long* vs, long* ve) {
+    static const char canon[] = "\"ad_id\": \"";   // bytes 103..112 of a generator line
+    if (n > 150 && std::memcmp(s + 103, canon, 10) == 0 && s[149] == '"' &&
+        std::memchr(s + 113, '"', 36) == nullptr && std::memchr(s + 113, '\\', 36) == nullptr &&
+        std::memcmp(s, "{\"user_id\": \"", 13) == 0) {
+        // the fixed prefix is only trusted when the two UUIDs before it are plain
+        if (!std::memchr(s + 13, '"', 36) && !std::memchr(s + 64, '"', 36) &&
+            !std::memchr(s + 13, '\\', 36) && !std::memchr(s + 64, '\\', 36) &&
+            std::memcmp(s + 49, "\", \"page_id\": \"", 15) == 0 && std::memcmp(s + 100, "\", ", 3) == 0) {
+            *vs = 113;
+            *ve = 149;
+            return true;
+        }
+    }
+    long p = 0;
+    while (p < n && is_ws(s[p])) ++p;
+    if (p >= n || s[p] != '{') return false;
+    ++p;
+    while (true) {
+        while (p < n && is_ws(s[p])) ++p;
+        if (p >= n || s[p] != '"') return false;
+        const long ke = scan_string(s, p + 1, n);
+        if (ke < 0) return false;
+        const bool is_ad = ke - p - 1 == 5 && std::memcmp(s + p + 1, "ad_id", 5) == 0;
+        p = ke + 1;
+        while (p < n && is_ws(s[p])) ++p;
+        if (p >= n || s[p] != ':') return false;
+        ++p;
+        while (p < n && is_ws(s[p])) ++p;
+        if (p >= n) return false;
+        if (s[p] == '"') {
+            const long q = scan_string(s, p + 1, n);
+            if (q < 0) return false;
+            if (is_ad) {
+                *vs = p + 1;
+                *ve = q;
+                return true;
+            }
+            p = q + 1;
+        } else {
+            p = skip_value(s, p, n);
+            if (p < 0) return false;
+        }
+        while (p < n && is_ws(s[p])) ++p;
+        if (p < n && s[p] == ',') { ++p; continue; }
+        return false;   // '}' without an ad_id, or malformed
+    }
+}
+
+extern "C" {
+
+int ysb_group_block(uint32_t n_campaigns, int rank, int nranks, uint32_t* lo, uint32_t* hi) {
+    if (nranks < 1 || rank < 0 || rank >= nranks) return YSB_ERR_ARG;
+    const u32 cp = (n_campaigns + (u32)nranks - 1) / (u32)nranks * (u32)nranks;
+    const u32 per = cp / (u32)nranks;
+    const u32 l = std::min<u32>(n_campaigns, (u32)rank * per);
+    if (lo) *lo = l;
+    if (hi) *hi = std::min<u32>(n_campaigns, l + per);
+    return YSB_OK;
+}
+
+int ysb_route_lines(const uint8_t* bytes, uint64_t nbytes, const uint32_t* line_off, uint64_t n,
+                    uint32_t nranks, uint32_t* out_shard, uint64_t* shard_counts) {
+    if ((!bytes && nbytes) || (!line_off && n) || (!out_shard && n) || nranks == 0) return YSB_ERR_ARG;
+    if (shard_counts) std::fill(shard_counts, shard_counts + nranks, 0ull);
+    for (u64 i = 0; i < n; ++i) {
+        const u64 s = line_off[i];
+        const u64 e = i + 1 < n ? (u64)line_off[i + 1] : nbytes;
+        u32 r = 0;
+        long vs, ve;
+        if (s <= e && e <= nbytes && find_ad_id(bytes + s, (long)(e - s), &vs, &ve))
+            r = ysb_ad_shard(reinterpret_cast<const char*>(bytes + s + vs), (u32)(ve - vs), nranks);
+        out_shard[i] = r;
+        if (shard_counts) shard_counts[r]++;
+    }
+    return YSB_OK;
+}
+
+int ysb_gen_dump_shards(const ysb_gen_params* p, uint64_t n_events, const char* dir, uint32_t nranks) {
+    if (!p || !dir || nranks == 0) return YSB_ERR_ARG;
+    int rc = ysb_gen_dump(p, 0, dir);   // id files and both ad-map formats (no events)
+    if (rc) return rc;
+    std::vector<FILE*> f(nranks, nullptr);
+    for (u32 r = 0; r < nranks; ++r) {
+        const std::string path = std::string(dir) + "/kafka-json." + std::to_string(r) + ".txt";
+        f[r] = std::fopen(path.c_str(), "wb");
+        if (!f[r]) {
+            for (FILE* x : f) if (x) std::fclose(x);
+            return YSB_ERR_ARG;
+        }
+    }
+    const u64 chunk = 1 << 16;
+    const u64 cap = chunk * ysb_gen_max_line_bytes(p);
+    std::vector<u8> buf(cap);
+    std::vector<u32> off(chunk), shard(chunk);
+    for (u64 first = 0; first < n_events && rc == YSB_OK; first += chunk) {
+        const u64 m = std::min<u64>(chunk, n_events - first);
+        uint64_t nb = 0;
+        rc = ysb_gen_events_host(p, first, m, buf.data(), cap, off.data(), &nb);
+        if (rc) break;
+        rc = ysb_route_lines(buf.data(), nb, off.data(), m, nranks, shard.data(), nullptr);
+        for (u64 i = 0; i < m && rc == YSB_OK; ++i) {
+            const u64 e = i + 1 < m ? (u64)off[i + 1] : nb;
+            std::fwrite(buf.data() + off[i], 1, e - off[i], f[shard[i]]);
+        }
+    }
+    for (FILE* x : f) std::fclose(x);
+    return rc;
+}
+
+}  // extern "C"

@@ -47,7 +47,7 @@ class YsbGenParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("n_campaigns", C.c_uint32), ("ads_per_campaign", C.c_uint32),
                 ("t0_ms", C.c_int64), ("events_per_sec", C.c_uint64), ("with_skew", C.c_uint32),
                 ("n_users", C.c_uint32), ("ad_subset", C.POINTER(C.c_uint32)), ("n_ad_subset", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("event_stream", C.c_uint32)]
 
 
 _P = C.c_void_p
@@ -86,6 +86,8 @@ SIGNATURES = {
     "ysb_group_reduce_scatter": (_I, [_P]),
     "ysb_group_owned": (_I, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "ysb_ad_shard": (_U32, [C.c_char_p, _U32, _U32]),
+    "ysb_group_block": (_I, [_U32, _I, _I, C.POINTER(_U32), C.POINTER(_U32)]),
+    "ysb_route_lines": (_I, [_PU8, _U64, _PU32, _U64, _U32, _PU32, C.c_void_p]),
     "ysb_gen_default": (None, [C.POINTER(YsbGenParams)]),
     "ysb_gen_ids": (_I, [C.POINTER(YsbGenParams), C.c_char_p, C.c_char_p]),
     "ysb_gen_events_host": (_I, [C.POINTER(YsbGenParams), _U64, _U64, _PU8, _U64, _PU32, C.POINTER(_U64)]),
@@ -94,6 +96,7 @@ SIGNATURES = {
     "ysb_truth_accumulate": (_I, [_P, C.POINTER(YsbGenParams), _U64, _U64]),
     "ysb_truth_compare": (_I, [_P, C.POINTER(_U64), C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_gen_dump": (_I, [C.POINTER(YsbGenParams), _U64, C.c_char_p]),
+    "ysb_gen_dump_shards": (_I, [C.POINTER(YsbGenParams), _U64, C.c_char_p, _U32]),
 }
 
 _lib = None

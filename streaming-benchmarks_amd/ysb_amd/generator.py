@@ -19,7 +19,7 @@ class GenParams:
     t0 1.7e12 ms, 100,000 events per second of event time."""
 
     def __init__(self, seed=42, n_campaigns=100, ads_per_campaign=10, t0_ms=1_700_000_000_000,
-                 events_per_sec=100_000, with_skew=False, n_users=0, ad_subset=None):
+                 events_per_sec=100_000, with_skew=False, n_users=0, ad_subset=None, event_stream=0):
         self.c = YsbGenParams()
         lib().ysb_gen_default(C.byref(self.c))
         self.c.seed = seed
@@ -29,6 +29,7 @@ class GenParams:
         self.c.events_per_sec = events_per_sec
         self.c.with_skew = int(bool(with_skew))
         self.c.n_users = n_users
+        self.c.event_stream = event_stream
         self._subset = None
         if ad_subset is not None:
             self._subset = np.ascontiguousarray(ad_subset, dtype=np.uint32)
@@ -66,6 +67,10 @@ class GenParams:
 
     def dump(self, n_events, directory):
         check(lib().ysb_gen_dump(C.byref(self.c), n_events, str(directory).encode()))
+
+    def dump_shards(self, n_events, directory, nranks):
+        """Pre-sharded replay files kafka-json.<r>.txt (ad_id-hash routing) + id/map files."""
+        check(lib().ysb_gen_dump_shards(C.byref(self.c), n_events, str(directory).encode(), nranks))
 
 
 def ad_shard(ad_id: str, nranks: int) -> int:

@@ -1,0 +1,50 @@
+"""Multi-GPU partitioning: the host side of the keyBy(0) replacement
+(flink-benchmarks/.../AdvertisingTopologyNative.java:118-119).
+
+Each rank (one process per GPU) counts the events of its ad_id shard into its own
+[C_pad][W] (campaign, window) table; ysb_group_reduce_scatter (RCCL over xGMI, inside
+libysb_hip.so) then sums the tables so that rank r owns campaigns owned_block(C, r, N).
+These helpers are host functions of the same library (no GPU needed): the router for
+batches that are not pre-sharded, the ownership split, and the batch splitter.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import check, lib
+
+
+def owned_block(n_campaigns: int, rank: int, nranks: int):
+    """[lo, hi) campaign indices rank `rank` owns after the reduce-scatter."""
+    lo, hi = C.c_uint32(), C.c_uint32()
+    check(lib().ysb_group_block(n_campaigns, rank, nranks, C.byref(lo), C.byref(hi)))
+    return lo.value, hi.value
+
+
+def route_lines(raw, offs, nranks: int):
+    """(shard per line as uint32, lines per shard as uint64) of a host batch."""
+    raw = np.ascontiguousarray(raw, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint32)
+    n = offs.size
+    shard = np.zeros(max(n, 1), dtype=np.uint32)
+    counts = np.zeros(nranks, dtype=np.uint64)
+    check(lib().ysb_route_lines(C.c_void_p(raw.ctypes.data), raw.size, C.c_void_p(offs.ctypes.data), n,
+                                nranks, C.c_void_p(shard.ctypes.data), C.c_void_p(counts.ctypes.data)))
+    return shard[:n], counts
+
+
+def split_batch(raw, offs, shard, r: int):
+    """The lines of shard r as a new packed batch (bytes, u32 offsets)."""
+    raw = np.asarray(raw, dtype=np.uint8)
+    offs = np.asarray(offs, dtype=np.uint64)
+    ends = np.append(offs[1:], raw.size) if offs.size else offs
+    sel = np.nonzero(np.asarray(shard) == r)[0]
+    lens = (ends[sel] - offs[sel]).astype(np.uint64)
+    new_off = np.zeros(sel.size, dtype=np.uint64)
+    if sel.size:
+        new_off[1:] = np.cumsum(lens)[:-1]
+    idx = np.concatenate([np.arange(offs[i], ends[i], dtype=np.uint64) for i in sel]) if sel.size else \
+        np.zeros(0, dtype=np.uint64)
+    return raw[idx.astype(np.int64)], new_off.astype(np.uint32)

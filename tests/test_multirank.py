@@ -1,0 +1,142 @@
+"""CPU (gloo, world_size 2 and 3) rehearsal of the multi-GPU path: ad_id-hash routing,
+the campaign-major (campaign, window) tables, one reduce-scatter, owner blocks.
+The per-rank counting is the CPU oracle; what is under test is the partitioning and
+exchange logic the GPU path shares (libysb_hip.so host functions + the collective's
+semantics).  See tests/multirank_worker.py."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from collections import Counter
+
+import pytest
+
+import golden_data as gd
+from oracle import oracle
+from ysb_amd import GenParams, owned_block, route_lines, split_batch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_ranks(scenario, world, tmp_path):
+    port = free_port()
+    procs, outs = [], []
+    for r in range(world):
+        out = tmp_path / ("rank%d.json" % r)
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py"), scenario, str(out)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+        outs.append(out)
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=240)[0].decode(errors="replace"))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, lg in zip(procs, logs):
+        assert p.returncode == 0, lg[-3000:]
+    return [json.load(open(o)) for o in outs]
+
+
+def merged(rank_infos, key):
+    tot = Counter()
+    for info in rank_infos:
+        for c, b, n in info[key]:
+            tot[(c, b)] += n
+    return dict(tot)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_routed_fixture_reduce_scatter_equals_oracle(world, tmp_path):
+    res = run_ranks("route", world, tmp_path)
+    infos = res[0]["ranks"]
+    exp_rows, exp_st = gd.expected("gen_s7")
+    # every line went to exactly one rank
+    raw, offs = gd.events("gen_s7")
+    assert sum(r["lines"] for r in res) == len(offs)
+    assert sum(res[0]["shard_counts"]) == len(offs)
+    # the owners' rows after the exchange are exactly the single-process oracle's
+    assert merged(infos, "owned") == exp_rows
+    # and so is the plain sum of the per-rank tables (the exchange loses nothing)
+    assert merged(infos, "local") == exp_rows
+    for k in ("events", "views", "joined", "join_misses", "parse_errors"):
+        assert sum(i["stats"][k] for i in infos) == exp_st[k], k
+    # owner blocks tile [0, C)
+    blocks = sorted(tuple(i["block"]) for i in infos)
+    assert blocks[0][0] == 0 and blocks[-1][1] == len(gd.campaigns())
+    assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+
+
+def test_per_rank_generation_reduce_scatter(tmp_path):
+    res = run_ranks("gen", 2, tmp_path)
+    assert all(r["all_routed_here"] for r in res)   # generator shards == router shards
+    infos = res[0]["ranks"]
+    # every rank's event stream draws the shared ad ids: no join misses anywhere
+    assert all(i["stats"]["join_misses"] == 0 and i["stats"]["joined"] > 0 for i in infos)
+    assert merged(infos, "owned") == merged(infos, "local")
+    assert sum(sum(n for _, _, n in i["owned"]) for i in infos) == sum(i["stats"]["joined"] for i in infos)
+
+
+def test_owned_block_matches_padding_rule():
+    for C in (1, 7, 100, 1_000_000):
+        for N in (1, 2, 3, 8):
+            cp = (C + N - 1) // N * N
+            prev = 0
+            for r in range(N):
+                lo, hi = owned_block(C, r, N)
+                assert lo == min(C, r * (cp // N)) and hi == min(C, lo + cp // N)
+                assert lo == prev
+                prev = hi
+            assert prev == C
+
+
+def test_router_is_deterministic_and_consistent_with_ad_shard():
+    from ysb_amd import ad_shard
+    raw, offs = gd.events("gen_s7")
+    import numpy as np
+    a = np.frombuffer(raw, dtype=np.uint8)
+    s1, c1 = route_lines(a, offs, 4)
+    s2, _ = route_lines(a, offs, 4)
+    assert (s1 == s2).all() and int(c1.sum()) == len(offs)
+    ends = list(offs[1:]) + [len(raw)]
+    for i in range(0, len(offs), 97):
+        ev = json.loads(raw[offs[i]:ends[i]])
+        assert s1[i] == ad_shard(ev["ad_id"], 4)
+    # a non-canonical layout routes by the same key
+    line = b'{ "ad_id" : "%s", "event_type": "view", "user_id": "u", "page_id": "p", "ad_type": "x", ' \
+           b'"event_time": "1"}\n' % json.loads(raw[offs[0]:ends[0]])["ad_id"].encode()
+    s3, _ = route_lines(np.frombuffer(line, dtype=np.uint8), np.zeros(1, dtype=np.uint32), 4)
+    assert s3[0] == s1[0]
+    # split + oracle over all shards == oracle over the batch
+    ads, camp = gd.ad_arrays()
+    am = oracle.AdMap(ads, camp)
+    tot = Counter()
+    for r in range(4):
+        br, bo = split_batch(a, offs, s1, r)
+        rows, _ = oracle.run(am, br.tobytes(), bo)
+        tot.update(rows)
+    assert dict(tot) == gd.expected("gen_s7")[0]
+
+
+def test_dump_shards(tmp_path):
+    g = GenParams(seed=3, n_campaigns=5, ads_per_campaign=4, events_per_sec=100)
+    g.dump(300, tmp_path)
+    whole = (tmp_path / "kafka-json.txt").read_bytes().splitlines()
+    g.dump_shards(300, tmp_path, 3)
+    parts = [(tmp_path / ("kafka-json.%d.txt" % r)).read_bytes().splitlines() for r in range(3)]
+    assert sorted(whole) == sorted(sum(parts, []))
+    from ysb_amd import ad_shard
+    for r, lines in enumerate(parts):
+        assert all(ad_shard(json.loads(ln)["ad_id"], 3) == r for ln in lines)
