@@ -121,6 +121,10 @@ const char* ysb_last_error(const ysb_ctx* ctx);
 int         ysb_load_ad_map(ysb_ctx* ctx, const char* const* ad_ids,
                             const uint32_t* ad_id_lens, const uint32_t* campaign_idx,
                             uint64_t n);
+/* Same for n keys of key_len bytes packed back to back (a JNI byte[] of UUIDs; config 3
+ * loads 10M ads this way). */
+int         ysb_load_ad_map_packed(ysb_ctx* ctx, const char* keys, uint32_t key_len,
+                                   const uint32_t* campaign_idx, uint64_t n);
 
 /* ---- batches --------------------------------------------------------------------
  * A batch is n_events JSON lines packed back to back in `bytes`; line i spans
@@ -160,6 +164,12 @@ int         ysb_stats_get(ysb_ctx* ctx, ysb_stats* out);
 int         ysb_reset(ysb_ctx* ctx);
 /* Bucket range currently held by the ring: [*lo, *lo + window_ring). */
 int         ysb_ring_range(ysb_ctx* ctx, int64_t* lo, uint32_t* width);
+/* Moves the ring to [new_lo, new_lo + window_ring) (streaming: follow the watermark).
+ * Counts of buckets leaving the ring move to the exact host-side list and are reported
+ * by later drains; events of buckets outside the new range keep going to the side list.
+ * Replaces the LRU eviction of old buckets (LRUHashMap(10), CampaignProcessorCommon.java:37,
+ * LRUHashMap.java:18-19) without its loss of counts.  Single-rank contexts only. */
+int         ysb_ring_advance(ysb_ctx* ctx, int64_t new_lo);
 
 /* ---- measurement -------------------------------------------------------------------- */
 /* With YSB_F_TIMING: total device time of the scan kernel launches (HIP events on

@@ -43,6 +43,9 @@ struct ysb_ctx {
     unsigned long long* d_owned = nullptr;    // [c_pad / nranks][W] after reduce-scatter
     unsigned long long* d_rs_tmp = nullptr;
     bool ring_agreed = false;                 // ranks' ring bases checked equal
+    TableRow* d_rows = nullptr;               // drain compaction output
+    u64 rows_cap = 0;
+    u32* d_rows_n = nullptr;
     i64* d_ring = nullptr;                // [lo, set]
     i64* h_ring = nullptr;                // pinned mirror
     hipEvent_t ev_ring = nullptr;
@@ -137,6 +140,8 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_counts);
     hipFree(c->d_owned);
     hipFree(c->d_rs_tmp);
+    hipFree(c->d_rows);
+    hipFree(c->d_rows_n);
     hipFree(c->d_ring);
     hipHostFree(c->h_ring);
     hipFree(c->d_ovf);
@@ -255,6 +260,16 @@ int ysb_close(ysb_ctx* c) {
 
 // ---- ad table -------------------------------------------------------------------------
 
+int ysb_load_ad_map_packed(ysb_ctx* c, const char* keys, uint32_t key_len, const uint32_t* campaign_idx,
+                           uint64_t n) {
+    if (!c) return YSB_ERR_ARG;
+    if (n && (!keys || !campaign_idx)) return fail(c, YSB_ERR_ARG, "NULL ad map arrays");
+    std::vector<const char*> ptr(n);
+    std::vector<u32> len(n, key_len);
+    for (u64 i = 0; i < n; ++i) ptr[i] = keys + i * key_len;
+    return ysb_load_ad_map(c, ptr.data(), len.data(), campaign_idx, n);
+}
+
 int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens, const uint32_t* campaign_idx,
                     uint64_t n) {
     if (!c) return YSB_ERR_ARG;
@@ -299,18 +314,15 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
     HIPCHK(c, hipMemcpy(c->d_table, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
     // every 36-byte key also goes into the two-choice cuckoo table (load <= 1/4)
     typedef std::array<u32, CKEY_WORDS> Key36;
+    // the distinct 36-byte keys with their final (later-wins) campaign: the general
+    // table already holds exactly that set
     std::vector<std::pair<Key36, u32>> keys36;
-    {
-        std::map<Key36, size_t> where;
-        for (u64 i = 0; i < n; ++i) {
-            const u32 len = lens ? lens[i] : 36u;
-            if (len != 36) continue;
-            Key36 k;
-            std::memcpy(k.data(), ad_ids[i], 36);
-            auto it = where.find(k);
-            if (it != where.end()) keys36[it->second].second = campaign_idx[i];   // later wins
-            else { where[k] = keys36.size(); keys36.push_back({k, campaign_idx[i]}); }
-        }
+    for (u64 sl = 0; sl < slots; ++sl) {
+        const u32* e = &tab[sl * SLOT_WORDS];
+        if (e[1] == EMPTY_SLOT || e[0] != 36) continue;
+        Key36 k;
+        std::memcpy(k.data(), e + 2, 36);
+        keys36.push_back({k, e[1]});
     }
     bool partial = false;
     if (c->cfg.flags & YSB_F_SPARSE_FAST_JOIN) {
@@ -581,41 +593,65 @@ static int pull_side_list(ysb_ctx* c) {
     return YSB_OK;
 }
 
+// Non-zero ring cells of buckets [blo, bhi) (rank-local table + owned block), compacted
+// on the device (two passes: count, then rows), added to `into`; clear zeroes them.
+static int ring_rows(ysb_ctx* c, i64 blo, i64 bhi, bool clear, std::map<std::pair<u32, i64>, u64>& into) {
+    if (!c->ring_known) return YSB_OK;
+    const u32 W = c->cfg.window_ring;
+    const i64 lo = c->ring_lo;
+    const i64 a = std::max<i64>(blo, lo), b = std::min<i64>(bhi, lo + (i64)W);
+    if (a >= b) return YSB_OK;
+    const u32 nb = (u32)(b - a);
+    struct Tab { unsigned long long* t; u32 rows, off; };
+    std::vector<Tab> tabs{{c->d_counts, c->cfg.n_campaigns, 0u}};
+    if (c->d_owned) {
+        u32 olo = 0, ohi = 0;
+        ysb_group_block(c->cfg.n_campaigns, c->rank, c->nranks, &olo, &ohi);
+        if (ohi > olo) tabs.push_back({c->d_owned, ohi - olo, olo});
+    }
+    if (!c->d_rows_n) HIPCHK(c, hipMalloc(&c->d_rows_n, 8));
+    for (const Tab& t : tabs) {
+        u32 n = 0;
+        HIPCHK(c, hipMemsetAsync(c->d_rows_n, 0, 4, c->s_comp));
+        launch_compact(t.t, t.rows, W, a, nb, t.off, true, false, nullptr, c->d_rows_n, 0, c->s_comp);
+        HIPCHK(c, hipMemcpyAsync(&n, c->d_rows_n, 4, hipMemcpyDeviceToHost, c->s_comp));
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        if (!n) continue;
+        if (n > c->rows_cap) {
+            hipFree(c->d_rows);
+            c->d_rows = nullptr;
+            const u64 cap = std::max<u64>(n, 4096);
+            HIPCHK(c, hipMalloc(&c->d_rows, cap * sizeof(TableRow)));
+            c->rows_cap = cap;
+        }
+        std::vector<TableRow> h(n);
+        u32 m = 0;
+        HIPCHK(c, hipMemsetAsync(c->d_rows_n, 0, 4, c->s_comp));
+        launch_compact(t.t, t.rows, W, a, nb, t.off, false, clear, c->d_rows, c->d_rows_n, n, c->s_comp);
+        HIPCHK(c, hipMemcpyAsync(&m, c->d_rows_n, 4, hipMemcpyDeviceToHost, c->s_comp));
+        HIPCHK(c, hipMemcpyAsync(h.data(), c->d_rows, (u64)n * sizeof(TableRow), hipMemcpyDeviceToHost, c->s_comp));
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        if (m != n) return fail(c, YSB_ERR_STATE, "table changed during drain (%u vs %u cells)", m, n);
+        for (const TableRow& r : h) into[{r.campaign, r.bucket}] += r.count;
+    }
+    return YSB_OK;
+}
+
 int ysb_drain(ysb_ctx* c, int64_t blo, int64_t bhi, int clear, ysb_count* out, uint64_t cap, uint64_t* n_out) {
     if (!c || !n_out) return c ? fail(c, YSB_ERR_ARG, "n_out is NULL") : YSB_ERR_ARG;
     int rc = ysb_sync(c);
     if (rc) return rc;
     if ((rc = read_ring(c))) return rc;
     if ((rc = pull_side_list(c))) return rc;
-    const u32 W = c->cfg.window_ring;
-    const u32 C = c->cfg.n_campaigns;
     std::map<std::pair<u32, i64>, u64> rows;
-    // side list
-    for (auto it = c->side.lower_bound({0, INT64_MIN}); it != c->side.end(); ++it)
-        if (it->first.second >= blo && it->first.second < bhi && it->second) rows[it->first] += it->second;
-    // ring: rank-local remnants for every campaign, plus the owned block after a reduce-scatter
-    std::vector<unsigned long long> loc((u64)C * W), own;
-    u32 own_lo = 0, own_hi = 0;
-    if (c->ring_known) {
-        HIPCHK(c, hipMemcpy(loc.data(), c->d_counts, loc.size() * 8, hipMemcpyDeviceToHost));
-        if (c->d_owned) {
-            const u32 per = c->c_pad / c->nranks;
-            own_lo = std::min<u32>(C, (u32)c->rank * per);
-            own_hi = std::min<u32>(C, own_lo + per);
-            own.resize((u64)per * W);
-            HIPCHK(c, hipMemcpy(own.data(), c->d_owned, own.size() * 8, hipMemcpyDeviceToHost));
-        }
-        const i64 lo = c->ring_lo;
-        auto bucket_of = [&](u32 j) { return lo + (i64)(((u64)j - (u64)lo) & (W - 1)); };
-        for (u32 cc = 0; cc < C; ++cc)
-            for (u32 j = 0; j < W; ++j) {
-                const i64 b = bucket_of(j);
-                if (b < blo || b >= bhi) continue;
-                u64 v = loc[(u64)cc * W + j];
-                if (cc >= own_lo && cc < own_hi) v += own[(u64)(cc - own_lo) * W + j];
-                if (v) rows[{cc, b}] += v;
-            }
+    if (clear && out) {
+        // move the ring range into the host map first: nothing is lost if `cap` is short
+        if ((rc = ring_rows(c, blo, bhi, true, c->side))) return rc;
+    } else if ((rc = ring_rows(c, blo, bhi, false, rows))) {
+        return rc;
     }
+    for (auto it = c->side.begin(); it != c->side.end(); ++it)
+        if (it->first.second >= blo && it->first.second < bhi && it->second) rows[it->first] += it->second;
     *n_out = rows.size();
     if (!out) return YSB_OK;
     if (cap < rows.size()) return fail(c, YSB_ERR_CAPACITY, "drain needs %llu rows, cap %llu", (unsigned long long)rows.size(), (unsigned long long)cap);
@@ -628,26 +664,34 @@ int ysb_drain(ysb_ctx* c, int64_t blo, int64_t bhi, int clear, ysb_count* out, u
         ++k;
     }
     if (clear) {
-        for (auto it = c->side.begin(); it != c->side.end();)
+        for (auto it = c->side.begin(); it != c->side.end();) {
             if (it->first.second >= blo && it->first.second < bhi) it = c->side.erase(it);
             else ++it;
-        if (c->ring_known) {
-            const i64 lo = c->ring_lo;
-            bool dirty = false;
-            for (u32 j = 0; j < W; ++j) {
-                const i64 b = lo + (i64)(((u64)j - (u64)lo) & (W - 1));
-                if (b < blo || b >= bhi) continue;
-                dirty = true;
-                for (u32 cc = 0; cc < C; ++cc) loc[(u64)cc * W + j] = 0;
-                if (!own.empty())
-                    for (u32 cc = own_lo; cc < own_hi; ++cc) own[(u64)(cc - own_lo) * W + j] = 0;
-            }
-            if (dirty) {
-                HIPCHK(c, hipMemcpy(c->d_counts, loc.data(), loc.size() * 8, hipMemcpyHostToDevice));
-                if (!own.empty()) HIPCHK(c, hipMemcpy(c->d_owned, own.data(), own.size() * 8, hipMemcpyHostToDevice));
-            }
         }
     }
+    return YSB_OK;
+}
+
+int ysb_ring_advance(ysb_ctx* c, int64_t new_lo) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = ysb_sync(c);
+    if (rc) return rc;
+    if ((rc = read_ring(c))) return rc;
+    if (c->comm) return fail(c, YSB_ERR_STATE, "ysb_ring_advance is not available after ysb_group_init "
+                                               "(every rank's ring must move together)");
+    if (new_lo <= INT64_MIN / 2 || new_lo >= INT64_MAX / 2) return fail(c, YSB_ERR_ARG, "ring base out of range");
+    if (c->ring_known && new_lo != c->ring_lo) {
+        const i64 lo = c->ring_lo, W = (i64)c->cfg.window_ring;
+        // buckets of the old range that the new range does not hold move to the host map
+        const i64 a = new_lo > lo ? lo : std::max<i64>(new_lo + W, lo);
+        const i64 b = new_lo > lo ? std::min<i64>(new_lo, lo + W) : lo + W;
+        if (a < b && (rc = ring_rows(c, a, b, true, c->side))) return rc;
+    }
+    i64 r[2] = {new_lo, 1};
+    HIPCHK(c, hipMemcpy(c->d_ring, r, 16, hipMemcpyHostToDevice));
+    c->ring_known = true;
+    c->ring_lo = new_lo;
+    c->ring_query_pending = false;
     return YSB_OK;
 }
 

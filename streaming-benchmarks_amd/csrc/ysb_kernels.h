@@ -70,4 +70,16 @@ void launch_compare(const unsigned long long* a, const unsigned long long* b, u6
                     unsigned long long* out, hipStream_t s);
 void launch_add_u64(unsigned long long* dst, const unsigned long long* src, u64 n, hipStream_t s);
 
+// Table maintenance (ysb_table.hip): the non-zero cells of buckets [blo, blo + nb) of a
+// campaign-major [rows][W] table as rows (campaign + c_off), optionally cleared.  With
+// count_only only *out_n is incremented (by the number of such cells).
+struct TableRow {
+    u32 campaign;
+    u32 pad;
+    i64 bucket;
+    unsigned long long count;
+};
+void launch_compact(unsigned long long* table, u32 rows, u32 W, i64 blo, u32 nb, u32 c_off, bool count_only,
+                    bool clear, TableRow* out, u32* out_n, u32 cap, hipStream_t s);
+
 }  // namespace ysb

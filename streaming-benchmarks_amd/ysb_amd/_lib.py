@@ -66,6 +66,7 @@ SIGNATURES = {
     "ysb_close": (_I, [_P]),
     "ysb_last_error": (C.c_char_p, [_P]),
     "ysb_load_ad_map": (_I, [_P, C.POINTER(C.c_char_p), C.POINTER(_U32), C.POINTER(_U32), _U64]),
+    "ysb_load_ad_map_packed": (_I, [_P, C.c_void_p, _U32, C.c_void_p, _U64]),
     "ysb_slot_buffers": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_P)]),
     "ysb_submit": (_I, [_P, _I, _PU8, _U64, _PU32, _U64]),
     "ysb_wait": (_I, [_P, _I]),
@@ -75,6 +76,7 @@ SIGNATURES = {
     "ysb_stats_get": (_I, [_P, C.POINTER(YsbStats)]),
     "ysb_reset": (_I, [_P]),
     "ysb_ring_range": (_I, [_P, C.POINTER(_I64), C.POINTER(_U32)]),
+    "ysb_ring_advance": (_I, [_P, _I64]),
     "ysb_kernel_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64)]),
     "ysb_stream": (_P, [_P]),
     "ysb_device_alloc": (_I, [_P, _U64, C.POINTER(_P)]),
@@ -89,7 +91,7 @@ SIGNATURES = {
     "ysb_group_block": (_I, [_U32, _I, _I, C.POINTER(_U32), C.POINTER(_U32)]),
     "ysb_route_lines": (_I, [_PU8, _U64, _PU32, _U64, _U32, _PU32, C.c_void_p]),
     "ysb_gen_default": (None, [C.POINTER(YsbGenParams)]),
-    "ysb_gen_ids": (_I, [C.POINTER(YsbGenParams), C.c_char_p, C.c_char_p]),
+    "ysb_gen_ids": (_I, [C.POINTER(YsbGenParams), _P, _P]),
     "ysb_gen_events_host": (_I, [C.POINTER(YsbGenParams), _U64, _U64, _PU8, _U64, _PU32, C.POINTER(_U64)]),
     "ysb_gen_events_device": (_I, [_P, C.POINTER(YsbGenParams), _U64, _U64, _PU8, _U64, _PU32, C.POINTER(_U64)]),
     "ysb_gen_max_line_bytes": (_U64, [C.POINTER(YsbGenParams)]),

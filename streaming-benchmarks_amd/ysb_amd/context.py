@@ -75,6 +75,14 @@ class YsbContext:
         camp = (C.c_uint32 * max(n, 1))(*[int(c) for c in campaign_idx])
         self._c(lib().ysb_load_ad_map(self._h, arr, lens, camp, n))
 
+    def load_ad_map_packed(self, keys, campaign_idx, key_len=36):
+        """keys: uint8 array of n * key_len bytes; campaign_idx: n uint32."""
+        k = np.ascontiguousarray(keys, dtype=np.uint8)
+        cidx = np.ascontiguousarray(campaign_idx, dtype=np.uint32)
+        if k.size != cidx.size * key_len:
+            raise ValueError("keys must hold n * key_len bytes")
+        self._c(lib().ysb_load_ad_map_packed(self._h, _ptr(k), key_len, _ptr(cidx), cidx.size))
+
     # -- batches -----------------------------------------------------------------------
     def slot_buffers(self, slot):
         b, o = C.c_void_p(), C.c_void_p()
@@ -122,6 +130,10 @@ class YsbContext:
         lo, w = C.c_int64(), C.c_uint32()
         self._c(lib().ysb_ring_range(self._h, C.byref(lo), C.byref(w)))
         return lo.value, w.value
+
+    def ring_advance(self, new_lo):
+        """Moves the ring to [new_lo, new_lo + W); leaving buckets go to the exact host list."""
+        self._c(lib().ysb_ring_advance(self._h, int(new_lo)))
 
     def kernel_time(self):
         """(total ms, launches) of the scan kernel since the last call (needs timing=True)."""

@@ -49,6 +49,16 @@ class GenParams:
         return ([craw[36 * i:36 * i + 36] for i in range(self.c.n_campaigns)],
                 [araw[36 * i:36 * i + 36] for i in range(self.n_ads)])
 
+    def ids_packed(self):
+        """(campaign ids, ad ids) as uint8 arrays of 36-byte UUIDs back to back (large maps)."""
+        cb = np.zeros(36 * self.c.n_campaigns, dtype=np.uint8)
+        ab = np.zeros(36 * self.n_ads, dtype=np.uint8)
+        check(lib().ysb_gen_ids(C.byref(self.c), C.c_void_p(cb.ctypes.data), C.c_void_p(ab.ctypes.data)))
+        return cb, ab
+
+    def ad_campaign_index_array(self):
+        return (np.arange(self.n_ads, dtype=np.uint64) // self.c.ads_per_campaign).astype(np.uint32)
+
     def ad_campaign_index(self):
         return [a // self.c.ads_per_campaign for a in range(self.n_ads)]
 
