@@ -121,6 +121,8 @@ class StreamingOperator:
         self.flushes = 0
         self.totals = {}          # (campaign, bucket) -> count, everything written
         self.open_at_end = 0
+        self.flushed_wm = None    # watermark at the previous flush
+        self.first_wm = None      # watermark after the first batch
 
     # -- filling -----------------------------------------------------------------------
     def free_space(self):
@@ -190,6 +192,8 @@ class StreamingOperator:
             self.max_time = t if self.max_time is None else max(self.max_time, t)
             wm = self.max_time - self.ooo
             closes = self.watermark is not None and wm // self.s.divisor > self.watermark // self.s.divisor
+            if self.watermark is None:
+                self.first_wm = wm
             self.watermark = wm if self.watermark is None else max(self.watermark, wm)
             if closes:
                 self.flush()           # a window ended under the watermark: close it now
@@ -201,8 +205,15 @@ class StreamingOperator:
         rows = self.s.drain_rows()
         self.flushes += 1
         self.last_flush_ms = now
+        d = self.s.divisor
         for c, b, n in rows:
-            self.seen_buckets.add(b)
+            if b not in self.seen_buckets:
+                self.seen_buckets.add(b)
+                # first seen after the previous flush's watermark had passed its end:
+                # a window of late events only, not a window that closes (no latency)
+                ref = self.flushed_wm if self.flushed_wm is not None else self.first_wm
+                if ref is not None and (b + 1) * d <= ref:
+                    self.closed[b] = None
             if b in self.closed:
                 self.late_rows += 1
             self.totals[(c, b)] = self.totals.get((c, b), 0) + n
@@ -210,7 +221,7 @@ class StreamingOperator:
             self.sink([(c, b * self.s.divisor, n) for c, b, n in rows])
         self.rows_written += len(rows)
         if self.watermark is not None:
-            d = self.s.divisor
+            self.flushed_wm = self.watermark
             for b in sorted(self.seen_buckets):
                 if b not in self.closed and (b + 1) * d <= self.watermark:
                     self.closed[b] = now - (b + 1) * d
@@ -232,8 +243,10 @@ class StreamingOperator:
 
     # -- report ------------------------------------------------------------------------
     def latency_summary(self):
-        v = np.array(sorted(self.closed.values()), dtype=np.float64)
+        v = np.array(sorted(x for x in self.closed.values() if x is not None), dtype=np.float64)
+        late_only = sum(1 for x in self.closed.values() if x is None)
         if v.size == 0:
-            return {"windows": 0}
+            return {"windows": 0, "late_only_windows": late_only}
         return {"windows": int(v.size), "p50_ms": float(np.percentile(v, 50)),
-                "p99_ms": float(np.percentile(v, 99)), "max_ms": float(v.max())}
+                "p99_ms": float(np.percentile(v, 99)), "max_ms": float(v.max()),
+                "late_only_windows": late_only}
