@@ -54,6 +54,10 @@ struct ysb_ctx {
     i64 ring_lo = 0;
     OvfEntry* d_ovf = nullptr;
     u32* d_ovf_count = nullptr;
+    SideSlot* d_side = nullptr;               // out-of-ring cells (device hash map)
+    u64 side_slots = 0;
+    u32 side_cbits = 1;
+    u32* d_side_used = nullptr;
     unsigned long long* d_stats = nullptr;
     u64 batches = 0;
     std::map<std::pair<u32, i64>, u64> side;   // drained side-list deltas
@@ -146,6 +150,8 @@ static void destroy(ysb_ctx* c) {
     hipHostFree(c->h_ring);
     hipFree(c->d_ovf);
     hipFree(c->d_ovf_count);
+    hipFree(c->d_side);
+    hipFree(c->d_side_used);
     hipFree(c->d_stats);
     hipFree(c->d_truth);
     hipFree(c->d_truth_out);
@@ -224,6 +230,22 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
         return bad(YSB_ERR_HIP);
     }
     if ((rc = alloc_counts(c)) != YSB_OK) return bad(rc);
+    // out-of-ring map: load <= 1/2 at overflow_capacity distinct cells
+    c->side_slots = 64;
+    while (c->side_slots < 2 * cfg.overflow_capacity) c->side_slots <<= 1;
+    c->side_cbits = 1;
+    while (c->side_cbits < 32 && (1ull << c->side_cbits) <= cfg.n_campaigns) ++c->side_cbits;   // bit_width
+    if (hipMalloc(&c->d_side, c->side_slots * sizeof(SideSlot)) != hipSuccess ||
+        hipMalloc(&c->d_side_used, 8) != hipSuccess ||
+        hipMemset(c->d_side_used, 0, 8) != hipSuccess) {
+        fail(c, YSB_ERR_NOMEM, "device allocation failed");
+        return bad(YSB_ERR_NOMEM);
+    }
+    launch_side_clear(c->d_side, c->side_slots, c->s_comp);
+    if (hipStreamSynchronize(c->s_comp) != hipSuccess) {
+        fail(c, YSB_ERR_HIP, "side map initialisation failed");
+        return bad(YSB_ERR_HIP);
+    }
     if (hipMalloc(&c->d_ring, 16) != hipSuccess || hipHostMalloc(&c->h_ring, 16) != hipSuccess ||
         hipMalloc(&c->d_ovf, cfg.overflow_capacity * sizeof(OvfEntry)) != hipSuccess ||
         hipMalloc(&c->d_ovf_count, 16) != hipSuccess || hipMalloc(&c->d_stats, ST_COUNT_ * 8) != hipSuccess) {
@@ -416,6 +438,10 @@ static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u
     p.require_mask = (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu;
     p.ring = c->d_ring;
     p.div = c->div;
+    p.side = c->d_side;
+    p.side_used = c->d_side_used;
+    p.side_mask = (u32)(c->side_slots - 1);
+    p.side_cbits = c->side_cbits;
     p.ovf = c->d_ovf;
     p.ovf_count = c->d_ovf_count;
     p.ovf_cap = (u32)c->cfg.overflow_capacity;
@@ -590,6 +616,35 @@ static int pull_side_list(ysb_ctx* c) {
         for (const auto& e : v) c->side[{e.campaign, e.bucket}] += e.count;
     }
     if (cnt) HIPCHK(c, hipMemset(c->d_ovf_count, 0, 4));
+    // the out-of-ring map: every occupied slot to the host map, then the map is emptied
+    u32 used = 0;
+    HIPCHK(c, hipMemcpy(&used, c->d_side_used, 4, hipMemcpyDeviceToHost));
+    if (used) {
+        if (!c->d_rows_n) HIPCHK(c, hipMalloc(&c->d_rows_n, 8));
+        u32 k = 0;
+        HIPCHK(c, hipMemsetAsync(c->d_rows_n, 0, 4, c->s_comp));
+        launch_side_compact(c->d_side, c->side_slots, c->side_cbits, true, nullptr, c->d_rows_n, 0, c->s_comp);
+        HIPCHK(c, hipMemcpyAsync(&k, c->d_rows_n, 4, hipMemcpyDeviceToHost, c->s_comp));
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        if (k > c->rows_cap) {
+            hipFree(c->d_rows);
+            c->d_rows = nullptr;
+            const u64 cap = std::max<u64>(k, 4096);
+            HIPCHK(c, hipMalloc(&c->d_rows, cap * sizeof(TableRow)));
+            c->rows_cap = cap;
+        }
+        if (k) {
+            std::vector<TableRow> h(k);
+            HIPCHK(c, hipMemsetAsync(c->d_rows_n, 0, 4, c->s_comp));
+            launch_side_compact(c->d_side, c->side_slots, c->side_cbits, false, c->d_rows, c->d_rows_n, k, c->s_comp);
+            HIPCHK(c, hipMemcpyAsync(h.data(), c->d_rows, (u64)k * sizeof(TableRow), hipMemcpyDeviceToHost, c->s_comp));
+            HIPCHK(c, hipStreamSynchronize(c->s_comp));
+            for (const TableRow& r : h) c->side[{r.campaign, r.bucket}] += r.count;
+        }
+        launch_side_clear(c->d_side, c->side_slots, c->s_comp);
+        HIPCHK(c, hipMemsetAsync(c->d_side_used, 0, 4, c->s_comp));
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    }
     return YSB_OK;
 }
 
@@ -724,6 +779,9 @@ int ysb_reset(ysb_ctx* c) {
     if (c->d_truth) HIPCHK(c, hipMemset(c->d_truth, 0, cells * 8));
     if (c->d_truth_out) HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
     HIPCHK(c, hipMemset(c->d_ovf_count, 0, 16));
+    launch_side_clear(c->d_side, c->side_slots, c->s_comp);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    HIPCHK(c, hipMemset(c->d_side_used, 0, 4));
     HIPCHK(c, hipMemset(c->d_stats, 0, ST_COUNT_ * 8));
     c->side.clear();
     c->batches = 0;
@@ -979,7 +1037,8 @@ int ysb_gen_events_device(ysb_ctx* c, const ysb_gen_params* p, uint64_t first, u
     const GenSpec s = spec_of(p, dsub);
     hipError_t e = gen_events_device(s, first, n, d_out, std::min<u64>(cap, 0xFFFFFFFFull), d_off, nbytes, c->s_comp);
     if (e == hipErrorInvalidValue && *nbytes > cap)
-        return fail(c, YSB_ERR_CAPACITY, "generator output %llu B exceeds cap %llu B", (unsigned long long)*nbytes, (unsigned long long)cap);
+        return fail(c, YSB_ERR_CAPACITY, "generator output %llu B exceeds cap %llu B (u32 offsets: <= 4 GiB per batch)",
+                    (unsigned long long)*nbytes, (unsigned long long)cap);
     if (e != hipSuccess) return fail(c, YSB_ERR_HIP, "device generator: %s", hipGetErrorString(e));
     return YSB_OK;
 }

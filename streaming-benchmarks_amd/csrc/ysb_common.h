@@ -298,6 +298,16 @@ enum : u32 {
     ST_OUT_OF_RING, ST_OVF_DROPPED, ST_DEFERRED, ST_COUNT_
 };
 
+// Out-of-ring (campaign, bucket) cells: an open-addressing device hash map with one
+// 64-bit key per cell (bucket offset by 2^(63 - cbits) in the high bits, campaign in
+// the low cbits = bit_width(n_campaigns) bits, so the all-ones key never occurs and marks
+// an empty slot).  Insert = one 64-bit CAS, then a 64-bit atomic add.
+struct SideSlot {
+    unsigned long long key;
+    unsigned long long count;
+};
+constexpr unsigned long long SIDE_EMPTY = ~0ull;
+
 struct OvfEntry {
     u32 campaign;
     u32 count;

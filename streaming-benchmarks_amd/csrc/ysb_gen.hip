@@ -6,10 +6,17 @@
 
 namespace ysb {
 
-__global__ void gen_len_kernel(GenSpec s, u64 first, u64 n, u32* len) {
+// Line lengths, plus their exact 64-bit total (the u32 offsets of a batch must not wrap).
+__global__ void gen_len_kernel(GenSpec s, u64 first, u64 n, u32* len, unsigned long long* total) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    len[i] = gen_line_len(gen_event(s, first + i));
+    u32 l = 0;
+    if (i < n) {
+        l = gen_line_len(gen_event(s, first + i));
+        len[i] = l;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+    if ((threadIdx.x & 63) == 0 && l) atomicAdd(total, (unsigned long long)l);
 }
 
 // One line per thread, assembled in registers and written as bytes.
@@ -27,10 +34,20 @@ hipError_t gen_events_device(const GenSpec& spec, u64 first, u64 n, u8* d_out, u
                              u64* nbytes, hipStream_t s) {
     if (n == 0) { *nbytes = 0; return hipSuccess; }
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(gen_len_kernel, dim3(blocks), dim3(256), 0, s, spec, first, n, d_off);
-    u32 last_len = 0;
-    hipError_t err = hipMemcpyAsync(&last_len, d_off + n - 1, 4, hipMemcpyDeviceToHost, s);
+    unsigned long long* d_total = nullptr;
+    hipError_t err = hipMalloc(&d_total, 8);
     if (err != hipSuccess) return err;
+    err = hipMemsetAsync(d_total, 0, 8, s);
+    hipLaunchKernelGGL(gen_len_kernel, dim3(blocks), dim3(256), 0, s, spec, first, n, d_off, d_total);
+    unsigned long long total64 = 0;
+    if (err == hipSuccess) err = hipMemcpyAsync(&total64, d_total, 8, hipMemcpyDeviceToHost, s);
+    if (err == hipSuccess) err = hipStreamSynchronize(s);
+    hipFree(d_total);
+    if (err != hipSuccess) return err;
+    if (total64 > cap) {   // includes every total the u32 offsets cannot express
+        *nbytes = total64;
+        return hipErrorInvalidValue;
+    }
     size_t temp = 0;
     err = hipcub::DeviceScan::ExclusiveSum(nullptr, temp, d_off, d_off, (int)n, s);
     if (err != hipSuccess) return err;
@@ -38,14 +55,10 @@ hipError_t gen_events_device(const GenSpec& spec, u64 first, u64 n, u8* d_out, u
     err = hipMalloc(&d_temp, temp ? temp : 16);
     if (err != hipSuccess) return err;
     err = hipcub::DeviceScan::ExclusiveSum(d_temp, temp, d_off, d_off, (int)n, s);
-    u32 last_off = 0;
-    if (err == hipSuccess) err = hipMemcpyAsync(&last_off, d_off + n - 1, 4, hipMemcpyDeviceToHost, s);
     if (err == hipSuccess) err = hipStreamSynchronize(s);
     hipFree(d_temp);
     if (err != hipSuccess) return err;
-    const u64 total = (u64)last_off + last_len;
-    *nbytes = total;
-    if (total > cap) return hipErrorInvalidValue;
+    *nbytes = total64;
     hipLaunchKernelGGL(gen_write_kernel, dim3(blocks), dim3(256), 0, s, spec, first, n, d_off, d_out);
     return hipStreamSynchronize(s);
 }

@@ -38,7 +38,11 @@ struct ScanParams {
     u32 require_mask;           // required-key bit mask
     const i64* ring;            // ring[0] = first bucket, ring[1] = 1 when set
     DivMagic div;
-    OvfEntry* ovf;
+    SideSlot* side;             // out-of-ring cells (hash map)
+    u32* side_used;             // slots taken
+    u32 side_mask;              // slots - 1
+    u32 side_cbits;             // campaign bits of a key
+    OvfEntry* ovf;              // fallback list: buckets a key cannot express, or a full map
     u32* ovf_count;
     u32 ovf_cap;
     u32 tiles_per_block;
@@ -81,5 +85,10 @@ struct TableRow {
 };
 void launch_compact(unsigned long long* table, u32 rows, u32 W, i64 blo, u32 nb, u32 c_off, bool count_only,
                     bool clear, TableRow* out, u32* out_n, u32 cap, hipStream_t s);
+// Empties the out-of-ring map (keys SIDE_EMPTY, counts 0).
+void launch_side_clear(SideSlot* t, u64 slots, hipStream_t s);
+// Every occupied slot of the out-of-ring map as rows (count_only: just the number).
+void launch_side_compact(const SideSlot* t, u64 slots, u32 cbits, bool count_only, TableRow* out, u32* out_n,
+                         u32 cap, hipStream_t s);
 
 }  // namespace ysb

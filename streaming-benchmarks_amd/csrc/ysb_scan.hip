@@ -637,8 +637,27 @@ __device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, const CanonB
     return ok;
 }
 
+// Out-of-ring cell (c, b) += v in the device hash map; false if the key cannot express
+// the bucket or 64 probes find no slot (the caller then appends to the fallback list).
+__device__ __noinline__ bool side_add(const ScanParams& P, u32 c, i64 b, u32 v) {
+    const i64 half = (i64)1 << (63 - P.side_cbits);
+    if (b < -half || b >= half) return false;
+    const unsigned long long key = ((unsigned long long)(b + half) << P.side_cbits) | c;
+    const u32 h = (u32)(mix64(key) >> 32);
+    for (u32 i = 0; i < 64u && i <= P.side_mask; ++i) {
+        SideSlot* sl = &P.side[(h + i) & P.side_mask];
+        const unsigned long long k = atomicCAS(&sl->key, SIDE_EMPTY, key);
+        if (k == SIDE_EMPTY || k == key) {
+            if (k == SIDE_EMPTY) atomicAdd(P.side_used, 1u);
+            atomicAdd(&sl->count, (unsigned long long)v);
+            return true;
+        }
+    }
+    return false;
+}
+
 // Adds v views to (campaign, bucket): the ring cell if the bucket is live, else the
-// exact side list.
+// exact side map (or its fallback list).
 __device__ __forceinline__ void global_add(const ScanParams& P, i64 ring_lo, bool ring_set,
                                            u32 c, i64 b, u32 v, Tally& t) {
     if (ring_set) {
@@ -649,6 +668,7 @@ __device__ __forceinline__ void global_add(const ScanParams& P, i64 ring_lo, boo
         }
     }
     t.oor += v;
+    if (side_add(P, c, b, v)) return;
     const u32 idx = atomicAdd(P.ovf_count, 1u);
     if (idx < P.ovf_cap) {
         OvfEntry en;

@@ -54,4 +54,53 @@ void launch_compact(unsigned long long* table, u32 rows, u32 W, i64 blo, u32 nb,
                        c_off, count_only ? 1 : 0, clear ? 1 : 0, out, out_n, cap);
 }
 
+__global__ __launch_bounds__(AUX_TPB) void side_compact_kernel(const SideSlot* t, u64 slots, u32 cbits,
+                                                               int count_only, TableRow* out, u32* out_n, u32 cap) {
+    u32 mine = 0;
+    const i64 half = (i64)1 << (63 - cbits);
+    for (u64 i = (u64)blockIdx.x * AUX_TPB + threadIdx.x; i < slots; i += (u64)gridDim.x * AUX_TPB) {
+        const SideSlot sl = t[i];
+        if (sl.key == SIDE_EMPTY || sl.count == 0) continue;
+        if (count_only) { ++mine; continue; }
+        const u32 k = atomicAdd(out_n, 1u);
+        if (k < cap) {
+            TableRow r;
+            r.campaign = (u32)(sl.key & ((1ull << cbits) - 1));
+            r.pad = 0;
+            r.bucket = (i64)(sl.key >> cbits) - half;
+            r.count = sl.count;
+            out[k] = r;
+        }
+    }
+    if (count_only) {
+        u32 s = mine;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if ((threadIdx.x & 63) == 0 && s) atomicAdd(out_n, s);
+    }
+}
+
+__global__ __launch_bounds__(AUX_TPB) void side_clear_kernel(SideSlot* t, u64 slots) {
+    for (u64 i = (u64)blockIdx.x * AUX_TPB + threadIdx.x; i < slots; i += (u64)gridDim.x * AUX_TPB) {
+        SideSlot e;
+        e.key = SIDE_EMPTY;
+        e.count = 0;
+        t[i] = e;
+    }
+}
+
+void launch_side_clear(SideSlot* t, u64 slots, hipStream_t s) {
+    if (!slots) return;
+    const u64 blocks = std::min<u64>((slots + AUX_TPB - 1) / AUX_TPB, 4096);
+    hipLaunchKernelGGL(side_clear_kernel, dim3((unsigned)blocks), dim3(AUX_TPB), 0, s, t, slots);
+}
+
+void launch_side_compact(const SideSlot* t, u64 slots, u32 cbits, bool count_only, TableRow* out, u32* out_n,
+                         u32 cap, hipStream_t s) {
+    if (!slots) return;
+    const u64 blocks = std::min<u64>((slots + AUX_TPB - 1) / AUX_TPB, 4096);
+    hipLaunchKernelGGL(side_compact_kernel, dim3((unsigned)blocks), dim3(AUX_TPB), 0, s, t, slots, cbits,
+                       count_only ? 1 : 0, out, out_n, cap);
+}
+
 }  // namespace ysb
