@@ -49,6 +49,10 @@ extern "C" {
                                    AdvertisingTopologyNative.java:267-272)      */
 #define YSB_F_NO_LDS_COUNT 0x4u /* disable the per-workgroup LDS window counters
                                    (every joined view becomes a global atomic)   */
+#define YSB_F_FORMAT_TBL  0x10u /* batches are the fork's pipe-delimited .tbl lines
+                                   user_id|page_id|ad_id|ad_type|event_type|event_time
+                                   (MockWindowedFlatMap, AdvertisingTopologyNative.java:
+                                   197-226) instead of JSON                       */
 #define YSB_F_SPARSE_FAST_JOIN 0x8u /* test hook: leave every other 36-byte key out of
                                    the fast-path cuckoo table, as a failed cuckoo
                                    placement would; its misses then take the
@@ -257,6 +261,14 @@ int         ysb_truth_compare(ysb_ctx* ctx, uint64_t* mismatched_cells,
  * (ad,campaign lines, AdvertisingTopologyNative.java:52) and kafka-json.txt with
  * n_events events (core.clj:76-97). */
 int         ysb_gen_dump(const ysb_gen_params* p, uint64_t n_events, const char* dir);
+/* The fork's events.tbl rows from generator-format JSON lines (the external tool that
+ * wrote conf/benchmarkConf.yaml:6's events.tbl is not in the reference):
+ * user_id|page_id|ad_id|ad_type|event_type|event_time\n per line, values copied raw.
+ * YSB_ERR_FORMAT for a line that is not 7 unescaped "key": "value" pairs in the
+ * generator's key order (core.clj:90-96); YSB_ERR_CAPACITY if out (cap bytes) is short. */
+int         ysb_json_to_tbl(const uint8_t* bytes, uint64_t nbytes, const uint32_t* line_off,
+                            uint64_t n, uint8_t* out, uint64_t cap, uint32_t* out_off,
+                            uint64_t* out_nbytes);
 /* Sharded file-dump mode (config 4's pre-sharded replay files): the id and map files
  * as ysb_gen_dump, and events [0, n_events) split by ysb_route_lines into
  * kafka-json.<r>.txt for r in [0, nranks). */

@@ -59,6 +59,23 @@ def parse_event(line: bytes, require_ip: bool = False) -> dict:
     return out
 
 
+def parse_tbl(line: bytes) -> dict:
+    """MockWindowedFlatMap (AdvertisingTopologyNative.java:197-226): readLine, then
+    line.split("\\|") with Java's limit-0 semantics (trailing empty items dropped);
+    items[5] missing -> ParseError (ArrayIndexOutOfBounds)."""
+    text = line.decode("utf-8", errors="surrogateescape")
+    if text.endswith("\n"):
+        text = text[:-1]
+    if text.endswith("\r"):
+        text = text[:-1]
+    items = text.split("|")
+    while items and items[-1] == "":
+        items.pop()
+    if len(items) < 6:
+        raise ParseError("ArrayIndexOutOfBounds")
+    return dict(zip(("user_id", "page_id", "ad_id", "ad_type", "event_type", "event_time"), items[:6]))
+
+
 def parse_long(s: str) -> int:
     """java.lang.Long.parseLong for ASCII input."""
     if not _LONG.match(s):
@@ -89,13 +106,14 @@ class Result:
                 ("events", "views", "joined", "join_misses", "parse_errors", "time_errors")}
 
 
-def run(lines, ad_to_campaign: dict, divisor: int = 10000, require_ip: bool = False) -> Result:
-    """lines: iterable of bytes (one event each); ad_to_campaign: str -> campaign key."""
+def run(lines, ad_to_campaign: dict, divisor: int = 10000, require_ip: bool = False, fmt: str = "json") -> Result:
+    """lines: iterable of bytes (one event each); ad_to_campaign: str -> campaign key;
+    fmt "json" (DeserializeBolt) or "tbl" (MockWindowedFlatMap's .tbl rows)."""
     r = Result()
     for line in lines:
         r.events += 1
         try:
-            ev = parse_event(line, require_ip)
+            ev = parse_tbl(line) if fmt == "tbl" else parse_event(line, require_ip)
         except ParseError:
             r.parse_errors += 1
             continue

@@ -43,6 +43,9 @@ def lib():
         L.oracle_run.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int64,
                                  C.c_int, C.c_int, C.POINTER(C.POINTER(OracleRow)), C.POINTER(C.c_uint64),
                                  C.POINTER(OracleStats)]
+        L.oracle_run_fmt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int64,
+                                     C.c_int, C.c_int, C.c_int, C.POINTER(C.POINTER(OracleRow)),
+                                     C.POINTER(C.c_uint64), C.POINTER(OracleStats)]
         L.oracle_free_rows.argtypes = [C.POINTER(OracleRow)]
         _LIB = L
     return _LIB
@@ -62,16 +65,17 @@ class AdMap:
             self._h = None
 
 
-def run(admap: AdMap, data, offsets, divisor=10000, require_ip=False, threads=1):
-    """Returns (rows dict {(campaign, bucket): count}, stats dict)."""
+def run(admap: AdMap, data, offsets, divisor=10000, require_ip=False, threads=1, fmt="json"):
+    """Returns (rows dict {(campaign, bucket): count}, stats dict).  fmt: "json" or "tbl"."""
     L = lib()
     buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint32)
     rows = C.POINTER(OracleRow)()
     nrows = C.c_uint64()
     st = OracleStats()
-    rc = L.oracle_run(admap._h, buf.ctypes.data, buf.size, off.ctypes.data, off.size, int(divisor),
-                      int(require_ip), int(threads), C.byref(rows), C.byref(nrows), C.byref(st))
+    rc = L.oracle_run_fmt(admap._h, buf.ctypes.data, buf.size, off.ctypes.data, off.size, int(divisor),
+                          int(require_ip), int(fmt == "tbl"), int(threads), C.byref(rows), C.byref(nrows),
+                          C.byref(st))
     if rc:
         raise RuntimeError("oracle_run failed")
     out = {(rows[i].campaign, rows[i].bucket): rows[i].count for i in range(nrows.value)}

@@ -24,6 +24,7 @@
  *                             Long.parseLong(event_time) / 10000L; seenCount++
  *                             streaming-benchmark-common/.../CampaignProcessorCommon.java:57-67
  *   dostats                   campaign -> bucket -> count                 data/src/setup/core.clj:101-128
+ *   MockWindowedFlatMap       .tbl rows: line.split("\\|")                   :197-226 (oracle_run_fmt)
  *
  * JSON contract (shared with the GPU path, see DESIGN.md "Parity contract"):
  * RFC 8259 objects; raw control characters inside strings are accepted
@@ -304,6 +305,37 @@ static int parse_event(const unsigned char* s, size_t n, unsigned require, field
     return (seen & require) == require;
 }
 
+/* The fork's .tbl rows: MockWindowedFlatMap.flatMap (AdvertisingTopologyNative.java:
+ * 197-226) -- items = line.split("\\|") (java.lang.String.split, limit 0: trailing empty
+ * items dropped), items[0..5] = user_id, page_id, ad_id, ad_type, event_type, event_time;
+ * fewer than 6 items throw (ArrayIndexOutOfBounds).  The line is the batch line minus
+ * its "\n" / "\r\n" terminator (BufferedReader.readLine, :153-159).
+ * 1 = parsed; 0 = the reference would have thrown. */
+static void copy_field(const unsigned char* s, long a, long b, unsigned char* out, size_t cap, long* len) {
+    *len = b - a;
+    if ((size_t)(b - a) <= cap) memcpy(out, s + a, (size_t)(b - a));
+}
+
+static int parse_tbl(const unsigned char* s, size_t n, fields* f) {
+    long e = (long)n;
+    if (e > 0 && s[e - 1] == '\n') --e;
+    if (e > 0 && s[e - 1] == '\r') --e;
+    long bar[6];
+    int k = 0;
+    for (long i = 0; i < e && k < 6; ++i)
+        if (s[i] == '|') bar[k++] = i;
+    if (k < 5) return 0;
+    if (k == 5) bar[5] = e;
+    /* items[5] exists iff a non-'|' byte follows the fifth '|' */
+    int tail = 0;
+    for (long i = bar[4] + 1; i < e && !tail; ++i) tail = s[i] != '|';
+    if (!tail) return 0;
+    copy_field(s, bar[1] + 1, bar[2], f->ad, sizeof f->ad, &f->ad_len);
+    copy_field(s, bar[3] + 1, bar[4], f->et, sizeof f->et, &f->et_len);
+    copy_field(s, bar[4] + 1, bar[5], f->tm, sizeof f->tm, &f->tm_len);
+    return 1;
+}
+
 /* Long.parseLong: [+-]?[0-9]+ in int64 range */
 static int parse_long(const unsigned char* s, long n, int64_t* out) {
     if (n <= 0) return 0;
@@ -360,6 +392,7 @@ typedef struct {
     uint64_t lo, hi, n;
     int64_t divisor;
     unsigned require;
+    int tbl;                 /* 1: .tbl rows instead of JSON */
     count_map out;
     oracle_stats st;
 } job;
@@ -372,7 +405,9 @@ static void* run_job(void* arg) {
         j->st.events++;
         if (e < s || e > j->nbytes) { j->st.parse_errors++; continue; }
         f.ad_len = f.et_len = f.tm_len = 0;
-        if (!parse_event(j->bytes + s, (size_t)(e - s), j->require, &f)) { j->st.parse_errors++; continue; }
+        const int ok = j->tbl ? parse_tbl(j->bytes + s, (size_t)(e - s), &f)
+                              : parse_event(j->bytes + s, (size_t)(e - s), j->require, &f);
+        if (!ok) { j->st.parse_errors++; continue; }
         if (!(f.et_len == 4 && memcmp(f.et, "view", 4) == 0)) continue;           /* EventFilterBolt */
         j->st.views++;
         uint32_t campaign;
@@ -400,9 +435,20 @@ static int row_cmp(const void* a, const void* b) {
 /* Runs the chain over n lines ([off[i], off[i+1]) / last ends at nbytes) with
  * `threads` workers (contiguous line ranges).  Rows are sorted by
  * (campaign, bucket).  Returns 0 on success. */
+int oracle_run_fmt(const void* admap, const uint8_t* bytes, uint64_t nbytes, const uint32_t* off, uint64_t n,
+                   int64_t divisor, int require_ip, int tbl, int threads, oracle_row** rows_out, uint64_t* nrows,
+                   oracle_stats* st);
+
 int oracle_run(const void* admap, const uint8_t* bytes, uint64_t nbytes, const uint32_t* off, uint64_t n,
                int64_t divisor, int require_ip, int threads, oracle_row** rows_out, uint64_t* nrows,
                oracle_stats* st) {
+    return oracle_run_fmt(admap, bytes, nbytes, off, n, divisor, require_ip, 0, threads, rows_out, nrows, st);
+}
+
+/* Same, tbl = 1 for the fork's .tbl rows. */
+int oracle_run_fmt(const void* admap, const uint8_t* bytes, uint64_t nbytes, const uint32_t* off, uint64_t n,
+                   int64_t divisor, int require_ip, int tbl, int threads, oracle_row** rows_out, uint64_t* nrows,
+                   oracle_stats* st) {
     if (divisor < 1 || threads < 1) return -1;
     if ((uint64_t)threads > n && n) threads = (int)n;
     if (n == 0) threads = 1;
@@ -418,6 +464,7 @@ int oracle_run(const void* admap, const uint8_t* bytes, uint64_t nbytes, const u
         jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
         jobs[t].divisor = divisor;
         jobs[t].require = require_ip ? 0x7Fu : 0x3Fu;
+        jobs[t].tbl = tbl;
         if (threads > 1) pthread_create(&th[t], NULL, run_job, &jobs[t]);
         else run_job(&jobs[t]);
     }

@@ -493,8 +493,10 @@ static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_
     p.dbg = c->d_dbg;
 #endif
     poll_ring(c);
+    const bool tbl = (c->cfg.flags & YSB_F_FORMAT_TBL) != 0;
     if (!c->ring_known) {
-        launch_ring_autobase(p, c->s_comp);
+        if (tbl) launch_tbl_ring_autobase(p, c->s_comp);
+        else launch_ring_autobase(p, c->s_comp);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(c->h_ring, c->d_ring, 16, hipMemcpyDeviceToHost, c->s_comp));
         HIPCHK(c, hipEventRecord(c->ev_ring, c->s_comp));
@@ -513,11 +515,14 @@ static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_
         c->tev_used++;
         HIPCHK(c, hipEventRecord(e0, c->s_comp));
     }
-    launch_scan(p, c->s_comp);
+    if (tbl) launch_tbl_scan(p, c->s_comp);
+    else launch_scan(p, c->s_comp);
     HIPCHK(c, hipGetLastError());
     if (e1) HIPCHK(c, hipEventRecord(e1, c->s_comp));
-    launch_defer(p, c->cus, c->s_comp);
-    HIPCHK(c, hipGetLastError());
+    if (!tbl) {
+        launch_defer(p, c->cus, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+    }
     c->batches++;
     return YSB_OK;
 }

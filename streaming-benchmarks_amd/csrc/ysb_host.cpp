@@ -6,6 +6,7 @@
 //   ysb_group_block      campaign block a rank owns after ysb_group_reduce_scatter
 //   ysb_route_lines      per-line ad_id shard of a host batch (host router)
 //   ysb_gen_dump_shards  kafka-json.<r>.txt per shard (config 4's pre-sharded files)
+//   ysb_json_to_tbl      the fork's events.tbl rows from generator JSON lines
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -135,6 +136,50 @@ int ysb_route_lines(const uint8_t* bytes, uint64_t nbytes, const uint32_t* line_
         out_shard[i] = r;
         if (shard_counts) shard_counts[r]++;
     }
+    return YSB_OK;
+}
+
+int ysb_json_to_tbl(const uint8_t* bytes, uint64_t nbytes, const uint32_t* line_off, uint64_t n, uint8_t* out,
+                    uint64_t cap, uint32_t* out_off, uint64_t* out_nbytes) {
+    if ((!bytes && nbytes) || (!line_off && n) || (n && (!out || !out_off)) || !out_nbytes) return YSB_ERR_ARG;
+    static const char* const keys[7] = {"user_id", "page_id", "ad_id", "ad_type", "event_type", "event_time",
+                                        "ip_address"};
+    u64 o = 0;
+    for (u64 i = 0; i < n; ++i) {
+        const u64 s = line_off[i];
+        const u64 e = i + 1 < n ? (u64)line_off[i + 1] : nbytes;
+        if (s > e || e > nbytes) return YSB_ERR_FORMAT;
+        // the quoted strings of the line: key, value, key, value, ...
+        long q[14][2];
+        int k = 0;
+        for (u64 p = s; p < e; ++p) {
+            if (bytes[p] == '\\') return YSB_ERR_FORMAT;
+            if (bytes[p] != '"') continue;
+            u64 t = p + 1;
+            while (t < e && bytes[t] != '"' && bytes[t] != '\\') ++t;
+            if (t >= e || bytes[t] != '"' || k == 14) return YSB_ERR_FORMAT;
+            q[k][0] = (long)(p + 1);
+            q[k][1] = (long)t;
+            ++k;
+            p = t;
+        }
+        if (k != 14) return YSB_ERR_FORMAT;
+        for (int f = 0; f < 7; ++f) {
+            const size_t kl = std::strlen(keys[f]);
+            if ((size_t)(q[2 * f][1] - q[2 * f][0]) != kl || std::memcmp(bytes + q[2 * f][0], keys[f], kl) != 0)
+                return YSB_ERR_FORMAT;
+        }
+        if (o > 0xFFFFFFFFull) return YSB_ERR_CAPACITY;
+        out_off[i] = (u32)o;
+        for (int f = 0; f < 6; ++f) {   // items[0..5] (the .tbl rows carry no ip_address)
+            const u64 len = (u64)(q[2 * f + 1][1] - q[2 * f + 1][0]);
+            if (o + len + 1 > cap) return YSB_ERR_CAPACITY;
+            std::memcpy(out + o, bytes + q[2 * f + 1][0], len);
+            o += len;
+            out[o++] = f < 5 ? '|' : '\n';
+        }
+    }
+    *out_nbytes = o;
     return YSB_OK;
 }
 

@@ -62,6 +62,9 @@ void launch_scan(const ScanParams& p, hipStream_t s);
 void launch_defer(const ScanParams& p, int blocks, hipStream_t s);
 // Sets ring[0..1] from the first lines of a batch if ring[1] == 0.
 void launch_ring_autobase(const ScanParams& p, hipStream_t s);
+// The pipe-delimited .tbl input format (YSB_F_FORMAT_TBL): scan + ring auto-base.
+void launch_tbl_scan(const ScanParams& p, hipStream_t s);
+void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s);
 
 // Generator kernels (ysb_gen.hip).
 hipError_t gen_events_device(const GenSpec& spec, u64 first, u64 n, u8* d_out, u64 cap,

@@ -1076,6 +1076,154 @@ __global__ __launch_bounds__(AUX_TPB) void ring_autobase_kernel(ScanParams P, i6
     }
 }
 
+// ---------------------------------------------------------------------------
+// The fork's live input format: pipe-delimited .tbl lines
+// (MockWindowedFlatMap.flatMap, flink-benchmarks/.../AdvertisingTopologyNative.java:197-226):
+//   items = line.split("\\|")   (java.lang.String.split: trailing empty items dropped)
+//   (items[0..5]) = (user_id, page_id, ad_id, ad_type, event_type, event_time)
+// fewer than 6 items after the trailing-empty drop -> ArrayIndexOutOfBounds (a parse
+// error); then the same filter / join / bucket as the JSON chain (event_time = items[5],
+// the Storm/Spark projection).  The line is the batch line minus its "\n" / "\r\n"
+// terminator (BufferedReader.readLine, :153-159).
+// ---------------------------------------------------------------------------
+template <class S>
+__device__ __forceinline__ bool process_tbl_line(const S& src, int s, int e, const ScanParams& P, Tally& t,
+                                                 u32& campaign, i64& bucket) {
+    t.ev++;
+    if (e > s && src.b(e - 1) == '\n') --e;
+    if (e > s && src.b(e - 1) == '\r') --e;
+    // the first six '|' (p[5] = e when there are only five)
+    int p[6];
+    int k = 0;
+    for (int q = s; q < e && k < 6; ++q)
+        if (src.b(q) == '|') p[k++] = q;
+    if (k < 5) { t.perr++; return false; }
+    if (k == 5) p[5] = e;
+    // items[5] exists iff something other than '|' follows the fifth '|'
+    bool tail = p[5] > p[4] + 1;
+    for (int q = p[5]; !tail && q < e; ++q) tail = src.b(q) != '|';
+    if (!tail) { t.perr++; return false; }
+    const Span et{p[3] + 1, p[4], 0};
+    if (!(et.e - et.s == 4 && src.load4(et.s) == VIEW_W)) return false;   // EventFilterBolt
+    t.view++;
+    const Span ad{p[1] + 1, p[2], 0};
+    u32 kw[KEY_WORDS];
+    u32 klen = 0;
+    int c = -1;
+    if (span_key(src, ad, kw, klen)) c = probe(P.table, P.table_mask, kw, klen);   // RedisJoinBolt
+    if (c < 0) { t.miss++; return false; }
+    t.join++;
+    i64 tv;
+    if (!parse_digits(src, p[4] + 1, p[5], tv)) { t.terr++; return false; }   // Long.parseLong
+    campaign = (u32)c;
+    bucket = div_trunc(tv, P.div);
+    return true;
+}
+
+// One wave per 64-line tile, staged through LDS like the JSON scan; one line per lane.
+__global__ __launch_bounds__(SCAN_TPB) void tbl_scan_kernel(ScanParams P) {
+    extern __shared__ __attribute__((aligned(16))) u8 smem[];
+    u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
+    u32* tb = reinterpret_cast<u32*>(smem + OFF_TB);
+    const int tid = threadIdx.x;
+    const u64 t_begin = (u64)blockIdx.x * P.tiles_per_block;
+    if (t_begin >= P.n_tiles) return;
+    const u64 t_end = min(t_begin + P.tiles_per_block, P.n_tiles);
+    const i64 ring_lo = P.ring[0];
+    const bool ring_set = P.ring[1] != 0;
+    for (u32 i = tid; i <= (u32)(t_end - t_begin); i += SCAN_TPB) {
+        const u64 f = (t_begin + i) * SCAN_TPB;
+        tb[i] = f < P.n ? P.off[f] : (u32)P.nbytes;
+    }
+    __syncthreads();
+    Tally tl{0, 0, 0, 0, 0, 0, 0};
+    uint4 pre[CHUNKS_PER_THREAD];
+    u32 pre_off = 0, pre_end = 0;
+    TileInfo nxt = tile_info(P, t_begin, t_begin, tb);
+    issue_tile_loads(P, nxt, pre, pre_off, pre_end);
+    const LdsSrc lsrc{tile32};
+    for (u64 t = t_begin; t < t_end; ++t) {
+        const TileInfo cur = nxt;
+        const u32 my_off = pre_off;
+        const u32 my_end = (cur.first + tid + 1 < P.n) ? pre_end : (u32)P.nbytes;
+        if (!cur.oversize) {
+#pragma unroll
+            for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
+                const u32 k = (u32)(j * SCAN_TPB + tid);
+                if (j * SCAN_TPB + SCAN_TPB <= TILE_CHUNKS || k < (u32)TILE_CHUNKS) reinterpret_cast<uint4*>(tile32)[k] = pre[j];
+            }
+        }
+        __syncthreads();
+        if (t + 1 < t_end) nxt = tile_info(P, t + 1, t_begin, tb);
+        else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
+        issue_tile_loads(P, nxt, pre, pre_off, pre_end);
+        if ((u32)tid < cur.count) {
+            u32 campaign;
+            i64 bucket;
+            bool ok;
+            if (!cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
+                const int ls = (int)(my_off - cur.s0 + cur.delta), le = (int)(my_end - cur.s0 + cur.delta);
+                ok = process_tbl_line(lsrc, ls, le, P, tl, campaign, bucket);
+            } else if (my_off <= my_end && my_end <= P.nbytes && my_end - my_off <= 0x7FFFFFFFu) {
+                const GlbSrc g{P.bytes + my_off, (u64)(my_end - my_off)};   // over-size tile: from HBM
+                ok = process_tbl_line(g, 0, (int)(my_end - my_off), P, tl, campaign, bucket);
+            } else {
+                tl.ev++;
+                tl.perr++;
+                ok = false;
+            }
+            if (ok) global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+        }
+        __syncthreads();
+    }
+    flush_tally(P, tl, threadIdx.x & 63);
+}
+
+// Ring auto-base for .tbl batches (the JSON one is ring_autobase_kernel).
+__global__ __launch_bounds__(AUX_TPB) void tbl_ring_autobase_kernel(ScanParams P, i64* ring) {
+    __shared__ i64 scratch[AUX_TPB / 64];
+    if (ring[1] != 0) return;
+    const int tid = threadIdx.x;
+    i64 b = INT64_MAX;
+    if ((u64)tid < P.n) {
+        const u64 ls = P.off[tid];
+        const u64 le = ((u64)tid + 1 < P.n) ? (u64)P.off[tid + 1] : P.nbytes;
+        if (ls <= le && le <= P.nbytes && le - ls < 0x7FFFFFFFull) {
+            Tally tl{0, 0, 0, 0, 0, 0, 0};
+            u32 c;
+            i64 bk;
+            const GlbSrc gsrc{P.bytes + ls, le - ls};
+            if (process_tbl_line(gsrc, 0, (int)(le - ls), P, tl, c, bk)) b = bk;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const i64 x = __shfl_xor(b, o, 64);
+        b = x < b ? x : b;
+    }
+    if ((tid & 63) == 0) scratch[tid >> 6] = b;
+    __syncthreads();
+    if (tid == 0) {
+        i64 r = scratch[0];
+        for (int w = 1; w < AUX_TPB / 64; ++w) r = scratch[w] < r ? scratch[w] : r;
+        if (r != INT64_MAX) {
+            ring[0] = r - (i64)(P.ring_w / 8);
+            ring[1] = 1;
+        }
+    }
+}
+
+void launch_tbl_scan(const ScanParams& p, hipStream_t s) {
+    if (p.n == 0) return;
+    const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;
+    hipLaunchKernelGGL(tbl_scan_kernel, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
+}
+
+void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s) {
+    if (p.n == 0) return;
+    hipLaunchKernelGGL(tbl_ring_autobase_kernel, dim3(1), dim3(AUX_TPB), 0, s, p, const_cast<i64*>(p.ring));
+}
+
 void launch_scan(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
     const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;

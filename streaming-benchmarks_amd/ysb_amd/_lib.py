@@ -22,6 +22,7 @@ YSB_F_TIMING = 0x1
 YSB_F_REQUIRE_IP = 0x2
 YSB_F_NO_LDS_COUNT = 0x4
 YSB_F_SPARSE_FAST_JOIN = 0x8
+YSB_F_FORMAT_TBL = 0x10
 INT64_MIN = -(1 << 63)
 UNIQUE_ID_BYTES = 128
 
@@ -98,6 +99,7 @@ SIGNATURES = {
     "ysb_truth_accumulate": (_I, [_P, C.POINTER(YsbGenParams), _U64, _U64]),
     "ysb_truth_compare": (_I, [_P, C.POINTER(_U64), C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_gen_dump": (_I, [C.POINTER(YsbGenParams), _U64, C.c_char_p]),
+    "ysb_json_to_tbl": (_I, [_PU8, _U64, _PU32, _U64, _PU8, _U64, _PU32, C.POINTER(_U64)]),
     "ysb_gen_dump_shards": (_I, [C.POINTER(YsbGenParams), _U64, C.c_char_p, _U32]),
 }
 

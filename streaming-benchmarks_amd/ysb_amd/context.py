@@ -24,7 +24,7 @@ class YsbContext:
     def __init__(self, device=0, n_campaigns=100, time_divisor_ms=10000, window_ring=1024,
                  max_batch_events=1 << 20, max_batch_bytes=256 << 20, ring_base_bucket=None,
                  overflow_capacity=1 << 20, timing=False, require_ip=False, lds_count=True,
-                 sparse_fast_join=False):
+                 sparse_fast_join=False, input_format="json"):
         L = lib()
         cfg = YsbConfig()
         L.ysb_config_default(C.byref(cfg))
@@ -37,7 +37,10 @@ class YsbContext:
         cfg.overflow_capacity = overflow_capacity
         cfg.flags = ((_lib.YSB_F_TIMING if timing else 0) | (_lib.YSB_F_REQUIRE_IP if require_ip else 0)
                      | (0 if lds_count else _lib.YSB_F_NO_LDS_COUNT)
-                     | (_lib.YSB_F_SPARSE_FAST_JOIN if sparse_fast_join else 0))
+                     | (_lib.YSB_F_SPARSE_FAST_JOIN if sparse_fast_join else 0)
+                 | (_lib.YSB_F_FORMAT_TBL if input_format == "tbl" else 0))
+        if input_format not in ("json", "tbl"):
+            raise ValueError("input_format must be 'json' or 'tbl'")
         h = C.c_void_p()
         check(L.ysb_open(C.byref(h), device, C.byref(cfg)), None)
         self._h = h

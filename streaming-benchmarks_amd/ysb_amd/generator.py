@@ -65,6 +65,10 @@ class GenParams:
     def max_line_bytes(self):
         return int(lib().ysb_gen_max_line_bytes(C.byref(self.c)))
 
+    def events_host_tbl(self, first, n):
+        """Events [first, first+n) as .tbl rows (bytes, u32 offsets)."""
+        return json_to_tbl(*self.events_host(first, n))
+
     def events_host(self, first, n):
         """(bytes as uint8 array, uint32 line offsets) of events [first, first+n)."""
         cap = n * self.max_line_bytes()
@@ -81,6 +85,18 @@ class GenParams:
     def dump_shards(self, n_events, directory, nranks):
         """Pre-sharded replay files kafka-json.<r>.txt (ad_id-hash routing) + id/map files."""
         check(lib().ysb_gen_dump_shards(C.byref(self.c), n_events, str(directory).encode(), nranks))
+
+
+def json_to_tbl(raw, offs):
+    """Generator-format JSON lines -> the fork's .tbl rows (bytes as uint8 array, u32 offsets)."""
+    raw = np.ascontiguousarray(raw, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint32)
+    out = np.empty(max(raw.size, 1), dtype=np.uint8)
+    oo = np.empty(max(offs.size, 1), dtype=np.uint32)
+    nb = C.c_uint64()
+    check(lib().ysb_json_to_tbl(C.c_void_p(raw.ctypes.data), raw.size, C.c_void_p(offs.ctypes.data), offs.size,
+                                C.c_void_p(out.ctypes.data), out.size, C.c_void_p(oo.ctypes.data), C.byref(nb)))
+    return out[:nb.value], oo[:offs.size]
 
 
 def ad_shard(ad_id: str, nranks: int) -> int:

@@ -12,6 +12,10 @@ Fixtures (all data, no reference source):
   gen_s7.campaign_ids.txt      campaign UUIDs (core.clj:24-31)
   edge.jsonl / edge_long.jsonl hand-written edge cases (boundaries, reordering,
                                escapes, errors, misses, an over-size line)
+  gen_s7.tbl                   the same 1500 events as the fork's pipe-delimited rows
+                               (MockWindowedFlatMap, AdvertisingTopologyNative.java:197-226)
+  edge_tbl.tbl                 hand-written .tbl edge cases (String.split trailing-empty
+                               rule, too few items, \r\n, empty fields, misses, errors)
   *.expected.csv               campaign_uuid,window_ms,count from oracle/dostats.py
   *.expected.json              the chain's counters (events, views, joined, ...)
 
@@ -174,8 +178,42 @@ def long_lines(ads):
     return out
 
 
-def write_expected(stem, lines, ad_map, campaign_of, require_ip=False):
-    r = dostats.run(lines, ad_map, 10000, require_ip)
+def to_tbl(json_line: bytes) -> bytes:
+    ev = json.loads(json_line)
+    return ("|".join(ev[k] for k in ("user_id", "page_id", "ad_id", "ad_type", "event_type", "event_time"))
+            + "\n").encode()
+
+
+def tbl_edge_lines(ads):
+    a0, a1 = ads[0], ads[7]
+    L = [
+        "u|p|%s|banner|view|1700000000000" % a0,               # no terminator (last line style)
+        "u|p|%s|banner|view|1700000009999\r" % a0,             # \r\n terminator
+        "u|p|%s|banner|view|1700000010000|extra|fields" % a0,  # more than 6 items
+        "u|p|%s|banner|view|" % a0,                            # trailing empty dropped: 5 items
+        "u|p|%s|banner|view||" % a0,                           # still 5 after the drop
+        "u|p|%s|banner|view||x" % a0,                          # items[5] = "" -> parseLong throws
+        "u|p|%s|banner|view" % a0,                             # 5 items
+        "|p|%s||view|1700000020000" % a1,                      # empty items kept
+        "u|p|%s|banner|View|1700000020000" % a1,               # case-sensitive filter
+        "u|p|%s|banner|click|1700000020000" % a1,
+        "u|p|nope|banner|view|1700000020000",                  # join miss
+        "u|p|%s|banner|view|+1700000030000" % a1,              # Long.parseLong accepts '+'
+        "u|p|%s|banner|view|-5" % a1,                          # bucket 0 (truncation)
+        "u|p|%s|banner|view|-10001" % a1,                      # bucket -1
+        "u|p|%s|banner|view|17e3" % a1,                        # time error
+        "u|p|%s|banner|view|9223372036854775807" % a1,         # Long.MAX_VALUE
+        "u|p|%s|banner|view|9223372036854775808" % a1,         # overflow -> time error
+        "",                                                    # empty line
+        "||||||",                                              # all empty
+        "u|p|%s |banner|view|1700000040000" % a1,              # key with a space: miss
+        "u|p|%s|banner|view|1700000040000|" % a1,              # trailing '|' after items[5]
+    ]
+    return [ln.encode() + b"\n" for ln in L]
+
+
+def write_expected(stem, lines, ad_map, campaign_of, require_ip=False, fmt="json"):
+    r = dostats.run(lines, ad_map, 10000, require_ip, fmt)
     suffix = ".ip" if require_ip else ""
     with open(os.path.join(HERE, stem + suffix + ".expected.csv"), "w") as f:
         f.write("campaign_id,window_ms,count\n")
@@ -211,6 +249,14 @@ def main():
     with open(os.path.join(HERE, "edge_long.jsonl"), "wb") as f:
         f.write(b"".join(lng))
     write_expected("edge_long", lng, ad_map, campaign_of)
+    tbl = [to_tbl(ln) for ln in gen]
+    with open(os.path.join(HERE, "gen_s7.tbl"), "wb") as f:
+        f.write(b"".join(tbl))
+    write_expected("gen_s7_tbl", tbl, ad_map, campaign_of, fmt="tbl")
+    et = tbl_edge_lines(ads)
+    with open(os.path.join(HERE, "edge_tbl.tbl"), "wb") as f:
+        f.write(b"".join(et))
+    write_expected("edge_tbl", et, ad_map, campaign_of, fmt="tbl")
     with open(os.path.join(HERE, "gen_s7.params.json"), "w") as f:
         json.dump(dict(GEN, n_events=N_GEN), f, indent=1, sort_keys=True)
         f.write("\n")

@@ -41,12 +41,17 @@ def gen_params():
         return json.load(f)
 
 
-def events(stem):
-    """(raw bytes, line offsets) of tests/golden/<stem>.jsonl."""
-    with open(path(stem + ".jsonl"), "rb") as f:
+def events(stem, ext=".jsonl"):
+    """(raw bytes, line offsets) of tests/golden/<stem><ext>."""
+    with open(path(stem + ext), "rb") as f:
         raw = f.read()
     _, offs = dostats.split_lines(raw)
     return raw, offs
+
+
+def tbl_events(stem):
+    """.tbl fixture (expected-output stem, data file): gen_s7_tbl -> gen_s7.tbl."""
+    return events(TBL_FILES[stem], ".tbl")
 
 
 def expected(stem, require_ip=False):
@@ -65,3 +70,6 @@ def expected(stem, require_ip=False):
 
 
 FIXTURES = [("gen_s7", False), ("edge", False), ("edge", True), ("edge_long", False)]
+# .tbl fixtures: expected-output stem -> data file stem (tests/golden/<file>.tbl)
+TBL_FILES = {"gen_s7_tbl": "gen_s7", "edge_tbl": "edge_tbl"}
+TBL_FIXTURES = sorted(TBL_FILES)

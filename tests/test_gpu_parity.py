@@ -218,3 +218,29 @@ def test_submit_before_ad_map_is_an_error():
     with YsbContext(n_campaigns=10) as ctx:
         with pytest.raises(YsbError):
             ctx.submit(b"{}\n", [0])
+
+
+@pytest.mark.parametrize("stem", gd.TBL_FIXTURES)
+def test_tbl_fixture(stem):
+    """The fork's .tbl rows (YSB_F_FORMAT_TBL) against the golden expectations."""
+    ads, camp = gd.ad_arrays()
+    raw, offs = gd.tbl_events(stem)
+    with YsbContext(n_campaigns=10, input_format="tbl") as ctx:
+        ctx.load_ad_map(ads, camp)
+        ctx.submit(raw, offs)
+        check_against(ctx, *gd.expected(stem))
+
+
+def test_tbl_generated_stream_vs_oracle():
+    g = GenParams(seed=13, n_campaigns=50, ads_per_campaign=10, events_per_sec=1000, with_skew=True)
+    raw, offs = g.events_host_tbl(0, 200_000)
+    _, aids = g.ids()
+    rows, st = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), raw, offs, fmt="tbl", threads=8)
+    with YsbContext(n_campaigns=50, window_ring=64, input_format="tbl", max_batch_bytes=64 << 20,
+                    max_batch_events=1 << 18) as ctx:
+        ctx.load_ad_map(aids, g.ad_campaign_index())
+        ctx.submit(raw, offs)
+        assert ctx.drain_buckets() == rows
+        s = ctx.stats()
+        for k, v in st.items():
+            assert s[k] == v, k
