@@ -447,9 +447,10 @@ static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u
     p.ovf_cap = (u32)c->cfg.overflow_capacity;
     p.stats = c->d_stats;
     p.n_tiles = (n + SCAN_TPB - 1) / SCAN_TPB;
+    // whole rounds of resident workgroups (a partial last round would idle most CUs)
     const u64 resident = (u64)c->cus * SCAN_WG_PER_CU;
-    const u64 blocks = std::max<u64>(std::max<u64>(1, std::min<u64>(p.n_tiles, resident)),
-                                     (p.n_tiles + MAX_TILES_PER_BLOCK - 1) / MAX_TILES_PER_BLOCK);
+    const u64 rounds = std::max<u64>(1, (p.n_tiles + resident * MAX_TILES_PER_BLOCK - 1) / (resident * MAX_TILES_PER_BLOCK));
+    const u64 blocks = std::max<u64>(1, std::min<u64>(p.n_tiles, rounds * resident));
     p.tiles_per_block = (u32)((p.n_tiles + blocks - 1) / blocks);
     return p;
 }

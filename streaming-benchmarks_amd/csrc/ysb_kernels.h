@@ -11,12 +11,18 @@ namespace ysb {
 // and the two waves of a SIMD drift into different phases (one classifying while the
 // other parses), which hides each other's LDS latency.
 constexpr int SCAN_TPB = 64;                  // threads per scan workgroup = lines per tile
-constexpr int SCAN_WG_PER_CU = 8;             // resident scan workgroups per CU (LDS-bound)
+#ifndef YSB_WG_PER_CU
+#define YSB_WG_PER_CU 8
+#endif
+#ifndef YSB_MAX_TILES
+#define YSB_MAX_TILES 128
+#endif
+constexpr int SCAN_WG_PER_CU = YSB_WG_PER_CU; // resident scan workgroups per CU (LDS-bound)
 constexpr int TILE_CAP = SCAN_TPB * 260;      // LDS bytes of one tile (260 B/line average)
 constexpr int TILE_CHUNKS = TILE_CAP / 16;    // 16-byte chunks per tile
 constexpr int CHUNKS_PER_THREAD = (TILE_CHUNKS + SCAN_TPB - 1) / SCAN_TPB;  // 17
 constexpr int LCNT_CAP = 256;                 // u32 per-workgroup (campaign, window) counters
-constexpr int MAX_TILES_PER_BLOCK = 128;      // tile bounds preloaded into LDS
+constexpr int MAX_TILES_PER_BLOCK = YSB_MAX_TILES;   // tile bounds preloaded into LDS
 constexpr int AUX_TPB = 256;                  // threads per workgroup of the other kernels
 
 struct ScanParams {

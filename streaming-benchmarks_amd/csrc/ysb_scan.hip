@@ -639,7 +639,7 @@ __device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, const CanonB
 
 // Out-of-ring cell (c, b) += v in the device hash map; false if the key cannot express
 // the bucket or 64 probes find no slot (the caller then appends to the fallback list).
-__device__ __noinline__ bool side_add(const ScanParams& P, u32 c, i64 b, u32 v) {
+__device__ __forceinline__ bool side_add(const ScanParams& P, u32 c, i64 b, u32 v) {
     const i64 half = (i64)1 << (63 - P.side_cbits);
     if (b < -half || b >= half) return false;
     const unsigned long long key = ((unsigned long long)(b + half) << P.side_cbits) | c;
