@@ -187,6 +187,7 @@ int ysb_gen_dump_shards(const ysb_gen_params* p, uint64_t n_events, const char* 
     if (!p || !dir || nranks == 0) return YSB_ERR_ARG;
     int rc = ysb_gen_dump(p, 0, dir);   // id files and both ad-map formats (no events)
     if (rc) return rc;
+    std::remove((std::string(dir) + "/kafka-json.txt").c_str());
     std::vector<FILE*> f(nranks, nullptr);
     for (u32 r = 0; r < nranks; ++r) {
         const std::string path = std::string(dir) + "/kafka-json." + std::to_string(r) + ".txt";

@@ -127,3 +127,20 @@ def test_event_time_rate(rate):
     for k in range(3):
         j = raw.index(b'"event_time": "', off[k]) + 15
         assert int(raw[j:raw.index(b'"', j)]) == 1_700_000_000_000 + ((123456 + k) * 1000) // rate
+
+
+def test_cli_shards_and_tbl(tmp_path):
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "streaming-benchmarks_amd",
+                       "bin", "ysb_gen")
+    subprocess.run([exe, "-d", str(tmp_path), "-n", "500", "--shards", "2", "--tbl", "--seed", "5"], check=True)
+    parts = [(tmp_path / ("kafka-json.%d.txt" % r)).read_bytes().splitlines() for r in range(2)]
+    assert not (tmp_path / "kafka-json.txt").exists()
+    rows = (tmp_path / "events.tbl").read_bytes().splitlines()
+    assert len(rows) == 500 == sum(len(p) for p in parts)
+    import json as _json
+    tbl_set = set(rows)
+    for ln in parts[0] + parts[1]:
+        ev = _json.loads(ln)
+        assert "|".join(ev[k] for k in ("user_id", "page_id", "ad_id", "ad_type", "event_type",
+                                        "event_time")).encode() in tbl_set
