@@ -18,7 +18,10 @@ constexpr int SCAN_TPB = 64;                  // threads per scan workgroup = li
 #define YSB_MAX_TILES 128
 #endif
 constexpr int SCAN_WG_PER_CU = YSB_WG_PER_CU; // resident scan workgroups per CU (LDS-bound)
-constexpr int TILE_CAP = SCAN_TPB * 260;      // LDS bytes of one tile (260 B/line average)
+#ifndef YSB_TILE_LINE_BYTES
+#define YSB_TILE_LINE_BYTES 260
+#endif
+constexpr int TILE_CAP = SCAN_TPB * YSB_TILE_LINE_BYTES;   // LDS bytes of one tile (per-line average cap)
 constexpr int TILE_CHUNKS = TILE_CAP / 16;    // 16-byte chunks per tile
 constexpr int CHUNKS_PER_THREAD = (TILE_CHUNKS + SCAN_TPB - 1) / SCAN_TPB;  // 17
 constexpr int LCNT_CAP = 256;                 // u32 per-workgroup (campaign, window) counters

@@ -728,6 +728,20 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_
 // displace the join table from L2 (MI355X_MICROARCH.md, row nt-weights).
 constexpr int AUX_NT = 2;
 
+#ifndef YSB_LINE_INTERLEAVE
+#define YSB_LINE_INTERLEAVE 1
+#endif
+// The tile line a lane parses.  Interleaved: lanes 0..31 take the even lines, 32..63 the
+// odd ones, so the start banks of the lines a 32-lane half reads (dword mod 32, lines
+// ~63.5 dwords apart) step by one bank instead of crowding into half of them.
+__device__ __forceinline__ u32 lane_line(int tid) {
+#if YSB_LINE_INTERLEAVE
+    return ((u32)(tid & 31) << 1) | ((u32)tid >> 5);
+#else
+    return (u32)tid;
+#endif
+}
+
 // The next tile's bytes and line offsets, HBM -> registers.  Bounds-checked buffer
 // loads through per-tile descriptors (base = the tile, num_records = its length, so
 // chunks past the tile read zeros and never fault); per-lane offsets are
@@ -751,8 +765,9 @@ __device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const Tile
     const u32 nrec = (u32)min<u64>((u64)ti.count + 1u, left) * 4u;   // my_end of the tile's last line included
     const __amdgpu_buffer_rsrc_t ro =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<u32*>(P.off + min(ti.first, P.n)), 0, (int)nrec, 0x00020000);
-    my_off = __builtin_amdgcn_raw_buffer_load_b32(ro, 4 * tid, 0, 0);
-    my_end = __builtin_amdgcn_raw_buffer_load_b32(ro, 4 * tid + 4, 0, 0);   // 0 past the batch end
+    const u32 li = lane_line(tid);
+    my_off = __builtin_amdgcn_raw_buffer_load_b32(ro, 4 * li, 0, 0);
+    my_end = __builtin_amdgcn_raw_buffer_load_b32(ro, 4 * li + 4, 0, 0);   // 0 past the batch end
 }
 
 __device__ __forceinline__ u32 wave_sum(u32 v) {
@@ -860,7 +875,8 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
     for (u64 t = t_begin; t < t_end; ++t) {
         const TileInfo cur = nxt;
         const u32 my_off = pre_off;
-        const u32 my_end = (cur.first + tid + 1 < P.n) ? pre_end : (u32)P.nbytes;
+        const u32 li = lane_line(tid);
+        const u32 my_end = (cur.first + li + 1 < P.n) ? pre_end : (u32)P.nbytes;
 #ifdef YSB_STAMPS
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: separate the prefetch wait
         STAMP(6);
@@ -905,7 +921,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         CanonA ca;
 #pragma unroll
         for (int k = 0; k < 9; ++k) ca.kw[k] = 0u;
-        if ((u32)tid < cur.count && !cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
+        if (li < cur.count && !cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             ok1 = canon_stage1(lsrc, ls, le, ca);
@@ -915,7 +931,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         CanonB cb;
         cb.view = false;
         bool ok2 = false;
-        if ((u32)tid < cur.count) {
+        if (li < cur.count) {
             ok2 = ok1 && canon_stage2(lsrc, ls, le, ca, cb);
             dfr = !ok2;   // bad offsets, other layouts, escapes, over-size tiles
         }
@@ -938,7 +954,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
                 tok = canonical_bucket(lsrc, cb, ls + ca.e4 + 18, P, bucket);   // Long.parseLong
             }
         }
-        defer_append(P, dfr, cur.first + tid, lane);
+        defer_append(P, dfr, cur.first + li, lane);
         STAMP(2);
         // ---- prefetch the next tile (lands while this one is parsed) -----------
         // Issued on every iteration (the last one loads nothing: out-of-range buffer
@@ -972,7 +988,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
                 if (!tok) tl.terr++;
             }
         }
-        if (P.ctable_partial) defer_append(P, dfr2, cur.first + tid, lane);
+        if (P.ctable_partial) defer_append(P, dfr2, cur.first + li, lane);
         STAMP(3);
         // ---- count: LDS window counters; events outside go straight to the ring -----
         if (WL) {
@@ -1145,7 +1161,8 @@ __global__ __launch_bounds__(SCAN_TPB) void tbl_scan_kernel(ScanParams P) {
     for (u64 t = t_begin; t < t_end; ++t) {
         const TileInfo cur = nxt;
         const u32 my_off = pre_off;
-        const u32 my_end = (cur.first + tid + 1 < P.n) ? pre_end : (u32)P.nbytes;
+        const u32 li = lane_line(tid);
+        const u32 my_end = (cur.first + li + 1 < P.n) ? pre_end : (u32)P.nbytes;
         if (!cur.oversize) {
 #pragma unroll
             for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
@@ -1157,7 +1174,7 @@ __global__ __launch_bounds__(SCAN_TPB) void tbl_scan_kernel(ScanParams P) {
         if (t + 1 < t_end) nxt = tile_info(P, t + 1, t_begin, tb);
         else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
         issue_tile_loads(P, nxt, pre, pre_off, pre_end);
-        if ((u32)tid < cur.count) {
+        if (li < cur.count) {
             u32 campaign;
             i64 bucket;
             bool ok;
