@@ -1,0 +1,537 @@
+// ysb_topology.cpp -- implementation of ysb_topology.hpp (see there for what each class
+// restates from the reference).
+#include "ysb_topology.hpp"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <random>
+#include <sstream>
+
+namespace ysb {
+namespace topology {
+
+// ---- text helpers ----------------------------------------------------------------------------
+
+std::string readFile(const std::string& path) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) throw std::runtime_error("java.io.FileNotFoundException: " + path);
+    std::ostringstream ss;
+    ss << in.rdbuf();
+    return ss.str();
+}
+
+std::vector<std::string> readLines(const std::string& t) {
+    std::vector<std::string> out;
+    size_t p = 0;
+    while (p < t.size()) {
+        size_t q = p;
+        while (q < t.size() && t[q] != '\n' && t[q] != '\r') ++q;
+        out.emplace_back(t, p, q - p);
+        if (q < t.size() && t[q] == '\r' && q + 1 < t.size() && t[q + 1] == '\n') ++q;
+        p = q + 1;
+    }
+    return out;
+}
+
+std::vector<std::string> javaSplit(const std::string& s, char sep) {
+    std::vector<std::string> out;
+    size_t p = 0;
+    while (true) {
+        const size_t q = s.find(sep, p);
+        out.emplace_back(s, p, (q == std::string::npos ? s.size() : q) - p);
+        if (q == std::string::npos) break;
+        p = q + 1;
+    }
+    // "If the expression does not match any part of the input then the resulting array
+    // has just one element, namely this string" -- otherwise drop trailing empties
+    if (out.size() > 1)
+        while (!out.empty() && out.back().empty()) out.pop_back();
+    return out;
+}
+
+static std::string trim(const std::string& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
+    while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t')) --b;
+    return s.substr(a, b - a);
+}
+
+static std::string unquote(const std::string& v) {
+    if (v.size() >= 2 && ((v.front() == '"' && v.back() == '"') || (v.front() == '\'' && v.back() == '\'')))
+        return v.substr(1, v.size() - 2);
+    return v;
+}
+
+// A '#' that starts a comment (at the line start or after blank, outside quotes).
+static std::string strip_comment(const std::string& s) {
+    char q = 0;
+    for (size_t i = 0; i < s.size(); ++i) {
+        const char c = s[i];
+        if (q) {
+            if (c == q) q = 0;
+        } else if (c == '"' || c == '\'') {
+            q = c;
+        } else if (c == '#' && (i == 0 || s[i - 1] == ' ' || s[i - 1] == '\t')) {
+            return s.substr(0, i);
+        }
+    }
+    return s;
+}
+
+// ---- Config ---------------------------------------------------------------------------------
+
+Config Config::parse(const std::string& text) {
+    Config c;
+    std::string list_key;
+    int line_no = 0;
+    for (const std::string& raw : readLines(text)) {
+        ++line_no;
+        const std::string ln = trim(strip_comment(raw));
+        if (ln.empty() || ln == "---") continue;
+        if (ln[0] == '-') {
+            if (list_key.empty())
+                throw std::runtime_error("config line " + std::to_string(line_no) + ": list item without a key");
+            c.lists_[list_key].push_back(unquote(trim(ln.substr(1))));
+            continue;
+        }
+        size_t colon = std::string::npos;
+        for (size_t i = 0; i < ln.size(); ++i)
+            if (ln[i] == ':' && (i + 1 == ln.size() || ln[i + 1] == ' ' || ln[i + 1] == '\t')) { colon = i; break; }
+        if (colon == std::string::npos)
+            throw std::runtime_error("config line " + std::to_string(line_no) + ": expected `key: value`");
+        const std::string key = unquote(trim(ln.substr(0, colon)));
+        const std::string val = trim(ln.substr(colon + 1));
+        if (val.empty()) {
+            list_key = key;
+            c.lists_[key];
+            c.scalars_.erase(key);
+        } else {
+            list_key.clear();
+            c.scalars_[key] = unquote(val);
+            c.lists_.erase(key);
+        }
+    }
+    return c;
+}
+
+Config Config::findAndReadConfigFile(const std::string& path, bool mustExist) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) {
+        if (mustExist) throw std::runtime_error("Could not find config file on classpath " + path);
+        return Config();
+    }
+    std::ostringstream ss;
+    ss << in.rdbuf();
+    Config c = parse(ss.str());
+    if (mustExist && c.scalars_.empty() && c.lists_.empty())
+        throw std::runtime_error("Config file " + path + " doesn't have any valid storm configs");
+    return c;
+}
+
+bool Config::has(const std::string& k) const { return scalars_.count(k) || lists_.count(k); }
+
+const std::string& Config::get(const std::string& k) const {
+    auto it = scalars_.find(k);
+    if (it == scalars_.end()) throw std::runtime_error("No data for required key '" + k + "'");
+    return it->second;
+}
+
+std::string Config::get(const std::string& k, const std::string& dflt) const {
+    auto it = scalars_.find(k);
+    return it == scalars_.end() ? dflt : it->second;
+}
+
+long long Config::getLong(const std::string& k) const {
+    const std::string& v = get(k);
+    char* end = nullptr;
+    errno = 0;
+    const long long x = std::strtoll(v.c_str(), &end, 10);
+    if (errno || end == v.c_str() || *end) throw std::runtime_error("java.lang.NumberFormatException: " + v);
+    return x;
+}
+
+const std::vector<std::string>& Config::getList(const std::string& k) const {
+    auto it = lists_.find(k);
+    if (it == lists_.end()) throw std::runtime_error("No list for required key '" + k + "'");
+    return it->second;
+}
+
+// ---- AdCampaignMap ----------------------------------------------------------------------------
+
+void AdCampaignMap::put(const std::string& ad, const std::string& campaign) {
+    auto ci = campaignIndex_.find(campaign);
+    uint32_t c;
+    if (ci == campaignIndex_.end()) {
+        c = (uint32_t)campaigns.size();
+        campaignIndex_.emplace(campaign, c);
+        campaigns.push_back(campaign);
+    } else {
+        c = ci->second;
+    }
+    auto ai = adIndex_.find(ad);
+    if (ai == adIndex_.end()) {   // HashMap.put: a later duplicate wins
+        adIndex_.emplace(ad, (uint32_t)ads.size());
+        ads.push_back(ad);
+        adCampaign.push_back(c);
+    } else {
+        adCampaign[ai->second] = c;
+    }
+}
+
+AdCampaignMap AdCampaignMap::fromCsv(const std::string& text) {
+    AdCampaignMap m;
+    uint64_t n = 0;
+    for (const std::string& ln : readLines(text)) {
+        ++n;
+        const std::vector<std::string> kv = javaSplit(ln, ',');
+        if (kv.size() < 2)
+            throw std::runtime_error("java.lang.ArrayIndexOutOfBoundsException: 1 (ad map line " + std::to_string(n) + ")");
+        m.put(kv[0], kv[1]);
+    }
+    return m;
+}
+
+AdCampaignMap AdCampaignMap::fromJsonLines(const std::string& text) {
+    AdCampaignMap m;
+    uint64_t n = 0;
+    for (const std::string& ln : readLines(text)) {
+        ++n;
+        if (trim(ln).empty()) continue;
+        // `{ "AD": "CAMPAIGN"}`: the two strings of a one-entry object (no escapes)
+        std::vector<std::string> str;
+        size_t p = 0;
+        while ((p = ln.find('"', p)) != std::string::npos) {
+            const size_t q = ln.find('"', p + 1);
+            if (q == std::string::npos) break;
+            str.push_back(ln.substr(p + 1, q - p - 1));
+            p = q + 1;
+        }
+        if (str.size() != 2 || ln.find('\\') != std::string::npos)
+            throw std::runtime_error("ad map line " + std::to_string(n) + " is not { \"AD\": \"CAMPAIGN\"}");
+        m.put(str[0], str[1]);
+    }
+    return m;
+}
+
+AdCampaignMap AdCampaignMap::fromFile(const std::string& path) {
+    const std::string t = readFile(path);
+    size_t p = 0;
+    while (p < t.size() && (t[p] == ' ' || t[p] == '\n' || t[p] == '\r' || t[p] == '\t')) ++p;
+    return (p < t.size() && t[p] == '{') ? fromJsonLines(t) : fromCsv(t);
+}
+
+// ---- FileBasedDataSource -----------------------------------------------------------------------
+
+FileBasedDataSource::FileBasedDataSource(const std::string& path) {
+    f_ = std::fopen(path.c_str(), "rb");
+    if (!f_) throw std::runtime_error("java.io.FileNotFoundException: " + path);
+}
+
+FileBasedDataSource::~FileBasedDataSource() {
+    if (f_) std::fclose(f_);
+}
+
+uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, uint64_t maxLines, uint64_t* nbytes) {
+    *nbytes = 0;
+    if (!maxLines || !cap) return 0;
+    uint64_t have = std::min<uint64_t>(carry_.size(), cap);
+    if (carry_.size() > cap) throw std::runtime_error("a line is longer than the batch buffer");
+    std::memcpy(buf, carry_.data(), have);
+    carry_.clear();
+    if (!eof_ && have < cap) {
+        const size_t got = std::fread(buf + have, 1, cap - have, f_);
+        if (got < cap - have) eof_ = true;
+        have += got;
+    }
+    if (have == 0) return 0;
+    // complete lines: up to the last '\n' (at end of file, everything)
+    uint64_t end = have;
+    if (!eof_) {
+        const void* nl = memrchr(buf, '\n', have);
+        if (!nl) throw std::runtime_error("a line is longer than the batch buffer");
+        end = (uint64_t)((const uint8_t*)nl - buf) + 1;
+    }
+    uint64_t n = 0, p = 0;
+    while (p < end && n < maxLines) {
+        off[n++] = (uint32_t)p;
+        const void* q = std::memchr(buf + p, '\n', end - p);
+        p = q ? (uint64_t)((const uint8_t*)q - buf) + 1 : end;
+    }
+    // the rest (lines beyond maxLines, then the partial line) waits for the next call
+    carry_.assign(buf + p, buf + have);
+    *nbytes = p;
+    lines_ += n;
+    return n;
+}
+
+// ---- GpuAdCampaignOperator -----------------------------------------------------------------------
+
+GpuAdCampaignOperator::GpuAdCampaignOperator(const AdCampaignMap& map, const Options& o) : map_(map), o_(o) {}
+
+GpuAdCampaignOperator::~GpuAdCampaignOperator() {
+    if (ctx_) ysb_close(ctx_);
+}
+
+void GpuAdCampaignOperator::check(int rc, const char* what) {
+    if (rc != YSB_OK) throw std::runtime_error(std::string(what) + ": " + ysb_last_error(ctx_));
+}
+
+void GpuAdCampaignOperator::open() {
+    ysb_config cfg;
+    ysb_config_default(&cfg);
+    cfg.time_divisor_ms = o_.timeDivisorMs;
+    cfg.n_campaigns = (uint32_t)std::max<size_t>(1, map_.campaigns.size());
+    cfg.window_ring = o_.windowRing;
+    cfg.max_ads = map_.ads.size();
+    cfg.max_batch_bytes = o_.batchBytes;
+    cfg.max_batch_events = o_.batchEvents;
+    cfg.flags = (o_.tbl ? YSB_F_FORMAT_TBL : 0u) | (o_.requireIp ? YSB_F_REQUIRE_IP : 0u);
+    if (ysb_open(&ctx_, o_.device, &cfg) != YSB_OK)
+        throw std::runtime_error(std::string("ysb_open: ") + ysb_last_error(nullptr));
+    // RedisJoinBolt(Map) (:443-448): the whole map on the device
+    std::vector<const char*> keys(map_.ads.size());
+    std::vector<uint32_t> lens(map_.ads.size());
+    for (size_t i = 0; i < map_.ads.size(); ++i) {
+        keys[i] = map_.ads[i].data();
+        lens[i] = (uint32_t)map_.ads[i].size();
+    }
+    check(ysb_load_ad_map(ctx_, keys.data(), lens.data(), map_.adCampaign.data(), map_.ads.size()), "ysb_load_ad_map");
+    for (int s = 0; s < 2; ++s) check(ysb_slot_buffers(ctx_, s, &bytes_[s], &off_[s]), "ysb_slot_buffers");
+}
+
+void GpuAdCampaignOperator::flatMap(const char* line, uint64_t len) {
+    const bool nl = len && line[len - 1] == '\n';
+    const uint64_t need = len + (nl ? 0 : 1);
+    if (need > o_.batchBytes) throw std::runtime_error("record larger than the batch buffer");
+    if (fillBytes_ + need > o_.batchBytes || fillEvents_ == o_.batchEvents) submit();
+    off_[cur_][fillEvents_++] = (uint32_t)fillBytes_;
+    std::memcpy(bytes_[cur_] + fillBytes_, line, len);
+    fillBytes_ += len;
+    if (!nl) bytes_[cur_][fillBytes_++] = '\n';
+}
+
+uint64_t GpuAdCampaignOperator::fillFrom(FileBasedDataSource& src) {
+    uint64_t nb = 0;
+    const uint64_t n = src.fill(bytes_[cur_] + fillBytes_, o_.batchBytes - fillBytes_, off_[cur_] + fillEvents_,
+                                o_.batchEvents - fillEvents_, &nb);
+    for (uint64_t i = 0; i < n; ++i) off_[cur_][fillEvents_ + i] += (uint32_t)fillBytes_;
+    fillBytes_ += nb;
+    fillEvents_ += n;
+    return n;
+}
+
+void GpuAdCampaignOperator::submit() {
+    if (!fillEvents_) return;
+    check(ysb_submit(ctx_, cur_, bytes_[cur_], fillBytes_, off_[cur_], fillEvents_), "ysb_submit");
+    submitted_ += fillEvents_;
+    fillBytes_ = fillEvents_ = 0;
+    cur_ ^= 1;
+    check(ysb_wait(ctx_, cur_), "ysb_wait");   // the other slot's H2D is done: refill it
+}
+
+std::vector<WindowDelta> GpuAdCampaignOperator::flushWindows() {
+    uint64_t n = 0;
+    check(ysb_drain(ctx_, INT64_MIN, INT64_MAX, 0, nullptr, 0, &n), "ysb_drain");
+    std::vector<ysb_count> rows(n ? n : 1);
+    check(ysb_drain(ctx_, INT64_MIN, INT64_MAX, 1, rows.data(), n, &n), "ysb_drain");
+    std::vector<WindowDelta> out;
+    out.reserve(n);
+    for (uint64_t i = 0; i < n; ++i)
+        out.push_back({map_.campaigns[rows[i].campaign], rows[i].window_ms, rows[i].count});
+    return out;
+}
+
+void GpuAdCampaignOperator::close() {
+    submit();
+    check(ysb_sync(ctx_), "ysb_sync");
+}
+
+ysb_stats GpuAdCampaignOperator::stats() {
+    ysb_stats s;
+    check(ysb_stats_get(ctx_, &s), "ysb_stats_get");
+    return s;
+}
+
+// ---- RESP2 client and the Redis writer -----------------------------------------------------------
+
+class RespClient {
+public:
+    RespClient(const std::string& host, int port) {
+        addrinfo hints{}, *res = nullptr;
+        hints.ai_socktype = SOCK_STREAM;
+        if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) || !res)
+            throw std::runtime_error("redis: cannot resolve " + host);
+        fd_ = socket(res->ai_family, res->ai_socktype, res->ai_protocol);
+        const int rc = fd_ < 0 ? -1 : connect(fd_, res->ai_addr, res->ai_addrlen);
+        freeaddrinfo(res);
+        if (rc != 0) throw std::runtime_error("redis: cannot connect to " + host + ":" + std::to_string(port));
+    }
+    ~RespClient() {
+        if (fd_ >= 0) ::close(fd_);
+    }
+    struct Reply {
+        bool nil = false;
+        std::string str;
+        long long num = 0;
+    };
+    // Sends every command, then reads every reply in order.
+    std::vector<Reply> pipeline(const std::vector<std::vector<std::string>>& cmds) {
+        std::string out;
+        for (const auto& c : cmds) {
+            out += "*" + std::to_string(c.size()) + "\r\n";
+            for (const auto& a : c) out += "$" + std::to_string(a.size()) + "\r\n" + a + "\r\n";
+        }
+        for (size_t p = 0; p < out.size();) {
+            const ssize_t w = ::send(fd_, out.data() + p, out.size() - p, 0);
+            if (w <= 0) throw std::runtime_error("redis: send failed");
+            p += (size_t)w;
+        }
+        std::vector<Reply> r;
+        r.reserve(cmds.size());
+        for (size_t i = 0; i < cmds.size(); ++i) r.push_back(reply());
+        return r;
+    }
+
+private:
+    int fd_ = -1;
+    std::string buf_;
+    size_t pos_ = 0;
+    void more() {
+        char tmp[65536];
+        const ssize_t n = ::recv(fd_, tmp, sizeof tmp, 0);
+        if (n <= 0) throw std::runtime_error("redis: connection closed");
+        buf_.erase(0, pos_);
+        pos_ = 0;
+        buf_.append(tmp, (size_t)n);
+    }
+    std::string line() {
+        size_t e;
+        while ((e = buf_.find("\r\n", pos_)) == std::string::npos) more();
+        std::string s = buf_.substr(pos_, e - pos_);
+        pos_ = e + 2;
+        return s;
+    }
+    Reply reply() {
+        const std::string ln = line();
+        Reply r;
+        if (ln.empty()) throw std::runtime_error("redis: empty reply");
+        const std::string rest = ln.substr(1);
+        switch (ln[0]) {
+        case '+': r.str = rest; break;
+        case '-': throw std::runtime_error("redis: " + rest);
+        case ':': r.num = std::stoll(rest); break;
+        case '$': {
+            const long long n = std::stoll(rest);
+            if (n < 0) { r.nil = true; break; }
+            while (buf_.size() - pos_ < (size_t)n + 2) more();
+            r.str = buf_.substr(pos_, (size_t)n);
+            pos_ += (size_t)n + 2;
+            break;
+        }
+        case '*': {
+            const long long n = std::stoll(rest);
+            for (long long i = 0; i < n; ++i) reply();   // not used by the writer
+            break;
+        }
+        default: throw std::runtime_error("redis: bad reply " + ln);
+        }
+        return r;
+    }
+};
+
+std::string randomUuid() {
+    static thread_local std::mt19937_64 rng(std::random_device{}());
+    const uint64_t hi = (rng() & ~0xF000ull) | 0x4000ull;                        // version 4
+    const uint64_t lo = (rng() & 0x3FFFFFFFFFFFFFFFull) | 0x8000000000000000ull;   // IETF variant
+    char b[40];
+    std::snprintf(b, sizeof b, "%08llx-%04llx-%04llx-%04llx-%012llx", (unsigned long long)(hi >> 32),
+                  (unsigned long long)((hi >> 16) & 0xFFFF), (unsigned long long)(hi & 0xFFFF),
+                  (unsigned long long)(lo >> 48), (unsigned long long)(lo & 0xFFFFFFFFFFFFull));
+    return b;
+}
+
+RedisWindowWriter::RedisWindowWriter(const std::string& host, int port) : r_(new RespClient(host, port)) {}
+RedisWindowWriter::~RedisWindowWriter() = default;
+
+void RedisWindowWriter::writeWindows(const std::vector<WindowDelta>& rows) {
+    std::vector<std::pair<std::string, std::string>> need_w;
+    std::vector<std::string> need_l;
+    for (const WindowDelta& d : rows) {
+        if (!d.count) continue;
+        const auto k = std::make_pair(d.campaign, std::to_string(d.windowMs));
+        if (!windowUuid_.count(k) && std::find(need_w.begin(), need_w.end(), k) == need_w.end()) {
+            need_w.push_back(k);
+            if (!listUuid_.count(d.campaign) && std::find(need_l.begin(), need_l.end(), d.campaign) == need_l.end())
+                need_l.push_back(d.campaign);
+        }
+    }
+    // round trip 1: the window / list UUIDs not cached yet (hmget campaign ts, :70)
+    std::vector<std::vector<std::string>> reads;
+    for (const auto& k : need_w) reads.push_back({"HGET", k.first, k.second});
+    for (const auto& c : need_l) reads.push_back({"HGET", c, "windows"});
+    std::vector<RespClient::Reply> got;
+    if (!reads.empty()) {
+        got = r_->pipeline(reads);
+        ++trips_;
+    }
+    for (size_t i = 0; i < need_l.size(); ++i)
+        if (!got[need_w.size() + i].nil) listUuid_[need_l[i]] = got[need_w.size() + i].str;
+    std::vector<std::vector<std::string>> writes;
+    for (size_t i = 0; i < need_w.size(); ++i) {
+        if (!got[i].nil) {
+            windowUuid_[need_w[i]] = got[i].str;
+            continue;
+        }
+        const std::string w = randomUuid();                                          // :72-73
+        windowUuid_[need_w[i]] = w;
+        writes.push_back({"HSET", need_w[i].first, need_w[i].second, w});
+        auto l = listUuid_.find(need_w[i].first);
+        if (l == listUuid_.end()) {                                                  // :75-79
+            l = listUuid_.emplace(need_w[i].first, randomUuid()).first;
+            writes.push_back({"HSET", need_w[i].first, "windows", l->second});
+        }
+        writes.push_back({"LPUSH", l->second, need_w[i].second});                    // :80
+    }
+    // round trip 2: the deltas (:84, :87-88)
+    const std::string now = std::to_string(
+        std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch()).count());
+    for (const WindowDelta& d : rows) {
+        if (!d.count) continue;
+        const std::string& w = windowUuid_[std::make_pair(d.campaign, std::to_string(d.windowMs))];
+        writes.push_back({"HINCRBY", w, "seen_count", std::to_string(d.count)});
+        writes.push_back({"HSET", w, "time_updated", now});
+        writes.push_back({"LPUSH", "time_updated", now});
+    }
+    if (!writes.empty()) {
+        r_->pipeline(writes);
+        ++trips_;
+    }
+}
+
+// ---- CSV sink --------------------------------------------------------------------------------------
+
+void CsvWindowSink::add(const std::vector<WindowDelta>& rows) {
+    for (const WindowDelta& d : rows) totals_[{d.campaign, d.windowMs}] += d.count;
+}
+
+void CsvWindowSink::write(const std::string& path) const {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + path);
+    std::fprintf(f, "campaign_id,window_ms,count\n");
+    for (const auto& t : totals_)
+        if (t.second)
+            std::fprintf(f, "%s,%lld,%llu\n", t.first.first.c_str(), (long long)t.first.second,
+                         (unsigned long long)t.second);
+    std::fclose(f);
+}
+
+}  // namespace topology
+}  // namespace ysb

@@ -1,0 +1,59 @@
+"""GPU: the native runner (bin/ysb_topology) end to end -- config, map, events file,
+pinned double-buffered slots, the fused kernel, flushes -- against the golden
+expectations, through the CSV sink and the Redis sink (check-correct reads CORRECT)."""
+import csv
+import json
+import os
+import subprocess
+
+import pytest
+
+import golden_data as gd
+from fake_redis import FakeRedis
+from test_redis_sink import dostats_shape
+from test_topology import EXE, last_json, write_conf
+from ysb_amd.redis_sink import RespClient, check_correct
+
+pytestmark = pytest.mark.gpu
+
+
+def read_csv(path):
+    idx = gd.campaign_index()
+    with open(path) as f:
+        return {(idx[r["campaign_id"]], int(r["window_ms"]) // 10000): int(r["count"]) for r in csv.DictReader(f)}
+
+
+@pytest.mark.parametrize("events,admap,stem,extra", [
+    ("gen_s7.jsonl", "gen_s7.ad_to_campaign.txt", "gen_s7", []),
+    ("gen_s7.jsonl", "gen_s7.ad_to_campaign.csv", "gen_s7", ["--batch-bytes", "20000", "--batch-events", "50"]),
+    ("edge.jsonl", "gen_s7.ad_to_campaign.txt", "edge", []),
+    ("edge_long.jsonl", "gen_s7.ad_to_campaign.txt", "edge_long", []),
+    ("gen_s7.tbl", "gen_s7.ad_to_campaign.csv", "gen_s7_tbl", ["--batch-bytes", "8192"]),
+    ("edge_tbl.tbl", "gen_s7.ad_to_campaign.txt", "edge_tbl", []),
+])
+def test_runner_csv_sink_matches_golden(tmp_path, events, admap, stem, extra):
+    conf = write_conf(tmp_path, gd.path(events), gd.path(admap))
+    out_csv = tmp_path / "windows.csv"
+    r = subprocess.run([EXE, "--confPath", conf, "--sink", "csv:%s" % out_csv, "--flush-ms", "0"] + extra,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = last_json(r)
+    exp_rows, exp_st = gd.expected(stem)
+    assert read_csv(out_csv) == exp_rows
+    for k, v in exp_st.items():
+        assert out[k] == v, k
+
+
+def test_runner_redis_sink_check_correct(tmp_path):
+    conf = write_conf(tmp_path, gd.path("gen_s7.jsonl"), gd.path("gen_s7.ad_to_campaign.txt"))
+    srv = FakeRedis()
+    try:
+        r = subprocess.run([EXE, "--confPath", conf, "--sink", "redis:127.0.0.1:%d" % srv.port,
+                            "--batch-events", "100", "--flush-ms", "0"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        cli = RespClient("127.0.0.1", srv.port)
+        res = check_correct(cli, dostats_shape())
+        cli.close()
+        assert res and all(s == "CORRECT" for _, _, s, _ in res)
+    finally:
+        srv.close()

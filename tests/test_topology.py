@@ -1,0 +1,141 @@
+"""CPU: the native drop-in runner (streaming-benchmarks_amd/bin/ysb_topology, C++ above
+the C ABI) -- config loading (Utils.findAndReadConfigFile), both ad-map formats
+(getAdCampaignMap, core.clj:58), the events source (FileBasedDataSource) and the C++
+Redis writer, all without a GPU (--dry-run / --replay-rows).  The GPU runs are in
+tests/test_gpu_topology.py."""
+import json
+import os
+import subprocess
+
+import pytest
+
+import golden_data as gd
+from fake_redis import FakeRedis
+from test_redis_sink import canonical, dostats_shape, golden_rows
+from ysb_amd.redis_sink import RespClient, RedisWindowWriter, check_correct
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "streaming-benchmarks_amd", "bin", "ysb_topology")
+
+
+def write_conf(tmp_path, events, admap, extra=""):
+    p = tmp_path / "benchmarkConf.yaml"
+    p.write_text("""# a config with the reference's keys (conf/benchmarkConf.yaml)
+ad_to_campaign_path: "%s"
+
+events_path: '%s'
+kafka.brokers:
+    - "localhost"
+    - other   # a comment
+zookeeper.servers:
+    - "localhost"
+kafka.port: 9092
+redis.host: "localhost"
+redis.hashtable: "t1"
+window.size: 5000
+map.partitions: 3
+reduce.partitions: 1
+%s""" % (admap, events, extra))
+    return str(p)
+
+
+def run(*args, ok=True):
+    r = subprocess.run([EXE] + list(args), capture_output=True, text=True, timeout=120)
+    if ok:
+        assert r.returncode == 0, r.stderr
+    return r
+
+
+def last_json(r):
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("events,admap,n,fmt", [
+    ("gen_s7.jsonl", "gen_s7.ad_to_campaign.txt", 1500, "json"),
+    ("gen_s7.jsonl", "gen_s7.ad_to_campaign.csv", 1500, "json"),
+    ("gen_s7.tbl", "gen_s7.ad_to_campaign.csv", 1500, "tbl"),
+    ("edge_tbl.tbl", "gen_s7.ad_to_campaign.txt", 21, "tbl"),
+])
+def test_dry_run_reads_map_and_events(tmp_path, events, admap, n, fmt):
+    conf = write_conf(tmp_path, gd.path(events), gd.path(admap))
+    out = last_json(run("--confPath", conf, "--dry-run"))
+    assert out["events"] == n and out["format"] == fmt
+    assert out["ads"] == len(gd.ad_map()) and out["campaigns"] == len(gd.campaigns())
+
+
+def test_source_batches_carry_partial_lines(tmp_path):
+    conf = write_conf(tmp_path, gd.path("gen_s7.jsonl"), gd.path("gen_s7.ad_to_campaign.txt"))
+    size = os.path.getsize(gd.path("gen_s7.jsonl"))
+    for extra in (["--batch-bytes", "1000"], ["--batch-events", "7"], ["--batch-bytes", "4096", "--batch-events", "3"]):
+        out = last_json(run("--confPath", conf, "--dry-run", *extra))
+        assert out["events"] == 1500 and out["bytes"] == size and out["batches"] > 1
+
+
+def test_readline_terminators(tmp_path):
+    raw, offs = gd.events("gen_s7")
+    lines = raw.split(b"\n")[:-1]
+    ev = tmp_path / "crlf.jsonl"
+    ev.write_bytes(b"\r\n".join(lines[:100]))          # CRLF, no final terminator
+    conf = write_conf(tmp_path, str(ev), gd.path("gen_s7.ad_to_campaign.txt"))
+    assert last_json(run("--confPath", conf, "--dry-run"))["events"] == 100
+
+
+def test_print_config(tmp_path):
+    conf = write_conf(tmp_path, "/x/events.tbl", gd.path("gen_s7.ad_to_campaign.csv"))
+    r = run("--confPath", conf, "--print-config", "--dry-run", ok=False)
+    cfg = json.loads(r.stdout.splitlines()[0])
+    assert cfg["kafka.brokers"] == ["localhost", "other"]
+    assert cfg["events_path"] == "/x/events.tbl" and cfg["window.size"] == "5000"
+    assert cfg["redis.host"] == "localhost" and cfg["ad_to_campaign_path"].endswith(".csv")
+
+
+def test_reference_errors(tmp_path):
+    r = run("--confPath", str(tmp_path / "nope.yaml"), ok=False)
+    assert r.returncode == 1 and "Could not find config file" in r.stderr
+    bad = tmp_path / "bad.csv"
+    bad.write_text("a1,c1\na2\n")                       # split(",") -> 1 item: kv[1] throws
+    conf = write_conf(tmp_path, gd.path("gen_s7.jsonl"), str(bad))
+    r = run("--confPath", conf, "--dry-run", ok=False)
+    assert r.returncode == 1 and "ArrayIndexOutOfBounds" in r.stderr
+    conf = write_conf(tmp_path, str(tmp_path / "missing.jsonl"), gd.path("gen_s7.ad_to_campaign.csv"))
+    r = run("--confPath", conf, "--dry-run", ok=False)
+    assert r.returncode == 1 and "FileNotFoundException" in r.stderr
+    r = subprocess.run([EXE], capture_output=True, text=True)
+    assert r.returncode == 2 and "confPath" in r.stderr
+
+
+def test_csv_map_later_duplicate_wins(tmp_path):
+    m = tmp_path / "m.csv"
+    m.write_text("a1,c1\na2,c2\na1,c2\n")
+    conf = write_conf(tmp_path, gd.path("gen_s7.jsonl"), str(m))
+    out = last_json(run("--confPath", conf, "--dry-run"))
+    assert out["ads"] == 2 and out["campaigns"] == 2
+
+
+def test_cpp_redis_writer_matches_python_writer(tmp_path):
+    rows = golden_rows()
+    camps = gd.campaigns()
+    csv = tmp_path / "rows.csv"
+    csv.write_text("campaign_id,window_ms,count\n" + "".join("%s,%d,%d\n" % (camps[c], w, n) for c, w, n in rows))
+    conf = write_conf(tmp_path, gd.path("gen_s7.jsonl"), gd.path("gen_s7.ad_to_campaign.txt"))
+    a, b = FakeRedis(), FakeRedis()
+    try:
+        out = last_json(run("--confPath", conf, "--sink", "redis:127.0.0.1:%d" % a.port, "--replay-rows", str(csv)))
+        assert out["rows"] == len(rows) and out["round_trips"] == 2
+        cli = RespClient("127.0.0.1", a.port)
+        assert all(s == "CORRECT" for _, _, s, _ in check_correct(cli, dostats_shape()))
+        cli.close()
+        cb = RespClient("127.0.0.1", b.port)
+        RedisWindowWriter(cb, camps, clock_ms=lambda: 0).write(rows)
+        cb.close()
+        ca, cbb = canonical(a.kv), canonical(b.kv)
+        # time_updated values differ (wall clocks); everything else is identical
+        for kv in (ca, cbb):
+            kv.pop("time_updated")
+            for k, v in kv.items():
+                if isinstance(v, dict):
+                    v.pop("time_updated", None)
+        assert ca == cbb
+    finally:
+        a.close()
+        b.close()
