@@ -3,6 +3,7 @@
 #include "ysb_topology.hpp"
 
 #include <arpa/inet.h>
+#include <fcntl.h>
 #include <netdb.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -14,6 +15,7 @@
 #include <fstream>
 #include <random>
 #include <sstream>
+#include <thread>
 
 namespace ysb {
 namespace topology {
@@ -230,26 +232,58 @@ AdCampaignMap AdCampaignMap::fromFile(const std::string& path) {
 
 // ---- FileBasedDataSource -----------------------------------------------------------------------
 
-FileBasedDataSource::FileBasedDataSource(const std::string& path) {
-    f_ = std::fopen(path.c_str(), "rb");
-    if (!f_) throw std::runtime_error("java.io.FileNotFoundException: " + path);
+FileBasedDataSource::FileBasedDataSource(const std::string& path, unsigned threads) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("java.io.FileNotFoundException: " + path);
+    threads_ = threads ? threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 }
 
 FileBasedDataSource::~FileBasedDataSource() {
-    if (f_) std::fclose(f_);
+    if (fd_ >= 0) ::close(fd_);
+}
+
+// Runs f(t) for t in [0, n) on n threads (inline when n == 1).
+template <class F>
+static void parallel(unsigned n, F f) {
+    if (n <= 1) { f(0u); return; }
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < n; ++t) th.emplace_back(f, t);
+    f(0u);
+    for (auto& x : th) x.join();
 }
 
 uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, uint64_t maxLines, uint64_t* nbytes) {
     *nbytes = 0;
     if (!maxLines || !cap) return 0;
-    uint64_t have = std::min<uint64_t>(carry_.size(), cap);
     if (carry_.size() > cap) throw std::runtime_error("a line is longer than the batch buffer");
+    uint64_t have = carry_.size();
     std::memcpy(buf, carry_.data(), have);
     carry_.clear();
     if (!eof_ && have < cap) {
-        const size_t got = std::fread(buf + have, 1, cap - have, f_);
-        if (got < cap - have) eof_ = true;
-        have += got;
+        // parallel preads of disjoint pieces (>= 4 MiB each) straight into the buffer
+        const uint64_t want = cap - have;
+        const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads_, want >> 22));
+        std::vector<uint64_t> got(T, 0);
+        std::vector<int> err(T, 0);
+        parallel(T, [&](unsigned t) {
+            const uint64_t a = want * t / T, b = want * (t + 1) / T;
+            uint64_t p = a;
+            while (p < b) {
+                const ssize_t r = ::pread(fd_, buf + have + p, b - p, (off_t)(pos_ + p));
+                if (r < 0) { if (errno == EINTR) continue; err[t] = errno; break; }
+                if (r == 0) break;
+                p += (uint64_t)r;
+            }
+            got[t] = p - a;
+        });
+        uint64_t read = 0;
+        for (unsigned t = 0; t < T; ++t) {
+            if (err[t]) throw std::runtime_error(std::string("read: ") + std::strerror(err[t]));
+            read += got[t];
+            if (got[t] < want * (t + 1) / T - want * t / T) { eof_ = true; break; }   // short piece: file end
+        }
+        pos_ += read;
+        have += read;
     }
     if (have == 0) return 0;
     // complete lines: up to the last '\n' (at end of file, everything)
@@ -259,15 +293,31 @@ uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, ui
         if (!nl) throw std::runtime_error("a line is longer than the batch buffer");
         end = (uint64_t)((const uint8_t*)nl - buf) + 1;
     }
-    uint64_t n = 0, p = 0;
-    while (p < end && n < maxLines) {
-        off[n++] = (uint32_t)p;
-        const void* q = std::memchr(buf + p, '\n', end - p);
-        p = q ? (uint64_t)((const uint8_t*)q - buf) + 1 : end;
-    }
+    // line starts: 0 and every byte after a '\n' below `end`, found in parallel pieces
+    const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads_, end >> 22));
+    std::vector<std::vector<uint32_t>> starts(T);
+    parallel(T, [&](unsigned t) {
+        const uint64_t a = end * t / T, b = end * (t + 1) / T;
+        auto& v = starts[t];
+        v.reserve((b - a) / 200 + 16);
+        if (t == 0) v.push_back(0);
+        for (uint64_t p = a; p < b;) {
+            const void* q = std::memchr(buf + p, '\n', b - p);
+            if (!q) break;
+            const uint64_t s = (uint64_t)((const uint8_t*)q - buf) + 1;
+            if (s < end) v.push_back((uint32_t)s);
+            p = s;
+        }
+    });
+    uint64_t n = 0, p_end = end;
+    for (unsigned t = 0; t < T && n < maxLines; ++t)
+        for (uint32_t s : starts[t]) {
+            if (n == maxLines) { p_end = s; break; }
+            off[n++] = s;
+        }
     // the rest (lines beyond maxLines, then the partial line) waits for the next call
-    carry_.assign(buf + p, buf + have);
-    *nbytes = p;
+    carry_.assign(buf + p_end, buf + have);
+    *nbytes = p_end;
     lines_ += n;
     return n;
 }

@@ -82,7 +82,8 @@ private:
 // returns them.
 class FileBasedDataSource {
 public:
-    explicit FileBasedDataSource(const std::string& path);
+    // threads: readers/splitters per block (0 = min(16, hardware threads)).
+    explicit FileBasedDataSource(const std::string& path, unsigned threads = 0);
     ~FileBasedDataSource();
     FileBasedDataSource(const FileBasedDataSource&) = delete;
     FileBasedDataSource& operator=(const FileBasedDataSource&) = delete;
@@ -92,7 +93,9 @@ public:
     uint64_t linesRead() const { return lines_; }
 
 private:
-    FILE* f_ = nullptr;
+    int fd_ = -1;
+    uint64_t pos_ = 0;                  // file offset of the next read
+    unsigned threads_ = 1;
     std::vector<uint8_t> carry_;
     bool eof_ = false;
     uint64_t lines_ = 0;

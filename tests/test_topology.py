@@ -139,3 +139,16 @@ def test_cpp_redis_writer_matches_python_writer(tmp_path):
     finally:
         a.close()
         b.close()
+
+
+def test_parallel_source_on_a_large_file(tmp_path):
+    """Blocks of >= 8 MiB take the multi-threaded pread + split path."""
+    d = tmp_path / "gen"
+    d.mkdir()
+    gen = os.path.join(ROOT, "streaming-benchmarks_amd", "bin", "ysb_gen")
+    subprocess.run([gen, "-d", str(d), "-n", "250000", "--seed", "9"], check=True)
+    ev = d / "kafka-json.txt"
+    conf = write_conf(tmp_path, str(ev), str(d / "ad-to-campaign.csv"))
+    for extra in (["--batch-mb", "16"], ["--batch-mb", "9", "--batch-events", "40000"], ["--batch-mb", "256"]):
+        out = last_json(run("--confPath", conf, "--dry-run", *extra))
+        assert out["events"] == 250000 and out["bytes"] == os.path.getsize(ev), extra
