@@ -12,6 +12,7 @@ e.g. campaign-ids.txt, core.clj:24-31); the index space is what the device count
 from __future__ import annotations
 
 import json
+import re
 
 
 class AdCampaignMap:
@@ -35,9 +36,17 @@ class AdCampaignMap:
 
     @classmethod
     def from_csv(cls, data: bytes, campaigns=None):
+        """readLine + String.split(",") (trailing empty items dropped) + kv[0] -> kv[1];
+        a line with fewer than two items raises IndexError (ArrayIndexOutOfBounds)."""
+        text = data.decode("utf-8")
+        lines = re.split(r"\r\n|\r|\n", text)
+        if text.endswith(("\n", "\r")) or not text:
+            lines.pop()                       # readLine: no empty line after the last terminator
         pairs = []
-        for ln in data.decode("utf-8").splitlines():
+        for ln in lines:
             kv = ln.split(",")
+            while len(kv) > 1 and kv[-1] == "":
+                kv.pop()
             pairs.append((kv[0], kv[1]))
         return cls(pairs, campaigns)
 
