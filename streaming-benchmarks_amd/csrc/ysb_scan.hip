@@ -728,6 +728,9 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_
 // displace the join table from L2 (MI355X_MICROARCH.md, row nt-weights).
 constexpr int AUX_NT = 2;
 
+#ifndef YSB_SETPRIO
+#define YSB_SETPRIO 1
+#endif
 #ifndef YSB_LINE_INTERLEAVE
 #define YSB_LINE_INTERLEAVE 1
 #endif
@@ -871,6 +874,11 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
 
     const LdsSrc lsrc{tile32};
     const uint4* ct4 = reinterpret_cast<const uint4*>(P.ctable);
+#if YSB_SETPRIO
+    // static priority for every other workgroup: the two waves of a SIMD stop trading
+    // VALU issue by age (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+#endif
     STAMP_DECL
     for (u64 t = t_begin; t < t_end; ++t) {
         const TileInfo cur = nxt;
