@@ -152,3 +152,38 @@ def test_line_larger_than_slot_is_an_error():
     op = StreamingOperator(OracleSlots(oracle.AdMap(ads, camp), cap_bytes=64, cap_events=4), clock_ms=Clock())
     with pytest.raises(ValueError):
         op.append(np.frombuffer(raw, dtype=np.uint8), np.asarray(offs, dtype=np.uint32))
+
+
+def test_sharded_streaming_operators_share_one_redis():
+    """configs[4] across GPUs: one operator per rank on its ad_id shard of the stream
+    (ysb_route_lines); their HINCRBY deltas meet in one Redis, exactly as the reference's
+    parallel CampaignProcessor instances' do -- no exchange needed on the streaming path."""
+    from fake_redis import FakeRedis
+    from ysb_amd import route_lines, split_batch
+    from ysb_amd.redis_sink import RedisWindowWriter, RespClient, check_correct
+    g = GenParams(seed=23, n_campaigns=10, ads_per_campaign=10, events_per_sec=2000, with_skew=True,
+                  t0_ms=1_700_000_000_000)
+    raw, offs = g.events_host(0, 60_000)
+    camps, aids = g.ids()
+    shard, _ = route_lines(raw, offs, 3)
+    srv = FakeRedis()
+    try:
+        for r in range(3):
+            br, bo = split_batch(raw, offs, shard, r)
+            cli = RespClient("127.0.0.1", srv.port)
+            writer = RedisWindowWriter(cli, camps, clock_ms=lambda: 0)
+            op = StreamingOperator(OracleSlots(admap_gen(g), cap_bytes=1 << 18, cap_events=700),
+                                   sink=writer.write, clock_ms=Clock(1_700_000_000_000.0))
+            op.append(br, bo)
+            op.close()
+            cli.close()
+        ref, _ = oracle.run(admap_gen(g), raw, offs)
+        expected = {}
+        for (c, b), n in ref.items():
+            expected.setdefault(camps[c], {})[b] = n
+        cli = RespClient("127.0.0.1", srv.port)
+        res = check_correct(cli, expected)
+        cli.close()
+        assert res and all(s == "CORRECT" for _, _, s, _ in res)
+    finally:
+        srv.close()
