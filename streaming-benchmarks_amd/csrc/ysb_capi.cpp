@@ -430,6 +430,8 @@ static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u
     p.ctable_mask = (u32)(c->ctable_slots - 1);
     p.cseed = c->cseed;
     p.ctable_partial = c->ctable_partial ? 1u : 0u;
+    // tables far beyond the L2s (32 MiB) go to HBM per probe: serial slots halve the lines
+    p.probe_serial = c->ctable_slots * CSLOT_WORDS * 4 > (64ull << 20) ? 1u : 0u;
     p.n_campaigns = c->cfg.n_campaigns;
     p.counts = c->d_counts;
     p.ring_w = c->cfg.window_ring;

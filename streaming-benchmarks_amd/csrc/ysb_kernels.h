@@ -38,6 +38,7 @@ struct ScanParams {
     const u32* ctable;          // 36-byte-key cuckoo table, CSLOT_WORDS u32 per slot
     u32 ctable_mask;
     u32 ctable_partial;         // 1: some 36-byte key missed the cuckoo build (misses defer)
+    u32 probe_serial;           // 1: probe the second cuckoo slot only after a first-slot miss
     CuckooSeed cseed;
     u32 n_campaigns;
     unsigned long long* counts; // [c_pad][W] u64, campaign-major

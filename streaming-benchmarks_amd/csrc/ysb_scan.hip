@@ -835,6 +835,9 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #define STAMP(i) do { } while (0)
 #endif
 
+// SERIAL: probe the second cuckoo slot only after a first-slot miss (HBM-resident table);
+// a separate instantiation so the cache-resident configuration's code is untouched.
+template <bool SERIAL>
 __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(ScanParams P) {
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
     u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
@@ -948,12 +951,20 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         // of the lanes: scattered loads cost address-unit time per lane), issued before
         // the time parse and the next tile's prefetch so their latency hides under both
         // and waiting for them never waits for the prefetch.
+        // Cache-resident table (config 2): both slots at once.  HBM-resident table
+        // (config 3, P.probe_serial): the second slot only after the first missed -- the
+        // build places almost every key in its first slot, so this halves the random
+        // HBM lines per view at the price of a dependent load for the few others.
         uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, a2 = a0, b0 = a0, b1 = a0, b2 = a0;
+        u32 ib_s = 0;
         if (pend) {
             u32 ia, ib;
             cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
             a0 = ct4[3 * (u64)ia]; a1 = ct4[3 * (u64)ia + 1]; a2 = ct4[3 * (u64)ia + 2];
-            b0 = ct4[3 * (u64)ib]; b1 = ct4[3 * (u64)ib + 1]; b2 = ct4[3 * (u64)ib + 2];
+            ib_s = ib;
+            if constexpr (!SERIAL) {
+                b0 = ct4[3 * (u64)ib]; b1 = ct4[3 * (u64)ib + 1]; b2 = ct4[3 * (u64)ib + 2];
+            }
         }
         if (ok2) {
             tl.ev++;
@@ -974,6 +985,14 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         // ---- Phase B2: join result ------------------------------------------------
         bool valid = false, dfr2 = false;
         u32 campaign = 0;
+        if (SERIAL && pend) {   // the second slot only when the first does not hold the key
+            const u32* k = ca.kw;
+            const u32 da0 = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
+                            (a1.y ^ k[5]) | (a1.z ^ k[6]) | (a1.w ^ k[7]) | (a2.x ^ k[8]);
+            if (da0 != 0u || a2.y == EMPTY_SLOT) {
+                b0 = ct4[3 * (u64)ib_s]; b1 = ct4[3 * (u64)ib_s + 1]; b2 = ct4[3 * (u64)ib_s + 2];
+            }
+        }
         if (pend) {
             const u32* k = ca.kw;
             const u32 da = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
@@ -1010,7 +1029,9 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
                 }
             }
         } else if (valid) {
+#ifndef YSB_DIAG_NO_COUNT
             global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+#endif
         }
         STAMP(4);
         __syncthreads();
@@ -1252,7 +1273,8 @@ void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s) {
 void launch_scan(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
     const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    hipLaunchKernelGGL(scan_kernel, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
+    if (p.probe_serial) hipLaunchKernelGGL(scan_kernel<true>, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
+    else hipLaunchKernelGGL(scan_kernel<false>, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
 }
 
 void launch_defer(const ScanParams& p, int blocks, hipStream_t s) {
