@@ -127,11 +127,12 @@ def stream(args):
     g = GenParams(seed=7, n_campaigns=100, ads_per_campaign=10, events_per_sec=rate, with_skew=True, n_users=100,
                   t0_ms=t0_ms)
     _, aids = g.ids()
-    per_batch = max(1, rate // 10)
+    per_batch = max(1, rate * args.batch_ms // 1000)
     cap_b = per_batch * g.max_line_bytes() * 2
     ctx = YsbContext(n_campaigns=100, window_ring=16, max_batch_bytes=cap_b, max_batch_events=per_batch * 2)
     ctx.load_ad_map(aids, g.ad_campaign_index())
-    op = StreamingOperator(SlotContext(ctx), batch_interval_ms=100, flush_interval_ms=1000)
+    op = StreamingOperator(SlotContext(ctx), batch_interval_ms=args.batch_ms, flush_interval_ms=1000,
+                           max_out_of_orderness_ms=args.ooo_ms)
     n_total = rate * args.seconds
     produced = 0
     behind_max = 0.0
@@ -179,8 +180,9 @@ def stream(args):
         ref = c2.drain_buckets()
     lat = op.latency_summary()
     return {"config": "configs[4] on 1 GPU: real-time producer %d events/s for %d s, skew +-50 ms, late p=1e-5 "
-                      "(core.clj:166-174); 100 ms batches, watermark close" % (rate, args.seconds),
+                      "(core.clj:166-174); %d ms batches, watermark close" % (rate, args.seconds, args.batch_ms),
             "events": op.events, "batches": op.batches, "flushes": op.flushes, "window_close_latency": lat,
+            "batch_interval_ms": args.batch_ms, "max_out_of_orderness_ms": args.ooo_ms,
             "late_rows": op.late_rows, "open_at_end": op.open_at_end,
             "producer_max_behind_ms": round(behind_max, 1),
             "exact_vs_batch_path": op.totals == ref, "rows": len(ref)}
@@ -196,6 +198,8 @@ def main():
     ap.add_argument("--seconds", type=int, default=10)
     ap.add_argument("--rate", type=int, default=1_000_000)
     ap.add_argument("--ring", type=int, default=128)
+    ap.add_argument("--batch-ms", type=int, default=100)
+    ap.add_argument("--ooo-ms", type=int, default=100)
     args = ap.parse_args()
     out = {"config3": config3, "pcie": pcie, "stream": stream}[args.mode](args)
     print(json.dumps(out), flush=True)
