@@ -199,7 +199,10 @@ YSB_HD u32 key_hash(const u32* w, u32 len) {
 // colliding key family seed-dependent, so a failed build is cured by a new seed),
 // then avalanches: x = XOR rotl(w_k + s_k, R_k), y = SUM (w_k ^ s'_k).
 // ---------------------------------------------------------------------------
-enum : u32 { CSLOT_WORDS = 12, CKEY_WORDS = 9, CSLOT_CAMP = 9 };
+#ifndef YSB_CSLOT_WORDS
+#define YSB_CSLOT_WORDS 12
+#endif
+enum : u32 { CSLOT_WORDS = YSB_CSLOT_WORDS, CKEY_WORDS = 9, CSLOT_CAMP = 9, CSLOT_Q = YSB_CSLOT_WORDS / 4 };
 
 struct CuckooSeed {
     u32 s[CKEY_WORDS];   // additive salts of the XOR fold

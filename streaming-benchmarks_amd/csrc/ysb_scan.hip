@@ -960,10 +960,10 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         if (pend) {
             u32 ia, ib;
             cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
-            a0 = ct4[3 * (u64)ia]; a1 = ct4[3 * (u64)ia + 1]; a2 = ct4[3 * (u64)ia + 2];
+            a0 = ct4[CSLOT_Q * (u64)ia]; a1 = ct4[CSLOT_Q * (u64)ia + 1]; a2 = ct4[CSLOT_Q * (u64)ia + 2];
             ib_s = ib;
             if constexpr (!SERIAL) {
-                b0 = ct4[3 * (u64)ib]; b1 = ct4[3 * (u64)ib + 1]; b2 = ct4[3 * (u64)ib + 2];
+                b0 = ct4[CSLOT_Q * (u64)ib]; b1 = ct4[CSLOT_Q * (u64)ib + 1]; b2 = ct4[CSLOT_Q * (u64)ib + 2];
             }
         }
         if (ok2) {
@@ -990,7 +990,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
             const u32 da0 = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
                             (a1.y ^ k[5]) | (a1.z ^ k[6]) | (a1.w ^ k[7]) | (a2.x ^ k[8]);
             if (da0 != 0u || a2.y == EMPTY_SLOT) {
-                b0 = ct4[3 * (u64)ib_s]; b1 = ct4[3 * (u64)ib_s + 1]; b2 = ct4[3 * (u64)ib_s + 2];
+                b0 = ct4[CSLOT_Q * (u64)ib_s]; b1 = ct4[CSLOT_Q * (u64)ib_s + 1]; b2 = ct4[CSLOT_Q * (u64)ib_s + 2];
             }
         }
         if (pend) {
