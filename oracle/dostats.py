@@ -1,14 +1,18 @@
-"""Second, independent CPU restatement of the YSB hot path, on Python's json module.
+"""Second CPU restatement of the YSB hot path, in Python.
 
 TEST INFRASTRUCTURE ONLY (imported by tests/ and tests/golden/make_golden.py); the
 product never imports it.  Parity status: UNPINNED against the reference itself --
 the reference is Java/Clojure, cannot run here, and ships no golden vectors
 (data/test/setup/core_test.clj:8-10 always fails).  It exists to pin
-oracle/ysb_oracle.c through a different JSON implementation.
+oracle/ysb_oracle.c through an independent implementation.
 
 It follows:
   dostats                 data/src/setup/core.clj:101-128   (campaign -> bucket -> count)
   DeserializeBolt         flink-benchmarks/.../AdvertisingTopologyNative.java:263-272
+                          new JSONObject(line) + getString x6: oracle/orgjson.py (org.json
+                          20180813).  parse_event_strict is the Jackson-style strict view
+                          dostats itself reads the file with (clj-json 0.5.3, core.clj:103);
+                          on the generator's lines the two agree (tests/test_orgjson.py).
   EventFilterBolt         :434              event_type.equals("view")
   RedisJoinBolt           :461-474          map miss -> drop (dostats instead counts
                                             under a nil campaign, core.clj:112; the
@@ -21,6 +25,8 @@ from __future__ import annotations
 import json
 import re
 from dataclasses import dataclass, field
+
+from oracle import orgjson
 
 REQUIRED_FLINK = ("user_id", "page_id", "ad_id", "ad_type", "event_type", "event_time")
 RECOGNISED = REQUIRED_FLINK + ("ip_address",)
@@ -36,8 +42,25 @@ def _reject_constant(name):  # NaN / Infinity are not JSON
 
 
 def parse_event(line: bytes, require_ip: bool = False) -> dict:
-    """JSONObject(line) + getString of the required fields; raises ParseError where
-    org.json would throw (malformed, duplicate key, missing / non-string field)."""
+    """new JSONObject(line) + getString of the required fields (org.json 20180813,
+    oracle/orgjson.py); raises ParseError where DeserializeBolt would throw."""
+    try:
+        obj = orgjson.parse_object(line)
+    except (orgjson.JSONException, RecursionError) as e:
+        raise ParseError(str(e)) from None
+    out = {}
+    for k in (RECOGNISED if require_ip else REQUIRED_FLINK):
+        v = orgjson.string_value(obj.get(k.encode()))
+        if v is None:
+            raise ParseError("JSONObject[%s] not a string." % k)
+        out[k] = v.decode("utf-8", errors="surrogateescape")
+    return out
+
+
+def parse_event_strict(line: bytes, require_ip: bool = False) -> dict:
+    """The strict (RFC 8259, Jackson-style) reading of a line: dostats' own view of the
+    generator's file; raises ParseError on malformed JSON, a duplicate recognised key or
+    a missing / non-string field."""
     text = line.decode("utf-8", errors="surrogateescape")
     if not text.lstrip(" \t\n\r").startswith("{"):
         raise ParseError("not an object")
@@ -106,14 +129,17 @@ class Result:
                 ("events", "views", "joined", "join_misses", "parse_errors", "time_errors")}
 
 
-def run(lines, ad_to_campaign: dict, divisor: int = 10000, require_ip: bool = False, fmt: str = "json") -> Result:
+def run(lines, ad_to_campaign: dict, divisor: int = 10000, require_ip: bool = False, fmt: str = "json",
+        strict: bool = False) -> Result:
     """lines: iterable of bytes (one event each); ad_to_campaign: str -> campaign key;
-    fmt "json" (DeserializeBolt) or "tbl" (MockWindowedFlatMap's .tbl rows)."""
+    fmt "json" (DeserializeBolt, org.json) or "tbl" (MockWindowedFlatMap's .tbl rows);
+    strict=True reads JSON with parse_event_strict instead."""
     r = Result()
+    parse = parse_event_strict if strict else parse_event
     for line in lines:
         r.events += 1
         try:
-            ev = parse_tbl(line) if fmt == "tbl" else parse_event(line, require_ip)
+            ev = parse_tbl(line) if fmt == "tbl" else parse(line, require_ip)
         except ParseError:
             r.parse_errors += 1
             continue

@@ -8,8 +8,8 @@
  * Parity status: UNPINNED against the reference itself.  The reference is
  * Java/Clojure (no JDK, Leiningen or network here) and holds no golden vectors
  * (data/test/setup/core_test.clj:8-10 is a placeholder that always fails), so
- * this file is pinned by (a) an independent second restatement built on Python's
- * json module (oracle/dostats.py) over the committed fixtures in tests/golden/,
+ * this file is pinned by (a) an independent second restatement in Python
+ * (oracle/dostats.py + oracle/orgjson.py) over the committed fixtures in tests/golden/,
  * and (b) hand-derived known answers from the reference's arithmetic.
  *
  * What it restates, line by line:
@@ -26,10 +26,8 @@
  *   dostats                   campaign -> bucket -> count                 data/src/setup/core.clj:101-128
  *   MockWindowedFlatMap       .tbl rows: line.split("\\|")                   :197-226 (oracle_run_fmt)
  *
- * JSON contract (shared with the GPU path, see DESIGN.md "Parity contract"):
- * RFC 8259 objects; raw control characters inside strings are accepted
- * (json.loads(strict=False)); org.json leniencies (single quotes, unquoted
- * strings, trailing commas, '=' / ';' separators) are rejected.
+ * JSON contract (shared with the GPU path, see DESIGN.md "Parity contract"): org.json
+ * 20180813's own grammar, restated below (and independently in oracle/orgjson.py).
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -100,14 +98,72 @@ void oracle_admap_free(void* mp) {
     free(m);
 }
 
-/* ---------------- a strict JSON reader for one line ---------------- */
+/* ---------------- org.json 20180813: JSONTokener / JSONObject over one line ----------------
+ * Third-party dependency absent from /root/reference (org.json:json:20180813, pom.xml:24).
+ * Restated from its published algorithm, at byte level (structural chars are ASCII; every
+ * non-ASCII byte is >= ' ' and no delimiter, as Java's non-ASCII chars are):
+ *   next()        a NUL byte or the end of the line is the end of input
+ *   nextClean()   skips every char <= ' '
+ *   nextString(q) q is '"' or '\''; escapes b t n f r u " ' \ /; raw CR / LF / end throws;
+ *                 \uXXXX = (char) Integer.parseInt(next(4), 16) (a sign is accepted)
+ *   nextValue()   string | JSONObject | JSONArray | unquoted text up to a char < ' ' or one
+ *                 of ,:]}/\"[{;=#, String.trim()'d, "" throws, then stringToValue
+ *   JSONObject    '{' (key ':' value) separated by ',' or ';', a separator may precede '}';
+ *                 key = nextValue().toString(); any repeated key throws; nothing after the
+ *                 closing '}' is read
+ *   JSONArray     '[' values separated by ',', empty slots are nulls, "[1,]" closes
+ *   getString     the value must be a String
+ * Whenever org.json reads past the end and steps back, every continuation throws, so
+ * back() after the end fails at once.  Limits shared with oracle/orgjson.py and the GPU
+ * (DESIGN.md section 3): Double / container keys compare by source text; nesting depth
+ * TK_MAX_DEPTH; non-ASCII digits in \u escapes are rejected. */
+#define TK_MAX_DEPTH 64
+
+typedef struct { uint32_t off, len; } kspan;
 typedef struct {
     const unsigned char* s;
-    size_t n, p;
-} rd;
+    long n, p;
+    int eof;
+    unsigned char* arena; size_t acap, alen;   /* decoded key / value bytes */
+    kspan* keys; size_t kcap, klen;             /* keys of the open objects, innermost last */
+} tk;
 
-static int ws(int c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
-static void skipws(rd* r) { while (r->p < r->n && ws(r->s[r->p])) r->p++; }
+static int tk_next(tk* t) {
+    if (t->p >= t->n) { t->eof = 1; return -1; }
+    t->eof = 0;
+    return t->s[t->p++];
+}
+static int tk_back(tk* t) {
+    if (t->eof) return 0;
+    t->p--;
+    return 1;
+}
+static int tk_clean(tk* t) {
+    for (;;) {
+        int c = tk_next(t);
+        if (c < 0 || c > 0x20) return c;
+    }
+}
+static int ar_put(tk* t, int c) {
+    if (t->alen == t->acap) {
+        size_t nc = t->acap ? 2 * t->acap : 4096;
+        unsigned char* q = (unsigned char*)realloc(t->arena, nc);
+        if (!q) return 0;
+        t->arena = q;
+        t->acap = nc;
+    }
+    t->arena[t->alen++] = (unsigned char)c;
+    return 1;
+}
+static int ar_cp(tk* t, unsigned cp) {   /* UTF-8; lone surrogates in the 3-byte form */
+    if (cp < 0x80) return ar_put(t, (int)cp);
+    if (cp < 0x800) return ar_put(t, (int)(0xC0 | (cp >> 6))) && ar_put(t, (int)(0x80 | (cp & 0x3F)));
+    if (cp < 0x10000)
+        return ar_put(t, (int)(0xE0 | (cp >> 12))) && ar_put(t, (int)(0x80 | ((cp >> 6) & 0x3F))) &&
+               ar_put(t, (int)(0x80 | (cp & 0x3F)));
+    return ar_put(t, (int)(0xF0 | (cp >> 18))) && ar_put(t, (int)(0x80 | ((cp >> 12) & 0x3F))) &&
+           ar_put(t, (int)(0x80 | ((cp >> 6) & 0x3F))) && ar_put(t, (int)(0x80 | (cp & 0x3F)));
+}
 static int hexv(int c) {
     if (c >= '0' && c <= '9') return c - '0';
     if (c >= 'a' && c <= 'f') return c - 'a' + 10;
@@ -115,193 +171,383 @@ static int hexv(int c) {
     return -1;
 }
 
-/* Reads a string at r->p (which is '"'); decodes into out (cap bytes kept),
- * returns decoded length or -1.  Decoding to UTF-8 mirrors Java's String equality
- * of the decoded value. */
-static long read_string(rd* r, unsigned char* out, size_t cap) {
-    size_t n = 0;
-    r->p++;
-#define PUT(ch) do { if (n < cap) out[n] = (unsigned char)(ch); n++; } while (0)
-    while (r->p < r->n) {
-        int c = r->s[r->p];
-        if (c == '"') { r->p++; return (long)n; }
-        if (c != '\\') { PUT(c); r->p++; continue; }
-        if (r->p + 1 >= r->n) return -1;
-        int x = r->s[r->p + 1];
-        switch (x) {
-            case '"': PUT('"'); r->p += 2; break;
-            case '\\': PUT('\\'); r->p += 2; break;
-            case '/': PUT('/'); r->p += 2; break;
-            case 'b': PUT(8); r->p += 2; break;
-            case 'f': PUT(12); r->p += 2; break;
-            case 'n': PUT(10); r->p += 2; break;
-            case 'r': PUT(13); r->p += 2; break;
-            case 't': PUT(9); r->p += 2; break;
-            case 'u': {
-                if (r->p + 5 >= r->n) return -1;
-                unsigned cp = 0;
-                for (int k = 2; k < 6; ++k) {
-                    int h = hexv(r->s[r->p + k]);
-                    if (h < 0) return -1;
-                    cp = cp * 16 + (unsigned)h;
-                }
-                r->p += 6;
-                if (cp >= 0xD800 && cp < 0xDC00 && r->p + 5 < r->n && r->s[r->p] == '\\' && r->s[r->p + 1] == 'u') {
-                    unsigned lo = 0;
-                    int ok = 1;
-                    for (int k = 2; k < 6; ++k) {
-                        int h = hexv(r->s[r->p + k]);
-                        if (h < 0) { ok = 0; break; }
-                        lo = lo * 16 + (unsigned)h;
-                    }
-                    if (ok && lo >= 0xDC00 && lo < 0xE000) {
-                        cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
-                        r->p += 6;
-                    }
-                }
-                if (cp < 0x80) PUT(cp);
-                else if (cp < 0x800) { PUT(0xC0 | (cp >> 6)); PUT(0x80 | (cp & 0x3F)); }
-                else if (cp < 0x10000) { PUT(0xE0 | (cp >> 12)); PUT(0x80 | ((cp >> 6) & 0x3F)); PUT(0x80 | (cp & 0x3F)); }
-                else { PUT(0xF0 | (cp >> 18)); PUT(0x80 | ((cp >> 12) & 0x3F)); PUT(0x80 | ((cp >> 6) & 0x3F)); PUT(0x80 | (cp & 0x3F)); }
-                break;
-            }
-            default: return -1;
-        }
-    }
-#undef PUT
-    return -1;
-}
-
-static int read_value(rd* r, int depth);
-
-static int read_number(rd* r) {
-    size_t p = r->p;
-    if (p < r->n && r->s[p] == '-') p++;
-    if (p >= r->n) return 0;
-    if (r->s[p] == '0') p++;
-    else if (r->s[p] >= '1' && r->s[p] <= '9') { while (p < r->n && r->s[p] >= '0' && r->s[p] <= '9') p++; }
-    else return 0;
-    if (p < r->n && r->s[p] == '.') {
-        size_t q = ++p;
-        while (p < r->n && r->s[p] >= '0' && r->s[p] <= '9') p++;
-        if (p == q) return 0;
-    }
-    if (p < r->n && (r->s[p] == 'e' || r->s[p] == 'E')) {
-        p++;
-        if (p < r->n && (r->s[p] == '+' || r->s[p] == '-')) p++;
-        size_t q = p;
-        while (p < r->n && r->s[p] >= '0' && r->s[p] <= '9') p++;
-        if (p == q) return 0;
-    }
-    r->p = p;
-    return 1;
-}
-
-static int read_lit(rd* r, const char* w) {
-    size_t k = strlen(w);
-    if (r->p + k > r->n || memcmp(r->s + r->p, w, k) != 0) return 0;
-    r->p += k;
-    return 1;
-}
-
-static int read_container(rd* r, int depth, int obj) {
-    if (depth > 64) return 0;
-    r->p++;
-    skipws(r);
-    int close = obj ? '}' : ']';
-    if (r->p < r->n && r->s[r->p] == close) { r->p++; return 1; }
+/* nextString after the opening quote q: decoded bytes appended to the arena. */
+static int tk_string(tk* t, int q) {
+    int pend = -1;   /* high surrogate from \u waiting for its low half */
     for (;;) {
-        skipws(r);
-        if (obj) {
-            if (r->p >= r->n || r->s[r->p] != '"') return 0;
-            unsigned char tmp[1];
-            if (read_string(r, tmp, 0) < 0) return 0;
-            skipws(r);
-            if (r->p >= r->n || r->s[r->p] != ':') return 0;
-            r->p++;
-            skipws(r);
+        int c = tk_next(t);
+        if (c < 0 || c == '\n' || c == '\r') return 0;                 /* Unterminated string */
+        if (c == '\\') {
+            c = tk_next(t);
+            if (c == 'u') {
+                int d[4];
+                for (int k = 0; k < 4; ++k)
+                    if ((d[k] = tk_next(t)) < 0) return 0;                /* Substring bounds error */
+                int neg = d[0] == '-', k0 = (d[0] == '-' || d[0] == '+') ? 1 : 0;
+                int v = 0;
+                for (int k = k0; k < 4; ++k) {
+                    int h = hexv(d[k]);
+                    if (h < 0) return 0;                                  /* NumberFormatException */
+                    v = v * 16 + h;
+                }
+                unsigned u = (unsigned)(neg ? -v : v) & 0xFFFFu;
+                if (pend >= 0 && u >= 0xDC00 && u < 0xE000) {
+                    if (!ar_cp(t, 0x10000u + (((unsigned)pend - 0xD800u) << 10) + (u - 0xDC00u))) return 0;
+                    pend = -1;
+                    continue;
+                }
+                if (pend >= 0 && !ar_cp(t, (unsigned)pend)) return 0;
+                pend = -1;
+                if (u >= 0xD800 && u < 0xDC00) pend = (int)u;
+                else if (!ar_cp(t, u)) return 0;
+                continue;
+            }
+            int v;
+            switch (c) {
+                case 'b': v = 8; break;
+                case 't': v = 9; break;
+                case 'n': v = 10; break;
+                case 'f': v = 12; break;
+                case 'r': v = 13; break;
+                case '"': case '\'': case '\\': case '/': v = c; break;
+                default: return 0;                                        /* Illegal escape. */
+            }
+            if (pend >= 0 && !ar_cp(t, (unsigned)pend)) return 0;
+            pend = -1;
+            if (!ar_put(t, v)) return 0;
+            continue;
         }
-        if (!read_value(r, depth + 1)) return 0;
-        skipws(r);
-        if (r->p >= r->n) return 0;
-        if (r->s[r->p] == ',') { r->p++; continue; }
-        if (r->s[r->p] == close) { r->p++; return 1; }
-        return 0;
+        if (pend >= 0 && !ar_cp(t, (unsigned)pend)) return 0;
+        pend = -1;
+        if (c == q) return 1;
+        if (!ar_put(t, c)) return 0;
     }
 }
 
-static int read_value(rd* r, int depth) {
-    if (r->p >= r->n) return 0;
-    int c = r->s[r->p];
-    if (c == '"') { unsigned char tmp[1]; return read_string(r, tmp, 0) >= 0; }
-    if (c == '{') return read_container(r, depth, 1);
-    if (c == '[') return read_container(r, depth, 0);
-    if (c == 't') return read_lit(r, "true");
-    if (c == 'f') return read_lit(r, "false");
-    if (c == 'n') return read_lit(r, "null");
-    return read_number(r);
+/* ---- JSONObject.stringToValue: the type an unquoted token becomes ---- */
+enum { TOK_STR, TOK_BOOL_T, TOK_BOOL_F, TOK_NULL, TOK_LONG, TOK_DOUBLE };
+
+/* String.equalsIgnoreCase(w) for w in true/false/null: ASCII folding plus U+017F (long s,
+ * C5 BF), whose upper case is 'S'. */
+static int tok_ieq(const unsigned char* s, long n, const char* w) {
+    long i = 0;
+    for (; *w; ++w) {
+        if (i >= n) return 0;
+        int c = s[i];
+        if (*w == 's' && c == 0xC5 && i + 1 < n && s[i + 1] == 0xBF) { i += 2; continue; }
+        if (c >= 'A' && c <= 'Z') c += 32;
+        if (c != *w) return 0;
+        ++i;
+    }
+    return i == n;
+}
+
+static const char DBL_HALF[] =   /* 2^1024 - 2^970: at or above rounds to Infinity */
+    "179769313486231580793728971405303415079934132710037826936173778980444968292764750946649017977587207096330"
+    "286416692887910946555547851940402630657488671505820681908902000708383676273854845817711531764475730270069"
+    "855571366959622842914819860834936475292719074168444365510704342711559699508093042880177904174497792";
+
+static int is_sfx(int c) { return c == 'f' || c == 'F' || c == 'd' || c == 'D'; }
+
+/* Double.valueOf's hexadecimal branch after "0x": accepted and finite? */
+static int hex_double_finite(const unsigned char* s, long n) {
+    long i = 0, nd = 0, frac = 0, first = -1;
+    int dot = 0;
+    for (; i < n; ++i) {
+        if (hexv(s[i]) >= 0) {
+            if (first < 0 && hexv(s[i]) != 0) first = nd;
+            ++nd;
+            if (dot) ++frac;
+        } else if (s[i] == '.' && !dot) dot = 1;
+        else break;
+    }
+    const long mend = i;
+    if (nd == 0 || i >= n || (s[i] != 'p' && s[i] != 'P')) return 0;
+    ++i;
+    int neg = 0;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; ++i; }
+    long a = i;
+    int64_t e = 0, big = 0;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i) {
+        e = e * 10 + (s[i] - '0');
+        if (e > 0x7FFFFFFF) { big = 1; e = 0x7FFFFFFF; }
+    }
+    if (i == a) return 0;
+    if (i < n && !(i == n - 1 && is_sfx(s[i]))) return 0;
+    if (big) return neg;                             /* Integer.parseInt overflow: zero / Infinity */
+    if (first < 0) return 1;                         /* zero */
+    /* bit length of the significand from its first non-zero hex digit */
+    int lead = 0;
+    long k = 0, digit_idx = 0;
+    for (k = 0; k < mend; ++k) {
+        if (s[k] == '.') continue;
+        if (digit_idx == first) { lead = hexv(s[k]); break; }
+        ++digit_idx;
+    }
+    int lb = 0;
+    while ((1 << (lb + 1)) <= lead) ++lb;            /* floor(log2(lead)) */
+    const long L = 4 * (nd - first - 1) + lb + 1;    /* significant bits */
+    const int64_t top = L - 1 + (neg ? -e : e) - 4 * frac;
+    if (top != 1023) return top < 1023;
+    if (L <= 53) return 1;
+    /* rounds up to 2^1024 iff the leading 54 significant bits are all ones */
+    long need = 54, bit_pos = 0;
+    for (k = 0, digit_idx = 0; k < mend && bit_pos < need; ++k) {
+        if (s[k] == '.') continue;
+        if (digit_idx++ < first) continue;
+        int v = hexv(s[k]);
+        int nb = bit_pos == 0 ? lb + 1 : 4;
+        for (int b = nb - 1; b >= 0 && bit_pos < need; --b, ++bit_pos)
+            if (!((v >> b) & 1)) return 1;
+    }
+    return bit_pos < need;
+}
+
+/* Double.valueOf(s) accepted and finite (FloatingDecimal.readJavaFormatString). */
+static int double_finite(const unsigned char* s, long n) {
+    long i = 0;
+    if (i < n && (s[i] == '+' || s[i] == '-')) ++i;
+    if (i + 1 < n && s[i] == '0' && (s[i + 1] == 'x' || s[i + 1] == 'X')) return hex_double_finite(s + i + 2, n - i - 2);
+    long nd = 0, ints = 0, first = -1;
+    int dot = 0;
+    const long d0 = i;
+    for (; i < n; ++i) {
+        if (s[i] >= '0' && s[i] <= '9') {
+            if (first < 0 && s[i] != '0') first = nd;
+            ++nd;
+            if (!dot) ++ints;
+        } else if (s[i] == '.' && !dot) dot = 1;
+        else break;
+    }
+    const long dend = i;
+    if (nd == 0) return 0;
+    int64_t e = 0;
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+        ++i;
+        int neg = 0;
+        if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; ++i; }
+        long a = i;
+        for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i)
+            if (e < 100000000) e = e * 10 + (s[i] - '0');   /* saturates far beyond any boundary */
+        if (i == a) return 0;
+        if (neg) e = -e;
+    }
+    if (i < n && !(i == n - 1 && is_sfx(s[i]))) return 0;
+    if (first < 0) return 1;                                     /* zero */
+    const int64_t mag = ints - first + e;                         /* value = 0.d... x 10^mag */
+    if (mag != 309) return mag < 309;
+    long h = 0, k = 0, idx = 0;
+    for (k = d0; k < dend; ++k) {                                 /* compare the digits with DBL_HALF */
+        if (s[k] == '.') continue;
+        if (idx++ < first) continue;
+        int c = s[k], hc = h < 309 ? DBL_HALF[h] : '0';
+        ++h;
+        if (c != hc) return c < hc;
+    }
+    for (; h < 309; ++h)
+        if (DBL_HALF[h] != '0') return 1;
+    return 0;                                                     /* equal: ties to Infinity */
+}
+
+/* Long.valueOf(s) succeeds and Long.toString equals s. */
+static int long_roundtrip(const unsigned char* s, long n) {
+    long i = 0;
+    int neg = 0;
+    if (n > 0 && s[0] == '-') { neg = 1; i = 1; }
+    long nd = n - i;
+    if (nd <= 0 || nd > 19) return 0;
+    if (nd > 1 && s[i] == '0') return 0;
+    if (neg && nd == 1 && s[i] == '0') return 0;
+    for (long k = i; k < n; ++k)
+        if (s[k] < '0' || s[k] > '9') return 0;
+    if (nd < 19) return 1;
+    const char* lim = neg ? "9223372036854775808" : "9223372036854775807";
+    return memcmp(s + i, lim, 19) <= 0;
+}
+
+static int token_kind(const unsigned char* s, long n) {
+    if (tok_ieq(s, n, "true")) return TOK_BOOL_T;
+    if (tok_ieq(s, n, "false")) return TOK_BOOL_F;
+    if (tok_ieq(s, n, "null")) return TOK_NULL;
+    if ((s[0] >= '0' && s[0] <= '9') || s[0] == '-') {
+        int decimal = (n == 2 && s[0] == '-' && s[1] == '0');
+        for (long k = 0; k < n && !decimal; ++k) decimal = s[k] == '.' || s[k] == 'e' || s[k] == 'E';
+        if (decimal) { if (double_finite(s, n)) return TOK_DOUBLE; }
+        else if (long_roundtrip(s, n)) return TOK_LONG;
+    }
+    return TOK_STR;
 }
 
 /* The fields DeserializeBolt reads (AdvertisingTopologyNative.java:267-272) and,
  * for the Storm/Spark deserializers, ip_address (AdvertisingTopology.java:62). */
 static const char* const KEYS[7] = {"user_id", "page_id", "ad_id", "ad_type", "event_type", "event_time", "ip_address"};
 
-typedef struct {
+typedef struct fields_ {
     unsigned char ad[64]; long ad_len;
     unsigned char et[16]; long et_len;
     unsigned char tm[256]; long tm_len;
 } fields;
 
-/* 1 = parsed; 0 = org.json would have thrown */
-static int parse_event(const unsigned char* s, size_t n, unsigned require, fields* f) {
-    rd r = {s, n, 0};
-    unsigned seen = 0;
-    skipws(&r);
-    if (r.p >= r.n || s[r.p] != '{') return 0;
-    r.p++;
-    skipws(&r);
-    if (r.p < r.n && s[r.p] == '}') {
-        r.p++;
-    } else {
-        for (;;) {
-            skipws(&r);
-            if (r.p >= r.n || s[r.p] != '"') return 0;
-            unsigned char key[16];
-            long kl = read_string(&r, key, sizeof key);
-            if (kl < 0) return 0;
-            int kid = -1;
+/* nextValue: kind V_STR (decoded bytes at arena[a0, alen)), V_TOK (source [a, b)), V_OBJ,
+ * V_ARR (source [a, b)). */
+enum { V_STR, V_TOK, V_OBJ, V_ARR };
+typedef struct { int kind; long a, b; size_t a0; } tval;
+
+static int tk_object(tk* t, int depth, unsigned require, unsigned* seen, fields* f);
+static int tk_array(tk* t, int depth);
+
+static int tk_value(tk* t, int depth, tval* v) {
+    int c = tk_clean(t);
+    if (c == '"' || c == '\'') {
+        v->kind = V_STR;
+        v->a0 = t->alen;
+        return tk_string(t, c);
+    }
+    if (c == '{' || c == '[') {
+        if (!tk_back(t)) return 0;
+        v->kind = c == '{' ? V_OBJ : V_ARR;
+        v->a = t->p;
+        if (!(c == '{' ? tk_object(t, depth + 1, 0, NULL, NULL) : tk_array(t, depth + 1))) return 0;
+        v->b = t->p;
+        return 1;
+    }
+    v->kind = V_TOK;
+    v->a = c < 0 ? t->p : t->p - 1;
+    while (c >= 0x20 && !strchr(",:]}/\\\"[{;=#", c)) c = tk_next(t);
+    if (!tk_back(t)) return 0;
+    long b = t->p;
+    while (b > v->a && t->s[b - 1] == ' ') --b;                  /* String.trim() */
+    v->b = b;
+    return b > v->a;                                              /* "" -> Missing value */
+}
+
+
+static void keep(const unsigned char* src, long n, unsigned char* out, size_t cap, long* len) {
+    *len = n;
+    if ((size_t)n <= cap) memcpy(out, src, (size_t)n);
+}
+
+/* JSONObject(JSONTokener).  At depth 1, f / seen / require collect the event fields:
+ * seen gets bit k when KEYS[k] holds a String. */
+static int tk_object(tk* t, int depth, unsigned require, unsigned* seen, fields* f) {
+    (void)require;
+    if (depth > TK_MAX_DEPTH) return 0;
+    if (tk_clean(t) != '{') return 0;                            /* must begin with '{' */
+    const size_t kmark = t->klen, amark = t->alen;
+    int ok = 0;
+    for (;;) {
+        int c = tk_clean(t);
+        if (c < 0) break;                                         /* must end with '}' */
+        if (c == '}') { ok = 1; break; }
+        if (!tk_back(t)) break;
+        tval kv;
+        if (!tk_value(t, depth, &kv)) break;
+        /* key = nextValue().toString() into the arena */
+        size_t ka;
+        if (kv.kind == V_STR) {
+            ka = kv.a0;
+        } else {
+            ka = t->alen;
+            const char* lit = NULL;
+            if (kv.kind == V_TOK) {
+                int k = token_kind(t->s + kv.a, kv.b - kv.a);
+                lit = k == TOK_BOOL_T ? "true" : k == TOK_BOOL_F ? "false" : k == TOK_NULL ? "null" : NULL;
+            }
+            int good = 1;
+            if (lit) for (; *lit && good; ++lit) good = ar_put(t, *lit);
+            else for (long k = kv.a; k < kv.b && good; ++k) good = ar_put(t, t->s[k]);
+            if (!good) break;
+        }
+        const uint32_t klen = (uint32_t)(t->alen - ka);
+        if (tk_clean(t) != ':') break;                            /* Expected a ':' after a key */
+        int dup = 0;
+        for (size_t k = kmark; k < t->klen && !dup; ++k)
+            dup = t->keys[k].len == klen && memcmp(t->arena + t->keys[k].off, t->arena + ka, klen) == 0;
+        if (dup) break;                                           /* Duplicate key */
+        if (t->klen == t->kcap) {
+            size_t nc = t->kcap ? 2 * t->kcap : 64;
+            kspan* q = (kspan*)realloc(t->keys, nc * sizeof(kspan));
+            if (!q) break;
+            t->keys = q;
+            t->kcap = nc;
+        }
+        t->keys[t->klen].off = (uint32_t)ka;
+        t->keys[t->klen].len = klen;
+        t->klen++;
+        int kid = -1;
+        if (f)
             for (int k = 0; k < 7; ++k)
-                if ((size_t)kl == strlen(KEYS[k]) && memcmp(key, KEYS[k], (size_t)kl) == 0) kid = k;
-            skipws(&r);
-            if (r.p >= r.n || s[r.p] != ':') return 0;
-            r.p++;
-            skipws(&r);
-            if (r.p >= r.n) return 0;
-            if (kid >= 0) {
-                if (seen & (1u << kid)) return 0;   /* org.json: Duplicate key */
-                seen |= 1u << kid;
-            }
-            if (s[r.p] == '"') {
-                unsigned char scratch[1];
-                long vl;
-                if (kid == 2) { vl = read_string(&r, f->ad, sizeof f->ad); f->ad_len = vl; }
-                else if (kid == 4) { vl = read_string(&r, f->et, sizeof f->et); f->et_len = vl; }
-                else if (kid == 5) { vl = read_string(&r, f->tm, sizeof f->tm); f->tm_len = vl; }
-                else vl = read_string(&r, scratch, 0);
-                if (vl < 0) return 0;
+                if (klen == strlen(KEYS[k]) && memcmp(t->arena + ka, KEYS[k], klen) == 0) kid = k;
+        const size_t vmark = t->alen;
+        tval vv;
+        if (!tk_value(t, depth, &vv)) break;
+        if (kid >= 0) {   /* getString: a String, quoted or unquoted */
+            const unsigned char* vs = NULL;
+            long vn = 0;
+            if (vv.kind == V_STR) { vs = t->arena + vv.a0; vn = (long)(t->alen - vv.a0); }
+            else if (vv.kind == V_TOK && token_kind(t->s + vv.a, vv.b - vv.a) == TOK_STR) { vs = t->s + vv.a; vn = vv.b - vv.a; }
+            if (vs) {
+                *seen |= 1u << kid;
+                if (kid == 2) keep(vs, vn, f->ad, sizeof f->ad, &f->ad_len);
+                else if (kid == 4) keep(vs, vn, f->et, sizeof f->et, &f->et_len);
+                else if (kid == 5) keep(vs, vn, f->tm, sizeof f->tm, &f->tm_len);
             } else {
-                if (kid >= 0 && (require & (1u << kid))) return 0;   /* getString: not a string */
-                if (!read_value(&r, 1)) return 0;
+                *seen &= ~(1u << kid);
             }
-            skipws(&r);
-            if (r.p >= r.n) return 0;
-            if (s[r.p] == ',') { r.p++; continue; }
-            if (s[r.p] == '}') { r.p++; break; }
-            return 0;
+        }
+        t->alen = vmark;
+        c = tk_clean(t);
+        if (c == ',' || c == ';') {
+            if (tk_clean(t) == '}') { ok = 1; break; }
+            if (!tk_back(t)) break;
+        } else if (c == '}') {
+            ok = 1;
+            break;
+        } else {
+            break;                                                /* Expected a ',' or '}' */
         }
     }
-    skipws(&r);
-    if (r.p != r.n) return 0;
+    t->klen = kmark;
+    t->alen = amark;
+    return ok;
+}
+
+/* JSONArray(JSONTokener) */
+static int tk_array(tk* t, int depth) {
+    if (depth > TK_MAX_DEPTH) return 0;
+    if (tk_clean(t) != '[') return 0;
+    if (tk_clean(t) == ']') return 1;
+    if (!tk_back(t)) return 0;
+    const size_t amark = t->alen;
+    for (;;) {
+        if (tk_clean(t) == ',') {
+            if (!tk_back(t)) return 0;                            /* an empty slot: NULL */
+        } else {
+            tval v;
+            if (!tk_back(t) || !tk_value(t, depth, &v)) return 0;
+            t->alen = amark;
+        }
+        int c = tk_clean(t);
+        if (c == ',') {
+            if (tk_clean(t) == ']') return 1;
+            if (!tk_back(t)) return 0;
+        } else {
+            return c == ']';                                      /* Expected a ',' or ']' */
+        }
+    }
+}
+
+/* new JSONObject(line) + getString of the required fields.  1 = parsed; 0 = org.json
+ * (or getString) would have thrown. */
+static int parse_event(tk* t, const unsigned char* s, size_t n, unsigned require, fields* f) {
+    const unsigned char* z = (const unsigned char*)memchr(s, 0, n);
+    t->s = s;
+    t->n = z ? (long)(z - s) : (long)n;
+    t->p = 0;
+    t->eof = 0;
+    t->alen = t->klen = 0;
+    unsigned seen = 0;
+    if (!tk_object(t, 1, require, &seen, f)) return 0;
     return (seen & require) == require;
 }
 
@@ -400,13 +646,15 @@ typedef struct {
 static void* run_job(void* arg) {
     job* j = (job*)arg;
     fields f;
+    tk t;
+    memset(&t, 0, sizeof t);
     for (uint64_t i = j->lo; i < j->hi; ++i) {
         uint64_t s = j->off[i], e = i + 1 < j->n ? j->off[i + 1] : j->nbytes;
         j->st.events++;
         if (e < s || e > j->nbytes) { j->st.parse_errors++; continue; }
         f.ad_len = f.et_len = f.tm_len = 0;
         const int ok = j->tbl ? parse_tbl(j->bytes + s, (size_t)(e - s), &f)
-                              : parse_event(j->bytes + s, (size_t)(e - s), j->require, &f);
+                              : parse_event(&t, j->bytes + s, (size_t)(e - s), j->require, &f);
         if (!ok) { j->st.parse_errors++; continue; }
         if (!(f.et_len == 4 && memcmp(f.et, "view", 4) == 0)) continue;           /* EventFilterBolt */
         j->st.views++;
@@ -421,6 +669,8 @@ static void* run_job(void* arg) {
         int64_t bucket = t / j->divisor;   /* C99 truncates toward zero, as Java's long / does */
         cm_add(&j->out, campaign, bucket, 1);
     }
+    free(t.arena);
+    free(t.keys);
     return NULL;
 }
 

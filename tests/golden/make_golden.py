@@ -12,6 +12,10 @@ Fixtures (all data, no reference source):
   gen_s7.campaign_ids.txt      campaign UUIDs (core.clj:24-31)
   edge.jsonl / edge_long.jsonl hand-written edge cases (boundaries, reordering,
                                escapes, errors, misses, an over-size line)
+  edge_orgjson.jsonl           hand-written cases for org.json 20180813's own grammar
+                               (unquoted and single-quoted text, ';' separators, trailing
+                               commas, text after '}', duplicate keys at any level,
+                               stringToValue typing, NUL / control bytes)
   gen_s7.tbl                   the same 1500 events as the fork's pipe-delimited rows
                                (MockWindowedFlatMap, AdvertisingTopologyNative.java:197-226)
   edge_tbl.tbl                 hand-written .tbl edge cases (String.split trailing-empty
@@ -19,8 +23,9 @@ Fixtures (all data, no reference source):
   *.expected.csv               campaign_uuid,window_ms,count from oracle/dostats.py
   *.expected.json              the chain's counters (events, views, joined, ...)
 
-Expected outputs come from oracle/dostats.py (Python json module), i.e. a JSON
-implementation independent of both oracle/ysb_oracle.c and the GPU tokenizer.
+Expected outputs come from oracle/dostats.py, whose JSON reading is oracle/orgjson.py
+(the org.json 20180813 restatement), a Python implementation independent of both
+oracle/ysb_oracle.c and the GPU tokenizer.
 """
 from __future__ import annotations
 
@@ -212,6 +217,108 @@ def tbl_edge_lines(ads):
     return [ln.encode() + b"\n" for ln in L]
 
 
+def orgjson_lines(ads):
+    a0, a1, a2 = ads[0], ads[11], ads[57]
+    U = "0f8c1e7a-1111-4222-8333-944455556666"
+
+    def ev(t, ad=a0, et="view", at="banner", ip="1.2.3.4", extra=""):
+        return ('{"user_id": "%s", "page_id": "p", "ad_id": "%s", "ad_type": %s, "event_type": %s, '
+                '"event_time": %s, "ip_address": %s%s}' % (U, ad, at if at[:1] in "'\"" or at == "" else '"%s"' % at,
+                                                          et if et[:1] in "'\"" else '"%s"' % et,
+                                                          t if t[:1] in "'\"" else '"%s"' % t,
+                                                          ip if ip[:1] in "'\"" else '"%s"' % ip, extra))
+
+    def raw(at="banner", et="view", t="1700000100000", ip="1.2.3.4", ad=None, extra=""):
+        """unquoted values spliced in as given"""
+        return ('{"user_id": "u", "page_id": "p", "ad_id": "%s", "ad_type": %s, "event_type": %s, '
+                '"event_time": %s, "ip_address": %s%s}' % (ad or a1, at, et, t, ip, extra))
+
+    deep = "".join('{"k%d": ' % k for k in range(40)) + '"x"' + "}" * 40
+    L = [
+        # unquoted text (nextValue's unquoted branch; stringToValue leaves a String)
+        "{user_id: u, page_id: p, ad_id: %s, ad_type: banner, event_type: view, event_time: 01700000100000}" % a0,
+        "{user_id: u, page_id: p, ad_id: %s, ad_type: banner, event_type: view, event_time: 1700000100000}" % a0,
+        raw(et="view  ", t="'1700000100001'"),                    # trailing spaces trimmed
+        raw(et="vi ew", t="'1700000100002'"),                      # inner space kept
+        raw(et="VIEW", t="'1700000100003'"),
+        raw(et="true", t="'1700000100004'"),                       # Boolean: not a string
+        raw(et="nULl", t="'1700000100005'"),                       # JSONObject.NULL
+        raw(at="1.5", t="'1700000100006'"),                        # Double
+        raw(at="1e400", t="'1700000100007'"),                      # infinite: stays a String
+        raw(at="0x1p1", t="'1700000100008'"),                      # not decimal notation, not a Long
+        raw(at="0x1.8p1", t="'1700000100009'"),                    # hex Double
+        raw(at="-0", t="'1700000100010'"),                         # Double -0.0
+        raw(at="007", t="'1700000100011'"),                        # Long.toString != text: String
+        raw(at="9223372036854775808", t="'1700000100012'"),        # beyond Long: String
+        raw(at="-9223372036854775808", t="'1700000100013'"),       # Long.MIN_VALUE
+        raw(at="1.5f", t="'1700000100014'"),                       # Double (suffix)
+        raw(at="1e", t="'1700000100015'"),                         # bad exponent: String
+        raw(at="fal\u017fe", t="'1700000100016'"),   # long s folds to S
+        raw(at="1.7976931348623157e308", t="'1700000100017'"),     # Double.MAX_VALUE
+        raw(at="1.7976931348623159e308", t="'1700000100018'"),     # rounds to Infinity
+        raw(t="1700000100019"),                                    # Long event_time: not a string
+        raw(t="1.700000100019e12"),                                # Double event_time
+        raw(t="+1700000100020"),                                   # '+' first: String, parseLong ok
+        raw(ip="1.2.3.4", t="'1700000100021'"),                    # unquoted ip: a String
+        raw(ip="1.5", t="'1700000100022'"),                        # Double ip (require_ip only)
+        raw(ip="[1, 2]", t="'1700000100023'"),
+        raw(ad="'%s'" % a2, t="'1700000100024'").replace('"ad_id": "\'', '"ad_id": \'').replace("'\", \"ad_type", "', \"ad_type"),
+        # single quotes, escapes
+        ev("'1700000110000'", et="'view'", at="'mail'"),
+        ev("1700000110001", et="vi\\u0065w"),
+        ev("1700000110002", et="vi\\u+065w"),                    # Integer.parseInt accepts a sign
+        ev("1700000110003", et="vi\\u-065w"),                    # (char)-0x65 = U+FF9B
+        ev("1700000110004", extra=', "q": "it\\\'s"'),          # \' is an org.json escape
+        ev("1700000110005", extra=", 'q': \"a'b\", 'r': 'a\"b'"),  # the other quote is plain text
+        ev("1700000110006", extra=', "q": "\\x"'),               # illegal escape
+        ev("1700000110007", extra=', "q": "\\u12g4"'),
+        ev("1700000110008", extra=', "q": "a\x01b\x7fc"'),       # raw C0 / DEL inside strings: kept
+        # separators and structure
+        ev("1700000120000").replace(", ", "; "),                    # ';' between pairs
+        ev("1700000120001")[:-1] + ";}",                            # trailing ';'
+        ev("1700000120002")[:-1] + ",,}",                           # empty pair: Missing value
+        ev("1700000120003") + "}}}",                                # text after the object is never read
+        ev("1700000120004") + ' {"more": ',
+        ev("1700000120005").replace('"ad_type":', '"ad_type" ='),  # '=' is not a key separator
+        ev("1700000120006").replace('"ad_type": "banner"', '"ad_type": "banner" "x"'),
+        "x" + ev("1700000120007"),                                  # text before '{'
+        "\x01\x1f" + ev("1700000120008").replace(", ", ",\x02\x0b"),   # all C0 chars are whitespace
+        ev("1700000120009", extra=', "a": [,1,,]'),                 # empty array slots are nulls
+        ev("1700000120010", extra=', "a": [1;2]'),                  # ';' does not separate array items
+        ev("1700000120011", extra=', "a": [1, [2, {"b": [3]}],]'),
+        ev("1700000120012", extra=', "a": #'),                      # '#' ends unquoted text: Missing value
+        ev("1700000120013", extra=", \"a\": b/c"),                 # '/' ends unquoted text
+        ev("1700000120014", extra=', "": 1, "n": null'),
+        ev("1700000120015", extra=', "d": ' + deep),                # 41 levels of nesting
+        # keys
+        '{user_id: "u", page_id: "p", ad_id: "%s", ad_type: "t", event_type: "view", event_time: "1700000130000"}' % a2,
+        "{'user_id': 'u', 'page_id': 'p', 'ad_\\u0069d': '%s', 'ad_type': 't', 'event_type': 'view', "
+        "'event_time': '1700000130001'}" % a2,
+        ev("1700000130002", extra=', {"k": 1}: 2, [3]: 4, 5: 6'),  # container / number keys
+        # duplicate keys: org.json throws for any repeated key, at any level
+        ev("1700000140000", extra=', "x": 1, "x": 2'),
+        ev("1700000140001", extra=', "x": 1, x: 2'),
+        ev("1700000140002", extra=', "1": 1, 1: 2'),                # Integer 1 -> "1"
+        ev("1700000140003", extra=', "true": 1, TRUE: 2'),          # Boolean.TRUE -> "true"
+        ev("1700000140004", extra=', "null": 1, Null: 2'),
+        ev("1700000140005", extra=', "w": {"a": 1, "a": 2}'),       # nested
+        ev("1700000140006", extra=', "w": [{"a": 1}, {"a": 2}]'),   # different objects: fine
+        ev("1700000140007", extra=', "w": {"ad_id": "x", "event_type": 1}'),   # other object's keys
+        ev("1700000140008", extra=', "q\\u0031": 1, "q1": 2'),
+        ev("1700000140009", extra=', "01": 1, 01: 2'),              # "01" stays a String
+        # NUL is the end of input; a raw CR / LF inside a string throws
+        ev("1700000150000") + "\x00garbage",
+        ev("1700000150001").replace('"p"', '"p\x00"'),
+        ev("1700000150002").replace('"p"', '"p\rq"'),
+        ev("1700000150003").replace('"banner"', "banner\x00"),
+        "{" + "\x00",
+        "{'user_id': 'u",
+        "{\"a\": [",
+        "{\"a\": b",
+    ]
+    return [ln.encode("utf-8", errors="surrogatepass") + b"\n" for ln in L]
+
+
 def write_expected(stem, lines, ad_map, campaign_of, require_ip=False, fmt="json"):
     r = dostats.run(lines, ad_map, 10000, require_ip, fmt)
     suffix = ".ip" if require_ip else ""
@@ -245,6 +352,11 @@ def main():
         f.write(b"".join(edge))
     write_expected("edge", edge, ad_map, campaign_of)
     write_expected("edge", edge, ad_map, campaign_of, require_ip=True)
+    oj = orgjson_lines(ads)
+    with open(os.path.join(HERE, "edge_orgjson.jsonl"), "wb") as f:
+        f.write(b"".join(oj))
+    write_expected("edge_orgjson", oj, ad_map, campaign_of)
+    write_expected("edge_orgjson", oj, ad_map, campaign_of, require_ip=True)
     lng = long_lines(ads)
     with open(os.path.join(HERE, "edge_long.jsonl"), "wb") as f:
         f.write(b"".join(lng))

@@ -69,7 +69,8 @@ def expected(stem, require_ip=False):
     return rows, st
 
 
-FIXTURES = [("gen_s7", False), ("edge", False), ("edge", True), ("edge_long", False)]
+FIXTURES = [("gen_s7", False), ("edge", False), ("edge", True), ("edge_orgjson", False), ("edge_orgjson", True),
+            ("edge_long", False)]
 # .tbl fixtures: expected-output stem -> data file stem (tests/golden/<file>.tbl)
 TBL_FILES = {"gen_s7_tbl": "gen_s7", "edge_tbl": "edge_tbl"}
 TBL_FIXTURES = sorted(TBL_FILES)
