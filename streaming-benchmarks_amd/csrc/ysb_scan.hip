@@ -68,84 +68,11 @@ struct BufSrc {  // decoded (un-escaped) strings
 
 struct Span { int s, e; int esc; };
 
-__device__ __forceinline__ bool is_ws(u32 c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 __device__ __forceinline__ bool is_hex(u32 c) {
     return (c - '0') < 10u || ((c | 0x20u) - 'a') < 6u;
 }
 __device__ __forceinline__ u32 hex_val(u32 c) { return (c - '0') < 10u ? c - '0' : (c | 0x20u) - 'a' + 10; }
 
-template <class S>
-__device__ __forceinline__ int skip_ws(const S& src, int p, int e) {
-    while (p < e && is_ws(src.b(p))) ++p;
-    return p;
-}
-
-// Index of the closing quote of a string whose content starts at p, or -1.
-// Escapes follow RFC 8259 (\" \\ \/ \b \f \n \r \t \uXXXX); esc is set when any
-// escape occurs.  Raw control characters are accepted (documented in DESIGN.md).
-template <class S>
-__device__ __forceinline__ int scan_str(const S& src, int p, int e, int& esc) {
-    {
-        while (p < e) {
-            const u32 c = src.b(p);
-            if (c == '"') return p;
-            if (c == '\\') {
-                esc = 1;
-                if (p + 1 >= e) return -1;
-                const u32 x = src.b(p + 1);
-                if (x == 'u') {
-                    if (p + 5 >= e) return -1;
-                    if (!is_hex(src.b(p + 2)) || !is_hex(src.b(p + 3)) || !is_hex(src.b(p + 4)) ||
-                        !is_hex(src.b(p + 5)))
-                        return -1;
-                    p += 6;
-                } else if (x == '"' || x == '\\' || x == '/' || x == 'b' || x == 'f' || x == 'n' ||
-                           x == 'r' || x == 't') {
-                    p += 2;
-                } else {
-                    return -1;
-                }
-                continue;
-            }
-            ++p;
-        }
-        return -1;
-    }
-}
-
-// Decodes the (validated) escaped string [s, e) as UTF-8 into buf (at most cap
-// bytes written); returns the full decoded length.
-template <class S>
-__device__ __noinline__ int decode_str(const S& src, int s, int e, u8* buf, int cap) {
-    int n = 0, p = s;
-    auto put = [&](u32 c) { if (n < cap) buf[n] = (u8)c; ++n; };
-    while (p < e) {
-        const u32 c = src.b(p);
-        if (c != '\\') { put(c); ++p; continue; }
-        const u32 x = src.b(p + 1);
-        if (x == 'u') {
-            u32 cp = (hex_val(src.b(p + 2)) << 12) | (hex_val(src.b(p + 3)) << 8) |
-                     (hex_val(src.b(p + 4)) << 4) | hex_val(src.b(p + 5));
-            p += 6;
-            if (cp >= 0xD800 && cp < 0xDC00 && p + 5 < e && src.b(p) == '\\' && src.b(p + 1) == 'u') {
-                const u32 lo = (hex_val(src.b(p + 2)) << 12) | (hex_val(src.b(p + 3)) << 8) |
-                               (hex_val(src.b(p + 4)) << 4) | hex_val(src.b(p + 5));
-                if (lo >= 0xDC00 && lo < 0xE000) {
-                    cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
-                    p += 6;
-                }
-            }
-            if (cp < 0x80) put(cp);
-            else if (cp < 0x800) { put(0xC0 | (cp >> 6)); put(0x80 | (cp & 0x3F)); }
-            else if (cp < 0x10000) { put(0xE0 | (cp >> 12)); put(0x80 | ((cp >> 6) & 0x3F)); put(0x80 | (cp & 0x3F)); }
-            else { put(0xF0 | (cp >> 18)); put(0x80 | ((cp >> 12) & 0x3F)); put(0x80 | ((cp >> 6) & 0x3F)); put(0x80 | (cp & 0x3F)); }
-        } else {
-            put(x == 'b' ? 8u : x == 'f' ? 12u : x == 'n' ? 10u : x == 'r' ? 13u : x == 't' ? 9u : x);
-            p += 2;
-        }
-    }
-    return n;
-}
 
 // Key id of the key string [s, s+len) (0 = a key DeserializeBolt does not read).
 template <class S>
@@ -172,132 +99,11 @@ __device__ __forceinline__ u32 match_key_raw(const S& src, int s, int len) {
     return 0u;
 }
 
-template <class S>
-__device__ __noinline__ u32 match_key_esc(const S& src, int s, int e) {
-    u8 buf[20];
-    const int n = decode_str(src, s, e, buf, 16);
-    if (n > 12) return 0u;
-    for (int k = n; k < 20; ++k) buf[k] = 0;
-    return match_key_raw(BufSrc{buf}, 0, n);
-}
+}  // namespace ysb
 
-// Skips a non-string value (number, literal, nested object/array); returns the
-// position after it or -1.  Not on the generator's path (every value is a string).
-template <class S>
-__device__ __noinline__ int skip_value(const S& src, int p, int e) {
-    u32 c = src.b(p);
-    if (c == 't') return (p + 3 < e && src.load4(p) == w4('t', 'r', 'u', 'e')) ? p + 4 : -1;
-    if (c == 'n') return (p + 3 < e && src.load4(p) == w4('n', 'u', 'l', 'l')) ? p + 4 : -1;
-    if (c == 'f') return (p + 4 < e && src.load4(p + 1) == w4('a', 'l', 's', 'e')) ? p + 5 : -1;
-    if (c == '-' || (c - '0') < 10u) {   // -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
-        if (c == '-') { if (++p >= e) return -1; c = src.b(p); }
-        if (c == '0') ++p;
-        else if ((c - '1') < 9u) { while (p < e && (src.b(p) - '0') < 10u) ++p; }
-        else return -1;
-        if (p < e && src.b(p) == '.') {
-            ++p; const int q = p;
-            while (p < e && (src.b(p) - '0') < 10u) ++p;
-            if (p == q) return -1;
-        }
-        if (p < e && (src.b(p) | 0x20u) == 'e') {
-            ++p;
-            if (p < e && (src.b(p) == '+' || src.b(p) == '-')) ++p;
-            const int q = p;
-            while (p < e && (src.b(p) - '0') < 10u) ++p;
-            if (p == q) return -1;
-        }
-        return p;
-    }
-    if (c == '{' || c == '[') {   // bracket matching, strings skipped (contents not validated)
-        int depth = 0;
-        while (p < e) {
-            c = src.b(p);
-            if (c == '"') {
-                int esc = 0;
-                const int q = scan_str(src, p + 1, e, esc);
-                if (q < 0) return -1;
-                p = q + 1;
-                continue;
-            }
-            if (c == '{' || c == '[') ++depth;
-            else if (c == '}' || c == ']') { if (--depth == 0) return p + 1; }
-            ++p;
-        }
-        return -1;
-    }
-    return -1;
-}
+#include "ysb_orgjson.h"
 
-// Strict JSON object tokenizer for one line [s, e).  Returns false where org.json's
-// JSONObject(String) or getString(key) would throw (AdvertisingTopologyNative.java:263-272):
-// malformed JSON, a duplicate key among the recognised ones, a required key missing
-// or not a string.
-template <class S>
-__device__ __forceinline__ bool parse_line(const S& src, int s, int e, u32 require,
-                                           Span& ad, Span& et, Span& tm) {
-    int p = skip_ws(src, s, e);
-    if (p >= e || src.b(p) != '{') return false;
-    p = skip_ws(src, p + 1, e);
-    u32 seen = 0;
-    if (p < e && src.b(p) == '}') {
-        ++p;
-    } else {
-        while (true) {
-            if (p >= e || src.b(p) != '"') return false;
-            int kesc = 0;
-            const int ke = scan_str(src, p + 1, e, kesc);
-            if (ke < 0) return false;
-            const u32 kid = kesc ? match_key_esc(src, p + 1, ke) : match_key_raw(src, p + 1, ke - p - 1);
-            p = ke + 1;
-            // common case ": " then the value's quote
-            if (p + 2 < e && (src.load4(p) & 0xFFFFFFu) == w4(':', ' ', '"', 0)) {
-                p += 2;
-            } else {
-                p = skip_ws(src, p, e);
-                if (p >= e || src.b(p) != ':') return false;
-                p = skip_ws(src, p + 1, e);
-                if (p >= e) return false;
-            }
-            if (src.b(p) == '"') {
-                int vesc = 0;
-                const int ve = scan_str(src, p + 1, e, vesc);
-                if (ve < 0) return false;
-                if (kid) {
-                    if (seen & kid) return false;   // org.json: "Duplicate key"
-                    seen |= kid;
-                    const Span sp{p + 1, ve, vesc};
-                    if (kid == K_AD) ad = sp;
-                    else if (kid == K_ETYPE) et = sp;
-                    else if (kid == K_ETIME) tm = sp;
-                }
-                p = ve + 1;
-            } else {
-                const int q = skip_value(src, p, e);
-                if (q < 0) return false;
-                if (kid) {
-                    if (seen & kid) return false;
-                    seen |= kid;
-                    if (kid & require) return false;   // getString: "not a string."
-                }
-                p = q;
-            }
-            // common case ", " then the next key's quote
-            if (p + 2 < e && (src.load4(p) & 0xFFFFFFu) == w4(',', ' ', '"', 0)) {
-                p += 2;
-                continue;
-            }
-            p = skip_ws(src, p, e);
-            if (p >= e) return false;
-            const u32 c = src.b(p);
-            if (c == ',') { p = skip_ws(src, p + 1, e); continue; }
-            if (c == '}') { ++p; break; }
-            return false;
-        }
-    }
-    p = skip_ws(src, p, e);
-    return p == e && (seen & require) == require;
-}
-
+namespace ysb {
 
 template <class S>
 __device__ __forceinline__ bool span_is_view(const S& src, const Span& et) {
@@ -443,18 +249,21 @@ __device__ __forceinline__ bool parse_digits_regs(const u32 (&w)[5], int len, i6
 // ---------------------------------------------------------------------------
 // Fast path: the generator's layout (core.clj:90-96) -- the seven keys in order,
 // ": " and ", " separators, string values without quotes or backslashes, the
-// three UUID values 36 bytes long.  Every structural byte is compared, every value
-// byte is shown free of '"' and '\\', and the variable tail's quotes are located
-// exactly, which makes it exactly the JSON parse of such a line; any other line
-// returns false and takes the general tokenizer.  Two dependent LDS batches per line.
+// three UUID values 36 bytes long.  Every structural byte up to the closing '}' is
+// compared, every value byte is shown free of '"', '\\' and NUL / CR / LF, and the
+// variable tail's quotes are located exactly, which makes it exactly org.json's parse
+// of such a line; any other line returns false and takes the general parser
+// (ysb_orgjson.h).  Two dependent LDS batches per line.
 // ---------------------------------------------------------------------------
 
-// Per byte, bit 7 set if the byte may be '"' or '\\' (SWAR has-zero of w ^ '"' and
-// w ^ '\\').  Superset: a byte just above a true hit can be flagged falsely, never
-// missed, and every candidate the parser relies on is verified by a compare.
+// Per byte, bit 7 set if the byte may be '"', '\\' or a control byte below 0x0E (NUL
+// ends org.json's input; a raw CR / LF inside a string throws): SWAR has-zero of
+// w ^ '"' and w ^ '\\', has-less-than 0x0E of w.  Superset: a byte just above a true
+// hit can be flagged falsely, never missed, and every candidate the parser relies on
+// is verified by a compare (a control byte fails the compare and defers the line).
 __device__ __forceinline__ u32 cand_z(u32 w) {
     const u32 tq = w ^ 0x22222222u, tb = w ^ 0x5C5C5C5Cu;
-    return (((tq - 0x01010101u) & ~tq) | ((tb - 0x01010101u) & ~tb)) & 0x80808080u;
+    return (((tq - 0x01010101u) & ~tq) | ((tb - 0x01010101u) & ~tb) | ((w - 0x0E0E0E0Eu) & ~w)) & 0x80808080u;
 }
 // The same flags packed to bits 0..3 (bit i = byte i), via the full-rate 24-bit
 // multiply (bits 7/15/23 -> 28/29/30) plus bit 31.
@@ -551,7 +360,6 @@ struct CanonB {   // after the second LDS batch
 // Stage 2: the variable tail -- the three separators, the closing "}", the event_type
 // value and the event_time digits -- in one batch of LDS reads.
 __device__ __forceinline__ bool canon_stage2(const LdsSrc& src, int s, int e, const CanonA& a, CanonB& c) {
-    const int L = e - s;
     u32 t4[5], t5[5], t6[5], t7[1], ev[1];
     load_span(src, s + a.e3, t4);
     load_span(src, s + a.e4, t5);
@@ -566,13 +374,9 @@ __device__ __forceinline__ bool canon_stage2(const LdsSrc& src, int s, int e, co
     d |= (t6[0] ^ w4('"', ',', ' ', '"')) | (t6[1] ^ w4('i', 'p', '_', 'a')) | (t6[2] ^ w4('d', 'd', 'r', 'e')) |
          (t6[3] ^ w4('s', 's', '"', ':')) | ((t6[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
     d |= (t7[0] & 0xFFFFu) ^ w4('"', '}', 0, 0);
-    bool ok = d == 0u;
-    // trailing bytes after '}' must be JSON whitespace (normally just the '\n')
-    if (L > a.e6 + 2) ok &= is_ws((t7[0] >> 16) & 0xFFu);
-    if (L > a.e6 + 3) ok &= is_ws(t7[0] >> 24);
-    if (!ok) return false;
-    for (int p = a.e6 + 4; p < L; ++p)
-        if (!is_ws(src.b(s + p))) return false;
+    // org.json's JSONObject(String) stops at the closing '}': whatever follows it (normally
+    // the '\n') is never read.
+    if (d != 0u) return false;
     c.view = (a.e4 - (a.e3 + 18) == 4) && ev[0] == VIEW_W;
     c.tlen = a.e5 - (a.e4 + 18);
     return true;

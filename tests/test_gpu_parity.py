@@ -244,3 +244,69 @@ def test_tbl_generated_stream_vs_oracle():
         s = ctx.stats()
         for k, v in st.items():
             assert s[k] == v, k
+
+
+def _oracle_vs_gpu(lines, require_ip, lds=True):
+    """Submits the lines as one batch; on a mismatch, bisects to the first line whose
+    GPU counters differ from the C oracle's (for the failure message)."""
+    ads, camp = gd.ad_arrays()
+    am = oracle.AdMap(ads, camp)
+
+    def run_gpu(ls):
+        raw = b"".join(ls)
+        offs = np.cumsum([0] + [len(x) for x in ls[:-1]]).tolist()
+        with make_ctx(require_ip=require_ip, lds_count=lds) as ctx:
+            ctx.submit(raw, offs, slot=0)
+            rows = ctx.drain_buckets()
+            st = ctx.stats()
+        return rows, {k: st[k] for k in ("events", "views", "joined", "join_misses", "parse_errors", "time_errors")}
+
+    def run_cpu(ls):
+        raw = b"".join(ls)
+        offs = np.cumsum([0] + [len(x) for x in ls[:-1]]).tolist()
+        return oracle.run(am, raw, offs, require_ip=require_ip)
+
+    if run_gpu(lines) == run_cpu(lines):
+        return
+    lo, hi = 0, len(lines)   # first prefix length that differs
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if run_gpu(lines[:mid]) == run_cpu(lines[:mid]):
+            lo = mid
+        else:
+            hi = mid
+    bad = lines[hi - 1]
+    raise AssertionError("GPU differs from the oracle at line %d: %r gpu=%r cpu=%r"
+                         % (hi - 1, bad, run_gpu([bad]), run_cpu([bad])))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("require_ip", [False, True])
+def test_orgjson_fuzz_matches_oracle(seed, require_ip):
+    """org.json's grammar (tests/orgjson_fuzz.py) through the general path: every counter
+    and every (campaign, window) count equals the C restatement's."""
+    import orgjson_fuzz as fz
+    ads, _ = gd.ad_arrays()
+    _oracle_vs_gpu(fz.lines(seed, 3000, ads), require_ip)
+
+
+def test_canonical_lines_with_control_bytes_and_trailing_text():
+    """The fast path must hand a generator-layout line with a NUL / CR / LF inside a value
+    to the general path (org.json throws there) and must count one with text after '}'."""
+    raw, offs = gd.events("gen_s7")
+    offs = list(offs) + [len(raw)]
+    lines = [raw[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+    rng = np.random.default_rng(5)
+    out = []
+    for i, ln in enumerate(lines[:600]):
+        r = i % 6
+        if r == 1:                                   # a control byte inside some value
+            quotes = [k for k, c in enumerate(ln) if c == 0x22]
+            vals = [(quotes[k] + 1, quotes[k + 1]) for k in range(2, len(quotes) - 1, 4)]
+            a, b = vals[rng.integers(len(vals))]
+            p = int(rng.integers(a, b + 1))
+            ln = ln[:p] + bytes([int(rng.choice([0x00, 0x0A, 0x0D, 0x09, 0x0B]))]) + ln[p:]
+        elif r == 2:                                 # text after the closing brace
+            ln = ln[:-1] + rng.choice([b" x", b"}", b"\x00", b"garbage{", b"\r"]) + b"\n"
+        out.append(ln)
+    _oracle_vs_gpu(out, False)
