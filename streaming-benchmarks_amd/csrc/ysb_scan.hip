@@ -12,16 +12,17 @@
 //                     bucket = Long.parseLong(event_time) / 10000;
 //                     windows[bucket][campaign].seenCount++         (CampaignProcessorCommon.java:57-67)
 //
-// Structure (DESIGN.md "Kernel 1"): a workgroup of 256 threads walks a contiguous
-// run of 256-line tiles.  Phase A streams a tile's bytes HBM -> registers -> LDS
-// with 16-byte coalesced loads (the next tile's loads are issued before the
-// current tile is parsed, so they land under Phase B) and classifies every byte
-// once: a 1-bit-per-byte quote-candidate bitmap and a per-16-byte backslash flag.
-// Phase B gives each thread one line: a strict JSON tokenizer that jumps from
-// quote to quote through the bitmap, matches the required keys, and extracts the
-// ad_id / event_type / event_time values.  Joined views are counted into
-// per-workgroup LDS (campaign, window) counters that are flushed to the HBM ring
-// table with 64-bit atomics only when the workgroup's window moves.
+// Structure (DESIGN.md "Kernel 1"): one-wave workgroups (64 lines per tile), 8 per
+// CU, each walking a contiguous run of tiles.  Phase A streams a tile's bytes
+// HBM -> registers -> LDS with 16-byte nontemporal buffer loads issued one tile ahead.
+// Phase B gives each lane one line: the canonical fast path checks the generator's
+// layout against a compile-time template in two batches of LDS reads and extracts the
+// 36-byte ad_id, event_type and event_time; the join probes the 2-choice cuckoo table
+// (raw UUID words); joined views are counted into per-workgroup LDS (campaign, window)
+// counters flushed to the HBM ring with 64-bit atomics when the workgroup's window
+// moves.  Any other line goes to a deferred list that defer_kernel parses with the
+// general org.json parser (ysb_orgjson.h).  tbl_scan_kernel does the same for the
+// fork's pipe-delimited rows.
 #include "ysb_kernels.h"
 
 namespace ysb {
