@@ -39,7 +39,8 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--events", type=int, default=100_000_000, help="events per GPU")
+    ap.add_argument("--events", type=int, default=100_000_000,
+                    help="events per GPU (125000000 at --gpus 8 is configs[3]'s 1B events)")
     ap.add_argument("--segment", type=int, default=12_500_000, help="events per launch")
     ap.add_argument("--rate", type=int, default=100_000, help="events per second of event time")
     ap.add_argument("--cpu-sample", type=int, default=4_000_000, help="events in the CPU baseline sample")
@@ -236,7 +237,11 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: seeded generator, data/ core.clj:90-97 line format, generated in HBM",
-            "config": {"workload": "configs[1]: 100M JSON events per GPU, 100 campaigns x 10 ads, 10 s windows",
+            "config": {"workload": ("configs[1]: %dM JSON events per GPU, 100 campaigns x 10 ads, 10 s windows"
+                                    % (args.events // 1_000_000)) if d.world == 1 else
+                                   ("configs[3] layout at weak scaling: %dM JSON events per GPU (%dM total), "
+                                    "events sharded by ad_id hash, RCCL reduce-scatter of (campaign, window) counts"
+                                    % (args.events // 1_000_000, args.events * d.world // 1_000_000)),
                        "events_per_gpu": args.events, "campaigns": 100, "ads": 1000,
                        "event_time_rate_per_s": args.rate, "launches_per_step": len(segs),
                        "json_bytes_per_event": round(total_bytes / args.events, 3),
