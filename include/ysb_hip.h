@@ -234,7 +234,11 @@ typedef struct ysb_gen_params {
     uint32_t event_stream;      /* 0: the single-stream generator; k > 0: an independent
                                    event stream over the SAME campaign/ad ids (one per
                                    rank of a sharded run); ids depend on seed only     */
+    uint32_t format;            /* YSB_GEN_JSON (core.clj:90-97 lines) or YSB_GEN_TBL (the
+                                   fork's .tbl rows of the same events, :197-226)       */
 } ysb_gen_params;
+#define YSB_GEN_JSON 0u
+#define YSB_GEN_TBL  1u
 
 void        ysb_gen_default(ysb_gen_params* p);
 /* Campaign and ad UUIDs, 36 bytes each, no separators (ad a -> campaign a / ads_per_campaign). */

@@ -973,11 +973,12 @@ static GenSpec spec_of(const ysb_gen_params* p, const u32* subset) {
     s.n_users = p->n_users;
     s.subset = subset;
     s.n_pick = subset ? p->n_ad_subset : p->n_campaigns * p->ads_per_campaign;
+    s.tbl = p->format == YSB_GEN_TBL;
     return s;
 }
 
 static bool gen_ok(const ysb_gen_params* p) {
-    return p && p->n_campaigns && p->ads_per_campaign && p->events_per_sec &&
+    return p && p->n_campaigns && p->ads_per_campaign && p->events_per_sec && p->format <= YSB_GEN_TBL &&
            (!p->ad_subset || p->n_ad_subset) && (u64)p->n_campaigns * p->ads_per_campaign < (1ull << 32);
 }
 
@@ -1119,7 +1120,7 @@ int ysb_gen_dump(const ysb_gen_params* p, uint64_t n_events, const char* dir) {
     }
     std::fclose(f);
     std::fclose(g);
-    f = open("kafka-json.txt");   // core.clj:76-97
+    f = open(p->format == YSB_GEN_TBL ? "events.tbl" : "kafka-json.txt");   // core.clj:76-97 / conf :6
     if (!f) return fail(nullptr, YSB_ERR_ARG, "cannot write into %s", dir);
     const GenSpec s = spec_of(p, p->ad_subset);
     std::vector<char> buf(1 << 22);

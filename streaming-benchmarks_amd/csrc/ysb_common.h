@@ -92,7 +92,7 @@ struct GenSpec {
     u32 with_skew, n_users;
     const u32* subset;   // ad indices to draw from (nullptr: all)
     u32 n_pick;          // number of ads drawn from
-    u32 pad;
+    u32 tbl;             // 1: the fork's .tbl rows instead of JSON lines
 };
 
 struct GenEvent {
@@ -132,8 +132,9 @@ YSB_HD u32 dec_format(i64 v, char* out) {
     return n;
 }
 
-YSB_HD u32 gen_line_len(const GenEvent& e) {
-    return (u32)LINE_FIXED + ad_type_len(e.ad_type) + event_type_len(e.event_type) + dec_len(e.time_ms);
+YSB_HD u32 gen_line_len(const GenSpec& s, const GenEvent& e) {
+    const u32 var = ad_type_len(e.ad_type) + event_type_len(e.event_type) + dec_len(e.time_ms);
+    return (s.tbl ? 3u * 36u + 5u + 1u : (u32)LINE_FIXED) + var;
 }
 
 YSB_HD char* put_str(char* o, const char* s, u32 n) {
@@ -141,10 +142,33 @@ YSB_HD char* put_str(char* o, const char* s, u32 n) {
     return o + n;
 }
 
-// One event line, exactly the str of core.clj:90-96 plus the "\n" of :97.
+// One event line, exactly the str of core.clj:90-96 plus the "\n" of :97; with s.tbl
+// the same event as the fork's .tbl row (MockWindowedFlatMap, AdvertisingTopologyNative.
+// java:197-226): user_id|page_id|ad_id|ad_type|event_type|event_time\n, which is what
+// ysb_json_to_tbl makes of the JSON line.
 YSB_HD u32 gen_line_write(const GenSpec& s, u64 i, const GenEvent& e, char* out) {
     char* o = out;
     u64 hi, lo;
+    if (s.tbl) {
+        if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
+        else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);
+        uuid_format(hi, lo, o); o += 36;
+        *o++ = '|';
+        if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_PAGE), i, &hi, &lo);
+        else uuid_words(stream_key(s.ev_seed, S_PAGE), draw(stream_key(s.ev_seed, S_PAGEPOOL), i) % s.n_users, &hi, &lo);
+        uuid_format(hi, lo, o); o += 36;
+        *o++ = '|';
+        uuid_words(stream_key(s.seed, S_AD), e.ad, &hi, &lo);
+        uuid_format(hi, lo, o); o += 36;
+        *o++ = '|';
+        o = put_str(o, ad_type_str(e.ad_type), ad_type_len(e.ad_type));
+        *o++ = '|';
+        o = put_str(o, event_type_str(e.event_type), event_type_len(e.event_type));
+        *o++ = '|';
+        o += dec_format(e.time_ms, o);
+        *o++ = '\n';
+        return (u32)(o - out);
+    }
     o = put_str(o, YSB_P0, LEN_P0);
     if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
     else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);

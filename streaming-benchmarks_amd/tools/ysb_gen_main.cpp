@@ -46,25 +46,11 @@ int main(int argc, char** argv) {
     if (!dir) { std::fprintf(stderr, "usage: ysb_gen -d DIR [-n EVENTS] [options]\n"); return 2; }
     int rc = shards > 1 ? ysb_gen_dump_shards(&p, n, dir, shards) : ysb_gen_dump(&p, n, dir);
     if (rc) { std::fprintf(stderr, "ysb_gen: %s\n", ysb_last_error(nullptr)); return 1; }
-    if (tbl) {   // events.tbl: the same events as .tbl rows, in chunks
-        FILE* f = std::fopen((std::string(dir) + "/events.tbl").c_str(), "wb");
-        if (!f) { std::fprintf(stderr, "ysb_gen: cannot write events.tbl\n"); return 1; }
-        const unsigned long long chunk = 1 << 16;
-        const unsigned long long cap = chunk * ysb_gen_max_line_bytes(&p);
-        std::vector<unsigned char> js(cap), tb(cap);
-        std::vector<unsigned> off(chunk), toff(chunk);
-        for (unsigned long long first = 0; first < n; first += chunk) {
-            const unsigned long long m = n - first < chunk ? n - first : chunk;
-            uint64_t nb = 0, tnb = 0;
-            if (ysb_gen_events_host(&p, first, m, js.data(), cap, off.data(), &nb) ||
-                ysb_json_to_tbl(js.data(), nb, off.data(), m, tb.data(), cap, toff.data(), &tnb)) {
-                std::fprintf(stderr, "ysb_gen: .tbl conversion failed\n");
-                std::fclose(f);
-                return 1;
-            }
-            std::fwrite(tb.data(), 1, tnb, f);
-        }
-        std::fclose(f);
+    if (tbl) {   // events.tbl: the same events as .tbl rows (generator format YSB_GEN_TBL)
+        ysb_gen_params q = p;
+        q.format = YSB_GEN_TBL;
+        rc = ysb_gen_dump(&q, n, dir);
+        if (rc) { std::fprintf(stderr, "ysb_gen: %s\n", ysb_last_error(nullptr)); return 1; }
     }
     return 0;
 }

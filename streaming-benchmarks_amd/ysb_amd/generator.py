@@ -19,7 +19,8 @@ class GenParams:
     t0 1.7e12 ms, 100,000 events per second of event time."""
 
     def __init__(self, seed=42, n_campaigns=100, ads_per_campaign=10, t0_ms=1_700_000_000_000,
-                 events_per_sec=100_000, with_skew=False, n_users=0, ad_subset=None, event_stream=0):
+                 events_per_sec=100_000, with_skew=False, n_users=0, ad_subset=None, event_stream=0,
+                 fmt="json"):
         self.c = YsbGenParams()
         lib().ysb_gen_default(C.byref(self.c))
         self.c.seed = seed
@@ -30,6 +31,9 @@ class GenParams:
         self.c.with_skew = int(bool(with_skew))
         self.c.n_users = n_users
         self.c.event_stream = event_stream
+        if fmt not in ("json", "tbl"):
+            raise ValueError("fmt must be 'json' or 'tbl'")
+        self.c.format = 1 if fmt == "tbl" else 0   # YSB_GEN_TBL: the fork's .tbl rows
         self._subset = None
         if ad_subset is not None:
             self._subset = np.ascontiguousarray(ad_subset, dtype=np.uint32)

@@ -144,3 +144,12 @@ def test_cli_shards_and_tbl(tmp_path):
         ev = _json.loads(ln)
         assert "|".join(ev[k] for k in ("user_id", "page_id", "ad_id", "ad_type", "event_type",
                                         "event_time")).encode() in tbl_set
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(with_skew=True, events_per_sec=1000), dict(n_users=50, seed=9),
+                                dict(event_stream=3, ad_subset=list(range(0, 1000, 7)))])
+def test_tbl_format_is_json_to_tbl(kw):
+    """format YSB_GEN_TBL writes exactly what ysb_json_to_tbl makes of the JSON lines."""
+    rows, roff = GenParams(fmt="tbl", **kw).events_host(1000, 20_000)
+    conv, coff = GenParams(**kw).events_host_tbl(1000, 20_000)
+    assert rows.tobytes() == conv.tobytes() and list(roff) == list(coff)

@@ -310,3 +310,16 @@ def test_canonical_lines_with_control_bytes_and_trailing_text():
             ln = ln[:-1] + rng.choice([b" x", b"}", b"\x00", b"garbage{", b"\r"]) + b"\n"
         out.append(ln)
     _oracle_vs_gpu(out, False)
+
+
+def test_device_tbl_generator_matches_host():
+    g = GenParams(seed=21, with_skew=True, events_per_sec=3000, fmt="tbl")
+    raw, offs = g.events_host(0, 300_000)
+    with make_ctx() as ctx:
+        n = len(offs)
+        cap = n * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n)
+        nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+        assert nb == raw.size
+        assert ctx.d2h(np.empty(nb, dtype=np.uint8), d_b).tobytes() == raw.tobytes()
+        assert np.array_equal(ctx.d2h(np.empty(n, dtype=np.uint32), d_o), offs)

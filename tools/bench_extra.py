@@ -3,6 +3,10 @@
     python tools/bench_extra.py config3 [--events N] [--steps K]
         configs[2]: 1M campaigns / 10M ads (join table and count table in HBM);
         events/s and the scan kernel's algorithmic GB/s, generator-truth check.
+    python tools/bench_extra.py tbl [--events N] [--steps K]
+        configs[1]'s events as the fork's live .tbl rows (MockWindowedFlatMap,
+        AdvertisingTopologyNative.java:197-226), generated in HBM: tbl_scan_kernel's
+        events/s and algorithmic GB/s, generator-truth check.
     python tools/bench_extra.py pcie [--batch-mb M] [--seconds S]
         host-staged throughput: pre-staged pinned double-buffered slots -> H2D copy
         stream -> scan kernel (PCIe-inclusive rate; never bench.py's value).
@@ -81,6 +85,52 @@ def config3(args):
                       "join_misses": st["join_misses"], "parse_errors": st["parse_errors"],
                       "deferred": st["deferred"], "out_of_ring": st["out_of_ring"],
                       "overflow_dropped": st["overflow_dropped"]}}
+
+
+def tbl(args):
+    g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000, fmt="tbl")
+    _, aids = g.ids()
+    ctx = YsbContext(n_campaigns=100, window_ring=1024, timing=True, input_format="tbl",
+                     max_batch_bytes=16 << 20, max_batch_events=1 << 16)
+    ctx.load_ad_map(aids, g.ad_campaign_index())
+    segs, first = [], 0
+    while first < args.events:
+        n = min(args.segment, args.events - first)
+        cap = n * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
+        nb = ctx.gen_events_device(g, first, n, d_b, cap, d_o)
+        segs.append((first, n, d_b, nb, d_o))
+        first += n
+    total_bytes = sum(s[3] for s in segs)
+
+    def step():
+        for (_, n, d_b, nb, d_o) in segs:
+            ctx.submit_device(d_b, nb, d_o, n)
+    step()
+    ctx.sync()
+    ctx.kernel_time()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    el = time.perf_counter() - t0
+    kms, launches = ctx.kernel_time()
+    ctx.reset()
+    for (f, n, d_b, nb, d_o) in segs:
+        ctx.submit_device(d_b, nb, d_o, n)
+        ctx.truth_accumulate(g, f, n)
+    mism, truth, ring = ctx.truth_compare()
+    st = ctx.stats()
+    alg = (total_bytes + 4 * args.events) / len(segs)
+    ach = alg / (kms / launches * 1e-3) / 1e9
+    return {"config": "configs[1] events as .tbl rows: %d events, 100 campaigns x 10 ads" % args.events,
+            "tbl_bytes_per_event": round(total_bytes / args.events, 3),
+            "events_per_s": round(args.events * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
+            "scan_avg_launch_ms": round(kms / launches, 4), "scan_alg_GBs": round(ach, 1),
+            "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
+            "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
+                      "join_misses": st["join_misses"], "parse_errors": st["parse_errors"],
+                      "time_errors": st["time_errors"], "out_of_ring": st["out_of_ring"]}}
 
 
 def pcie(args):
@@ -190,7 +240,7 @@ def stream(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["config3", "pcie", "stream"])
+    ap.add_argument("mode", choices=["config3", "tbl", "pcie", "stream"])
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--segment", type=int, default=12_500_000)
     ap.add_argument("--steps", type=int, default=5)
@@ -201,7 +251,7 @@ def main():
     ap.add_argument("--batch-ms", type=int, default=100)
     ap.add_argument("--ooo-ms", type=int, default=100)
     args = ap.parse_args()
-    out = {"config3": config3, "pcie": pcie, "stream": stream}[args.mode](args)
+    out = {"config3": config3, "tbl": tbl, "pcie": pcie, "stream": stream}[args.mode](args)
     print(json.dumps(out), flush=True)
 
 
