@@ -249,7 +249,7 @@ def main():
                        else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "ysb::scan_kernel<false>", "avg_launch_ms": round(avg_launch_ms, 4),
+                         "kernel": "ysb::scan_kernel<false, false>", "avg_launch_ms": round(avg_launch_ms, 4),
                          "alg_bytes_per_launch": int(alg_bytes_launch)},
             "cpu_baseline": cpu,
             "check": check,

@@ -420,6 +420,7 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
 
 static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_off, u64 n) {
     ScanParams p{};
+    p.tbl = (c->cfg.flags & YSB_F_FORMAT_TBL) ? 1u : 0u;
     p.bytes = d_bytes;
     p.nbytes = nbytes;
     p.off = d_off;
@@ -518,14 +519,11 @@ static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_
         c->tev_used++;
         HIPCHK(c, hipEventRecord(e0, c->s_comp));
     }
-    if (tbl) launch_tbl_scan(p, c->s_comp);
-    else launch_scan(p, c->s_comp);
+    launch_scan(p, c->s_comp);
     HIPCHK(c, hipGetLastError());
     if (e1) HIPCHK(c, hipEventRecord(e1, c->s_comp));
-    if (!tbl) {
-        launch_defer(p, c->cus, c->s_comp);
-        HIPCHK(c, hipGetLastError());
-    }
+    launch_defer(p, c->cus, c->s_comp);
+    HIPCHK(c, hipGetLastError());
     c->batches++;
     return YSB_OK;
 }

@@ -39,6 +39,7 @@ struct ScanParams {
     u32 ctable_mask;
     u32 ctable_partial;         // 1: some 36-byte key missed the cuckoo build (misses defer)
     u32 probe_serial;           // 1: probe the second cuckoo slot only after a first-slot miss
+    u32 tbl;                    // 1: the fork's .tbl rows (YSB_F_FORMAT_TBL) instead of JSON lines
     CuckooSeed cseed;
     u32 n_campaigns;
     unsigned long long* counts; // [c_pad][W] u64, campaign-major
@@ -73,7 +74,6 @@ void launch_defer(const ScanParams& p, int blocks, hipStream_t s);
 // Sets ring[0..1] from the first lines of a batch if ring[1] == 0.
 void launch_ring_autobase(const ScanParams& p, hipStream_t s);
 // The pipe-delimited .tbl input format (YSB_F_FORMAT_TBL): scan + ring auto-base.
-void launch_tbl_scan(const ScanParams& p, hipStream_t s);
 void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s);
 
 // Generator kernels (ysb_gen.hip).

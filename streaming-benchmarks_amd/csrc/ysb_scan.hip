@@ -21,8 +21,8 @@
 // (raw UUID words); joined views are counted into per-workgroup LDS (campaign, window)
 // counters flushed to the HBM ring with 64-bit atomics when the workgroup's window
 // moves.  Any other line goes to a deferred list that defer_kernel parses with the
-// general org.json parser (ysb_orgjson.h).  tbl_scan_kernel does the same for the
-// fork's pipe-delimited rows.
+// general org.json parser (ysb_orgjson.h).  scan_kernel<*, true> does the same for the
+// fork's pipe-delimited rows (tbl_stage1/2, deferred rows through process_tbl_line).
 #include "ysb_kernels.h"
 
 namespace ysb {
@@ -299,8 +299,9 @@ constexpr PrefixTpl make_prefix_tpl() {
 }
 
 struct CanonA {   // after the first LDS batch
-    u32 kw[9];     // ad_id bytes 113..148
+    u32 kw[9];     // ad_id bytes 113..148 (.tbl: 74..109)
     int e3, e4, e5, e6;   // closing quotes of ad_type, event_type, event_time, ip_address
+                          // (.tbl: e3, e4 = the 4th and 5th '|'; e5, e6 = '|' bitmap of bytes 96..159)
 };
 
 // Stage 1: one batch of independent LDS reads -- the line's first 276 bytes as raw
@@ -381,6 +382,79 @@ __device__ __forceinline__ bool canon_stage2(const LdsSrc& src, int s, int e, co
     c.view = (a.e4 - (a.e3 + 18) == 4) && ev[0] == VIEW_W;
     c.tlen = a.e5 - (a.e4 + 18);
     return true;
+}
+
+// ---------------------------------------------------------------------------
+// .tbl fast path (YSB_F_FORMAT_TBL): the generator's rows, user|page|ad|ad_type|
+// event_type|event_time\n with 36-byte UUIDs -- the first three '|' at bytes 36, 73 and
+// 110, the next two found in a '|' bitmap of the line's first 160 bytes, no other '|'
+// before the terminator.  Then line.split("\\|") (MockWindowedFlatMap,
+// AdvertisingTopologyNative.java:197-226) has items[2] = bytes 74..109, items[4] between
+// the 4th and 5th '|', items[5] = the rest up to the "\n" / "\r\n" readLine strips.  Any
+// other row is deferred to process_tbl_line.  Same two-batch shape as the JSON path.
+// ---------------------------------------------------------------------------
+constexpr int TBL_WORDS = 40;                          // bytes 0..159 of the line
+constexpr int TBL_MIN_LEN = 116, TBL_MAX_LEN = 4 * TBL_WORDS;
+
+// Per byte, bit 7 set if the byte may be '|' (SWAR has-zero of w ^ '|'); the lowest flag
+// of a word is always a true '|', a flag above a true one may be false.
+__device__ __forceinline__ u32 bar_nib(u32 w) {
+    const u32 t = w ^ 0x7C7C7C7Cu;
+    const u32 z = ((t - 0x01010101u) & ~t) & 0x80808080u;
+    return (__umul24(z, 0x00204081u) | (z & 0x80000000u)) >> 28;
+}
+
+__device__ __forceinline__ bool tbl_stage1(const LdsSrc& src, int s, int e, CanonA& c) {
+    const int L = e - s;
+    if (L < TBL_MIN_LEN || L > TBL_MAX_LEN) return false;
+    const int a = s >> 2;
+    const u32 sb = (u32)(s & 3);
+    u32 P[TBL_WORDS + 1];
+#pragma unroll
+    for (int k = 0; k <= TBL_WORDS; ++k) P[k] = src.d[a + k];
+    u32 W[TBL_WORDS];
+    u32 B[5] = {0u, 0u, 0u, 0u, 0u};   // bit i = line byte i may be '|'
+#pragma unroll
+    for (int j = 0; j < TBL_WORDS; ++j) {
+        W[j] = __builtin_amdgcn_alignbyte(P[j + 1], P[j], sb);   // line bytes 4j..4j+3
+        B[j >> 3] |= bar_nib(W[j]) << (4 * (j & 7));
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(W[19 + k], W[18 + k], 2u);   // bytes 74..109
+    // the first three '|' exactly at 36, 73, 110 (each the lowest flag of its word: true)
+    const bool fixed = B[0] == 0u && B[1] == (1u << 4) && B[2] == (1u << 9) && (B[3] & 0x7FFFu) == (1u << 14);
+    const u64 hi = ((u64)B[4] << 32) | (B[3] & ~0x7FFFu);   // bytes 96..159, above 110
+    const int p3 = hi ? 96 + (int)__builtin_ctzll(hi) : (1 << 20);
+    const u64 hi2 = hi & (hi - 1);
+    const int p4 = hi2 ? 96 + (int)__builtin_ctzll(hi2) : (1 << 20);
+    c.e3 = p3;
+    c.e4 = p4;
+    c.e5 = (int)B[3];
+    c.e6 = (int)B[4];
+    return fixed && p4 + 2 <= L;
+}
+
+// Stage 2: the two '|' verified, the terminator stripped, no '|' after the fifth, the
+// event_type and event_time fetched -- one batch of LDS reads.
+__device__ __forceinline__ bool tbl_stage2(const LdsSrc& src, int s, int e, const CanonA& a, CanonB& c) {
+    u32 t3[2], t4[1], tl[1];
+    load_span(src, s + a.e3, t3);
+    load_span(src, s + a.e4, t4);
+    load_span(src, s + a.e4 + 1, c.td);
+    load_span(src, e - 4, tl);                            // the line's last 4 bytes
+    int end = e - s;                                      // readLine: "\n", then a '\r' before it
+    const bool nl = (tl[0] >> 24) == '\n';
+    end -= nl ? 1 : 0;
+    end -= (((tl[0] >> (nl ? 16 : 24)) & 0xFFu) == '\r') ? 1 : 0;
+    bool ok = (t3[0] & 0xFFu) == '|' && (t4[0] & 0xFFu) == '|' && end > a.e4 + 1;
+    // no '|' in (p4, end): bits of the 64-bit bitmap of bytes 96..159
+    const u64 bm = ((u64)(u32)a.e6 << 32) | (u32)a.e5;
+    const int lo = a.e4 + 1 - 96, hi = end - 96;          // [lo, hi) must be clear
+    const u64 m = (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
+    ok &= (bm & m) == 0ull;
+    c.view = a.e4 - a.e3 - 1 == 4 && __builtin_amdgcn_alignbyte(t3[1], t3[0], 1u) == VIEW_W;
+    c.tlen = end - (a.e4 + 1);
+    return ok;
 }
 
 // One line end to end: returns 0 not counted, 1 counted (campaign/bucket set).
@@ -642,7 +716,9 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 
 // SERIAL: probe the second cuckoo slot only after a first-slot miss (HBM-resident table);
 // a separate instantiation so the cache-resident configuration's code is untouched.
-template <bool SERIAL>
+// SERIAL: HBM-resident cuckoo table, second slot probed only after a first-slot miss.
+// TBL: the fork's .tbl rows (tbl_stage1/2) instead of JSON lines (canon_stage1/2).
+template <bool SERIAL, bool TBL>
 __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(ScanParams P) {
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
     u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
@@ -740,7 +816,8 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         if (li < cur.count && !cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
-            ok1 = canon_stage1(lsrc, ls, le, ca);
+            if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
+            else ok1 = canon_stage1(lsrc, ls, le, ca);
         }
         bool pend = false, dfr = false, tok = false;
         i64 bucket = 0;
@@ -748,7 +825,8 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         cb.view = false;
         bool ok2 = false;
         if (li < cur.count) {
-            ok2 = ok1 && canon_stage2(lsrc, ls, le, ca, cb);
+            if constexpr (TBL) ok2 = ok1 && tbl_stage2(lsrc, ls, le, ca, cb);
+            else ok2 = ok1 && canon_stage2(lsrc, ls, le, ca, cb);
             dfr = !ok2;   // bad offsets, other layouts, escapes, over-size tiles
         }
         pend = ok2 && cb.view;                                             // EventFilterBolt
@@ -775,7 +853,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
             tl.ev++;
             if (pend) {
                 tl.view++;
-                tok = canonical_bucket(lsrc, cb, ls + ca.e4 + 18, P, bucket);   // Long.parseLong
+                tok = canonical_bucket(lsrc, cb, ls + ca.e4 + (TBL ? 1 : 18), P, bucket);   // Long.parseLong
             }
         }
         defer_append(P, dfr, cur.first + li, lane);
@@ -854,6 +932,50 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
     flush_tally(P, tl, lane);
 }
 
+// ---------------------------------------------------------------------------
+// The fork's live input format: pipe-delimited .tbl lines
+// (MockWindowedFlatMap.flatMap, flink-benchmarks/.../AdvertisingTopologyNative.java:197-226):
+//   items = line.split("\\|")   (java.lang.String.split: trailing empty items dropped)
+//   (items[0..5]) = (user_id, page_id, ad_id, ad_type, event_type, event_time)
+// fewer than 6 items after the trailing-empty drop -> ArrayIndexOutOfBounds (a parse
+// error); then the same filter / join / bucket as the JSON chain (event_time = items[5],
+// the Storm/Spark projection).  The line is the batch line minus its "\n" / "\r\n"
+// terminator (BufferedReader.readLine, :153-159).
+// ---------------------------------------------------------------------------
+template <class S>
+__device__ __forceinline__ bool process_tbl_line(const S& src, int s, int e, const ScanParams& P, Tally& t,
+                                                 u32& campaign, i64& bucket) {
+    t.ev++;
+    if (e > s && src.b(e - 1) == '\n') --e;
+    if (e > s && src.b(e - 1) == '\r') --e;
+    // the first six '|' (p[5] = e when there are only five)
+    int p[6];
+    int k = 0;
+    for (int q = s; q < e && k < 6; ++q)
+        if (src.b(q) == '|') p[k++] = q;
+    if (k < 5) { t.perr++; return false; }
+    if (k == 5) p[5] = e;
+    // items[5] exists iff something other than '|' follows the fifth '|'
+    bool tail = p[5] > p[4] + 1;
+    for (int q = p[5]; !tail && q < e; ++q) tail = src.b(q) != '|';
+    if (!tail) { t.perr++; return false; }
+    const Span et{p[3] + 1, p[4], 0};
+    if (!(et.e - et.s == 4 && src.load4(et.s) == VIEW_W)) return false;   // EventFilterBolt
+    t.view++;
+    const Span ad{p[1] + 1, p[2], 0};
+    u32 kw[KEY_WORDS];
+    u32 klen = 0;
+    int c = -1;
+    if (span_key(src, ad, kw, klen)) c = probe(P.table, P.table_mask, kw, klen);   // RedisJoinBolt
+    if (c < 0) { t.miss++; return false; }
+    t.join++;
+    i64 tv;
+    if (!parse_digits(src, p[4] + 1, p[5], tv)) { t.terr++; return false; }   // Long.parseLong
+    campaign = (u32)c;
+    bucket = div_trunc(tv, P.div);
+    return true;
+}
+
 // Kernel 1b: the lines the fast path deferred (any layout other than the generator's,
 // escapes, non-canonical ad ids, over-size tiles, bad offsets) through the general
 // strict JSON tokenizer, straight from HBM.  Rare on generator data; exact always.
@@ -876,8 +998,9 @@ __global__ __launch_bounds__(AUX_TPB) void defer_kernel(ScanParams P) {
         u32 campaign;
         i64 bucket;
         const GlbSrc gsrc{P.bytes + ls, le - ls};
-        if (process_line(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket))
-            global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+        const bool ok = P.tbl ? process_tbl_line(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket)
+                              : process_line(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket);
+        if (ok) global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
     }
     flush_tally(P, tl, lane);
     __syncthreads();
@@ -926,109 +1049,8 @@ __global__ __launch_bounds__(AUX_TPB) void ring_autobase_kernel(ScanParams P, i6
     }
 }
 
-// ---------------------------------------------------------------------------
-// The fork's live input format: pipe-delimited .tbl lines
-// (MockWindowedFlatMap.flatMap, flink-benchmarks/.../AdvertisingTopologyNative.java:197-226):
-//   items = line.split("\\|")   (java.lang.String.split: trailing empty items dropped)
-//   (items[0..5]) = (user_id, page_id, ad_id, ad_type, event_type, event_time)
-// fewer than 6 items after the trailing-empty drop -> ArrayIndexOutOfBounds (a parse
-// error); then the same filter / join / bucket as the JSON chain (event_time = items[5],
-// the Storm/Spark projection).  The line is the batch line minus its "\n" / "\r\n"
-// terminator (BufferedReader.readLine, :153-159).
-// ---------------------------------------------------------------------------
-template <class S>
-__device__ __forceinline__ bool process_tbl_line(const S& src, int s, int e, const ScanParams& P, Tally& t,
-                                                 u32& campaign, i64& bucket) {
-    t.ev++;
-    if (e > s && src.b(e - 1) == '\n') --e;
-    if (e > s && src.b(e - 1) == '\r') --e;
-    // the first six '|' (p[5] = e when there are only five)
-    int p[6];
-    int k = 0;
-    for (int q = s; q < e && k < 6; ++q)
-        if (src.b(q) == '|') p[k++] = q;
-    if (k < 5) { t.perr++; return false; }
-    if (k == 5) p[5] = e;
-    // items[5] exists iff something other than '|' follows the fifth '|'
-    bool tail = p[5] > p[4] + 1;
-    for (int q = p[5]; !tail && q < e; ++q) tail = src.b(q) != '|';
-    if (!tail) { t.perr++; return false; }
-    const Span et{p[3] + 1, p[4], 0};
-    if (!(et.e - et.s == 4 && src.load4(et.s) == VIEW_W)) return false;   // EventFilterBolt
-    t.view++;
-    const Span ad{p[1] + 1, p[2], 0};
-    u32 kw[KEY_WORDS];
-    u32 klen = 0;
-    int c = -1;
-    if (span_key(src, ad, kw, klen)) c = probe(P.table, P.table_mask, kw, klen);   // RedisJoinBolt
-    if (c < 0) { t.miss++; return false; }
-    t.join++;
-    i64 tv;
-    if (!parse_digits(src, p[4] + 1, p[5], tv)) { t.terr++; return false; }   // Long.parseLong
-    campaign = (u32)c;
-    bucket = div_trunc(tv, P.div);
-    return true;
-}
 
 // One wave per 64-line tile, staged through LDS like the JSON scan; one line per lane.
-__global__ __launch_bounds__(SCAN_TPB) void tbl_scan_kernel(ScanParams P) {
-    extern __shared__ __attribute__((aligned(16))) u8 smem[];
-    u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
-    u32* tb = reinterpret_cast<u32*>(smem + OFF_TB);
-    const int tid = threadIdx.x;
-    const u64 t_begin = (u64)blockIdx.x * P.tiles_per_block;
-    if (t_begin >= P.n_tiles) return;
-    const u64 t_end = min(t_begin + P.tiles_per_block, P.n_tiles);
-    const i64 ring_lo = P.ring[0];
-    const bool ring_set = P.ring[1] != 0;
-    for (u32 i = tid; i <= (u32)(t_end - t_begin); i += SCAN_TPB) {
-        const u64 f = (t_begin + i) * SCAN_TPB;
-        tb[i] = f < P.n ? P.off[f] : (u32)P.nbytes;
-    }
-    __syncthreads();
-    Tally tl{0, 0, 0, 0, 0, 0, 0};
-    uint4 pre[CHUNKS_PER_THREAD];
-    u32 pre_off = 0, pre_end = 0;
-    TileInfo nxt = tile_info(P, t_begin, t_begin, tb);
-    issue_tile_loads(P, nxt, pre, pre_off, pre_end);
-    const LdsSrc lsrc{tile32};
-    for (u64 t = t_begin; t < t_end; ++t) {
-        const TileInfo cur = nxt;
-        const u32 my_off = pre_off;
-        const u32 li = lane_line(tid);
-        const u32 my_end = (cur.first + li + 1 < P.n) ? pre_end : (u32)P.nbytes;
-        if (!cur.oversize) {
-#pragma unroll
-            for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
-                const u32 k = (u32)(j * SCAN_TPB + tid);
-                if (j * SCAN_TPB + SCAN_TPB <= TILE_CHUNKS || k < (u32)TILE_CHUNKS) reinterpret_cast<uint4*>(tile32)[k] = pre[j];
-            }
-        }
-        __syncthreads();
-        if (t + 1 < t_end) nxt = tile_info(P, t + 1, t_begin, tb);
-        else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
-        issue_tile_loads(P, nxt, pre, pre_off, pre_end);
-        if (li < cur.count) {
-            u32 campaign;
-            i64 bucket;
-            bool ok;
-            if (!cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
-                const int ls = (int)(my_off - cur.s0 + cur.delta), le = (int)(my_end - cur.s0 + cur.delta);
-                ok = process_tbl_line(lsrc, ls, le, P, tl, campaign, bucket);
-            } else if (my_off <= my_end && my_end <= P.nbytes && my_end - my_off <= 0x7FFFFFFFu) {
-                const GlbSrc g{P.bytes + my_off, (u64)(my_end - my_off)};   // over-size tile: from HBM
-                ok = process_tbl_line(g, 0, (int)(my_end - my_off), P, tl, campaign, bucket);
-            } else {
-                tl.ev++;
-                tl.perr++;
-                ok = false;
-            }
-            if (ok) global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
-        }
-        __syncthreads();
-    }
-    flush_tally(P, tl, threadIdx.x & 63);
-}
 
 // Ring auto-base for .tbl batches (the JSON one is ring_autobase_kernel).
 __global__ __launch_bounds__(AUX_TPB) void tbl_ring_autobase_kernel(ScanParams P, i64* ring) {
@@ -1064,12 +1086,6 @@ __global__ __launch_bounds__(AUX_TPB) void tbl_ring_autobase_kernel(ScanParams P
     }
 }
 
-void launch_tbl_scan(const ScanParams& p, hipStream_t s) {
-    if (p.n == 0) return;
-    const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    hipLaunchKernelGGL(tbl_scan_kernel, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
-}
-
 void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
     hipLaunchKernelGGL(tbl_ring_autobase_kernel, dim3(1), dim3(AUX_TPB), 0, s, p, const_cast<i64*>(p.ring));
@@ -1078,8 +1094,14 @@ void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s) {
 void launch_scan(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
     const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    if (p.probe_serial) hipLaunchKernelGGL(scan_kernel<true>, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
-    else hipLaunchKernelGGL(scan_kernel<false>, dim3((unsigned)blocks), dim3(SCAN_TPB), LDS_BYTES, s, p);
+    const dim3 g((unsigned)blocks), b(SCAN_TPB);
+    if (p.tbl) {
+        if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, true>), g, b, LDS_BYTES, s, p);
+        else hipLaunchKernelGGL((scan_kernel<false, true>), g, b, LDS_BYTES, s, p);
+    } else {
+        if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false>), g, b, LDS_BYTES, s, p);
+        else hipLaunchKernelGGL((scan_kernel<false, false>), g, b, LDS_BYTES, s, p);
+    }
 }
 
 void launch_defer(const ScanParams& p, int blocks, hipStream_t s) {

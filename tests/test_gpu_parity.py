@@ -246,16 +246,16 @@ def test_tbl_generated_stream_vs_oracle():
             assert s[k] == v, k
 
 
-def _oracle_vs_gpu(lines, require_ip, lds=True):
+def _oracle_vs_gpu(lines, require_ip, lds=True, fmt="json", ad_map=None):
     """Submits the lines as one batch; on a mismatch, bisects to the first line whose
     GPU counters differ from the C oracle's (for the failure message)."""
-    ads, camp = gd.ad_arrays()
+    ads, camp = ad_map or gd.ad_arrays()
     am = oracle.AdMap(ads, camp)
 
     def run_gpu(ls):
         raw = b"".join(ls)
         offs = np.cumsum([0] + [len(x) for x in ls[:-1]]).tolist()
-        with make_ctx(require_ip=require_ip, lds_count=lds) as ctx:
+        with make_ctx(ads=(ads, camp), require_ip=require_ip, lds_count=lds, input_format=fmt) as ctx:
             ctx.submit(raw, offs, slot=0)
             rows = ctx.drain_buckets()
             st = ctx.stats()
@@ -264,7 +264,7 @@ def _oracle_vs_gpu(lines, require_ip, lds=True):
     def run_cpu(ls):
         raw = b"".join(ls)
         offs = np.cumsum([0] + [len(x) for x in ls[:-1]]).tolist()
-        return oracle.run(am, raw, offs, require_ip=require_ip)
+        return oracle.run(am, raw, offs, require_ip=require_ip, fmt=fmt)
 
     if run_gpu(lines) == run_cpu(lines):
         return
@@ -323,3 +323,45 @@ def test_device_tbl_generator_matches_host():
         assert nb == raw.size
         assert ctx.d2h(np.empty(nb, dtype=np.uint8), d_b).tobytes() == raw.tobytes()
         assert np.array_equal(ctx.d2h(np.empty(n, dtype=np.uint32), d_o), offs)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_tbl_mutations_match_oracle(seed):
+    """.tbl rows through the fast path and, mutated, through the deferred path: extra or
+    missing '|', '}' after a '|' (a SWAR false candidate), CR / CRLF / no terminator,
+    empty fields, long rows, non-digit times -- every counter equals the C oracle's."""
+    g = GenParams(seed=7, n_campaigns=10, ads_per_campaign=10, fmt="tbl", events_per_sec=1000)
+    _, aids = g.ids()
+    amap = (aids, list(g.ad_campaign_index()))
+    raw, offs = g.events_host(0, 4000)
+    raw = raw.tobytes()
+    bounds = list(offs) + [len(raw)]
+    rows = [raw[bounds[i]:bounds[i + 1]] for i in range(len(offs))]
+    rng = np.random.default_rng(seed)
+    out = []
+    for r in rows:
+        k = int(rng.integers(12))
+        body = r[:-1]
+        if k == 1:
+            p = int(rng.integers(len(body) + 1))
+            body = body[:p] + b"|" + body[p:]
+        elif k == 2:
+            p = int(rng.integers(len(body)))
+            body = body[:p] + body[p + 1:]
+        elif k == 3:
+            bars = [i for i, c in enumerate(body) if c == 0x7C]
+            p = bars[int(rng.integers(len(bars)))] + 1
+            body = body[:p] + b"}" + body[p:]
+        elif k == 4:
+            body = body + b"\r"
+        elif k == 5:
+            body = body.replace(b"|view|", b"||") if rng.integers(2) else body + b"|"
+        elif k == 6:
+            body = body + b"|x" * int(rng.integers(1, 12))
+        elif k == 7:
+            body = body[:-3] + bytes([int(rng.choice([0x41, 0x2D, 0x2B, 0x20]))]) + body[-2:]
+        elif k == 8:
+            body = body.replace(b"|", b"||", 1)
+        out.append(body + (b"" if k == 9 else b"\n"))
+    _oracle_vs_gpu(out, False, fmt="tbl", ad_map=amap)
+    _oracle_vs_gpu(out, False, lds=False, fmt="tbl", ad_map=amap)
