@@ -610,6 +610,9 @@ constexpr int AUX_NT = 2;
 #ifndef YSB_SETPRIO
 #define YSB_SETPRIO 1
 #endif
+#ifndef YSB_PREFETCH_DEPTH
+#define YSB_PREFETCH_DEPTH 1
+#endif
 #ifndef YSB_LINE_INTERLEAVE
 #define YSB_LINE_INTERLEAVE 1
 #endif
@@ -748,10 +751,18 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
     __syncthreads();
 
     Tally tl{0, 0, 0, 0, 0, 0, 0};
-    uint4 pre[CHUNKS_PER_THREAD];
-    u32 pre_off = 0, pre_end = 0;
-    TileInfo nxt = tile_info(P, t_begin, t_begin, tb);
-    issue_tile_loads(P, nxt, pre, pre_off, pre_end);
+    // Prefetch depth: tile t + PF_DEPTH is issued once tile t sits in LDS.  Depth 2 keeps
+    // two tiles in flight per wave (two register buffers, the loop unrolled by two).
+    constexpr int PF_DEPTH = YSB_PREFETCH_DEPTH;
+    const TileInfo none{P.n, 0u, 0u, 0u, 0u, 0u, true};
+    uint4 preA[CHUNKS_PER_THREAD], preB[CHUNKS_PER_THREAD];
+    u32 offA = 0, endA = 0, offB = 0, endB = 0;
+    TileInfo infA = tile_info(P, t_begin, t_begin, tb), infB = none;
+    issue_tile_loads(P, infA, preA, offA, endA);
+    if constexpr (PF_DEPTH == 2) {
+        if (t_begin + 1 < t_end) infB = tile_info(P, t_begin + 1, t_begin, tb);
+        issue_tile_loads(P, infB, preB, offB, endB);
+    }
     // The LDS window's base, identical in every thread (each applies the same requests).
     i64 lbase = 0;
     bool lset = false;
@@ -764,8 +775,10 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
     if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
 #endif
     STAMP_DECL
-    for (u64 t = t_begin; t < t_end; ++t) {
-        const TileInfo cur = nxt;
+    // One tile: its bytes arrive in pre (issued PF_DEPTH tiles ago), the tile PF_DEPTH
+    // ahead is issued into the same registers once they are in LDS.
+    auto tile_step = [&](u64 t, TileInfo& inf, uint4 (&pre)[CHUNKS_PER_THREAD], u32& pre_off, u32& pre_end) {
+        const TileInfo cur = inf;
         const u32 my_off = pre_off;
         const u32 li = lane_line(tid);
         const u32 my_end = (cur.first + li + 1 < P.n) ? pre_end : (u32)P.nbytes;
@@ -801,11 +814,10 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         if (tid == 0) misc64[par ^ 1] = INT64_MIN;   // every thread has read it
         STAMP(1);
 #ifdef YSB_DIAG_A_ONLY
-        if (t + 1 < t_end) nxt = tile_info(P, t + 1, t_begin, tb);
-        else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
-        issue_tile_loads(P, nxt, pre, pre_off, pre_end);
+        inf = t + PF_DEPTH < t_end ? tile_info(P, t + PF_DEPTH, t_begin, tb) : none;
+        issue_tile_loads(P, inf, pre, pre_off, pre_end);
         __syncthreads();
-        continue;
+        return;
 #endif
         // ---- Phase B1: canonical parse from LDS; any other line is deferred -------
         bool ok1 = false;
@@ -862,9 +874,8 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         // Issued on every iteration (the last one loads nothing: out-of-range buffer
         // loads return zeros) so every path has the same count of loads in flight and
         // the waits below stay counted.
-        if (t + 1 < t_end) nxt = tile_info(P, t + 1, t_begin, tb);
-        else nxt = TileInfo{P.n, 0u, 0u, 0u, 0u, 0u, true};
-        issue_tile_loads(P, nxt, pre, pre_off, pre_end);
+        inf = t + PF_DEPTH < t_end ? tile_info(P, t + PF_DEPTH, t_begin, tb) : none;
+        issue_tile_loads(P, inf, pre, pre_off, pre_end);
         // ---- Phase B2: join result ------------------------------------------------
         bool valid = false, dfr2 = false;
         u32 campaign = 0;
@@ -919,6 +930,14 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         STAMP(4);
         __syncthreads();
         STAMP(5);
+    };
+    if constexpr (PF_DEPTH == 2) {
+        for (u64 t = t_begin; t < t_end; t += 2) {
+            tile_step(t, infA, preA, offA, endA);
+            if (t + 1 < t_end) tile_step(t + 1, infB, preB, offB, endB);
+        }
+    } else {
+        for (u64 t = t_begin; t < t_end; ++t) tile_step(t, infA, preA, offA, endA);
     }
 #ifdef YSB_STAMPS
     if (lane == 0) {
