@@ -384,6 +384,106 @@ __device__ __forceinline__ bool canon_stage2(const LdsSrc& src, int s, int e, co
     return true;
 }
 
+// Four ASCII digits (byte 0 most significant) -> 0..9999; bad != 0 if any byte is not a digit.
+__device__ __forceinline__ u32 swar_digits4(u32 w, u32& bad) {
+    const u32 dgt = w - 0x30303030u;                                        // per byte, borrow-free when valid
+    bad |= (w & 0xF0F0F0F0u) ^ 0x30303030u;                                 // high nibbles must be 3
+    bad |= (dgt + 0x76767676u) & 0x80808080u;                               // low nibbles must be <= 9
+    const u32 pr = (dgt & 0x00FF00FFu) * 10u + ((dgt >> 8) & 0x00FF00FFu); // two 2-digit halves
+    return (pr & 0xFFFFu) * 100u + (pr >> 16);
+}
+
+// ---------------------------------------------------------------------------
+// Vocabulary fast path (YSB_VOCAB, the default): the generator's lines are the template
+// above with values from closed sets -- ad_type one of banner / modal / sponsored-search /
+// mail / mobile, event_type one of view / click / purchase (core.clj:68-69,164-165), a
+// 13-digit event_time and ip_address "1.2.3.4" (:96,:181).  Stage 1 reads the 164-byte
+// prefix plus 36 bytes (the ad_type value and where event_type starts), names the ad_type
+// by an exact compare and the event_type by its first byte; every later position then
+// follows, and stage 2 compares the rest of the line up to the closing '}' exactly
+// (separators, keys, the event_type value, the ip value) and checks the 13 time bytes are
+// digits.  So every byte up to '}' is either compared or shown to be a UUID byte free of
+// '"', '\\' and control bytes or a digit: the line parses exactly as org.json parses
+// it.  No candidate scan of the tail.  Any other line is deferred to the general parser.
+// ---------------------------------------------------------------------------
+#ifndef YSB_VOCAB
+#define YSB_VOCAB 1
+#endif
+constexpr int VOC_WORDS = 50;            // line bytes 0..199
+constexpr int VOC_MIN_LEN = 248;         // 240 + shortest ad_type (4) + event_type (4)
+
+__device__ __forceinline__ bool vocab_stage1(const LdsSrc& src, int s, int e, CanonA& c) {
+    constexpr PrefixTpl T = make_prefix_tpl();
+    const int L = e - s;
+    if (L < VOC_MIN_LEN) return false;
+    const int a = s >> 2;
+    const u32 sb = (u32)(s & 3);
+    u32 P[VOC_WORDS + 1];
+#pragma unroll
+    for (int k = 0; k <= VOC_WORDS; ++k) P[k] = src.d[a + k];
+    u32 d = 0, W[VOC_WORDS];
+#pragma unroll
+    for (int j = 0; j < VOC_WORDS; ++j) W[j] = __builtin_amdgcn_alignbyte(P[j + 1], P[j], sb);   // bytes 4j..4j+3
+#pragma unroll
+    for (int j = 0; j < PREFIX_WORDS; ++j) {
+        if (T.m[j] == 0xFFFFFFFFu) d |= W[j] ^ T.e[j];
+        else if (T.m[j] != 0u) d |= (W[j] ^ T.e[j]) & T.m[j];
+        if (T.v[j] != 0u) d |= cand_z(W[j]) & T.v[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(W[29 + k], W[28 + k], 1u);   // bytes 113..148
+    // ad_type at byte 164, exactly one of the five
+    const u32 a0 = W[41], a1 = W[42];
+    int La = 0;
+    if (a0 == w4('b', 'a', 'n', 'n') && (a1 & 0xFFFFu) == w4('e', 'r', 0, 0)) La = 6;
+    else if (a0 == w4('m', 'a', 'i', 'l')) La = 4;
+    else if (a0 == w4('m', 'o', 'd', 'a') && (a1 & 0xFFu) == 'l') La = 5;
+    else if (a0 == w4('m', 'o', 'b', 'i') && (a1 & 0xFFFFu) == w4('l', 'e', 0, 0)) La = 6;
+    else if (a0 == w4('s', 'p', 'o', 'n') && a1 == w4('s', 'o', 'r', 'e') && W[43] == w4('d', '-', 's', 'e') &&
+             W[44] == w4('a', 'r', 'c', 'h'))
+        La = 16;
+    // event_type's first byte at 164 + La + 18 (bytes 186 / 187 / 188 / 198)
+    const u32 et0 = La == 4 ? (W[46] >> 16) & 0xFFu : La == 5 ? W[46] >> 24 : La == 6 ? W[47] & 0xFFu
+                                                                                    : (W[49] >> 16) & 0xFFu;
+    const int Le = et0 == 'v' ? 4 : et0 == 'c' ? 5 : et0 == 'p' ? 8 : 0;
+    c.e3 = 164 + La;           // closing quote of ad_type
+    c.e4 = c.e3 + 18 + Le;     // of event_type
+    c.e5 = c.e4 + 18 + 13;     // of event_time
+    c.e6 = c.e5 + 18 + 7;      // of ip_address
+    return d == 0u && La != 0 && Le != 0 && c.e6 + 2 <= L;
+}
+
+__device__ __forceinline__ bool vocab_stage2(const LdsSrc& src, int s, int e, const CanonA& a, CanonB& c) {
+    u32 t4[5], ev[2], t5[5], t6[7];
+    load_span(src, s + a.e3, t4);
+    load_span(src, s + a.e3 + 18, ev);
+    load_span(src, s + a.e4, t5);
+    load_span(src, s + a.e4 + 18, c.td);
+    load_span(src, s + a.e5, t6);
+    u32 d = (t4[0] ^ w4('"', ',', ' ', '"')) | (t4[1] ^ w4('e', 'v', 'e', 'n')) | (t4[2] ^ w4('t', '_', 't', 'y')) |
+            (t4[3] ^ w4('p', 'e', '"', ':')) | ((t4[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
+    d |= (t5[0] ^ w4('"', ',', ' ', '"')) | (t5[1] ^ w4('e', 'v', 'e', 'n')) | (t5[2] ^ w4('t', '_', 't', 'i')) |
+         (t5[3] ^ w4('m', 'e', '"', ':')) | ((t5[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
+    d |= (t6[0] ^ w4('"', ',', ' ', '"')) | (t6[1] ^ w4('i', 'p', '_', 'a')) | (t6[2] ^ w4('d', 'd', 'r', 'e')) |
+         (t6[3] ^ w4('s', 's', '"', ':')) | (t6[4] ^ w4(' ', '"', '1', '.')) | (t6[5] ^ w4('2', '.', '3', '.')) |
+         ((t6[6] & 0xFFFFFFu) ^ w4('4', '"', '}', 0));
+    // the event_type value: exactly the one its first byte named
+    const int Le = a.e4 - a.e3 - 18;
+    const bool etok = Le == 4   ? ev[0] == w4('v', 'i', 'e', 'w')
+                      : Le == 5 ? (ev[0] == w4('c', 'l', 'i', 'c') && (ev[1] & 0xFFu) == 'k')
+                                : (ev[0] == w4('p', 'u', 'r', 'c') && ev[1] == w4('h', 'a', 's', 'e'));
+    // the event_time value: 13 ASCII digits
+    u32 bad = 0;
+    swar_digits4(c.td[0], bad);
+    swar_digits4(c.td[1], bad);
+    swar_digits4(c.td[2], bad);
+    bad |= ((c.td[3] & 0xFFu) - '0') > 9u;
+    c.view = Le == 4;
+    c.tlen = 13;
+    // org.json's JSONObject(String) stops at the closing '}': what follows is never read.
+    return d == 0u && etok && bad == 0u;
+}
+
 // ---------------------------------------------------------------------------
 // .tbl fast path (YSB_F_FORMAT_TBL): the generator's rows, user|page|ad|ad_type|
 // event_type|event_time\n with 36-byte UUIDs -- the first three '|' at bytes 36, 73 and
@@ -481,15 +581,6 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
     campaign = (u32)c;
     bucket = div_trunc(tv, P.div);
     return true;
-}
-
-// Four ASCII digits (byte 0 most significant) -> 0..9999; bad != 0 if any byte is not a digit.
-__device__ __forceinline__ u32 swar_digits4(u32 w, u32& bad) {
-    const u32 dgt = w - 0x30303030u;                                        // per byte, borrow-free when valid
-    bad |= (w & 0xF0F0F0F0u) ^ 0x30303030u;                                 // high nibbles must be 3
-    bad |= (dgt + 0x76767676u) & 0x80808080u;                               // low nibbles must be <= 9
-    const u32 pr = (dgt & 0x00FF00FFu) * 10u + ((dgt >> 8) & 0x00FF00FFu); // two 2-digit halves
-    return (pr & 0xFFFFu) * 100u + (pr >> 16);
 }
 
 // Long.parseLong of a canonical line's event_time, then the bucket.  13 unsigned digits
@@ -829,6 +920,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
+            else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1(lsrc, ls, le, ca);
             else ok1 = canon_stage1(lsrc, ls, le, ca);
         }
         bool pend = false, dfr = false, tok = false;
@@ -838,6 +930,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         bool ok2 = false;
         if (li < cur.count) {
             if constexpr (TBL) ok2 = ok1 && tbl_stage2(lsrc, ls, le, ca, cb);
+            else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2(lsrc, ls, le, ca, cb);
             else ok2 = ok1 && canon_stage2(lsrc, ls, le, ca, cb);
             dfr = !ok2;   // bad offsets, other layouts, escapes, over-size tiles
         }

@@ -365,3 +365,42 @@ def test_tbl_mutations_match_oracle(seed):
         out.append(body + (b"" if k == 9 else b"\n"))
     _oracle_vs_gpu(out, False, fmt="tbl", ad_map=amap)
     _oracle_vs_gpu(out, False, lds=False, fmt="tbl", ad_map=amap)
+
+
+def test_vocabulary_fast_path_edges_match_oracle():
+    """Generator-layout lines whose ad_type / event_type / event_time / ip_address leave
+    the generator's vocabulary (or hide a quote / backslash / control byte in it) must
+    reach the general parser; every counter equals the C oracle's."""
+    raw, offs = gd.events("gen_s7")
+    bounds = list(offs) + [len(raw)]
+    lines = [raw[bounds[i]:bounds[i + 1]] for i in range(len(offs))]
+    subs = [
+        (b'"ad_type": "banner"', [b'"ad_type": "bannerX"', b'"ad_type": "banne"', b'"ad_type": "Banner"',
+                                  b'"ad_type": "ban\\"er"', b'"ad_type": "b\\u0061nner"', b'"ad_type": "bann\x00r"']),
+        (b'"ad_type": "mail"', [b'"ad_type": "mai"', b'"ad_type": "maill"', b'"ad_type": "mobile"',
+                                b'"ad_type": "moda"', b'"ad_type": "modal"']),
+        (b'"ad_type": "sponsored-search"', [b'"ad_type": "sponsored-searcH"', b'"ad_type": "sponsored-searc"']),
+        (b'"event_type": "view"', [b'"event_type": "viewx"', b'"event_type": "vie"', b'"event_type": "click"',
+                                   b'"event_type": "purchase"', b'"event_type": "v\\"ew"', b'"event_type": "vi\rw"']),
+        (b'"event_type": "click"', [b'"event_type": "clicks"', b'"event_type": "view"', b'"event_type": "clock"']),
+        (b'"event_type": "purchase"', [b'"event_type": "purchas"', b'"event_type": "purchasE"']),
+        (b'"ip_address": "1.2.3.4"', [b'"ip_address": "1.2.3.5"', b'"ip_address": "1.2.3.4 "',
+                                      b'"ip_address": "1.2.3.4", "x": 1', b'"ip_address": 1.2']),
+    ]
+    rng = np.random.default_rng(11)
+    out = []
+    for i, ln in enumerate(lines):
+        if i % 3 == 0:
+            cands = [(a, b) for a, bs in subs if a in ln for b in bs]
+            a, b = cands[int(rng.integers(len(cands)))]
+            ln = ln.replace(a, b)
+        elif i % 3 == 1:                              # the 13 time bytes: length, sign, non-digits
+            j = ln.index(b'"event_time": "') + 15
+            k = ln.index(b'"', j)
+            t = ln[j:k]
+            t = [t[:-1], t + b"7", b"-" + t[1:], t[:5] + b"\"" + t[6:], t[:5] + b"a" + t[6:],
+                 t[:5] + b"\\" + t[6:], t[:7] + b"\x00" + t[8:], t[:12] + b" "][int(rng.integers(8))]
+            ln = ln[:j] + t + ln[k:]
+        out.append(ln)
+    _oracle_vs_gpu(out, False)
+    _oracle_vs_gpu(out, True, lds=False)
