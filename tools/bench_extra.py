@@ -7,6 +7,10 @@
         configs[1]'s events as the fork's live .tbl rows (MockWindowedFlatMap,
         AdvertisingTopologyNative.java:197-226), generated in HBM: tbl_scan_kernel's
         events/s and algorithmic GB/s, generator-truth check.
+    python tools/bench_extra.py general [--events N] [--steps K]
+        the same events re-laid-out so no line is in the generator's layout (no space
+        after ':'): every line through the deferred org.json parser (defer_kernel);
+        events/s, exact vs the C oracle on the same bytes.
     python tools/bench_extra.py pcie [--batch-mb M] [--seconds S]
         host-staged throughput: pre-staged pinned double-buffered slots -> H2D copy
         stream -> scan kernel (PCIe-inclusive rate; never bench.py's value).
@@ -133,6 +137,40 @@ def tbl(args):
                       "time_errors": st["time_errors"], "out_of_ring": st["out_of_ring"]}}
 
 
+def general(args):
+    from oracle import oracle as orc   # the checker (test infrastructure), not the measured path
+    g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000)
+    _, aids = g.ids()
+    n = min(args.events, 4_000_000)
+    raw, offs = g.events_host(0, n)
+    data = raw.tobytes().replace(b'": "', b'":"')            # not the generator's layout any more
+    offs2 = np.zeros(n, dtype=np.uint32)
+    nl = np.flatnonzero(np.frombuffer(data, dtype=np.uint8) == 0x0A)
+    offs2[1:] = (nl[:-1] + 1).astype(np.uint32)
+    ctx = YsbContext(n_campaigns=100, window_ring=1024, timing=True, max_batch_bytes=16 << 20,
+                     max_batch_events=1 << 16)
+    ctx.load_ad_map(aids, g.ad_campaign_index())
+    d_b, d_o = ctx.device_alloc(len(data) + 64), ctx.device_alloc(4 * n + 64)
+    ctx.h2d(d_b, np.frombuffer(data, dtype=np.uint8))
+    ctx.h2d(d_o, offs2)
+    ctx.submit_device(d_b, len(data), d_o, n)
+    ctx.sync()
+    ctx.reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.submit_device(d_b, len(data), d_o, n)
+    ctx.sync()
+    el = time.perf_counter() - t0
+    ctx.reset()
+    ctx.submit_device(d_b, len(data), d_o, n)
+    got = ctx.drain_buckets()
+    st = ctx.stats()
+    rows, ost = orc.run(orc.AdMap(aids, g.ad_campaign_index()), data, offs2.tolist(), threads=8)
+    return {"config": "%d generator events without the space after ':' (all through the general parser)" % n,
+            "events_per_s": round(n * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
+            "deferred": st["deferred"], "exact_vs_oracle": got == rows and all(st[k] == v for k, v in ost.items())}
+
+
 def pcie(args):
     g = GenParams(seed=42, events_per_sec=100_000)
     _, aids = g.ids()
@@ -240,7 +278,7 @@ def stream(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["config3", "tbl", "pcie", "stream"])
+    ap.add_argument("mode", choices=["config3", "tbl", "general", "pcie", "stream"])
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--segment", type=int, default=12_500_000)
     ap.add_argument("--steps", type=int, default=5)
@@ -251,7 +289,7 @@ def main():
     ap.add_argument("--batch-ms", type=int, default=100)
     ap.add_argument("--ooo-ms", type=int, default=100)
     args = ap.parse_args()
-    out = {"config3": config3, "tbl": tbl, "pcie": pcie, "stream": stream}[args.mode](args)
+    out = {"config3": config3, "tbl": tbl, "general": general, "pcie": pcie, "stream": stream}[args.mode](args)
     print(json.dumps(out), flush=True)
 
 
