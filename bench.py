@@ -93,11 +93,13 @@ class Dist:
         return obj[0]
 
 
-def torch_sync():
+def torch_sync(device=0):
+    """torch.cuda.synchronize() on this rank's own GPU (the contract's sync; the library's
+    streams are synchronised by ctx.sync() before it)."""
     try:
         import torch
         if torch.cuda.is_available():
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(device)
     except Exception:
         pass
 
@@ -184,13 +186,13 @@ def main():
         step()
     ctx.sync()
     ctx.kernel_time()   # discard warmup launches
-    torch_sync()
+    torch_sync(d.local)
     d.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     ctx.sync()
-    torch_sync()
+    torch_sync(d.local)
     d.barrier()
     el = d.max(time.perf_counter() - t0)
     kms, launches = ctx.kernel_time()
