@@ -451,7 +451,7 @@ static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u
     p.stats = c->d_stats;
     p.n_tiles = (n + SCAN_TPB - 1) / SCAN_TPB;
     // whole rounds of resident workgroups (a partial last round would idle most CUs)
-    const u64 resident = (u64)c->cus * SCAN_WG_PER_CU;
+    const u64 resident = (u64)c->cus * (p.tbl ? Geom<true>::WG_PER_CU : Geom<false>::WG_PER_CU);
     const u64 rounds = std::max<u64>(1, (p.n_tiles + resident * MAX_TILES_PER_BLOCK - 1) / (resident * MAX_TILES_PER_BLOCK));
     const u64 blocks = std::max<u64>(1, std::min<u64>(p.n_tiles, rounds * resident));
     p.tiles_per_block = (u32)((p.n_tiles + blocks - 1) / blocks);
@@ -488,7 +488,7 @@ static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_
     p.defer_done = c->d_defer_ctr + 1;
     p.defer_cap = (u32)c->defer_cap;
 #ifdef YSB_STAMPS
-    const u64 words = (u64)c->cus * SCAN_WG_PER_CU * (SCAN_TPB / 64) * N_STAMPS;
+    const u64 words = (u64)c->cus * std::max(Geom<true>::WG_PER_CU, Geom<false>::WG_PER_CU) * (SCAN_TPB / 64) * N_STAMPS;
     if (!c->d_dbg) {
         HIPCHK(c, hipMalloc(&c->d_dbg, words * 8));
         HIPCHK(c, hipMemset(c->d_dbg, 0, words * 8));

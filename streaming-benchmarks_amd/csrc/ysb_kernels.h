@@ -26,6 +26,31 @@ constexpr int TILE_CHUNKS = TILE_CAP / 16;    // 16-byte chunks per tile
 constexpr int CHUNKS_PER_THREAD = (TILE_CHUNKS + SCAN_TPB - 1) / SCAN_TPB;  // 17
 constexpr int LCNT_CAP = 256;                 // u32 per-workgroup (campaign, window) counters
 constexpr int MAX_TILES_PER_BLOCK = YSB_MAX_TILES;   // tile bounds preloaded into LDS
+// .tbl rows are ~140 B (JSON lines ~254 B): smaller tiles, so more workgroups fit a CU's
+// LDS and the bytes in flight per CU stay comparable.
+#ifndef YSB_TBL_LINE_BYTES
+#define YSB_TBL_LINE_BYTES 160
+#endif
+#ifndef YSB_TBL_WG_PER_CU
+#define YSB_TBL_WG_PER_CU 12
+#endif
+
+// Per-input-format geometry of the scan kernel: tile capacity, prefetch registers and
+// the LDS carve (tile | slack | window counters | misc | tile bounds).
+template <bool TBL>
+struct Geom {
+    static constexpr int WG_PER_CU = TBL ? YSB_TBL_WG_PER_CU : SCAN_WG_PER_CU;
+    static constexpr int CAP = SCAN_TPB * (TBL ? YSB_TBL_LINE_BYTES : YSB_TILE_LINE_BYTES);
+    static constexpr int CHUNKS = CAP / 16;
+    static constexpr int CPT = (CHUNKS + SCAN_TPB - 1) / SCAN_TPB;   // 16-byte chunks per thread
+    static constexpr int OFF_TILE = 0;
+    static constexpr int OFF_LCNT = OFF_TILE + CAP + 64;             // 64 B slack for reads past a tile
+    static constexpr int OFF_MISC = OFF_LCNT + LCNT_CAP * 4;
+    static constexpr int OFF_TB = OFF_MISC + 64;
+    static constexpr int LDS = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
+    static_assert(OFF_LCNT % 16 == 0 && OFF_MISC % 16 == 0 && OFF_TB % 16 == 0, "LDS carve must stay 16-byte aligned");
+    static_assert(LDS <= 163840 / WG_PER_CU, "WG_PER_CU workgroups must fit one CU's 160 KiB of LDS");
+};
 constexpr int AUX_TPB = 256;                  // threads per workgroup of the other kernels
 
 struct ScanParams {

@@ -652,15 +652,7 @@ __device__ __forceinline__ void global_add(const ScanParams& P, i64 ring_lo, boo
 // ---------------------------------------------------------------------------
 // LDS layout (dynamic, 16-byte aligned carve, no static __shared__)
 // ---------------------------------------------------------------------------
-constexpr int OFF_TILE = 0;
-// 64 bytes of slack after the tile: stage 1 reads up to 276 bytes from a line start
-constexpr int OFF_LCNT = OFF_TILE + TILE_CAP + 64;
-constexpr int OFF_MISC = OFF_LCNT + LCNT_CAP * 4;
-constexpr int OFF_TB = OFF_MISC + 64;
-constexpr int LDS_BYTES = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
-static_assert(OFF_LCNT % 16 == 0 &&
-              OFF_MISC % 16 == 0 && OFF_TB % 16 == 0, "LDS carve must stay 16-byte aligned");
-static_assert(LDS_BYTES <= 163840 / SCAN_WG_PER_CU, "SCAN_WG_PER_CU workgroups must fit one CU's 160 KiB of LDS");
+constexpr int LDS_BYTES = Geom<false>::LDS;   // the JSON geometry (Geom<true> for .tbl rows)
 
 struct TileInfo {
     u64 first;
@@ -674,6 +666,7 @@ struct TileInfo {
 
 // Tile bounds come from the LDS copy tb[] (loaded once per workgroup), so no HBM
 // round trip sits between two tiles.
+template <int CAP>
 __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_begin, const u32* tb) {
     TileInfo ti;
     ti.first = t * SCAN_TPB;
@@ -689,7 +682,7 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_
     ti.delta = s0 & 15u;   // P.bytes is 16-byte aligned
     const bool sane = (u64)s0 <= e && e <= P.nbytes;
     const u64 len = sane ? e - s0 + ti.delta : ~0ULL;
-    ti.oversize = !sane || len > (u64)TILE_CAP;
+    ti.oversize = !sane || len > (u64)CAP;
     ti.len = ti.oversize ? 0u : (u32)len;
     return ti;
 }
@@ -723,7 +716,8 @@ __device__ __forceinline__ u32 lane_line(int tid) {
 // chunks past the tile read zeros and never fault); per-lane offsets are
 // loop-invariant, so issuing costs no VALU.  Always the same number of loads per lane,
 // so later waits can count them (vmcnt) instead of draining everything.
-__device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const TileInfo& ti, uint4 (&pre)[CHUNKS_PER_THREAD],
+template <int CPT>
+__device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const TileInfo& ti, uint4 (&pre)[CPT],
                                                  u32& my_off, u32& my_end) {
     const int tid = threadIdx.x;
     const u8* tbase = P.bytes + (ti.s0 - ti.delta);
@@ -733,7 +727,7 @@ __device__ __forceinline__ void issue_tile_loads(const ScanParams& P, const Tile
     const __amdgpu_buffer_rsrc_t rb =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(tbase), 0, (int)((ti.len + 15u) & ~15u), 0x00020000);
 #pragma unroll
-    for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
+    for (int j = 0; j < CPT; ++j) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, 16 * (j * SCAN_TPB + tid), 0, AUX_NT);
         pre[j] = make_uint4(v[0], v[1], v[2], v[3]);
     }
@@ -813,12 +807,14 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // SERIAL: HBM-resident cuckoo table, second slot probed only after a first-slot miss.
 // TBL: the fork's .tbl rows (tbl_stage1/2) instead of JSON lines (canon_stage1/2).
 template <bool SERIAL, bool TBL>
-__global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(ScanParams P) {
+__global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<TBL>::WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(ScanParams P) {
+    using G = Geom<TBL>;
+    constexpr int CPT = G::CPT;
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
-    u32* tile32 = reinterpret_cast<u32*>(smem + OFF_TILE);
-    u32* lcnt = reinterpret_cast<u32*>(smem + OFF_LCNT);
-    i64* misc64 = reinterpret_cast<i64*>(smem + OFF_MISC);   // [0] lbase, [1] lset, [2..5] scratch
-    u32* tb = reinterpret_cast<u32*>(smem + OFF_TB);
+    u32* tile32 = reinterpret_cast<u32*>(smem + G::OFF_TILE);
+    u32* lcnt = reinterpret_cast<u32*>(smem + G::OFF_LCNT);
+    i64* misc64 = reinterpret_cast<i64*>(smem + G::OFF_MISC);   // [0] lbase, [1] lset, [2..5] scratch
+    u32* tb = reinterpret_cast<u32*>(smem + G::OFF_TB);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -846,12 +842,12 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
     // two tiles in flight per wave (two register buffers, the loop unrolled by two).
     constexpr int PF_DEPTH = YSB_PREFETCH_DEPTH;
     const TileInfo none{P.n, 0u, 0u, 0u, 0u, 0u, true};
-    uint4 preA[CHUNKS_PER_THREAD], preB[CHUNKS_PER_THREAD];
+    uint4 preA[CPT], preB[CPT];
     u32 offA = 0, endA = 0, offB = 0, endB = 0;
-    TileInfo infA = tile_info(P, t_begin, t_begin, tb), infB = none;
+    TileInfo infA = tile_info<G::CAP>(P, t_begin, t_begin, tb), infB = none;
     issue_tile_loads(P, infA, preA, offA, endA);
     if constexpr (PF_DEPTH == 2) {
-        if (t_begin + 1 < t_end) infB = tile_info(P, t_begin + 1, t_begin, tb);
+        if (t_begin + 1 < t_end) infB = tile_info<G::CAP>(P, t_begin + 1, t_begin, tb);
         issue_tile_loads(P, infB, preB, offB, endB);
     }
     // The LDS window's base, identical in every thread (each applies the same requests).
@@ -868,7 +864,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
     STAMP_DECL
     // One tile: its bytes arrive in pre (issued PF_DEPTH tiles ago), the tile PF_DEPTH
     // ahead is issued into the same registers once they are in LDS.
-    auto tile_step = [&](u64 t, TileInfo& inf, uint4 (&pre)[CHUNKS_PER_THREAD], u32& pre_off, u32& pre_end) {
+    auto tile_step = [&](u64 t, TileInfo& inf, uint4 (&pre)[CPT], u32& pre_off, u32& pre_end) {
         const TileInfo cur = inf;
         const u32 my_off = pre_off;
         const u32 li = lane_line(tid);
@@ -882,9 +878,9 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         // unconditionally; only the last round is cut at TILE_CHUNKS (a whole wave).
         if (!cur.oversize) {
 #pragma unroll
-            for (int j = 0; j < CHUNKS_PER_THREAD; ++j) {
+            for (int j = 0; j < CPT; ++j) {
                 const u32 k = (u32)(j * SCAN_TPB + tid);
-                if (j * SCAN_TPB + SCAN_TPB <= TILE_CHUNKS || k < (u32)TILE_CHUNKS) {
+                if (j * SCAN_TPB + SCAN_TPB <= G::CHUNKS || k < (u32)G::CHUNKS) {
                     reinterpret_cast<uint4*>(tile32)[k] = pre[j];
                 }
             }
@@ -905,7 +901,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         if (tid == 0) misc64[par ^ 1] = INT64_MIN;   // every thread has read it
         STAMP(1);
 #ifdef YSB_DIAG_A_ONLY
-        inf = t + PF_DEPTH < t_end ? tile_info(P, t + PF_DEPTH, t_begin, tb) : none;
+        inf = t + PF_DEPTH < t_end ? tile_info<G::CAP>(P, t + PF_DEPTH, t_begin, tb) : none;
         issue_tile_loads(P, inf, pre, pre_off, pre_end);
         __syncthreads();
         return;
@@ -967,7 +963,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(SCAN_W
         // Issued on every iteration (the last one loads nothing: out-of-range buffer
         // loads return zeros) so every path has the same count of loads in flight and
         // the waits below stay counted.
-        inf = t + PF_DEPTH < t_end ? tile_info(P, t + PF_DEPTH, t_begin, tb) : none;
+        inf = t + PF_DEPTH < t_end ? tile_info<G::CAP>(P, t + PF_DEPTH, t_begin, tb) : none;
         issue_tile_loads(P, inf, pre, pre_off, pre_end);
         // ---- Phase B2: join result ------------------------------------------------
         bool valid = false, dfr2 = false;
@@ -1208,11 +1204,11 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
     const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;
     const dim3 g((unsigned)blocks), b(SCAN_TPB);
     if (p.tbl) {
-        if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, true>), g, b, LDS_BYTES, s, p);
-        else hipLaunchKernelGGL((scan_kernel<false, true>), g, b, LDS_BYTES, s, p);
+        if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, true>), g, b, Geom<true>::LDS, s, p);
+        else hipLaunchKernelGGL((scan_kernel<false, true>), g, b, Geom<true>::LDS, s, p);
     } else {
-        if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false>), g, b, LDS_BYTES, s, p);
-        else hipLaunchKernelGGL((scan_kernel<false, false>), g, b, LDS_BYTES, s, p);
+        if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false>), g, b, Geom<false>::LDS, s, p);
+        else hipLaunchKernelGGL((scan_kernel<false, false>), g, b, Geom<false>::LDS, s, p);
     }
 }
 
