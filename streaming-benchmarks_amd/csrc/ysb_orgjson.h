@@ -25,6 +25,7 @@
 namespace ysb {
 
 constexpr int OJ_MAX_DEPTH = 64;
+constexpr int OJ_TOP_KEYS = 16;   // top-level keys checked through hashes (later ones: re-walk)
 
 __device__ __forceinline__ bool oj_delim(u32 c) {
     return c == ',' || c == ':' || c == ']' || c == '}' || c == '/' || c == '\\' || c == '"' || c == '[' ||
@@ -318,6 +319,15 @@ __device__ __noinline__ bool oj_key_equal(const S& src, const OjKey& a, const Oj
     }
 }
 
+// FNV-1a of a key's toString() bytes (the duplicate-key prefilter of the top-level object).
+template <class S>
+__device__ __noinline__ u32 oj_key_hash(const S& src, const OjKey& k) {
+    OjKeyIter<S> it(src, k);
+    u32 h = 2166136261u;
+    for (int c = it.next(); c >= 0; c = it.next()) h = (h ^ (u32)c) * 16777619u;
+    return h;
+}
+
 // ---- skipping over already-validated text ----------------------------------------------
 template <class S>
 __device__ __forceinline__ int oj_skip_clean(const S& src, int p, int e) {
@@ -398,10 +408,18 @@ struct OjTok {
     const S& src;
     int p, e;
     bool eof;
+    int wi = -1;   // index of the cached source word (sequential reads: one load per 4 bytes)
+    u32 w = 0;
     __device__ int next() {
         if (p >= e) { eof = true; return -1; }
         eof = false;
-        return (int)src.b(p++);
+        if ((p >> 2) != wi) {
+            wi = p >> 2;
+            w = src.load4(p & ~3);
+        }
+        const int c = (int)((w >> ((p & 3) << 3)) & 0xFFu);
+        ++p;
+        return c;
     }
     __device__ bool back() {
         if (eof) return false;
@@ -480,9 +498,19 @@ enum : int { OJS_KEY = 0, OJS_COLON, OJS_VALUE, OJS_OSEP, OJS_AFIRST, OJS_AELEM,
 // top-level ad_id / event_type / event_time.
 template <class S>
 __device__ __noinline__ bool parse_line(const S& src, int s, int e, u32 require, Span& ad, Span& et, Span& tm) {
-    int end = s;
-    while (end < e && src.b(end) != 0u) ++end;                            // NUL: end of input
-    OjTok<S> t{src, s, end, false};
+    int end = e;                                                           // NUL: end of input
+    for (int q = s & ~3; q < e; q += 4) {                                  // word at a time
+        const u32 w = src.load4(q);
+        const u32 z = (w - 0x01010101u) & ~w & 0x80808080u;                // a zero byte (exact for the lowest)
+        if (z == 0u) continue;
+        int k = 0;
+        for (; k < 4; ++k) {
+            const int pos = q + k;
+            if (pos >= s && pos < e && ((w >> (8 * k)) & 0xFFu) == 0u) break;
+        }
+        if (k < 4) { end = q + k; break; }
+    }
+    OjTok<S> t{src, s, end, false, -1, 0u};
     if (t.clean() != '{') return false;                                    // must begin with '{'
     int open[OJ_MAX_DEPTH + 1];                                            // each open container's bracket
     u8 role[OJ_MAX_DEPTH + 1];
@@ -492,6 +520,8 @@ __device__ __noinline__ bool parse_line(const S& src, int s, int e, u32 require,
     int state = OJS_KEY, kpos = 0;
     OjKey key{OJK_RAW, 0, 0};
     u32 kid = 0, seen = 0;
+    u32 khash[OJ_TOP_KEYS];   // the top-level object's key hashes so far
+    int ntop = 0;
     for (;;) {
         OjVal v;
         u8 nested = 0;          // != 0: v opened a container in this role
@@ -520,7 +550,20 @@ __device__ __noinline__ bool parse_line(const S& src, int s, int e, u32 require,
             continue;
         case OJS_COLON:
             if (t.clean() != ':') return false;                            // Expected a ':' after a key
-            if (oj_dup_key(src, open[depth], kpos, end, key)) return false;   // Duplicate key
+            if (depth == 1 && ntop < OJ_TOP_KEYS) {
+                // top level: compare hashes with the earlier keys', re-walk only on a hit
+                const u32 h = oj_key_hash(src, key);
+                bool hit = false;
+#pragma unroll
+                for (int k = 0; k < OJ_TOP_KEYS; ++k) hit |= k < ntop && khash[k] == h;
+                if (hit && oj_dup_key(src, open[depth], kpos, end, key)) return false;   // Duplicate key
+#pragma unroll
+                for (int k = 0; k < OJ_TOP_KEYS; ++k)
+                    if (k == ntop) khash[k] = h;
+                ++ntop;
+            } else if (oj_dup_key(src, open[depth], kpos, end, key)) {
+                return false;                                                   // Duplicate key
+            }
             state = OJS_VALUE;
             continue;
         case OJS_VALUE:

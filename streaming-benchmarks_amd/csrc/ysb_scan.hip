@@ -50,6 +50,18 @@ struct LdsSrc {
     }
 };
 
+// The same through an explicitly LDS-qualified pointer, for code that is not inlined into
+// the kernel (the general parser): ds_read instead of flat loads.
+typedef __attribute__((address_space(3))) const u32 lds_u32;
+struct LdsSrc3 {
+    lds_u32* d;
+    __device__ __forceinline__ u32 b(int p) const { return (d[p >> 2] >> ((p & 3) << 3)) & 0xFFu; }
+    __device__ __forceinline__ u32 load4(int p) const {
+        const u32 lo = d[p >> 2], hi = d[(p >> 2) + 1];
+        return __builtin_amdgcn_alignbyte(hi, lo, (u32)(p & 3));
+    }
+};
+
 struct GlbSrc {  // slow path for tiles that do not fit the LDS tile
     const u8* base;
     u64 n;
@@ -1086,15 +1098,24 @@ __device__ __forceinline__ bool process_tbl_line(const S& src, int s, int e, con
 
 // Kernel 1b: the lines the fast path deferred (any layout other than the generator's,
 // escapes, non-canonical ad ids, over-size tiles, bad offsets) through the general
-// strict JSON tokenizer, straight from HBM.  Rare on generator data; exact always.
+// org.json parser (ysb_orgjson.h; .tbl rows: process_tbl_line).  Each lane stages its
+// line into its own LDS region first (16-byte loads; regions 81 dwords apart, so the
+// lanes' byte reads fall in distinct banks; 83 KB per workgroup, one per CU) and parses
+// from there; longer lines are parsed straight from HBM.  Exact always; ~0 lines on generator data.
 // The last workgroup to finish resets the list for the next batch.
-__global__ __launch_bounds__(AUX_TPB) void defer_kernel(ScanParams P) {
+constexpr int DEFER_TPB = 256;
+constexpr int DEFER_REGION_DW = 81;                       // per-lane LDS region (odd: bank spread)
+constexpr int DEFER_STAGE_MAX = 4 * DEFER_REGION_DW - 16 - 16;   // line bytes staged (+ align, slack)
+
+__global__ __launch_bounds__(DEFER_TPB) void defer_kernel(ScanParams P) {
+    __shared__ u32 stage[DEFER_TPB * DEFER_REGION_DW];
     const int tid = threadIdx.x, lane = tid & 63;
     const u32 cnt = min(*P.defer_count, P.defer_cap);
     const i64 ring_lo = P.ring[0];
     const bool ring_set = P.ring[1] != 0;
     Tally tl{0, 0, 0, 0, 0, 0, 0};
-    for (u32 i = blockIdx.x * AUX_TPB + tid; i < cnt; i += gridDim.x * AUX_TPB) {
+    u32* region = stage + tid * DEFER_REGION_DW;
+    for (u32 i = blockIdx.x * DEFER_TPB + tid; i < cnt; i += gridDim.x * DEFER_TPB) {
         const u64 li = P.defer[i];
         const u64 ls = P.off[li];
         const u64 le = li + 1 < P.n ? (u64)P.off[li + 1] : P.nbytes;
@@ -1105,9 +1126,35 @@ __global__ __launch_bounds__(AUX_TPB) void defer_kernel(ScanParams P) {
         }
         u32 campaign;
         i64 bucket;
-        const GlbSrc gsrc{P.bytes + ls, le - ls};
-        const bool ok = P.tbl ? process_tbl_line(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket)
-                              : process_line(gsrc, 0, (int)(le - ls), P, tl, campaign, bucket);
+        bool ok;
+        const u64 a16 = ls & ~15ull;
+        const int sh = (int)(ls - a16), len = (int)(le - ls);
+        if (len <= DEFER_STAGE_MAX) {
+            const int nch = (sh + len + 15) >> 4;
+            for (int k = 0; k < nch; ++k) {
+                const u64 at = a16 + 16ull * (u64)k;
+                uint4 v;
+                if (at + 16 <= P.nbytes) {
+                    v = *reinterpret_cast<const uint4*>(P.bytes + at);   // P.bytes is 16-byte aligned
+                } else {                                               // the batch's last chunk: bytes, zeros past it
+                    u32 w[4] = {0u, 0u, 0u, 0u};
+                    for (int b = 0; b < 16 && at + b < P.nbytes; ++b) w[b >> 2] |= (u32)P.bytes[at + b] << (8 * (b & 3));
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                region[4 * k] = v.x;
+                region[4 * k + 1] = v.y;
+                region[4 * k + 2] = v.z;
+                region[4 * k + 3] = v.w;
+            }
+            region[4 * nch] = 0u;                           // slack for word reads past the end
+            const LdsSrc3 lsrc{(lds_u32*)region};
+            ok = P.tbl ? process_tbl_line(lsrc, sh, sh + len, P, tl, campaign, bucket)
+                       : process_line(lsrc, sh, sh + len, P, tl, campaign, bucket);
+        } else {
+            const GlbSrc gsrc{P.bytes + ls, le - ls};
+            ok = P.tbl ? process_tbl_line(gsrc, 0, len, P, tl, campaign, bucket)
+                       : process_line(gsrc, 0, len, P, tl, campaign, bucket);
+        }
         if (ok) global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
     }
     flush_tally(P, tl, lane);
@@ -1214,7 +1261,7 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
 
 void launch_defer(const ScanParams& p, int blocks, hipStream_t s) {
     if (p.n == 0) return;
-    hipLaunchKernelGGL(defer_kernel, dim3(blocks), dim3(AUX_TPB), 0, s, p);
+    hipLaunchKernelGGL(defer_kernel, dim3(blocks), dim3(DEFER_TPB), 0, s, p);
 }
 
 void launch_ring_autobase(const ScanParams& p, hipStream_t s) {
