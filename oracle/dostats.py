@@ -31,6 +31,7 @@ from oracle import orgjson
 REQUIRED_FLINK = ("user_id", "page_id", "ad_id", "ad_type", "event_type", "event_time")
 RECOGNISED = REQUIRED_FLINK + ("ip_address",)
 _LONG = re.compile(r"[+-]?[0-9]+\Z")
+_TERM = re.compile(rb"\r\n|\r|\n")
 
 
 class ParseError(Exception):
@@ -181,14 +182,16 @@ def load_ad_map_csv(data: bytes) -> dict:
 
 
 def split_lines(data: bytes):
-    """Lines as the reference's BufferedReader.readLine sees a '\\n'-terminated file,
-    with offsets (line i spans [off[i], off[i+1]))."""
+    """Lines as the reference's BufferedReader.readLine cuts them (AdvertisingTopologyNative.
+    java:153-159): "\\n", "\\r\\n" and a lone "\\r" end a line; each line keeps its
+    terminator bytes.  Returns (lines, offsets): line i spans [off[i], off[i+1])."""
     offs, lines, p = [], [], 0
     n = len(data)
-    while p < n:
-        q = data.find(b"\n", p)
-        q = n if q < 0 else q + 1
+    for m in _TERM.finditer(data):
         offs.append(p)
-        lines.append(data[p:q])
-        p = q
+        lines.append(data[p:m.end()])
+        p = m.end()
+    if p < n:
+        offs.append(p)
+        lines.append(data[p:])
     return lines, offs

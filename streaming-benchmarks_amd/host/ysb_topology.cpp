@@ -286,14 +286,26 @@ uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, ui
         have += read;
     }
     if (have == 0) return 0;
-    // complete lines: up to the last '\n' (at end of file, everything)
+    // BufferedReader.readLine's terminators: "\n", "\r\n" and a lone "\r" (:153-159).  A
+    // line keeps its terminator bytes in the batch (the parsers ignore them).
+    const bool any_cr = std::memchr(buf, '\r', have) != nullptr;   // generator files: none
+    // complete lines: up to the last terminator (at end of file, everything); a '\r' that
+    // ends the buffer may still be followed by '\n', so it waits for the next read
     uint64_t end = have;
     if (!eof_) {
-        const void* nl = memrchr(buf, '\n', have);
-        if (!nl) throw std::runtime_error("a line is longer than the batch buffer");
-        end = (uint64_t)((const uint8_t*)nl - buf) + 1;
+        end = 0;
+        for (uint64_t q = have; q > 0; --q) {
+            const uint8_t c = buf[q - 1];
+            if (c == '\n' || (c == '\r' && q < have)) { end = q; break; }
+            if (!any_cr) {   // only '\n' can end a line: jump to it
+                const void* nl = memrchr(buf, '\n', q);
+                end = nl ? (uint64_t)((const uint8_t*)nl - buf) + 1 : 0;
+                break;
+            }
+        }
+        if (end == 0) throw std::runtime_error("a line is longer than the batch buffer");
     }
-    // line starts: 0 and every byte after a '\n' below `end`, found in parallel pieces
+    // line starts: 0 and every byte after a terminator below `end`, in parallel pieces
     const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads_, end >> 22));
     std::vector<std::vector<uint32_t>> starts(T);
     parallel(T, [&](unsigned t) {
@@ -301,12 +313,20 @@ uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, ui
         auto& v = starts[t];
         v.reserve((b - a) / 200 + 16);
         if (t == 0) v.push_back(0);
-        for (uint64_t p = a; p < b;) {
-            const void* q = std::memchr(buf + p, '\n', b - p);
-            if (!q) break;
-            const uint64_t s = (uint64_t)((const uint8_t*)q - buf) + 1;
-            if (s < end) v.push_back((uint32_t)s);
-            p = s;
+        if (!any_cr) {
+            for (uint64_t p = a; p < b;) {
+                const void* q = std::memchr(buf + p, '\n', b - p);
+                if (!q) break;
+                const uint64_t s = (uint64_t)((const uint8_t*)q - buf) + 1;
+                if (s < end) v.push_back((uint32_t)s);
+                p = s;
+            }
+        } else {
+            for (uint64_t p = a; p < b; ++p) {
+                const uint8_t c = buf[p];
+                const bool term = c == '\n' || (c == '\r' && (p + 1 >= have || buf[p + 1] != '\n'));
+                if (term && p + 1 < end) v.push_back((uint32_t)(p + 1));
+            }
         }
     });
     uint64_t n = 0, p_end = end;

@@ -320,6 +320,7 @@ def orgjson_lines(ads):
 
 
 def write_expected(stem, lines, ad_map, campaign_of, require_ip=False, fmt="json"):
+    lines, _ = dostats.split_lines(b"".join(lines))   # the records readLine yields from the file
     r = dostats.run(lines, ad_map, 10000, require_ip, fmt)
     suffix = ".ip" if require_ip else ""
     with open(os.path.join(HERE, stem + suffix + ".expected.csv"), "w") as f:

@@ -106,3 +106,11 @@ def test_offsets_as_numpy(admap):
     raw, offs = gd.events("gen_s7")
     a = oracle.run(admap, np.frombuffer(raw, dtype=np.uint8), np.asarray(offs, dtype=np.uint32))
     assert a == oracle.run(admap, raw, offs)
+
+
+def test_split_lines_follows_readline():
+    # BufferedReader.readLine (AdvertisingTopologyNative.java:153-159): \n, \r\n, lone \r
+    lines, offs = dostats.split_lines(b"a\nb\r\nc\rd\r\re")
+    assert lines == [b"a\n", b"b\r\n", b"c\r", b"d\r", b"\r", b"e"] and offs == [0, 2, 5, 7, 9, 10]
+    assert dostats.split_lines(b"a\n\nb") == ([b"a\n", b"\n", b"b"], [0, 2, 3])
+    assert dostats.split_lines(b"") == ([], [])

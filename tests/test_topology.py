@@ -10,6 +10,7 @@ import subprocess
 import pytest
 
 import golden_data as gd
+from oracle import dostats
 from fake_redis import FakeRedis
 from test_redis_sink import canonical, dostats_shape, golden_rows
 from ysb_amd.redis_sink import RespClient, RedisWindowWriter, check_correct
@@ -78,6 +79,23 @@ def test_readline_terminators(tmp_path):
     ev.write_bytes(b"\r\n".join(lines[:100]))          # CRLF, no final terminator
     conf = write_conf(tmp_path, str(ev), gd.path("gen_s7.ad_to_campaign.txt"))
     assert last_json(run("--confPath", conf, "--dry-run"))["events"] == 100
+
+
+@pytest.mark.parametrize("batch", [[], ["--batch-bytes", "600"], ["--batch-bytes", "300"], ["--batch-bytes", "523"], ["--batch-bytes", "777"]])
+def test_readline_lone_cr_and_mixed_terminators(tmp_path, batch):
+    """BufferedReader.readLine ends a line at "\\n", "\\r\\n" or a lone "\\r": the source
+    yields the records oracle/dostats.split_lines does, also when a batch ends between
+    '\\r' and '\\n'."""
+    raw, _ = gd.events("gen_s7")
+    lines = raw.split(b"\n")[:-1][:60]
+    seps = [b"\n", b"\r\n", b"\r", b"\r\r", b"\n\n", b"\r\n\r"]
+    data = b"".join(ln + seps[i % len(seps)] for i, ln in enumerate(lines)) + b"x\ry"
+    ev = tmp_path / "mixed.jsonl"
+    ev.write_bytes(data)
+    conf = write_conf(tmp_path, str(ev), gd.path("gen_s7.ad_to_campaign.txt"))
+    want = len(dostats.split_lines(data)[0])
+    out = last_json(run("--confPath", conf, "--dry-run", *batch))
+    assert out["events"] == want and out["bytes"] == len(data)
 
 
 def test_print_config(tmp_path):
