@@ -245,7 +245,12 @@ def stream(args):
         produced += m
         return raw.size, m
 
+    last_log = time.time()
     while produced < n_total:
+        if time.time() - last_log > 20:                   # progress (long runs)
+            log("stream: %d / %d events, %d batches, %d windows closed" % (produced, n_total, op.batches,
+                                                                            op.latency_summary().get("windows", 0)))
+            last_log = time.time()
         op.fill_with(produce)
         behind = op.clock() - (t0_ms + produced * 1000.0 / rate)
         behind_max = max(behind_max, behind)
