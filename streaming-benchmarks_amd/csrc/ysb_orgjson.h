@@ -334,15 +334,18 @@ __device__ __forceinline__ int oj_skip_clean(const S& src, int p, int e) {
     while (p < e && src.b(p) <= 0x20u) ++p;
     return p;
 }
+// (The bounds below never bind on validated text; they keep a wave from spinning if
+// they ever did.)
 template <class S>
-__device__ __forceinline__ int oj_skip_string(const S& src, int p) {   // p at the opening quote
+__device__ __forceinline__ int oj_skip_string(const S& src, int p, int e) {   // p at the opening quote
     const u32 q = src.b(p++);
-    for (;;) {
+    while (p < e) {
         const u32 c = src.b(p);
         if (c == '\\') { p += 2; continue; }
         ++p;
         if (c == q) return p;
     }
+    return e;
 }
 template <class S>
 __device__ __forceinline__ int oj_token_end(const S& src, int p, int e) {
@@ -354,12 +357,13 @@ __device__ __noinline__ int oj_skip_value(const S& src, int p, int e) {   // p a
     int depth = 0;
     do {
         p = oj_skip_clean(src, p, e);
+        if (p >= e) return e;
         const u32 c = src.b(p);
-        if (c == '"' || c == '\'') p = oj_skip_string(src, p);
+        if (c == '"' || c == '\'') p = oj_skip_string(src, p, e);
         else if (c == '{' || c == '[') { ++depth; ++p; }
         else if (c == '}' || c == ']') { --depth; ++p; }
         else if (c == ',' || c == ':' || c == ';') ++p;
-        else p = oj_token_end(src, p, e);
+        else p = max(oj_token_end(src, p, e), p + 1);
     } while (depth > 0);
     return p;
 }
@@ -368,7 +372,7 @@ template <class S>
 __device__ __forceinline__ OjKey oj_key_at(const S& src, int p, int e, int* after) {
     const u32 c = src.b(p);
     if (c == '"' || c == '\'') {
-        const int q = oj_skip_string(src, p);
+        const int q = oj_skip_string(src, p, e);
         *after = q;
         return OjKey{OJK_STR, p + 1, q - 1};
     }
@@ -396,9 +400,11 @@ __device__ __noinline__ bool oj_dup_key(const S& src, int open, int kpos, int e,
         int q;
         const OjKey k2 = oj_key_at(src, p, e, &q);
         if (oj_key_equal(src, k, k2)) return true;
+        const int before = p;
         p = oj_skip_clean(src, q, e) + 1;                 // ':'
         p = oj_skip_value(src, p, e);
         p = oj_skip_clean(src, p, e) + 1;                 // ',' or ';'
+        if (p <= before) return false;
     }
 }
 
