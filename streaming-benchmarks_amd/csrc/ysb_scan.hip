@@ -1100,17 +1100,25 @@ __device__ __forceinline__ bool process_tbl_line(const S& src, int s, int e, con
 // escapes, non-canonical ad ids, over-size tiles, bad offsets) through the general
 // org.json parser (ysb_orgjson.h; .tbl rows: process_tbl_line).  Each lane stages its
 // line into its own LDS region first (16-byte loads; regions 81 dwords apart, so the
-// lanes' byte reads fall in distinct banks; 83 KB per workgroup, one per CU) and parses
-// from there; longer lines are parsed straight from HBM.  Exact always; ~0 lines on generator data.
+// lanes' byte reads fall in distinct banks) and parses from there; longer lines are
+// parsed straight from HBM.  With nothing deferred every workgroup returns at once.  Exact always; ~0 lines on generator data.
 // The last workgroup to finish resets the list for the next batch.
-constexpr int DEFER_TPB = 256;
+#ifndef YSB_DEFER_TPB
+#define YSB_DEFER_TPB 64          // one-wave workgroups, 20.7 KB of LDS each ...
+#endif
+#ifndef YSB_DEFER_WG_PER_CU
+#define YSB_DEFER_WG_PER_CU 7     // ... seven per CU (the parse is latency-bound: more waves)
+#endif
+constexpr int DEFER_TPB = YSB_DEFER_TPB;
 constexpr int DEFER_REGION_DW = 81;                       // per-lane LDS region (odd: bank spread)
 constexpr int DEFER_STAGE_MAX = 4 * DEFER_REGION_DW - 16 - 16;   // line bytes staged (+ align, slack)
 
 __global__ __launch_bounds__(DEFER_TPB) void defer_kernel(ScanParams P) {
     __shared__ u32 stage[DEFER_TPB * DEFER_REGION_DW];
     const int tid = threadIdx.x, lane = tid & 63;
-    const u32 cnt = min(*P.defer_count, P.defer_cap);
+    const u32 total = *P.defer_count;
+    if (total == 0u) return;   // nothing deferred (generator data): every workgroup leaves at once
+    const u32 cnt = min(total, P.defer_cap);
     const i64 ring_lo = P.ring[0];
     const bool ring_set = P.ring[1] != 0;
     Tally tl{0, 0, 0, 0, 0, 0, 0};
@@ -1261,7 +1269,7 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
 
 void launch_defer(const ScanParams& p, int blocks, hipStream_t s) {
     if (p.n == 0) return;
-    hipLaunchKernelGGL(defer_kernel, dim3(blocks), dim3(DEFER_TPB), 0, s, p);
+    hipLaunchKernelGGL(defer_kernel, dim3(YSB_DEFER_WG_PER_CU * blocks), dim3(DEFER_TPB), 0, s, p);
 }
 
 void launch_ring_autobase(const ScanParams& p, hipStream_t s) {
