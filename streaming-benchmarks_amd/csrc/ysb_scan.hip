@@ -792,7 +792,9 @@ __device__ __forceinline__ void flush_window(const ScanParams& P, u32* lcnt, u32
         const u32 v = lcnt[i];
         if (v) {
             lcnt[i] = 0;
+#ifndef YSB_DIAG_NO_FLUSH
             global_add(P, ring_lo, ring_set, i >> P.lds_wl_log2, lbase + (i64)(i & (WL - 1)), v, tl);
+#endif
         }
     }
 }
