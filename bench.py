@@ -41,7 +41,9 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--events", type=int, default=100_000_000,
                     help="events per GPU (125000000 at --gpus 8 is configs[3]'s 1B events)")
-    ap.add_argument("--segment", type=int, default=12_500_000, help="events per launch")
+    ap.add_argument("--segment", type=int, default=16_666_667,
+                    help="events per launch (6 launches per 100M: the largest that keep a launch's bytes "
+                         "under the 4 GiB of u32 line offsets; fewer, larger launches pay fewer tails)")
     ap.add_argument("--rate", type=int, default=100_000, help="events per second of event time")
     ap.add_argument("--cpu-sample", type=int, default=4_000_000, help="events in the CPU baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
