@@ -487,7 +487,7 @@ static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_
     p.defer_count = c->d_defer_ctr;
     p.defer_done = c->d_defer_ctr + 1;
     p.defer_cap = (u32)c->defer_cap;
-#ifdef YSB_STAMPS
+#if defined(YSB_STAMPS) || defined(YSB_WGTIME)
     const u64 words = (u64)c->cus * std::max(Geom<true>::WG_PER_CU, Geom<false>::WG_PER_CU) * (SCAN_TPB / 64) * N_STAMPS;
     if (!c->d_dbg) {
         HIPCHK(c, hipMalloc(&c->d_dbg, words * 8));
@@ -1132,7 +1132,7 @@ int ysb_gen_dump(const ysb_gen_params* p, uint64_t n_events, const char* dir) {
     return YSB_OK;
 }
 
-#ifdef YSB_STAMPS
+#if defined(YSB_STAMPS) || defined(YSB_WGTIME)
 // Diagnostic build only: the deferred-line list of the last batch.
 int ysb_debug_defer_list(ysb_ctx* c, uint32_t* out, uint64_t cap) {
     if (!c) return YSB_ERR_ARG;

@@ -832,6 +832,9 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+#ifdef YSB_WGTIME
+    const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const u64 t_begin = (u64)blockIdx.x * P.tiles_per_block;
     if (t_begin >= P.n_tiles) return;
     const u64 t_end = min(t_begin + P.tiles_per_block, P.n_tiles);
@@ -1052,6 +1055,15 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
     // ---- final flush + stats ---------------------------------------------------------
     if (WL && lset) flush_window(P, lcnt, ncells, WL, lbase, ring_lo, ring_set, tl);
     flush_tally(P, tl, lane);
+#ifdef YSB_WGTIME
+    // diagnostic build (tools/wgtime.py): the workgroup's start / end, 100 MHz clock
+    if (lane == 0) {
+        unsigned long long* o = P.dbg + (u64)blockIdx.x * N_STAMPS;
+        o[0] = wg_t0;
+        o[1] = __builtin_amdgcn_s_memrealtime();
+        o[2] = t_end - t_begin;
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
