@@ -49,6 +49,9 @@ def main():
               (s.max(), e.min(), e.mean(), np.percentile(e, 99), e.max()))
         print("  duration: mean %.1f sd %.1f min %.1f max %.1f us" % (d.mean(), d.std(), d.min(), d.max()))
         print("  mean end by blockIdx %% 8: " + " ".join("%.1f" % e[xcd == k].mean() for k in range(8)))
+        odd = (np.arange(len(w)) & 1) == 1
+        print("  end: odd workgroups (s_setprio 1) mean %.1f max %.1f; even mean %.1f max %.1f us" %
+              (e[odd].mean(), e[odd].max(), e[~odd].mean(), e[~odd].max()))
         print("  tail (max end - mean end): %.1f us = %.1f %% of the launch" %
               (e.max() - e.mean(), 100.0 * (e.max() - e.mean()) / e.max()))
 
