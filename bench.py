@@ -2,8 +2,9 @@
 
 One step = one pass of parse + view filter + ad->campaign join + 10 s window count
 over the rank's whole resident batch: 100M generator-format JSON events per GPU
-(100 campaigns x 10 ads, 10 s windows), HBM-resident before timing starts, as
-8 launches of 12.5M events (u32 line offsets cap one launch at 4 GiB).  With N > 1
+(100 campaigns x 10 ads, 10 s windows), HBM-resident before timing starts, as six
+batches of 16.67M events (u32 line offsets cap a batch at 4 GiB) scanned by ONE kernel
+launch (ysb_submit_device_segments; --per-batch: one launch per batch).  With N > 1
 ranks (torchrun), events are sharded by ad_id hash (each rank draws from its own ad
 shard, per-GPU work fixed: weak scaling) and every step ends with the RCCL
 reduce-scatter of the (campaign, window) tables over xGMI.
@@ -42,8 +43,10 @@ def parse_args():
     ap.add_argument("--events", type=int, default=100_000_000,
                     help="events per GPU (125000000 at --gpus 8 is configs[3]'s 1B events)")
     ap.add_argument("--segment", type=int, default=16_666_667,
-                    help="events per launch (6 launches per 100M: the largest that keep a launch's bytes "
-                         "under the 4 GiB of u32 line offsets; fewer, larger launches pay fewer tails)")
+                    help="events per batch (6 per 100M: the largest that keep a batch's bytes under the "
+                         "4 GiB of u32 line offsets)")
+    ap.add_argument("--per-batch", action="store_true",
+                    help="one launch per batch (ysb_submit_device) instead of one launch over all batches")
     ap.add_argument("--rate", type=int, default=100_000, help="events per second of event time")
     ap.add_argument("--cpu-sample", type=int, default=4_000_000, help="events in the CPU baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -178,9 +181,16 @@ def main():
     log("rank %d: generated %d events, %.2f GB in %.1f s" % (d.rank, args.events, total_bytes / 1e9,
                                                             time.perf_counter() - t_gen))
 
+    def submit_all():
+        if args.per_batch:
+            for (_, n, d_b, nb, d_o) in segs:
+                ctx.submit_device(d_b, nb, d_o, n)
+        else:
+            ctx.submit_device_segments([(d_b, nb, d_o, n) for (_, n, d_b, nb, d_o) in segs])
+    launches_per_step = len(segs) if args.per_batch else 1
+
     def step():
-        for (_, n, d_b, nb, d_o) in segs:
-            ctx.submit_device(d_b, nb, d_o, n)
+        submit_all()
         if d.world > 1:
             ctx.group_reduce_scatter()
 
@@ -201,14 +211,15 @@ def main():
 
     events_all = args.events * d.world * args.steps
     value = events_all / el
-    alg_bytes_launch = (total_bytes + 4 * args.events) / len(segs)   # B = L_json + 4 per event
+    alg_bytes_launch = (total_bytes + 4 * args.events) / launches_per_step   # B = L_json + 4 per event
     avg_launch_ms = kms / max(launches, 1)
     achieved = alg_bytes_launch / (avg_launch_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            if tj.get("segment_events") == args.segment and tj.get("events_per_sec") == args.rate:
+            if (tj.get("segment_events") == args.segment and tj.get("events_per_sec") == args.rate
+                    and tj.get("launches_per_step", 6) == launches_per_step):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -216,8 +227,8 @@ def main():
     check = None
     if not args.no_check:
         ctx.reset()
+        submit_all()
         for (f, n, d_b, nb, d_o) in segs:
-            ctx.submit_device(d_b, nb, d_o, n)
             ctx.truth_accumulate(g, f, n)
         ctx.sync()
         mism, truth, ring = ctx.truth_compare()
@@ -247,7 +258,8 @@ def main():
                                     "events sharded by ad_id hash, RCCL reduce-scatter of (campaign, window) counts"
                                     % (args.events // 1_000_000, args.events * d.world // 1_000_000)),
                        "events_per_gpu": args.events, "campaigns": 100, "ads": 1000,
-                       "event_time_rate_per_s": args.rate, "launches_per_step": len(segs),
+                       "event_time_rate_per_s": args.rate, "batches_per_step": len(segs),
+                       "launches_per_step": launches_per_step,
                        "json_bytes_per_event": round(total_bytes / args.events, 3),
                        "parallelism": "ad_id-hash shards x%d, RCCL reduce-scatter" % d.world if d.world > 1
                        else "1 GPU"},

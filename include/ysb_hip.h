@@ -149,6 +149,20 @@ int         ysb_wait(ysb_ctx* ctx, int slot);
 /* Device-resident batch (HBM pointers, e.g. from ysb_device_alloc). Asynchronous. */
 int         ysb_submit_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes,
                               const uint32_t* d_line_off, uint64_t n_events);
+/* Several device-resident batches in ONE kernel launch.  Each segment is a batch as
+ * for ysb_submit_device (its own u32 line offsets, so each stays under 4 GiB); every
+ * scan workgroup walks its run of tiles in segment 0, then segment 1, ..., so a step
+ * over many batches pays one launch tail instead of one per batch.  Results are the
+ * same as n_segs ysb_submit_device calls in order.  At most 16 segments and 2^31-1
+ * events per call.  Replaces the same flatMap chain as ysb_submit (:111-119), for a
+ * replay file larger than 4 GiB (FileBasedDataSource.run, :144-165). */
+typedef struct ysb_segment {
+    const uint8_t*  d_bytes;       /* HBM, 16-byte aligned */
+    uint64_t        nbytes;        /* < 4 GiB */
+    const uint32_t* d_line_off;    /* HBM, n_events offsets into d_bytes */
+    uint64_t        n_events;
+} ysb_segment;
+int         ysb_submit_device_segments(ysb_ctx* ctx, const ysb_segment* segs, uint32_t n_segs);
 /* Wait for every submitted batch. */
 int         ysb_sync(ysb_ctx* ctx);
 

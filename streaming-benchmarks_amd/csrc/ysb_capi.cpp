@@ -418,13 +418,15 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
 
 // ---- batches ---------------------------------------------------------------------------
 
-static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_off, u64 n) {
+// segs: 1..MAX_SEGS batches, none empty
+static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     ScanParams p{};
     p.tbl = (c->cfg.flags & YSB_F_FORMAT_TBL) ? 1u : 0u;
-    p.bytes = d_bytes;
-    p.nbytes = nbytes;
-    p.off = d_off;
-    p.n = n;
+    p.bytes = segs[0].d_bytes;
+    p.nbytes = segs[0].nbytes;
+    p.off = segs[0].d_line_off;
+    p.n = segs[0].n_events;
+    p.line_base = 0;
     p.table = c->d_table;
     p.table_mask = (u32)(c->table_slots - 1);
     p.ctable = c->d_ctable;
@@ -449,12 +451,29 @@ static ScanParams make_params(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u
     p.ovf_count = c->d_ovf_count;
     p.ovf_cap = (u32)c->cfg.overflow_capacity;
     p.stats = c->d_stats;
-    p.n_tiles = (n + SCAN_TPB - 1) / SCAN_TPB;
-    // whole rounds of resident workgroups (a partial last round would idle most CUs)
+    // Each segment is split over the grid on its own: whole rounds of resident workgroups
+    // (a partial last round would idle most CUs), at most MAX_TILES_PER_BLOCK tiles per
+    // workgroup and segment (the LDS copy of the run's tile bounds).
     const u64 resident = (u64)c->cus * (p.tbl ? Geom<true>::WG_PER_CU : Geom<false>::WG_PER_CU);
-    const u64 rounds = std::max<u64>(1, (p.n_tiles + resident * MAX_TILES_PER_BLOCK - 1) / (resident * MAX_TILES_PER_BLOCK));
-    const u64 blocks = std::max<u64>(1, std::min<u64>(p.n_tiles, rounds * resident));
-    p.tiles_per_block = (u32)((p.n_tiles + blocks - 1) / blocks);
+    u64 grid = 1, line_base = 0;
+    p.n_segs = nseg;
+    for (u32 i = 0; i < nseg; ++i) {
+        ScanSeg& sg = p.seg[i];
+        sg.bytes = segs[i].d_bytes;
+        sg.off = segs[i].d_line_off;
+        sg.n = segs[i].n_events;
+        sg.nbytes = segs[i].nbytes;
+        sg.line_base = line_base;
+        line_base += sg.n;
+        sg.n_tiles = (sg.n + SCAN_TPB - 1) / SCAN_TPB;
+        const u64 rounds = std::max<u64>(1, (sg.n_tiles + resident * MAX_TILES_PER_BLOCK - 1) / (resident * MAX_TILES_PER_BLOCK));
+        const u64 blocks = std::max<u64>(1, std::min<u64>(sg.n_tiles, rounds * resident));
+        sg.tiles_per_block = (u32)((sg.n_tiles + blocks - 1) / blocks);
+        grid = std::max<u64>(grid, (sg.n_tiles + sg.tiles_per_block - 1) / sg.tiles_per_block);
+    }
+    p.n_tiles = p.seg[0].n_tiles;
+    p.tiles_per_block = p.seg[0].tiles_per_block;
+    p.grid = (u32)grid;
     return p;
 }
 
@@ -466,10 +485,15 @@ static void poll_ring(ysb_ctx* c) {
     }
 }
 
-static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_off, u64 n) {
+static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     if (!c->table_loaded) return fail(c, YSB_ERR_STATE, "ysb_load_ad_map has not been called");
-    if (n == 0) { c->batches++; return YSB_OK; }
-    if (n >= (1ull << 30)) return fail(c, YSB_ERR_CAPACITY, "at most 2^30-1 events per batch");
+    ysb_segment segs[MAX_SEGS];
+    u32 nseg = 0;
+    u64 n = 0;
+    for (u32 i = 0; i < nin; ++i)
+        if (in[i].n_events) { segs[nseg++] = in[i]; n += in[i].n_events; }
+    if (n == 0) { c->batches += nin; return YSB_OK; }
+    if (n >= (1ull << 31)) return fail(c, YSB_ERR_CAPACITY, "at most 2^31-1 events per launch");
     if (n > c->defer_cap) {   // the deferred-line list can hold every line of a batch
         HIPCHK(c, hipStreamSynchronize(c->s_comp));
         hipFree(c->d_defer);
@@ -482,7 +506,7 @@ static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_
         HIPCHK(c, hipMalloc(&c->d_defer_ctr, 16));
         HIPCHK(c, hipMemset(c->d_defer_ctr, 0, 16));
     }
-    ScanParams p = make_params(c, d_bytes, nbytes, d_off, n);
+    ScanParams p = make_params(c, segs, nseg);
     p.defer = c->d_defer;
     p.defer_count = c->d_defer_ctr;
     p.defer_done = c->d_defer_ctr + 1;
@@ -524,7 +548,7 @@ static int enqueue_scan(ysb_ctx* c, const u8* d_bytes, u64 nbytes, const u32* d_
     if (e1) HIPCHK(c, hipEventRecord(e1, c->s_comp));
     launch_defer(p, c->cus, c->s_comp);
     HIPCHK(c, hipGetLastError());
-    c->batches++;
+    c->batches += nin;   // each segment counts as the batch it is
     return YSB_OK;
 }
 
@@ -570,7 +594,8 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
     if (n) HIPCHK(c, hipMemcpyAsync(c->d_off[slot], c->h_off[slot], n * 4, hipMemcpyHostToDevice, c->s_copy));
     HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
     HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_h2d[slot], 0));
-    rc = enqueue_scan(c, c->d_bytes[slot], nbytes, c->d_off[slot], n);
+    const ysb_segment sg{c->d_bytes[slot], nbytes, c->d_off[slot], n};
+    rc = enqueue_scan(c, &sg, 1);
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev_kdone[slot], c->s_comp));
     return YSB_OK;
@@ -590,7 +615,25 @@ int ysb_submit_device(ysb_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const
     if ((nbytes && !d_bytes) || (n && !d_off)) return fail(c, YSB_ERR_ARG, "NULL batch buffers");
     if (reinterpret_cast<uintptr_t>(d_bytes) & 15) return fail(c, YSB_ERR_ARG, "d_bytes must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
-    return enqueue_scan(c, d_bytes, nbytes, d_off, n);
+    const ysb_segment sg{d_bytes, nbytes, d_off, n};
+    return enqueue_scan(c, &sg, 1);
+}
+
+int ysb_submit_device_segments(ysb_ctx* c, const ysb_segment* segs, uint32_t n_segs) {
+    if (!c) return YSB_ERR_ARG;
+    if (n_segs > (u32)MAX_SEGS) return fail(c, YSB_ERR_CAPACITY, "at most %d segments per launch", MAX_SEGS);
+    if (n_segs && !segs) return fail(c, YSB_ERR_ARG, "NULL segment list");
+    for (u32 i = 0; i < n_segs; ++i) {
+        const ysb_segment& s = segs[i];
+        if (s.nbytes > (4ull << 30) - 64)
+            return fail(c, YSB_ERR_CAPACITY, "segment %u larger than 4 GiB (u32 offsets)", i);
+        if ((s.nbytes && !s.d_bytes) || (s.n_events && !s.d_line_off))
+            return fail(c, YSB_ERR_ARG, "NULL buffers in segment %u", i);
+        if (reinterpret_cast<uintptr_t>(s.d_bytes) & 15)
+            return fail(c, YSB_ERR_ARG, "segment %u: d_bytes must be 16-byte aligned", i);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    return enqueue_scan(c, segs, n_segs);
 }
 
 int ysb_sync(ysb_ctx* c) {

@@ -53,11 +53,30 @@ struct Geom {
 };
 constexpr int AUX_TPB = 256;                  // threads per workgroup of the other kernels
 
+// One batch of a multi-batch launch (ysb_submit_device_segments): each keeps its own
+// u32 line offsets (so each stays under 4 GiB), and one launch scans them all -- every
+// workgroup walks its run of tiles in segment 0, then in segment 1, ..., without a
+// grid-wide drain between batches (one launch tail per step instead of one per batch).
+constexpr int MAX_SEGS = 16;
+struct ScanSeg {
+    const u8* bytes;            // 16-byte aligned
+    const u32* off;
+    u64 n;
+    u64 nbytes;
+    u64 line_base;              // index of the segment's first line among all segments
+    u64 n_tiles;
+    u32 tiles_per_block;
+    u32 pad;
+};
+
 struct ScanParams {
+    // the batch being scanned: segment 0 on the host side; scan_kernel sets them to each
+    // segment in turn, defer_kernel to the segment of each deferred line
     const u8* bytes;            // batch bytes (16-byte aligned)
     u64 nbytes;
     const u32* off;             // n line offsets
     u64 n;
+    u64 line_base;              // segment's first line among all segments (defer list indices)
     const u32* table;           // ad table, SLOT_WORDS u32 per slot (every key)
     u32 table_mask;             // slots - 1
     const u32* ctable;          // 36-byte-key cuckoo table, CSLOT_WORDS u32 per slot
@@ -83,6 +102,9 @@ struct ScanParams {
     u32 ovf_cap;
     u32 tiles_per_block;
     u64 n_tiles;
+    u32 grid;                   // scan workgroups: max over segments of ceil(n_tiles / tiles_per_block)
+    u32 n_segs;                 // >= 1
+    ScanSeg seg[MAX_SEGS];
     unsigned long long* stats;  // ST_COUNT_ u64
     unsigned long long* dbg;    // diagnostic build only (YSB_STAMPS): per-wave phase cycles
     u32* defer;                 // line indices for the general path (defer_kernel)

@@ -821,7 +821,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // SERIAL: HBM-resident cuckoo table, second slot probed only after a first-slot miss.
 // TBL: the fork's .tbl rows (tbl_stage1/2) instead of JSON lines (canon_stage1/2).
 template <bool SERIAL, bool TBL>
-__global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<TBL>::WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(ScanParams P) {
+__global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<TBL>::WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(const ScanParams P0) {
     using G = Geom<TBL>;
     constexpr int CPT = G::CPT;
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
@@ -835,9 +835,9 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
 #ifdef YSB_WGTIME
     const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    const u64 t_begin = (u64)blockIdx.x * P.tiles_per_block;
-    if (t_begin >= P.n_tiles) return;
-    const u64 t_end = min(t_begin + P.tiles_per_block, P.n_tiles);
+    // P: the launch parameters with the batch fields (bytes, off, n, nbytes, line_base)
+    // of the segment being scanned
+    ScanParams P = P0;
 
     const i64 ring_lo = P.ring[0];
     const bool ring_set = P.ring[1] != 0;
@@ -847,26 +847,18 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
     // rebase requests of the LDS window (double-buffered by tile parity): the largest
     // bucket that fell ahead of the window, INT64_MIN = none
     if (tid < 2) misc64[tid] = INT64_MIN;
-    // tile bounds of this workgroup's run: off[t * 256] for t in [t_begin, t_end], nbytes past the end
-    for (u32 i = tid; i <= (u32)(t_end - t_begin); i += SCAN_TPB) {
-        const u64 f = (t_begin + i) * SCAN_TPB;
-        tb[i] = f < P.n ? P.off[f] : (u32)P.nbytes;
-    }
-    __syncthreads();
 
     Tally tl{0, 0, 0, 0, 0, 0, 0};
     // Prefetch depth: tile t + PF_DEPTH is issued once tile t sits in LDS.  Depth 2 keeps
     // two tiles in flight per wave (two register buffers, the loop unrolled by two).
     constexpr int PF_DEPTH = YSB_PREFETCH_DEPTH;
-    const TileInfo none{P.n, 0u, 0u, 0u, 0u, 0u, true};
+    // this workgroup's run of tiles [t_begin, t_end) in the current segment
+    u64 t_begin = 0, t_end = 0, n_run = 0;
+    TileInfo none{0, 0u, 0u, 0u, 0u, 0u, true};
     uint4 preA[CPT], preB[CPT];
     u32 offA = 0, endA = 0, offB = 0, endB = 0;
-    TileInfo infA = tile_info<G::CAP>(P, t_begin, t_begin, tb), infB = none;
-    issue_tile_loads(P, infA, preA, offA, endA);
-    if constexpr (PF_DEPTH == 2) {
-        if (t_begin + 1 < t_end) infB = tile_info<G::CAP>(P, t_begin + 1, t_begin, tb);
-        issue_tile_loads(P, infB, preB, offB, endB);
-    }
+    TileInfo infA = none, infB = none;
+    u32 tseq = 0;   // tiles stepped so far (window-request parity across segments)
     // The LDS window's base, identical in every thread (each applies the same requests).
     i64 lbase = 0;
     bool lset = false;
@@ -904,7 +896,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
         }
         // The previous tile asked to move the LDS window: flush it (its counts are all
         // in, the end barrier saw to that) and re-centre, before this tile counts.
-        const int par = (int)(t & 1);
+        const int par = (int)(tseq++ & 1);
         if (WL) {
             const i64 req = misc64[par ^ 1];
             if (req != INT64_MIN) {
@@ -974,7 +966,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
                 tok = canonical_bucket(lsrc, cb, ls + ca.e4 + (TBL ? 1 : 18), P, bucket);   // Long.parseLong
             }
         }
-        defer_append(P, dfr, cur.first + li, lane);
+        defer_append(P, dfr, P.line_base + cur.first + li, lane);
         STAMP(2);
         // ---- prefetch the next tile (lands while this one is parsed) -----------
         // Issued on every iteration (the last one loads nothing: out-of-range buffer
@@ -1015,7 +1007,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
                 if (!tok) tl.terr++;
             }
         }
-        if (P.ctable_partial) defer_append(P, dfr2, cur.first + li, lane);
+        if (P.ctable_partial) defer_append(P, dfr2, P.line_base + cur.first + li, lane);
         STAMP(3);
         // ---- count: LDS window counters; events outside go straight to the ring -----
         if (WL) {
@@ -1037,19 +1029,44 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
         __syncthreads();
         STAMP(5);
     };
-    if constexpr (PF_DEPTH == 2) {
-        for (u64 t = t_begin; t < t_end; t += 2) {
-            tile_step(t, infA, preA, offA, endA);
-            if (t + 1 < t_end) tile_step(t + 1, infB, preB, offB, endB);
+    for (u32 sgi = 0; sgi < P0.n_segs; ++sgi) {
+        const ScanSeg& sg = P0.seg[sgi];
+        t_begin = (u64)blockIdx.x * sg.tiles_per_block;
+        if (t_begin >= sg.n_tiles) continue;
+        t_end = min(t_begin + sg.tiles_per_block, sg.n_tiles);
+        P.bytes = sg.bytes;
+        P.off = sg.off;
+        P.n = sg.n;
+        P.nbytes = sg.nbytes;
+        P.line_base = sg.line_base;
+        none.first = sg.n;
+        n_run += t_end - t_begin;
+        // tile bounds of this run: off[t * 64] for t in [t_begin, t_end], nbytes past the
+        // end (the previous segment's last step ended at a barrier: tb is free)
+        for (u32 i = tid; i <= (u32)(t_end - t_begin); i += SCAN_TPB) {
+            const u64 f = (t_begin + i) * SCAN_TPB;
+            tb[i] = f < P.n ? P.off[f] : (u32)P.nbytes;
         }
-    } else {
-        for (u64 t = t_begin; t < t_end; ++t) tile_step(t, infA, preA, offA, endA);
+        __syncthreads();
+        infA = tile_info<G::CAP>(P, t_begin, t_begin, tb);
+        issue_tile_loads(P, infA, preA, offA, endA);
+        if constexpr (PF_DEPTH == 2) {
+            infB = t_begin + 1 < t_end ? tile_info<G::CAP>(P, t_begin + 1, t_begin, tb) : none;
+            issue_tile_loads(P, infB, preB, offB, endB);
+            for (u64 t = t_begin; t < t_end; t += 2) {
+                tile_step(t, infA, preA, offA, endA);
+                if (t + 1 < t_end) tile_step(t + 1, infB, preB, offB, endB);
+            }
+        } else {
+            for (u64 t = t_begin; t < t_end; ++t) tile_step(t, infA, preA, offA, endA);
+        }
     }
+    if (n_run == 0) return;   // no segment has tiles for this workgroup (nothing touched)
 #ifdef YSB_STAMPS
     if (lane == 0) {
         unsigned long long* o = P.dbg + ((u64)blockIdx.x * (SCAN_TPB / 64) + (threadIdx.x >> 6)) * N_STAMPS;
         for (int i = 0; i < 7; ++i) o[i] += st_acc[i];
-        o[7] += t_end - t_begin;
+        o[7] += n_run;
     }
 #endif
     // ---- final flush + stats ---------------------------------------------------------
@@ -1061,7 +1078,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
         unsigned long long* o = P.dbg + (u64)blockIdx.x * N_STAMPS;
         o[0] = wg_t0;
         o[1] = __builtin_amdgcn_s_memrealtime();
-        o[2] = t_end - t_begin;
+        o[2] = n_run;
     }
 #endif
 }
@@ -1127,8 +1144,9 @@ constexpr int DEFER_TPB = YSB_DEFER_TPB;
 constexpr int DEFER_REGION_DW = 81;                       // per-lane LDS region (odd: bank spread)
 constexpr int DEFER_STAGE_MAX = 4 * DEFER_REGION_DW - 16 - 16;   // line bytes staged (+ align, slack)
 
-__global__ __launch_bounds__(DEFER_TPB) void defer_kernel(ScanParams P) {
+__global__ __launch_bounds__(DEFER_TPB) void defer_kernel(const ScanParams P0) {
     __shared__ u32 stage[DEFER_TPB * DEFER_REGION_DW];
+    ScanParams P = P0;   // batch fields: the segment of the line being parsed
     const int tid = threadIdx.x, lane = tid & 63;
     const u32 total = *P.defer_count;
     if (total == 0u) return;   // nothing deferred (generator data): every workgroup leaves at once
@@ -1138,7 +1156,14 @@ __global__ __launch_bounds__(DEFER_TPB) void defer_kernel(ScanParams P) {
     Tally tl{0, 0, 0, 0, 0, 0, 0};
     u32* region = stage + tid * DEFER_REGION_DW;
     for (u32 i = blockIdx.x * DEFER_TPB + tid; i < cnt; i += gridDim.x * DEFER_TPB) {
-        const u64 li = P.defer[i];
+        u64 li = P.defer[i];   // index among all segments' lines
+        u32 sgi = 0;
+        while (sgi + 1 < P0.n_segs && li >= P0.seg[sgi + 1].line_base) ++sgi;
+        P.bytes = P0.seg[sgi].bytes;
+        P.off = P0.seg[sgi].off;
+        P.n = P0.seg[sgi].n;
+        P.nbytes = P0.seg[sgi].nbytes;
+        li -= P0.seg[sgi].line_base;
         const u64 ls = P.off[li];
         const u64 le = li + 1 < P.n ? (u64)P.off[li + 1] : P.nbytes;
         if (ls > le || le > P.nbytes || le - ls > 0x7FFFFFFFull) {
@@ -1270,8 +1295,7 @@ void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s) {
 
 void launch_scan(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
-    const u64 blocks = (p.n_tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    const dim3 g((unsigned)blocks), b(SCAN_TPB);
+    const dim3 g(p.grid), b(SCAN_TPB);
     if (p.tbl) {
         if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, true>), g, b, Geom<true>::LDS, s, p);
         else hipLaunchKernelGGL((scan_kernel<false, true>), g, b, Geom<true>::LDS, s, p);

@@ -44,6 +44,11 @@ class YsbCount(C.Structure):
                 ("count", C.c_uint64)]
 
 
+class YsbSegment(C.Structure):
+    _fields_ = [("d_bytes", C.c_void_p), ("nbytes", C.c_uint64), ("d_line_off", C.c_void_p),
+                ("n_events", C.c_uint64)]
+
+
 class YsbGenParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("n_campaigns", C.c_uint32), ("ads_per_campaign", C.c_uint32),
                 ("t0_ms", C.c_int64), ("events_per_sec", C.c_uint64), ("with_skew", C.c_uint32),
@@ -73,6 +78,7 @@ SIGNATURES = {
     "ysb_submit": (_I, [_P, _I, _PU8, _U64, _PU32, _U64]),
     "ysb_wait": (_I, [_P, _I]),
     "ysb_submit_device": (_I, [_P, _PU8, _U64, _PU32, _U64]),
+    "ysb_submit_device_segments": (_I, [_P, C.c_void_p, _U32]),
     "ysb_sync": (_I, [_P]),
     "ysb_drain": (_I, [_P, _I64, _I64, _I, C.POINTER(YsbCount), _U64, C.POINTER(_U64)]),
     "ysb_stats_get": (_I, [_P, C.POINTER(YsbStats)]),

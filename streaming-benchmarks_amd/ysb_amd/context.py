@@ -13,7 +13,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import INT64_MIN, YsbConfig, YsbCount, YsbStats, check, lib
+from ._lib import INT64_MIN, YsbConfig, YsbCount, YsbSegment, YsbStats, check, lib
 
 
 def _ptr(a):
@@ -103,6 +103,13 @@ class YsbContext:
 
     def submit_device(self, d_bytes, nbytes, d_off, n):
         self._c(lib().ysb_submit_device(self._h, C.c_void_p(d_bytes), nbytes, C.c_void_p(d_off), n))
+
+    def submit_device_segments(self, segs):
+        """Several device batches [(d_bytes, nbytes, d_off, n), ...] in one kernel launch."""
+        arr = (YsbSegment * max(len(segs), 1))()
+        for i, (d_b, nb, d_o, n) in enumerate(segs):
+            arr[i] = YsbSegment(d_b, nb, d_o, n)
+        self._c(lib().ysb_submit_device_segments(self._h, arr, len(segs)))
 
     def sync(self):
         self._c(lib().ysb_sync(self._h))
