@@ -8,6 +8,7 @@
 #include <array>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -85,7 +86,9 @@ struct ysb_ctx {
     u32 d_subset_n = 0;
     u32* d_defer = nullptr;                // deferred (general-path) line indices
     u64 defer_cap = 0;
-    u32* d_defer_ctr = nullptr;            // [count, done]
+    u32* d_defer_ctr = nullptr;            // [count, done, pad, pad, dynamic-claim counters[MAX_SEGS]]
+    u32 dyn_pct = 0;                       // % of a large segment's tiles claimed dynamically (YSB_DYN_PCT; measured neutral, off)
+    u32 dyn_chunk = 16;                    // tiles per claim (YSB_DYN_CHUNK)
     unsigned long long* d_dbg = nullptr;   // YSB_STAMPS diagnostic build
     u64 dbg_words = 0;
 };
@@ -213,6 +216,9 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
     if (hipSetDevice(device) != hipSuccess) { fail(c, YSB_ERR_HIP, "hipSetDevice(%d) failed", device); return bad(YSB_ERR_HIP); }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->cus = prop.multiProcessorCount;
+    // scan schedule overrides (timing experiments): YSB_DYN_PCT=0 -> all static
+    if (const char* e = getenv("YSB_DYN_PCT")) c->dyn_pct = (u32)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("YSB_DYN_CHUNK")) c->dyn_chunk = (u32)strtoul(e, nullptr, 10);
     if (hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking) != hipSuccess) {
         fail(c, YSB_ERR_HIP, "stream creation failed");
@@ -451,11 +457,15 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     p.ovf_count = c->d_ovf_count;
     p.ovf_cap = (u32)c->cfg.overflow_capacity;
     p.stats = c->d_stats;
-    // Each segment is split over the grid on its own: whole rounds of resident workgroups
-    // (a partial last round would idle most CUs), at most MAX_TILES_PER_BLOCK tiles per
-    // workgroup and segment (the LDS copy of the run's tile bounds).
+    // Each segment's tiles: a static share split evenly over the grid, and for large
+    // segments (>= 8 tiles per resident workgroup) a dynamic share of dyn_pct % claimed in
+    // chunks by the workgroups that finish first.  The grid is whole rounds of resident
+    // workgroups (a partial last round would idle most CUs), enough that no static run
+    // exceeds MAX_TILES_PER_BLOCK tiles (the LDS copy of a run's tile bounds).
     const u64 resident = (u64)c->cus * (p.tbl ? Geom<true>::WG_PER_CU : Geom<false>::WG_PER_CU);
-    u64 grid = 1, line_base = 0;
+    const u32 chunk = std::min<u32>(c->dyn_chunk, MAX_TILES_PER_BLOCK);
+    u64 line_base = 0, max_static = 0;
+    bool any_dyn = false;
     p.n_segs = nseg;
     for (u32 i = 0; i < nseg; ++i) {
         ScanSeg& sg = p.seg[i];
@@ -466,11 +476,19 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
         sg.line_base = line_base;
         line_base += sg.n;
         sg.n_tiles = (sg.n + SCAN_TPB - 1) / SCAN_TPB;
-        const u64 rounds = std::max<u64>(1, (sg.n_tiles + resident * MAX_TILES_PER_BLOCK - 1) / (resident * MAX_TILES_PER_BLOCK));
-        const u64 blocks = std::max<u64>(1, std::min<u64>(sg.n_tiles, rounds * resident));
-        sg.tiles_per_block = (u32)((sg.n_tiles + blocks - 1) / blocks);
-        grid = std::max<u64>(grid, (sg.n_tiles + sg.tiles_per_block - 1) / sg.tiles_per_block);
+        const bool dyn = chunk && c->dyn_pct && sg.n_tiles >= 8 * resident;
+        sg.n_static = dyn ? sg.n_tiles - sg.n_tiles * std::min<u32>(c->dyn_pct, 100) / 100 : sg.n_tiles;
+        any_dyn |= sg.n_static < sg.n_tiles;
+        max_static = std::max(max_static, sg.n_static);
     }
+    const u64 rounds = std::max<u64>(1, (max_static + resident * MAX_TILES_PER_BLOCK - 1) / (resident * MAX_TILES_PER_BLOCK));
+    const u64 grid = std::max<u64>(1, std::min<u64>(max_static, rounds * resident));
+    for (u32 i = 0; i < nseg; ++i) {
+        ScanSeg& sg = p.seg[i];
+        sg.tiles_per_block = (u32)(sg.n_static / grid);
+        sg.static_rem = (u32)(sg.n_static % grid);
+    }
+    p.dyn_chunk = any_dyn ? chunk : 0u;
     p.n_tiles = p.seg[0].n_tiles;
     p.tiles_per_block = p.seg[0].tiles_per_block;
     p.grid = (u32)grid;
@@ -503,13 +521,14 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
         c->defer_cap = cap;
     }
     if (!c->d_defer_ctr) {
-        HIPCHK(c, hipMalloc(&c->d_defer_ctr, 16));
-        HIPCHK(c, hipMemset(c->d_defer_ctr, 0, 16));
+        HIPCHK(c, hipMalloc(&c->d_defer_ctr, 16 + 4 * MAX_SEGS));
+        HIPCHK(c, hipMemset(c->d_defer_ctr, 0, 16 + 4 * MAX_SEGS));
     }
     ScanParams p = make_params(c, segs, nseg);
     p.defer = c->d_defer;
     p.defer_count = c->d_defer_ctr;
     p.defer_done = c->d_defer_ctr + 1;
+    p.dyn_ctr = c->d_defer_ctr + 4;
     p.defer_cap = (u32)c->defer_cap;
 #if defined(YSB_STAMPS) || defined(YSB_WGTIME)
     const u64 words = (u64)c->cus * std::max(Geom<true>::WG_PER_CU, Geom<false>::WG_PER_CU) * (SCAN_TPB / 64) * N_STAMPS;

@@ -65,8 +65,9 @@ struct ScanSeg {
     u64 nbytes;
     u64 line_base;              // index of the segment's first line among all segments
     u64 n_tiles;
-    u32 tiles_per_block;
-    u32 pad;
+    u64 n_static;               // tiles [0, n_static) split over the grid, the rest claimed in chunks
+    u32 tiles_per_block;        // static tiles per workgroup (q) ...
+    u32 static_rem;             // ... plus one for workgroups b < static_rem
 };
 
 struct ScanParams {
@@ -104,6 +105,8 @@ struct ScanParams {
     u64 n_tiles;
     u32 grid;                   // scan workgroups: max over segments of ceil(n_tiles / tiles_per_block)
     u32 n_segs;                 // >= 1
+    u32 dyn_chunk;              // tiles per dynamic claim (0: all static)
+    u32* dyn_ctr;               // [MAX_SEGS] claim counters, zero at launch
     ScanSeg seg[MAX_SEGS];
     unsigned long long* stats;  // ST_COUNT_ u64
     unsigned long long* dbg;    // diagnostic build only (YSB_STAMPS): per-wave phase cycles

@@ -1029,20 +1029,11 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
         __syncthreads();
         STAMP(5);
     };
-    for (u32 sgi = 0; sgi < P0.n_segs; ++sgi) {
-        const ScanSeg& sg = P0.seg[sgi];
-        t_begin = (u64)blockIdx.x * sg.tiles_per_block;
-        if (t_begin >= sg.n_tiles) continue;
-        t_end = min(t_begin + sg.tiles_per_block, sg.n_tiles);
-        P.bytes = sg.bytes;
-        P.off = sg.off;
-        P.n = sg.n;
-        P.nbytes = sg.nbytes;
-        P.line_base = sg.line_base;
-        none.first = sg.n;
+    // One run of tiles [t_begin, t_end) of the current segment (P's batch fields).
+    auto run_tiles = [&]() {
         n_run += t_end - t_begin;
         // tile bounds of this run: off[t * 64] for t in [t_begin, t_end], nbytes past the
-        // end (the previous segment's last step ended at a barrier: tb is free)
+        // end (the previous run's last step ended at a barrier: tb is free)
         for (u32 i = tid; i <= (u32)(t_end - t_begin); i += SCAN_TPB) {
             const u64 f = (t_begin + i) * SCAN_TPB;
             tb[i] = f < P.n ? P.off[f] : (u32)P.nbytes;
@@ -1059,6 +1050,55 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
             }
         } else {
             for (u64 t = t_begin; t < t_end; ++t) tile_step(t, infA, preA, offA, endA);
+        }
+    };
+    auto use_segment = [&](const ScanSeg& sg) {
+        P.bytes = sg.bytes;
+        P.off = sg.off;
+        P.n = sg.n;
+        P.nbytes = sg.nbytes;
+        P.line_base = sg.line_base;
+        none.first = sg.n;
+    };
+    // Static share: the first n_static tiles of each segment, split evenly over the grid
+    // (workgroup b: q tiles, one more for b < r).
+    const u64 wg = blockIdx.x;
+    for (u32 sgi = 0; sgi < P0.n_segs; ++sgi) {
+        const ScanSeg& sg = P0.seg[sgi];
+        t_begin = wg * sg.tiles_per_block + (wg < sg.static_rem ? wg : (u64)sg.static_rem);
+        t_end = t_begin + sg.tiles_per_block + (wg < sg.static_rem ? 1u : 0u);
+        if (t_begin >= t_end) continue;
+        use_segment(sg);
+        run_tiles();
+    }
+    // Dynamic share: the tiles past n_static, claimed in chunks of dyn_chunk from one
+    // counter per segment by whichever workgroups finish their static share first (the
+    // slower CUs' lag is absorbed instead of becoming the launch's tail).  The next
+    // claim is issued before the current chunk runs, so its latency hides under it.
+    if (P0.dyn_chunk) {
+        u32 sgi = 0;
+        u32 claim = 0;
+        auto claim_next = [&](u32 si) -> u32 {
+            u32 c = 0;
+            if (lane == 0) c = atomicAdd(&P0.dyn_ctr[si], 1u);
+            return c;
+        };
+        while (sgi < P0.n_segs && P0.seg[sgi].n_static >= P0.seg[sgi].n_tiles) ++sgi;
+        if (sgi < P0.n_segs) claim = claim_next(sgi);
+        while (sgi < P0.n_segs) {
+            const ScanSeg& sg = P0.seg[sgi];
+            const u32 c = (u32)__builtin_amdgcn_readfirstlane(__shfl(claim, 0, 64));
+            t_begin = sg.n_static + (u64)c * P0.dyn_chunk;
+            if (t_begin >= sg.n_tiles) {   // this segment's pool is empty: the next one
+                ++sgi;
+                while (sgi < P0.n_segs && P0.seg[sgi].n_static >= P0.seg[sgi].n_tiles) ++sgi;
+                if (sgi < P0.n_segs) claim = claim_next(sgi);
+                continue;
+            }
+            t_end = min<u64>(t_begin + P0.dyn_chunk, sg.n_tiles);
+            claim = claim_next(sgi);
+            use_segment(sg);
+            run_tiles();
         }
     }
     if (n_run == 0) return;   // no segment has tiles for this workgroup (nothing touched)
@@ -1147,6 +1187,8 @@ constexpr int DEFER_STAGE_MAX = 4 * DEFER_REGION_DW - 16 - 16;   // line bytes s
 __global__ __launch_bounds__(DEFER_TPB) void defer_kernel(const ScanParams P0) {
     __shared__ u32 stage[DEFER_TPB * DEFER_REGION_DW];
     ScanParams P = P0;   // batch fields: the segment of the line being parsed
+    // the scan's dynamic-claim counters are back at zero for the next launch (stream order)
+    if (blockIdx.x == 0 && threadIdx.x < MAX_SEGS && P0.dyn_chunk) P0.dyn_ctr[threadIdx.x] = 0u;
     const int tid = threadIdx.x, lane = tid & 63;
     const u32 total = *P.defer_count;
     if (total == 0u) return;   // nothing deferred (generator data): every workgroup leaves at once

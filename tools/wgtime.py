@@ -1,7 +1,9 @@
 """Diagnostic: per-workgroup start / end times of one scan launch (YSB_WGTIME build),
 to see how much of a launch is its tail.  Never used for results.
 
-    YSB_LIB_VARIANT=wgtime python tools/wgtime.py [events]      (on the GPU box)
+    YSB_LIB_VARIANT=wgtime python tools/wgtime.py [events] [segments]   (on the GPU box)
+
+segments > 1: that many batches of `events` each, in one ysb_submit_device_segments launch.
 """
 import ctypes as C
 import os
@@ -19,17 +21,21 @@ from ysb_amd._lib import lib  # noqa: E402
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 16_666_667
+    k = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     g = GenParams(seed=42, events_per_sec=100_000)
     _, aids = g.ids()
     ctx = YsbContext(n_campaigns=100)
     ctx.load_ad_map(aids, g.ad_campaign_index())
     cap = n * g.max_line_bytes()
-    d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n)
-    nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+    segs = []
+    for i in range(k):
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n)
+        nb = ctx.gen_events_device(g, i * n, n, d_b, cap, d_o)
+        segs.append((d_b, nb, d_o, n))
     L = lib()
     L.ysb_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     for rep in range(4):
-        ctx.submit_device(d_b, nb, d_o, n)
+        ctx.submit_device_segments(segs)
         ctx.sync()
         cnt = C.c_uint64()
         L.ysb_debug_stamps(ctx._h, None, 0, C.byref(cnt))
