@@ -42,6 +42,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def submit_segments(ctx, segs, per_batch):
+    """The resident batches: one launch over all (default) or one launch per batch."""
+    if per_batch:
+        for (_, n, d_b, nb, d_o) in segs:
+            ctx.submit_device(d_b, nb, d_o, n)
+    else:
+        ctx.submit_device_segments([(d_b, nb, d_o, n) for (_, n, d_b, nb, d_o) in segs])
+
+
 def config3(args):
     g = GenParams(seed=42, n_campaigns=1_000_000, ads_per_campaign=10, events_per_sec=100_000)
     t = time.perf_counter()
@@ -62,8 +71,7 @@ def config3(args):
     total_bytes = sum(s[3] for s in segs)
 
     def step():
-        for (_, n, d_b, nb, d_o) in segs:
-            ctx.submit_device(d_b, nb, d_o, n)
+        submit_segments(ctx, segs, args.per_batch)
     step()
     ctx.sync()
     ctx.kernel_time()
@@ -74,15 +82,16 @@ def config3(args):
     el = time.perf_counter() - t0
     kms, launches = ctx.kernel_time()
     ctx.reset()
+    submit_segments(ctx, segs, args.per_batch)
     for (f, n, d_b, nb, d_o) in segs:
-        ctx.submit_device(d_b, nb, d_o, n)
         ctx.truth_accumulate(g, f, n)
     mism, truth, ring = ctx.truth_compare()
     st = ctx.stats()
-    alg = (total_bytes + 4 * args.events) / len(segs)
+    alg = (total_bytes + 4 * args.events) / (len(segs) if args.per_batch else 1)
     ach = alg / (kms / launches * 1e-3) / 1e9
     return {"config": "configs[2]: 1M campaigns / 10M ads, %d events, W=%d" % (args.events, args.ring),
             "events_per_s": round(args.events * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
+            "batches_per_step": len(segs), "launches_per_step": len(segs) if args.per_batch else 1,
             "scan_avg_launch_ms": round(kms / launches, 4), "scan_alg_GBs": round(ach, 1),
             "hbm_frac": round(ach / HBM_PEAK_GBS, 4), "ad_map_load_s": round(t_load, 2),
             "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
@@ -108,8 +117,7 @@ def tbl(args):
     total_bytes = sum(s[3] for s in segs)
 
     def step():
-        for (_, n, d_b, nb, d_o) in segs:
-            ctx.submit_device(d_b, nb, d_o, n)
+        submit_segments(ctx, segs, args.per_batch)
     step()
     ctx.sync()
     ctx.kernel_time()
@@ -120,16 +128,17 @@ def tbl(args):
     el = time.perf_counter() - t0
     kms, launches = ctx.kernel_time()
     ctx.reset()
+    submit_segments(ctx, segs, args.per_batch)
     for (f, n, d_b, nb, d_o) in segs:
-        ctx.submit_device(d_b, nb, d_o, n)
         ctx.truth_accumulate(g, f, n)
     mism, truth, ring = ctx.truth_compare()
     st = ctx.stats()
-    alg = (total_bytes + 4 * args.events) / len(segs)
+    alg = (total_bytes + 4 * args.events) / (len(segs) if args.per_batch else 1)
     ach = alg / (kms / launches * 1e-3) / 1e9
     return {"config": "configs[1] events as .tbl rows: %d events, 100 campaigns x 10 ads" % args.events,
             "tbl_bytes_per_event": round(total_bytes / args.events, 3),
             "events_per_s": round(args.events * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
+            "batches_per_step": len(segs), "launches_per_step": len(segs) if args.per_batch else 1,
             "scan_avg_launch_ms": round(kms / launches, 4), "scan_alg_GBs": round(ach, 1),
             "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
             "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
@@ -287,6 +296,7 @@ def main():
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--segment", type=int, default=12_500_000)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--per-batch", action="store_true", help="one scan launch per batch (config3 / tbl)")
     ap.add_argument("--batch-mb", type=int, default=64)
     ap.add_argument("--seconds", type=int, default=10)
     ap.add_argument("--rate", type=int, default=1_000_000)
