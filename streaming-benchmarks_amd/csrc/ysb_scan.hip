@@ -852,12 +852,15 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
     // Prefetch depth: tile t + PF_DEPTH is issued once tile t sits in LDS.  Depth 2 keeps
     // two tiles in flight per wave (two register buffers, the loop unrolled by two).
     constexpr int PF_DEPTH = YSB_PREFETCH_DEPTH;
+    // Depth 2 (two register buffers) measured -2 % on v11 and spills to scratch inside the
+    // per-segment run loop: only depth 1 is built.
+    static_assert(PF_DEPTH == 1, "YSB_PREFETCH_DEPTH must be 1");
     // this workgroup's run of tiles [t_begin, t_end) in the current segment
     u64 t_begin = 0, t_end = 0, n_run = 0;
     TileInfo none{0, 0u, 0u, 0u, 0u, 0u, true};
-    uint4 preA[CPT], preB[CPT];
-    u32 offA = 0, endA = 0, offB = 0, endB = 0;
-    TileInfo infA = none, infB = none;
+    uint4 preA[CPT];
+    u32 offA = 0, endA = 0;
+    TileInfo infA = none;
     u32 tseq = 0;   // tiles stepped so far (window-request parity across segments)
     // The LDS window's base, identical in every thread (each applies the same requests).
     i64 lbase = 0;
@@ -1041,16 +1044,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
         __syncthreads();
         infA = tile_info<G::CAP>(P, t_begin, t_begin, tb);
         issue_tile_loads(P, infA, preA, offA, endA);
-        if constexpr (PF_DEPTH == 2) {
-            infB = t_begin + 1 < t_end ? tile_info<G::CAP>(P, t_begin + 1, t_begin, tb) : none;
-            issue_tile_loads(P, infB, preB, offB, endB);
-            for (u64 t = t_begin; t < t_end; t += 2) {
-                tile_step(t, infA, preA, offA, endA);
-                if (t + 1 < t_end) tile_step(t + 1, infB, preB, offB, endB);
-            }
-        } else {
-            for (u64 t = t_begin; t < t_end; ++t) tile_step(t, infA, preA, offA, endA);
-        }
+        for (u64 t = t_begin; t < t_end; ++t) tile_step(t, infA, preA, offA, endA);
     };
     auto use_segment = [&](const ScanSeg& sg) {
         P.bytes = sg.bytes;
