@@ -706,9 +706,6 @@ constexpr int AUX_NT = 2;
 #ifndef YSB_SETPRIO
 #define YSB_SETPRIO 1
 #endif
-#ifndef YSB_EARLY_PF
-#define YSB_EARLY_PF 0
-#endif
 #ifndef YSB_PREFETCH_DEPTH
 #define YSB_PREFETCH_DEPTH 1
 #endif
@@ -915,12 +912,6 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
         __syncthreads();
         if (tid == 0) misc64[par ^ 1] = INT64_MIN;   // every thread has read it
         STAMP(1);
-#if YSB_EARLY_PF
-        // the tile's bytes are in LDS: the next tile's loads go out now and land under
-        // this tile's whole parse (waiting for the join probe below then waits for them too)
-        inf = t + PF_DEPTH < t_end ? tile_info<G::CAP>(P, t + PF_DEPTH, t_begin, tb) : none;
-        issue_tile_loads(P, inf, pre, pre_off, pre_end);
-#endif
 #ifdef YSB_DIAG_A_ONLY
         inf = t + PF_DEPTH < t_end ? tile_info<G::CAP>(P, t + PF_DEPTH, t_begin, tb) : none;
         issue_tile_loads(P, inf, pre, pre_off, pre_end);
@@ -984,10 +975,8 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
         // Issued on every iteration (the last one loads nothing: out-of-range buffer
         // loads return zeros) so every path has the same count of loads in flight and
         // the waits below stay counted.
-#if !YSB_EARLY_PF
         inf = t + PF_DEPTH < t_end ? tile_info<G::CAP>(P, t + PF_DEPTH, t_begin, tb) : none;
         issue_tile_loads(P, inf, pre, pre_off, pre_end);
-#endif
         // ---- Phase B2: join result ------------------------------------------------
         bool valid = false, dfr2 = false;
         u32 campaign = 0;
