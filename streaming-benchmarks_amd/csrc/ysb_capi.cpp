@@ -475,7 +475,7 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
         sg.nbytes = segs[i].nbytes;
         sg.line_base = line_base;
         line_base += sg.n;
-        sg.n_tiles = (sg.n + SCAN_TPB - 1) / SCAN_TPB;
+        sg.n_tiles = (sg.n + TILE_LINES - 1) / TILE_LINES;
         const bool dyn = chunk && c->dyn_pct && sg.n_tiles >= 8 * resident;
         sg.n_static = dyn ? sg.n_tiles - sg.n_tiles * std::min<u32>(c->dyn_pct, 100) / 100 : sg.n_tiles;
         any_dyn |= sg.n_static < sg.n_tiles;

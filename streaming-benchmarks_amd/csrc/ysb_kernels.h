@@ -10,7 +10,14 @@ namespace ysb {
 // One wave per workgroup: no intra-workgroup barrier ever waits for a slower wave,
 // and the two waves of a SIMD drift into different phases (one classifying while the
 // other parses), which hides each other's LDS latency.
-constexpr int SCAN_TPB = 64;                  // threads per scan workgroup = lines per tile
+constexpr int SCAN_TPB = 64;                  // threads per scan workgroup (one wave)
+#ifndef YSB_TILE_LINES
+#define YSB_TILE_LINES 64
+#endif
+// lines per tile: one per lane (fewer than 64 leaves lanes idle but shrinks the LDS tile,
+// so more workgroups fit a CU)
+constexpr int TILE_LINES = YSB_TILE_LINES;
+static_assert(TILE_LINES >= 1 && TILE_LINES <= SCAN_TPB, "one line per lane at most");
 #ifndef YSB_WG_PER_CU
 #define YSB_WG_PER_CU 8
 #endif
@@ -21,7 +28,7 @@ constexpr int SCAN_WG_PER_CU = YSB_WG_PER_CU; // resident scan workgroups per CU
 #ifndef YSB_TILE_LINE_BYTES
 #define YSB_TILE_LINE_BYTES 260
 #endif
-constexpr int TILE_CAP = SCAN_TPB * YSB_TILE_LINE_BYTES;   // LDS bytes of one tile (per-line average cap)
+constexpr int TILE_CAP = TILE_LINES * YSB_TILE_LINE_BYTES;   // LDS bytes of one tile (per-line average cap)
 constexpr int TILE_CHUNKS = TILE_CAP / 16;    // 16-byte chunks per tile
 constexpr int CHUNKS_PER_THREAD = (TILE_CHUNKS + SCAN_TPB - 1) / SCAN_TPB;  // 17
 constexpr int LCNT_CAP = 256;                 // u32 per-workgroup (campaign, window) counters
@@ -40,7 +47,7 @@ constexpr int MAX_TILES_PER_BLOCK = YSB_MAX_TILES;   // tile bounds preloaded in
 template <bool TBL>
 struct Geom {
     static constexpr int WG_PER_CU = TBL ? YSB_TBL_WG_PER_CU : SCAN_WG_PER_CU;
-    static constexpr int CAP = SCAN_TPB * (TBL ? YSB_TBL_LINE_BYTES : YSB_TILE_LINE_BYTES);
+    static constexpr int CAP = TILE_LINES * (TBL ? YSB_TBL_LINE_BYTES : YSB_TILE_LINE_BYTES);
     static constexpr int CHUNKS = CAP / 16;
     static constexpr int CPT = (CHUNKS + SCAN_TPB - 1) / SCAN_TPB;   // 16-byte chunks per thread
     static constexpr int OFF_TILE = 0;

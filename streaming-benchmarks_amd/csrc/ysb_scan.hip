@@ -681,9 +681,9 @@ struct TileInfo {
 template <int CAP>
 __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_begin, const u32* tb) {
     TileInfo ti;
-    ti.first = t * SCAN_TPB;
+    ti.first = t * TILE_LINES;
     const u64 rem = P.n - ti.first;
-    ti.count = rem < (u64)SCAN_TPB ? (u32)rem : (u32)SCAN_TPB;
+    ti.count = rem < (u64)TILE_LINES ? (u32)rem : (u32)TILE_LINES;
     // wave-uniform by construction; readfirstlane lets the compiler keep them (and the
     // buffer descriptors built from them) in SGPRs (no waterfall loops)
     // (readfirstlane returns int: keep it unsigned before widening, offsets reach 4 GiB)
@@ -821,7 +821,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // SERIAL: HBM-resident cuckoo table, second slot probed only after a first-slot miss.
 // TBL: the fork's .tbl rows (tbl_stage1/2) instead of JSON lines (canon_stage1/2).
 template <bool SERIAL, bool TBL>
-__global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<TBL>::WG_PER_CU * SCAN_TPB / 256))) void scan_kernel(const ScanParams P0) {
+__global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<TBL>::WG_PER_CU * SCAN_TPB + 255) / 256))) void scan_kernel(const ScanParams P0) {
     using G = Geom<TBL>;
     constexpr int CPT = G::CPT;
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
@@ -1035,10 +1035,10 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu(Geom<T
     // One run of tiles [t_begin, t_end) of the current segment (P's batch fields).
     auto run_tiles = [&]() {
         n_run += t_end - t_begin;
-        // tile bounds of this run: off[t * 64] for t in [t_begin, t_end], nbytes past the
+        // tile bounds of this run: off[t * TILE_LINES] for t in [t_begin, t_end], nbytes past the
         // end (the previous run's last step ended at a barrier: tb is free)
         for (u32 i = tid; i <= (u32)(t_end - t_begin); i += SCAN_TPB) {
-            const u64 f = (t_begin + i) * SCAN_TPB;
+            const u64 f = (t_begin + i) * TILE_LINES;
             tb[i] = f < P.n ? P.off[f] : (u32)P.nbytes;
         }
         __syncthreads();
