@@ -134,3 +134,37 @@ def test_segment_arguments_rejected():
         ctx.submit_device_segments([(d, 0, d, 0)])
         ctx.sync()
         assert ctx.stats()["events"] == 0
+
+
+@pytest.mark.parametrize("pct,chunk", [(20, 16), (50, 5)])
+def test_dynamic_share_equals_static(monkeypatch, pct, chunk):
+    """The optional dynamic tile claims (YSB_DYN_PCT / YSB_DYN_CHUNK, read at ysb_open;
+    off by default) count exactly what the static schedule counts: 3.2M skewed events in
+    two segments large enough for the dynamic share, half the keys deferred."""
+    g = GenParams(seed=2024, events_per_sec=5000, with_skew=True)
+    _, aids = g.ids()
+    camp = g.ad_campaign_index()
+    sizes = [1_700_000, 1_500_000]
+    out = []
+    for env in (None, (pct, chunk)):
+        if env:
+            monkeypatch.setenv("YSB_DYN_PCT", str(env[0]))
+            monkeypatch.setenv("YSB_DYN_CHUNK", str(env[1]))
+        with make_ctx(n_campaigns=100, ads=(aids[:980], camp[:980]), sparse_fast_join=True,
+                      window_ring=64, overflow_capacity=1 << 22) as ctx:
+            segs, first = [], 0
+            for n in sizes:
+                cap = n * g.max_line_bytes() + 64
+                d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
+                nb = ctx.gen_events_device(g, first, n, d_b, cap, d_o)
+                segs.append((d_b, nb, d_o, n))
+                first += n
+            ctx.submit_device_segments(segs)
+            ctx.submit_device_segments(segs)   # twice: the claim counters are reset between launches
+            out.append((ctx.drain_buckets(), ctx.stats()))
+        monkeypatch.delenv("YSB_DYN_PCT", raising=False)
+        monkeypatch.delenv("YSB_DYN_CHUNK", raising=False)
+    (rows_s, st_s), (rows_d, st_d) = out
+    assert st_s["events"] == 2 * sum(sizes) and st_s["deferred"] > 0 and st_s["join_misses"] > 0
+    assert st_d == st_s
+    assert rows_d == rows_s
