@@ -549,6 +549,8 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
         HIPCHK(c, hipEventRecord(c->ev_ring, c->s_comp));
         c->ring_query_pending = true;
     }
+    // dynamic claims (off by default) count from zero in every launch
+    if (p.dyn_chunk) HIPCHK(c, hipMemsetAsync(p.dyn_ctr, 0, 4 * MAX_SEGS, c->s_comp));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->cfg.flags & YSB_F_TIMING) {
         if (c->tev_used == c->tev.size()) {

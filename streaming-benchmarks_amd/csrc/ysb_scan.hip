@@ -1181,8 +1181,6 @@ constexpr int DEFER_STAGE_MAX = 4 * DEFER_REGION_DW - 16 - 16;   // line bytes s
 __global__ __launch_bounds__(DEFER_TPB) void defer_kernel(const ScanParams P0) {
     __shared__ u32 stage[DEFER_TPB * DEFER_REGION_DW];
     ScanParams P = P0;   // batch fields: the segment of the line being parsed
-    // the scan's dynamic-claim counters are back at zero for the next launch (stream order)
-    if (blockIdx.x == 0 && threadIdx.x < MAX_SEGS && P0.dyn_chunk) P0.dyn_ctr[threadIdx.x] = 0u;
     const int tid = threadIdx.x, lane = tid & 63;
     const u32 total = *P.defer_count;
     if (total == 0u) return;   // nothing deferred (generator data): every workgroup leaves at once
