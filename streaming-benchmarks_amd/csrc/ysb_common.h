@@ -218,13 +218,16 @@ YSB_HD u32 key_hash(const u32* w, u32 len) {
 // any 36 bytes) sits in one of its two slots, so a lookup is exactly two slot loads
 // issued together and a raw 9-word compare -- no decoding, no key validation.
 // Slot words: [key bytes 0..35 as 9 little-endian u32, campaign (EMPTY_SLOT = free),
-// 0, 0] = 48 bytes, three 16-byte loads.
+// 0 x 6] = 64 bytes, of which a probe loads the first 48 (three 16-byte loads).  The
+// 64-byte stride keeps every slot inside one 128-byte line (48-byte slots straddle two
+// for a quarter of the probes): config 3's HBM-resident table +3 %, config 2 +0.3 %
+// (gpurun_out/c16, c16h, c16i).
 // The slot hash folds the words with per-seed additive salts (the carries make a
 // colliding key family seed-dependent, so a failed build is cured by a new seed),
 // then avalanches: x = XOR rotl(w_k + s_k, R_k), y = SUM (w_k ^ s'_k).
 // ---------------------------------------------------------------------------
 #ifndef YSB_CSLOT_WORDS
-#define YSB_CSLOT_WORDS 12
+#define YSB_CSLOT_WORDS 16
 #endif
 enum : u32 { CSLOT_WORDS = YSB_CSLOT_WORDS, CKEY_WORDS = 9, CSLOT_CAMP = 9, CSLOT_Q = YSB_CSLOT_WORDS / 4 };
 
