@@ -701,7 +701,10 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_
 
 // Cache policy of the once-read batch stream: nontemporal (aux 2), so it does not
 // displace the join table from L2 (MI355X_MICROARCH.md, row nt-weights).
-constexpr int AUX_NT = 2;
+#ifndef YSB_AUX_NT
+#define YSB_AUX_NT 2
+#endif
+constexpr int AUX_NT = YSB_AUX_NT;
 
 #ifndef YSB_SETPRIO
 #define YSB_SETPRIO 1
