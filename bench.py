@@ -39,7 +39,8 @@ def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps (~40 ms; the clocks reach their steady state after ~8)")
     ap.add_argument("--events", type=int, default=100_000_000,
                     help="events per GPU (125000000 at --gpus 8 is configs[3]'s 1B events)")
     ap.add_argument("--segment", type=int, default=16_666_667,
@@ -194,6 +195,9 @@ def main():
         if d.world > 1:
             ctx.group_reduce_scatter()
 
+    # torch's own CUDA context is created here, before the warmup: created between warmup
+    # and timing it idles the GPU ~1.5 s and the first timed steps run at ramping clocks
+    torch_sync(d.local)
     for _ in range(args.warmup):
         step()
     ctx.sync()

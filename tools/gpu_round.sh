@@ -22,7 +22,7 @@ for s in $STAGES; do
       timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     trace)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-         -d "$OUT/trace" -o run -- python3 "$REPO/bench.py" --steps 20 --warmup 3 --no-cpu --no-check \
+         -d "$OUT/trace" -o run -- python3 "$REPO/bench.py" --steps 20 --warmup 10 --no-cpu --no-check \
          > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err") ;;
     pmc)
       (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv \
