@@ -72,7 +72,8 @@ def config3(args):
 
     def step():
         submit_segments(ctx, segs, args.per_batch)
-    step()
+    for _ in range(args.warmup):   # steady clocks before timing (bench.py)
+        step()
     ctx.sync()
     ctx.kernel_time()
     t0 = time.perf_counter()
@@ -118,7 +119,8 @@ def tbl(args):
 
     def step():
         submit_segments(ctx, segs, args.per_batch)
-    step()
+    for _ in range(args.warmup):   # steady clocks before timing (bench.py)
+        step()
     ctx.sync()
     ctx.kernel_time()
     t0 = time.perf_counter()
@@ -295,7 +297,8 @@ def main():
     ap.add_argument("mode", choices=["config3", "tbl", "general", "pcie", "stream"])
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--segment", type=int, default=12_500_000)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--per-batch", action="store_true", help="one scan launch per batch (config3 / tbl)")
     ap.add_argument("--batch-mb", type=int, default=64)
     ap.add_argument("--seconds", type=int, default=10)
