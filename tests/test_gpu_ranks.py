@@ -1,0 +1,67 @@
+"""One-GPU rehearsal of bench.py's N-rank setup (the driver runs N = 2/4/8 on a full node;
+RCCL refuses two ranks on one device, so the collective itself is not run here).
+
+Each rank's context is built exactly as bench.py builds it (its own generator stream
+over its shard of the shared ad ids, window_ring 1024, no explicit ring base), all on
+cuda:0.  What ysb_group_reduce_scatter needs before summing tables cell by cell is
+checked directly: every rank's ring starts at the same bucket (the exchange refuses
+otherwise, ysb_capi.cpp ysb_group_reduce_scatter), every rank counts exactly its
+generator truth, and the sum over ranks equals the campaign-major reduce-scatter
+result (owner blocks, ysb_group_owned's padding rule)."""
+from collections import Counter
+
+import pytest
+
+from ysb_amd import GenParams, YsbContext, owned_block, shard_ads
+
+pytestmark = pytest.mark.gpu
+
+
+def rank_params(world, rank, rate=100_000):
+    # bench.py main(): base ids, then per-rank stream 1 + rank over shard_ads(...)[rank]
+    base = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=rate)
+    cids, aids = base.ids()
+    camp = base.ad_campaign_index()
+    if world == 1:
+        return base, aids, camp
+    subset = shard_ads(aids, world)[rank]
+    g = GenParams(seed=42, event_stream=1 + rank, n_campaigns=100, ads_per_campaign=10,
+                  events_per_sec=rate, ad_subset=subset)
+    return g, aids, camp
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_ranks_share_ring_base_and_sum_to_truth(world):
+    n = 2_000_000
+    rings, tables, total_joined = [], [], 0
+    for rank in range(world):
+        g, aids, camp = rank_params(world, rank)
+        with YsbContext(device=0, n_campaigns=100, window_ring=1024,
+                        max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
+            ctx.load_ad_map(aids, camp)
+            cap = n * g.max_line_bytes()
+            d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
+            nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+            ctx.submit_device_segments([(d_b, nb, d_o, n)])
+            ctx.sync()
+            ctx.truth_accumulate(g, 0, n)
+            mism, truth, ring = ctx.truth_compare()
+            st = ctx.stats()
+            assert st["events"] == n and st["parse_errors"] == 0 and st["join_misses"] == 0
+            assert mism == 0 and truth == ring == st["joined"], (rank, mism, truth, ring)
+            rings.append(ctx.ring_range())
+            tables.append(ctx.drain_buckets())
+            total_joined += st["joined"]
+    # the reduce-scatter precondition: one ring base on every rank
+    assert len(set(rings)) == 1, rings
+    merged = Counter()
+    for t in tables:
+        merged.update(t)
+    assert sum(merged.values()) == total_joined
+    # owner blocks tile the campaigns; each owner's block of the merged table is what its
+    # d_owned holds after the exchange
+    blocks = [owned_block(100, r, world) for r in range(world)]
+    assert blocks[0][0] == 0 and blocks[-1][1] == 100
+    assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+    owned = sum(v for (c, _), v in merged.items() for lo, hi in blocks if lo <= c < hi)
+    assert owned == total_joined
