@@ -1,15 +1,25 @@
-"""Benchmark of the MI355X YSB advertising hot path (BASELINE.json configs[1]).
+"""Benchmark of the MI355X YSB advertising hot path (BASELINE.json configs[1] / configs[3]).
 
 One step = one pass of parse + view filter + ad->campaign join + 10 s window count
-over the rank's whole resident batch: 100M generator-format JSON events per GPU
-(100 campaigns x 10 ads, 10 s windows), HBM-resident before timing starts, as six
-batches of 16.67M events (u32 line offsets cap a batch at 4 GiB) scanned by ONE kernel
-launch (ysb_submit_device_segments; --per-batch: one launch per batch).  With N > 1
-ranks (torchrun), events are sharded by ad_id hash (each rank draws from its own ad
-shard, per-GPU work fixed: weak scaling) and every step ends with the RCCL
-reduce-scatter of the (campaign, window) tables over xGMI.
+over the rank's whole resident batch: generator-format JSON events (100 campaigns x 10
+ads, 10 s windows), HBM-resident before timing starts, as batches of 16.67M events (u32
+line offsets cap a batch at 4 GiB) scanned by ONE kernel launch
+(ysb_submit_device_segments; --per-batch: one launch per batch).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+--gpus 1 (default): configs[1], 100M events.  Then, after the headline line's numbers
+are taken, the same process times configs[2] (1M campaigns / 10M ads) and the fork's
+.tbl rows as extra keys (--no-extras skips them).
+
+--gpus N > 1: one process per GPU.  Started without torchrun (WORLD_SIZE unset), this
+process is only a launcher: it starts N rank processes (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_* set, 127.0.0.1) before anything touches a GPU and exits with their status;
+under torchrun each rank runs directly.  Events are sharded by ad_id hash (rank r draws
+from its own ad shard; per-GPU work fixed: weak scaling; 1B / N events per GPU at N >= 8,
+so N = 8 is configs[3]'s 1B events), every step ends with the RCCL reduce-scatter of the
+(campaign, window) tables over xGMI, and after timing the owners' rows are checked
+against the generator truth summed over ranks (check.exchange).
 
 Rank 0 prints one JSON line (metric/value/unit/... + roofline + cpu_baseline).
 """
@@ -18,6 +28,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,20 +41,21 @@ import numpy as np  # noqa: E402
 
 METRIC = "events/sec (parse+filter+join+window count) at 1/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+TOTAL_EVENTS_8 = 1_000_000_000   # configs[3]
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10,
                     help="untimed steps (~40 ms; the clocks reach their steady state after ~8)")
-    ap.add_argument("--events", type=int, default=100_000_000,
-                    help="events per GPU (125000000 at --gpus 8 is configs[3]'s 1B events)")
+    ap.add_argument("--events", type=int, default=None,
+                    help="events per GPU (default 100M; 1B / N at N >= 8: configs[3]'s 1B events at N = 8)")
     ap.add_argument("--segment", type=int, default=16_666_667,
                     help="events per batch (6 per 100M: the largest that keep a batch's bytes under the "
                          "4 GiB of u32 line offsets)")
@@ -53,9 +66,61 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-check", action="store_true", help="skip the generator-truth check")
+    ap.add_argument("--no-extras", action="store_true", help="skip the configs[2] / .tbl extra measurements")
+    ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch the ranks and set up torch.distributed, then stop before any GPU call")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.events is None:
+        a.events = TOTAL_EVENTS_8 // a.gpus if a.gpus >= 8 else 100_000_000
+    return a
 
+
+# ---- launcher ----------------------------------------------------------------------------
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv):
+    """Starts n rank processes of this script (one per GPU) and waits for them.  Called
+    before anything in this process touches a GPU (no HIP call, no torch.cuda): the
+    children are fresh processes, and this one only waits.  If a rank fails, the others
+    are stopped (they would wait forever in a collective)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    failed = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and not failed:
+            failed = bad[0]
+            log("bench: a rank exited with %d; stopping the others" % failed)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.time() + 20
+            while time.time() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.2)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        if all(c is not None for c in (p.poll() for p in procs)):
+            break
+        time.sleep(0.2)
+    return failed or max(abs(p.returncode) for p in procs)
+
+
+# ---- ranks --------------------------------------------------------------------------------
 
 class Dist:
     def __init__(self, n):
@@ -91,12 +156,44 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return int(t.item())
 
+    def sum_array(self, a):
+        """Elementwise sum over ranks of a uint64 array (counts < 2^63)."""
+        if not self.dist:
+            return a
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).clone()
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t.numpy().view(np.uint64).reshape(a.shape)
+
+    def gather(self, obj):
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def bcast_bytes(self, b):
         if not self.dist:
             return b
         obj = [b]
         self.dist.broadcast_object_list(obj, src=0)
         return obj[0]
+
+
+def dry_run(d, args):
+    """Launch rehearsal: every rank reports its environment; nothing touches a GPU.
+    YSB_BENCH_FAIL_RANK=r makes rank r exit with status 3 first (tests the launcher's
+    stop-the-others path: the remaining ranks would wait in the gather forever)."""
+    if os.environ.get("YSB_BENCH_FAIL_RANK") == str(d.rank):
+        sys.exit(3)
+    info = {"rank": d.rank, "local_rank": d.local, "world": d.world, "pid": os.getpid(),
+            "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")),
+            "events_per_gpu": args.events}
+    allinfo = d.gather(info)
+    if d.rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": d.world, "ranks": allinfo}), flush=True)
+    if d.dist:
+        d.dist.destroy_process_group()
 
 
 def torch_sync(device=0):
@@ -145,22 +242,161 @@ def cpu_baseline(ctx, d_b, d_o, nb_seg, n_seg, ads, camp, sample, seconds):
                       "that sample: %s" % (n, end / 1e9, threads, el, res[1][0], same)}
 
 
+def gen_segments(ctx, g, events, segment):
+    segs, first = [], 0
+    while first < events:
+        n = min(segment, events - first)
+        cap = n * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
+        nb = ctx.gen_events_device(g, first, n, d_b, cap, d_o)
+        segs.append((first, n, d_b, nb, d_o))
+        first += n
+    return segs
+
+
+def free_segments(ctx, segs):
+    for (_, _, d_b, _, d_o) in segs:
+        ctx.device_free(d_b)
+        ctx.device_free(d_o)
+
+
+def timed_extra(name, ctx, g, segs, steps, warmup, kernel):
+    """One extra configuration: warmup, `steps` timed single-launch steps, then the
+    generator-truth check of one more pass."""
+    sub = [(d_b, nb, d_o, n) for (_, n, d_b, nb, d_o) in segs]
+    for _ in range(warmup):
+        ctx.submit_device_segments(sub)
+    ctx.sync()
+    ctx.kernel_time()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.submit_device_segments(sub)
+    ctx.sync()
+    el = time.perf_counter() - t0
+    kms, launches = ctx.kernel_time()
+    ctx.reset()
+    ctx.submit_device_segments(sub)
+    for (f, n, _, _, _) in segs:
+        ctx.truth_accumulate(g, f, n)
+    mism, truth, ring = ctx.truth_compare()
+    st = ctx.stats()
+    events = sum(s[1] for s in segs)
+    nbytes = sum(s[3] for s in segs)
+    alg = nbytes + 4 * events
+    avg = kms / max(launches, 1)
+    ach = alg / (avg * 1e-3) / 1e9
+    return {"workload": name, "events": events, "bytes_per_event": round(nbytes / events, 3),
+            "events_per_s": round(events * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
+            "kernel": kernel, "avg_launch_ms": round(avg, 4), "alg_GBs": round(ach, 1),
+            "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
+            "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
+                      "join_misses": st["join_misses"], "parse_errors": st["parse_errors"],
+                      "deferred": st["deferred"], "out_of_ring": st["out_of_ring"],
+                      "overflow_dropped": st["overflow_dropped"]}}
+
+
+def extras(args, device):
+    """configs[2] (1M campaigns / 10M ads: join and count tables in HBM) and configs[1]'s
+    events as the fork's .tbl rows, each timed like the headline (one launch per step)."""
+    from ysb_amd import GenParams, YsbContext
+    out = {}
+    t = time.perf_counter()
+    g = GenParams(seed=42, n_campaigns=1_000_000, ads_per_campaign=10, events_per_sec=args.rate)
+    _, ab = g.ids_packed()
+    with YsbContext(device=device, n_campaigns=1_000_000, window_ring=128, timing=True,
+                    max_batch_bytes=1 << 20, max_batch_events=1 << 12) as ctx:
+        ctx.load_ad_map_packed(ab, g.ad_campaign_index_array())
+        load_s = time.perf_counter() - t
+        segs = gen_segments(ctx, g, 100_000_000, 12_500_000)
+        r = timed_extra("configs[2]: 100M JSON events, 1M campaigns x 10 ads (10M-ad join table and "
+                        "1M x 128-bucket count ring in HBM)", ctx, g, segs, args.extra_steps, args.warmup,
+                        "ysb::scan_kernel<true, false>")
+        r["ad_map_load_s"] = round(load_s, 2)
+        out["config3"] = r
+        free_segments(ctx, segs)
+    log("extras: config3 %.2f G events/s" % (out["config3"]["events_per_s"] / 1e9))
+    g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, fmt="tbl")
+    _, aids = g.ids()
+    with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True, input_format="tbl",
+                    max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
+        ctx.load_ad_map(aids, g.ad_campaign_index())
+        segs = gen_segments(ctx, g, 100_000_000, 12_500_000)
+        out["tbl"] = timed_extra("configs[1]'s 100M events as the fork's .tbl rows (MockWindowedFlatMap, "
+                                 "AdvertisingTopologyNative.java:197-226)", ctx, g, segs, args.extra_steps,
+                                 args.warmup, "ysb::scan_kernel<false, true>")
+        free_segments(ctx, segs)
+    log("extras: tbl %.2f G events/s" % (out["tbl"]["events_per_s"] / 1e9))
+    return out
+
+
+def exchange_check(d, ctx, g, segs, submit_all):
+    """After the timed loop (N > 1): one more pass with the generator truth, one
+    reduce-scatter, every owner drains its block; rank 0 compares the owners' rows with
+    the truth summed over ranks (host gloo, independent of RCCL)."""
+    from ysb_amd import exchange_mismatches, table_rows
+    ctx.reset()
+    submit_all()
+    for (f, n, _, _, _) in segs:
+        ctx.truth_accumulate(g, f, n)
+    ctx.sync()
+    mism_local, truth_local, ring_local = ctx.truth_compare()
+    truth, ring_lo = ctx.truth_read()
+    st = ctx.stats()
+    ctx.group_reduce_scatter()
+    rows = ctx.drain_buckets()
+    lo, hi = ctx.group_owned()
+    rrank, rn = ctx.group_info()
+    truth_sum = d.sum_array(truth)
+    los = d.gather(ring_lo)
+    per = d.gather((lo, hi, rows, rrank, rn, int(st["out_of_ring"])))
+    sums = [int(d.sum(v)) for v in (mism_local, truth_local, ring_local, st["parse_errors"], st["deferred"],
+                                    st["join_misses"], st["out_of_ring"])]
+    if d.rank != 0:
+        return None
+    expected = table_rows(truth_sum, ring_lo)
+    mism, outside, cells = exchange_mismatches(expected, [(p[0], p[1], p[2]) for p in per])
+    return {"truth_mismatched_cells": sums[0], "truth_views": sums[1], "counted_views": sums[2],
+            "parse_errors": sums[3], "deferred_to_general_path": sums[4], "join_misses": sums[5],
+            "out_of_ring": sums[6],
+            "note": "truth_* / counted_views: sum over ranks of each rank's table vs its own truth, before the "
+                    "exchange; exchange: the owners' rows after the RCCL reduce-scatter vs the truth summed "
+                    "over ranks",
+            "exchange": {"post_exchange_mismatched_cells": mism, "cells_compared": cells,
+                         "owner_rows_outside_block": outside,
+                         "owned_views": int(sum(sum(p[2].values()) for p in per)),
+                         "truth_views_summed": int(truth_sum.sum()),
+                         "ring_bases_equal": len(set(los)) == 1,
+                         "rccl_ranks": sorted(set(p[4] for p in per)), "rccl_user_ranks": [p[3] for p in per],
+                         "owned_blocks": [[p[0], p[1]] for p in per]}}
+
+
 def main():
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launcher: nothing here touches a GPU before the ranks are started
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     d = Dist(args.gpus)
+    if args.dry_run:
+        dry_run(d, args)
+        return
     from ysb_amd import GenParams, YsbContext, shard_ads
 
     base = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate)
     cids, aids = base.ids()
     camp = base.ad_campaign_index()
+    W = 1024
+    ring_base = None
     if d.world > 1:
         subset = shard_ads(aids, d.world)[d.rank]
         g = GenParams(seed=42, event_stream=1 + d.rank, n_campaigns=100, ads_per_campaign=10,
                       events_per_sec=args.rate, ad_subset=subset)
+        # every rank derives the same ring base from the shared t0 (the library would also
+        # agree on one at ysb_group_init / the first exchange)
+        ring_base = g.c.t0_ms // 10000 - W // 8
     else:
         g = base
 
-    ctx = YsbContext(device=d.local, n_campaigns=100, window_ring=1024, timing=True,
+    ctx = YsbContext(device=d.local, n_campaigns=100, window_ring=W, timing=True, ring_base_bucket=ring_base,
                      max_batch_bytes=16 << 20, max_batch_events=1 << 16)
     ctx.load_ad_map(aids, camp)
     if d.world > 1:
@@ -168,16 +404,8 @@ def main():
         ctx.group_init(d.rank, d.world, uid)
 
     # ---- resident input: generated straight into HBM ----------------------------------
-    segs = []
     t_gen = time.perf_counter()
-    first = 0
-    while first < args.events:
-        n = min(args.segment, args.events - first)
-        cap = n * g.max_line_bytes()
-        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
-        nb = ctx.gen_events_device(g, first, n, d_b, cap, d_o)
-        segs.append((first, n, d_b, nb, d_o))
-        first += n
+    segs = gen_segments(ctx, g, args.events, args.segment)
     total_bytes = sum(s[3] for s in segs)
     log("rank %d: generated %d events, %.2f GB in %.1f s" % (d.rank, args.events, total_bytes / 1e9,
                                                             time.perf_counter() - t_gen))
@@ -223,6 +451,7 @@ def main():
         try:
             tj = json.load(open(args.traffic))
             if (tj.get("segment_events") == args.segment and tj.get("events_per_sec") == args.rate
+                    and tj.get("events_per_gpu", 100_000_000) == args.events
                     and tj.get("launches_per_step", 6) == launches_per_step):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
@@ -230,25 +459,30 @@ def main():
 
     check = None
     if not args.no_check:
-        ctx.reset()
-        submit_all()
-        for (f, n, d_b, nb, d_o) in segs:
-            ctx.truth_accumulate(g, f, n)
-        ctx.sync()
-        mism, truth, ring = ctx.truth_compare()
-        st = ctx.stats()
-        vals = [mism, truth, ring, st["parse_errors"], st["out_of_ring"], st["deferred"], st["join_misses"]]
-        vals = [int(d.sum(v)) for v in vals]   # over all ranks
-        check = {"truth_mismatched_cells": vals[0], "truth_views": vals[1], "counted_views": vals[2],
-                 "parse_errors": vals[3], "out_of_ring": vals[4], "deferred_to_general_path": vals[5],
-                 "join_misses": vals[6]}
         if d.world > 1:
-            check["note"] = "sum over ranks of rank-local table (before reduce-scatter) vs rank-local truth"
+            check = exchange_check(d, ctx, g, segs, submit_all)
+        else:
+            ctx.reset()
+            submit_all()
+            for (f, n, d_b, nb, d_o) in segs:
+                ctx.truth_accumulate(g, f, n)
+            ctx.sync()
+            mism, truth, ring = ctx.truth_compare()
+            st = ctx.stats()
+            check = {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
+                     "parse_errors": st["parse_errors"], "out_of_ring": st["out_of_ring"],
+                     "deferred_to_general_path": st["deferred"], "join_misses": st["join_misses"]}
 
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         s0 = segs[0]
         cpu = cpu_baseline(ctx, s0[2], s0[4], s0[3], s0[1], aids, camp, args.cpu_sample, args.cpu_seconds)
+
+    extra = None
+    if d.world == 1 and not args.no_extras:
+        free_segments(ctx, segs)
+        ctx.close()
+        extra = extras(args, d.local)
 
     if d.rank == 0:
         out = {
@@ -274,6 +508,8 @@ def main():
             "cpu_baseline": cpu,
             "check": check,
         }
+        if extra is not None:
+            out["extras"] = extra
         print(json.dumps(out), flush=True)
     if d.dist:
         d.dist.destroy_process_group()

@@ -163,7 +163,11 @@ typedef struct ysb_segment {
     uint64_t        n_events;
 } ysb_segment;
 int         ysb_submit_device_segments(ysb_ctx* ctx, const ysb_segment* segs, uint32_t n_segs);
-/* Wait for every submitted batch. */
+/* Wait for every submitted batch.  YSB_ERR_CAPACITY if joined views were lost because
+ * the out-of-ring map and its fallback list (overflow_capacity) both filled within one
+ * launch (stats.overflow_dropped > 0): counts are then not exact, and every ysb_sync /
+ * ysb_drain reports it until ysb_reset.  Between launches the map is emptied into the
+ * exact host-side list once it is a quarter full, so it never fills across batches. */
 int         ysb_sync(ysb_ctx* ctx);
 
 /* ---- results ------------------------------------------------------------------------
@@ -208,12 +212,20 @@ int         ysb_memcpy_d2h(ysb_ctx* ctx, void* h_dst, const void* d_src, uint64_
  * owner of campaigns [r*Cp/N, (r+1)*Cp/N), Cp = n_campaigns padded to N. */
 #define YSB_UNIQUE_ID_BYTES 128
 int         ysb_group_unique_id(uint8_t uid[YSB_UNIQUE_ID_BYTES]);
+/* Collective.  Also agrees on the ring base (every rank's ring must start at the same
+ * bucket: the tables are summed cell by cell): the smallest base any rank holds wins; a
+ * rank whose ring starts later moves the buckets the common range does not hold to its
+ * exact side list.  If no rank has a base yet, the first ysb_group_reduce_scatter agrees.
+ * After ysb_group_init, ysb_ring_advance is collective too (same new_lo on every rank). */
 int         ysb_group_init(ysb_ctx* ctx, int rank, int nranks,
                            const uint8_t uid[YSB_UNIQUE_ID_BYTES]);
 /* Asynchronous on the compute stream; sums the ring tables into the owner rank.
  * Every rank's ring part is consumed (zeroed) by the call. */
 int         ysb_group_reduce_scatter(ysb_ctx* ctx);
 int         ysb_group_owned(ysb_ctx* ctx, uint32_t* campaign_lo, uint32_t* campaign_hi);
+/* The communicator as RCCL sees it (ncclCommUserRank / ncclCommCount): a check that the
+ * exchange really spans the ranks the launcher started. */
+int         ysb_group_info(ysb_ctx* ctx, int* rank, int* nranks);
 /* Shard of an ad_id under the partitioning above (host function). */
 uint32_t    ysb_ad_shard(const char* ad_id, uint32_t len, uint32_t nranks);
 /* Campaign block [*lo, *hi) that rank `rank` of `nranks` owns after
@@ -274,6 +286,10 @@ int         ysb_truth_accumulate(ysb_ctx* ctx, const ysb_gen_params* p, uint64_t
                                  uint64_t n);
 int         ysb_truth_compare(ysb_ctx* ctx, uint64_t* mismatched_cells,
                               uint64_t* truth_total, uint64_t* ring_total);
+/* The truth table itself: n_campaigns x window_ring u64, campaign-major, cell (c, b mod W)
+ * holding bucket b of [*ring_lo, *ring_lo + W) (cells >= n_campaigns * window_ring).  Lets
+ * a multi-rank check sum the ranks' truths and compare them with the owners' drains. */
+int         ysb_truth_read(ysb_ctx* ctx, uint64_t* out, uint64_t cells, int64_t* ring_lo);
 /* Writes the generator's files into dir: campaign-ids.txt, ad-ids.txt (core.clj:24-34),
  * ad-to-campaign-ids.txt ({ "AD": "CAMPAIGN"} lines, core.clj:58), ad-to-campaign.csv
  * (ad,campaign lines, AdvertisingTopologyNative.java:52) and kafka-json.txt with

@@ -58,8 +58,8 @@ struct ysb_ctx {
     SideSlot* d_side = nullptr;               // out-of-ring cells (device hash map)
     u64 side_slots = 0;
     u32 side_cbits = 1;
-    u32* d_side_used = nullptr;
-    unsigned long long* d_stats = nullptr;
+    u32* d_side_used = nullptr;               // = (u32*)(d_stats + ST_COUNT_)
+    unsigned long long* d_stats = nullptr;    // ST_COUNT_ u64, then the map's slot count
     u64 batches = 0;
     std::map<std::pair<u32, i64>, u64> side;   // drained side-list deltas
     DivMagic div{};
@@ -119,6 +119,9 @@ static u32 log2u(u64 x) { u32 l = 0; while (((u64)1 << l) < x) ++l; return l; }
 
 extern "C" {
 
+static int agree_ring(ysb_ctx* c);
+static int allreduce_max(ysb_ctx* c, i64* h, int n);
+
 int ysb_abi_version(void) { return YSB_ABI_VERSION; }
 
 void ysb_config_default(ysb_config* c) {
@@ -154,7 +157,6 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_ovf);
     hipFree(c->d_ovf_count);
     hipFree(c->d_side);
-    hipFree(c->d_side_used);
     hipFree(c->d_stats);
     hipFree(c->d_truth);
     hipFree(c->d_truth_out);
@@ -241,12 +243,14 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
     while (c->side_slots < 2 * cfg.overflow_capacity) c->side_slots <<= 1;
     c->side_cbits = 1;
     while (c->side_cbits < 32 && (1ull << c->side_cbits) <= cfg.n_campaigns) ++c->side_cbits;   // bit_width
+    // stats and the map's slot count share one allocation: ysb_sync reads both in one copy
     if (hipMalloc(&c->d_side, c->side_slots * sizeof(SideSlot)) != hipSuccess ||
-        hipMalloc(&c->d_side_used, 8) != hipSuccess ||
-        hipMemset(c->d_side_used, 0, 8) != hipSuccess) {
+        hipMalloc(&c->d_stats, (ST_COUNT_ + 1) * 8) != hipSuccess ||
+        hipMemset(c->d_stats, 0, (ST_COUNT_ + 1) * 8) != hipSuccess) {
         fail(c, YSB_ERR_NOMEM, "device allocation failed");
         return bad(YSB_ERR_NOMEM);
     }
+    c->d_side_used = reinterpret_cast<u32*>(c->d_stats + ST_COUNT_);
     launch_side_clear(c->d_side, c->side_slots, c->s_comp);
     if (hipStreamSynchronize(c->s_comp) != hipSuccess) {
         fail(c, YSB_ERR_HIP, "side map initialisation failed");
@@ -254,7 +258,7 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
     }
     if (hipMalloc(&c->d_ring, 16) != hipSuccess || hipHostMalloc(&c->h_ring, 16) != hipSuccess ||
         hipMalloc(&c->d_ovf, cfg.overflow_capacity * sizeof(OvfEntry)) != hipSuccess ||
-        hipMalloc(&c->d_ovf_count, 16) != hipSuccess || hipMalloc(&c->d_stats, ST_COUNT_ * 8) != hipSuccess) {
+        hipMalloc(&c->d_ovf_count, 16) != hipSuccess) {
         fail(c, YSB_ERR_NOMEM, "device allocation failed");
         return bad(YSB_ERR_NOMEM);
     }
@@ -266,7 +270,7 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
         c->ring_lo = cfg.ring_base_bucket;
     }
     if (hipMemcpy(c->d_ring, ring, 16, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(c->d_ovf_count, 0, 16) != hipSuccess || hipMemset(c->d_stats, 0, ST_COUNT_ * 8) != hipSuccess) {
+        hipMemset(c->d_ovf_count, 0, 16) != hipSuccess) {
         fail(c, YSB_ERR_HIP, "initialisation copy failed");
         return bad(YSB_ERR_HIP);
     }
@@ -657,13 +661,43 @@ int ysb_submit_device_segments(ysb_ctx* c, const ysb_segment* segs, uint32_t n_s
     return enqueue_scan(c, segs, n_segs);
 }
 
-int ysb_sync(ysb_ctx* c) {
-    if (!c) return YSB_ERR_ARG;
+static int sync_streams(ysb_ctx* c) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->s_copy));
     HIPCHK(c, hipStreamSynchronize(c->s_comp));
     poll_ring(c);
     return YSB_OK;
+}
+
+static int pull_side_list(ysb_ctx* c);
+
+// After the streams are idle: the out-of-ring map is emptied into the exact host-side
+// list once it is a quarter full (so it never fills across launches: the side list
+// grows on demand), and counts the device could not place anywhere (the map full
+// within one launch AND the fallback list full) fail the call -- results would no
+// longer be exact.  The loss is sticky until ysb_reset.
+static int check_capacity(ysb_ctx* c) {
+    unsigned long long v[ST_COUNT_ + 1];
+    HIPCHK(c, hipMemcpy(v, c->d_stats, sizeof v, hipMemcpyDeviceToHost));
+    const u32 used = (u32)v[ST_COUNT_];
+    if ((u64)used * 4 > c->side_slots) {
+        int rc = pull_side_list(c);
+        if (rc) return rc;
+    }
+    if (v[ST_OVF_DROPPED])
+        return fail(c, YSB_ERR_CAPACITY,
+                    "%llu joined views outside the window ring were lost: the out-of-ring map and its "
+                    "fallback list (overflow_capacity %llu) filled within one launch; counts are not exact "
+                    "until ysb_reset (raise overflow_capacity or window_ring, or submit smaller batches)",
+                    (unsigned long long)v[ST_OVF_DROPPED], (unsigned long long)c->cfg.overflow_capacity);
+    return YSB_OK;
+}
+
+int ysb_sync(ysb_ctx* c) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = sync_streams(c);
+    if (rc) return rc;
+    return check_capacity(c);
 }
 
 // ---- results --------------------------------------------------------------------------------
@@ -797,17 +831,13 @@ int ysb_drain(ysb_ctx* c, int64_t blo, int64_t bhi, int clear, ysb_count* out, u
     return YSB_OK;
 }
 
-int ysb_ring_advance(ysb_ctx* c, int64_t new_lo) {
-    if (!c) return YSB_ERR_ARG;
-    int rc = ysb_sync(c);
-    if (rc) return rc;
-    if ((rc = read_ring(c))) return rc;
-    if (c->comm) return fail(c, YSB_ERR_STATE, "ysb_ring_advance is not available after ysb_group_init "
-                                               "(every rank's ring must move together)");
-    if (new_lo <= INT64_MIN / 2 || new_lo >= INT64_MAX / 2) return fail(c, YSB_ERR_ARG, "ring base out of range");
+// Moves the ring to [new_lo, new_lo + W): buckets of the old range that the new range
+// does not hold go to the exact host-side list (both the rank-local table and, after an
+// exchange, the owned block); cells are indexed by bucket mod W, so the rest stays put.
+static int move_ring(ysb_ctx* c, i64 new_lo) {
+    int rc;
     if (c->ring_known && new_lo != c->ring_lo) {
         const i64 lo = c->ring_lo, W = (i64)c->cfg.window_ring;
-        // buckets of the old range that the new range does not hold move to the host map
         const i64 a = new_lo > lo ? lo : std::max<i64>(new_lo + W, lo);
         const i64 b = new_lo > lo ? std::min<i64>(new_lo, lo + W) : lo + W;
         if (a < b && (rc = ring_rows(c, a, b, true, c->side))) return rc;
@@ -820,9 +850,28 @@ int ysb_ring_advance(ysb_ctx* c, int64_t new_lo) {
     return YSB_OK;
 }
 
+int ysb_ring_advance(ysb_ctx* c, int64_t new_lo) {
+    if (!c) return YSB_ERR_ARG;
+    // (no capacity check here: after ysb_group_init this is a collective, and a rank must
+    // not leave before the others' all-reduce; ysb_sync / ysb_drain report a loss)
+    int rc = sync_streams(c);
+    if (rc) return rc;
+    if ((rc = read_ring(c))) return rc;
+    if (c->comm) {
+        // collective after ysb_group_init: every rank's ring moves together (all ranks call
+        // it with the same new_lo; a disagreement fails on every rank alike)
+        if (!c->ring_agreed && (rc = agree_ring(c))) return rc;
+        i64 h[2] = {new_lo, -new_lo};
+        if ((rc = allreduce_max(c, h, 2))) return rc;
+        if (h[0] != -h[1]) return fail(c, YSB_ERR_ARG, "ysb_ring_advance: ranks asked for different ring bases");
+    }
+    if (new_lo <= INT64_MIN / 2 || new_lo >= INT64_MAX / 2) return fail(c, YSB_ERR_ARG, "ring base out of range");
+    return move_ring(c, new_lo);
+}
+
 int ysb_stats_get(ysb_ctx* c, ysb_stats* s) {
     if (!c || !s) return c ? fail(c, YSB_ERR_ARG, "NULL stats") : YSB_ERR_ARG;
-    int rc = ysb_sync(c);
+    int rc = sync_streams(c);   // readable after a capacity loss (overflow_dropped tells it)
     if (rc) return rc;
     unsigned long long v[ST_COUNT_];
     HIPCHK(c, hipMemcpy(v, c->d_stats, sizeof v, hipMemcpyDeviceToHost));
@@ -841,7 +890,7 @@ int ysb_stats_get(ysb_ctx* c, ysb_stats* s) {
 
 int ysb_reset(ysb_ctx* c) {
     if (!c) return YSB_ERR_ARG;
-    int rc = ysb_sync(c);
+    int rc = sync_streams(c);
     if (rc) return rc;
     const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
     HIPCHK(c, hipMemset(c->d_counts, 0, cells * 8));
@@ -871,7 +920,7 @@ int ysb_ring_range(ysb_ctx* c, int64_t* lo, uint32_t* width) {
 
 int ysb_kernel_time(ysb_ctx* c, double* total_ms, uint64_t* launches) {
     if (!c) return YSB_ERR_ARG;
-    int rc = ysb_sync(c);
+    int rc = sync_streams(c);
     if (rc) return rc;
     double t = 0;
     for (size_t i = 0; i < c->tev_used; ++i) {
@@ -916,6 +965,40 @@ int ysb_memcpy_d2h(ysb_ctx* c, void* h, const void* d, uint64_t bytes) {
 
 // ---- multi-GPU ---------------------------------------------------------------------------------
 
+// h[0..n) <- elementwise max over the ranks (one small RCCL all-reduce, synchronous).
+static int allreduce_max(ysb_ctx* c, i64* h, int n) {
+    i64* d = nullptr;
+    HIPCHK(c, hipMalloc(&d, sizeof(i64) * n));
+    hipError_t e = hipMemcpy(d, h, sizeof(i64) * n, hipMemcpyHostToDevice);
+    ncclResult_t r = ncclSuccess;
+    if (e == hipSuccess) r = ncclAllReduce(d, d, n, ncclInt64, ncclMax, c->comm, c->s_comp);
+    if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(h, d, sizeof(i64) * n, hipMemcpyDeviceToHost, c->s_comp);
+    if (e == hipSuccess && r == ncclSuccess) e = hipStreamSynchronize(c->s_comp);
+    hipFree(d);
+    if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    if (e != hipSuccess) return fail(c, YSB_ERR_HIP, "%s", hipGetErrorString(e));
+    return YSB_OK;
+}
+
+// Ring-base agreement (collective: every rank calls it at the same point and takes the
+// same decision from the reduced values, so no rank skips a collective the others
+// enter).  The common base is the smallest base any rank holds.  A rank whose ring
+// starts later moves the buckets the common range no longer holds, [common + W, lo + W),
+// to its exact host-side list (cells are indexed by bucket mod W, so the rest stays in
+// place); a rank without a base takes the common one.  Skewed per-rank streams
+// (core.clj:166-174) that auto-based differently therefore still exchange.
+static int agree_ring(ysb_ctx* c) {
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    int rc = read_ring(c);
+    if (rc) return rc;
+    i64 h[2] = {c->ring_known ? -c->ring_lo : INT64_MIN + 1, c->ring_known ? 1 : 0};
+    if ((rc = allreduce_max(c, h, 2))) return rc;
+    if (!h[1]) return YSB_OK;   // no rank has a base yet: agreed at the next exchange
+    if ((rc = move_ring(c, -h[0]))) return rc;
+    c->ring_agreed = true;
+    return YSB_OK;
+}
+
 int ysb_group_unique_id(uint8_t uid[YSB_UNIQUE_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == YSB_UNIQUE_ID_BYTES, "ncclUniqueId size");
     ncclUniqueId id;
@@ -946,13 +1029,23 @@ int ysb_group_init(ysb_ctx* c, int rank, int nranks, const uint8_t uid[YSB_UNIQU
         HIPCHK(c, hipMemset(c->d_counts, 0, (u64)cp * W * 8));
         HIPCHK(c, hipMemcpy(c->d_counts, old, (u64)c->c_pad * W * 8, hipMemcpyDeviceToDevice));
         hipFree(old);
+        if (c->d_truth) {   // the generator-truth table has the ring's layout: grow it too
+            unsigned long long* ot = c->d_truth;
+            c->d_truth = nullptr;
+            HIPCHK(c, hipMalloc(&c->d_truth, (u64)cp * W * 8));
+            HIPCHK(c, hipMemset(c->d_truth, 0, (u64)cp * W * 8));
+            HIPCHK(c, hipMemcpy(c->d_truth, ot, (u64)c->c_pad * W * 8, hipMemcpyDeviceToDevice));
+            hipFree(ot);
+        }
         c->c_pad = cp;
     }
     const u64 per = (u64)c->c_pad / nranks * c->cfg.window_ring;
     HIPCHK(c, hipMalloc(&c->d_owned, per * 8));
     HIPCHK(c, hipMemset(c->d_owned, 0, per * 8));
     HIPCHK(c, hipMalloc(&c->d_rs_tmp, per * 8));
-    return YSB_OK;
+    // every rank's ring must start at the same bucket (the tables are summed cell by
+    // cell): agreed here if any rank already knows its base, else at the first exchange
+    return agree_ring(c);
 }
 
 int ysb_group_reduce_scatter(ysb_ctx* c) {
@@ -960,35 +1053,26 @@ int ysb_group_reduce_scatter(ysb_ctx* c) {
     if (!c->comm) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->ring_agreed) {
-        // The tables are summed cell by cell (cell = bucket mod W): every rank's ring must
-        // start at the same bucket.  Checked once, on the first exchange (one small
-        // all-reduce of {lo, -lo, set} with max).
-        HIPCHK(c, hipStreamSynchronize(c->s_comp));
-        int rc = read_ring(c);
+        int rc = agree_ring(c);
         if (rc) return rc;
-        // every rank takes the same decision from the reduced values (no rank may skip
-        // the collective the others enter): {max lo, -min lo, max set, -min set}
-        i64 h[4] = {c->ring_known ? c->ring_lo : INT64_MIN + 1, c->ring_known ? -c->ring_lo : INT64_MIN + 1,
-                    c->ring_known ? 1 : 0, c->ring_known ? -1 : 0};
-        i64* d = nullptr;
-        HIPCHK(c, hipMalloc(&d, sizeof h));
-        HIPCHK(c, hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice));
-        ncclResult_t r = ncclAllReduce(d, d, 4, ncclInt64, ncclMax, c->comm, c->s_comp);
-        hipError_t e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->s_comp);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->s_comp);
-        hipFree(d);
-        if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
-        if (e != hipSuccess) return fail(c, YSB_ERR_HIP, "%s", hipGetErrorString(e));
-        const bool any = h[2] != 0, all = h[3] == -1;
-        if (any && (!all || h[0] != -h[1]))
-            return fail(c, YSB_ERR_STATE, "ranks hold different ring bases (set ysb_config.ring_base_bucket)");
-        c->ring_agreed = any;
     }
     const u64 per = (u64)c->c_pad / c->nranks * c->cfg.window_ring;
     ncclResult_t r = ncclReduceScatter(c->d_counts, c->d_rs_tmp, per, ncclUint64, ncclSum, c->comm, c->s_comp);
     if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
     launch_add_u64(c->d_owned, c->d_rs_tmp, per, c->s_comp);
     HIPCHK(c, hipMemsetAsync(c->d_counts, 0, (u64)c->c_pad * c->cfg.window_ring * 8, c->s_comp));
+    return YSB_OK;
+}
+
+int ysb_group_info(ysb_ctx* c, int* rank, int* nranks) {
+    if (!c) return YSB_ERR_ARG;
+    if (!c->comm) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
+    int n = 0, r = 0;
+    ncclResult_t e = ncclCommCount(c->comm, &n);
+    if (e == ncclSuccess) e = ncclCommUserRank(c->comm, &r);
+    if (e != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclCommCount: %s", ncclGetErrorString(e));
+    if (rank) *rank = r;
+    if (nranks) *nranks = n;
     return YSB_OK;
 }
 
@@ -1151,6 +1235,19 @@ int ysb_truth_compare(ysb_ctx* c, uint64_t* mismatched, uint64_t* truth_total, u
     if (mismatched) *mismatched = r[0];
     if (truth_total) *truth_total = r[1] + outside;
     if (ring_total) *ring_total = r[2];
+    return YSB_OK;
+}
+
+int ysb_truth_read(ysb_ctx* c, uint64_t* out, uint64_t cells, int64_t* ring_lo) {
+    if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
+    if (!c->d_truth) return fail(c, YSB_ERR_STATE, "no truth accumulated");
+    const u64 need = (u64)c->cfg.n_campaigns * c->cfg.window_ring;
+    if (cells < need) return fail(c, YSB_ERR_CAPACITY, "truth table needs %llu cells", (unsigned long long)need);
+    int rc = sync_streams(c);
+    if (rc) return rc;
+    if ((rc = read_ring(c))) return rc;
+    HIPCHK(c, hipMemcpy(out, c->d_truth, need * 8, hipMemcpyDeviceToHost));
+    if (ring_lo) *ring_lo = c->ring_lo;
     return YSB_OK;
 }
 

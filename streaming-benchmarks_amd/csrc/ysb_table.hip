@@ -33,8 +33,10 @@ __global__ __launch_bounds__(AUX_TPB) void compact_kernel(unsigned long long* ta
             r.bucket = b;
             r.count = v;
             out[k] = r;
+            // cleared only once written out: a cell past cap keeps its count (the host
+            // reports "table changed during drain" and nothing is lost)
+            if (clear) *cell = 0;
         }
-        if (clear) *cell = 0;
     }
     if (count_only) {
         // one atomic per wave

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <fstream>
 #include <random>
+#include <set>
 #include <sstream>
 #include <thread>
 
@@ -532,15 +533,18 @@ RedisWindowWriter::RedisWindowWriter(const std::string& host, int port) : r_(new
 RedisWindowWriter::~RedisWindowWriter() = default;
 
 void RedisWindowWriter::writeWindows(const std::vector<WindowDelta>& rows) {
+    // the (campaign, window) keys and campaigns not cached yet, each once, in first-seen
+    // order (sets beside the vectors: a config-3 flush holds millions of rows)
     std::vector<std::pair<std::string, std::string>> need_w;
     std::vector<std::string> need_l;
+    std::set<std::pair<std::string, std::string>> seen_w;
+    std::set<std::string> seen_l;
     for (const WindowDelta& d : rows) {
         if (!d.count) continue;
-        const auto k = std::make_pair(d.campaign, std::to_string(d.windowMs));
-        if (!windowUuid_.count(k) && std::find(need_w.begin(), need_w.end(), k) == need_w.end()) {
-            need_w.push_back(k);
-            if (!listUuid_.count(d.campaign) && std::find(need_l.begin(), need_l.end(), d.campaign) == need_l.end())
-                need_l.push_back(d.campaign);
+        auto k = std::make_pair(d.campaign, std::to_string(d.windowMs));
+        if (!windowUuid_.count(k) && seen_w.insert(k).second) {
+            need_w.push_back(std::move(k));
+            if (!listUuid_.count(d.campaign) && seen_l.insert(d.campaign).second) need_l.push_back(d.campaign);
         }
     }
     // round trip 1: the window / list UUIDs not cached yet (hmget campaign ts, :70)

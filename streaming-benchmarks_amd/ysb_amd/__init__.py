@@ -7,4 +7,5 @@ from ._lib import LIB_PATH, YsbError, lib  # noqa: F401
 from .admap import AdCampaignMap  # noqa: F401
 from .context import YsbContext  # noqa: F401
 from .generator import AD_TYPES, EVENT_TYPES, GenParams, ad_shard, json_to_tbl, shard_ads  # noqa: F401
-from .group import owned_block, route_lines, split_batch  # noqa: F401
+from .group import (exchange_mismatches, owned_block, ring_agreement, route_lines, split_batch,  # noqa: F401
+                    table_rows)

@@ -95,6 +95,7 @@ SIGNATURES = {
     "ysb_group_init": (_I, [_P, _I, _I, C.c_char_p]),
     "ysb_group_reduce_scatter": (_I, [_P]),
     "ysb_group_owned": (_I, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
+    "ysb_group_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I)]),
     "ysb_ad_shard": (_U32, [C.c_char_p, _U32, _U32]),
     "ysb_group_block": (_I, [_U32, _I, _I, C.POINTER(_U32), C.POINTER(_U32)]),
     "ysb_route_lines": (_I, [_PU8, _U64, _PU32, _U64, _U32, _PU32, C.c_void_p]),
@@ -105,6 +106,7 @@ SIGNATURES = {
     "ysb_gen_max_line_bytes": (_U64, [C.POINTER(YsbGenParams)]),
     "ysb_truth_accumulate": (_I, [_P, C.POINTER(YsbGenParams), _U64, _U64]),
     "ysb_truth_compare": (_I, [_P, C.POINTER(_U64), C.POINTER(_U64), C.POINTER(_U64)]),
+    "ysb_truth_read": (_I, [_P, C.c_void_p, _U64, C.POINTER(_I64)]),
     "ysb_gen_dump": (_I, [C.POINTER(YsbGenParams), _U64, C.c_char_p]),
     "ysb_json_to_tbl": (_I, [_PU8, _U64, _PU32, _U64, _PU8, _U64, _PU32, C.POINTER(_U64)]),
     "ysb_gen_dump_shards": (_I, [C.POINTER(YsbGenParams), _U64, C.c_char_p, _U32]),

@@ -184,6 +184,12 @@ class YsbContext:
     def group_reduce_scatter(self):
         self._c(lib().ysb_group_reduce_scatter(self._h))
 
+    def group_info(self):
+        """(rank, nranks) as RCCL's communicator reports them (ncclCommUserRank / ncclCommCount)."""
+        r, n = C.c_int(), C.c_int()
+        self._c(lib().ysb_group_info(self._h, C.byref(r), C.byref(n)))
+        return r.value, n.value
+
     def group_owned(self):
         lo, hi = C.c_uint32(), C.c_uint32()
         self._c(lib().ysb_group_owned(self._h, C.byref(lo), C.byref(hi)))
@@ -198,6 +204,13 @@ class YsbContext:
 
     def truth_accumulate(self, params, first, n):
         self._c(lib().ysb_truth_accumulate(self._h, C.byref(params.c), first, n))
+
+    def truth_read(self):
+        """(truth table [n_campaigns][W] uint64, ring base bucket): the generator truth."""
+        out = np.zeros((self.cfg.n_campaigns, self.cfg.window_ring), dtype=np.uint64)
+        lo = C.c_int64()
+        self._c(lib().ysb_truth_read(self._h, _ptr(out), out.size, C.byref(lo)))
+        return out, lo.value
 
     def truth_compare(self):
         m, t, r = C.c_uint64(), C.c_uint64(), C.c_uint64()

@@ -48,3 +48,40 @@ def split_batch(raw, offs, shard, r: int):
     idx = np.concatenate([np.arange(offs[i], ends[i], dtype=np.uint64) for i in sel]) if sel.size else \
         np.zeros(0, dtype=np.uint64)
     return raw[idx.astype(np.int64)], new_off.astype(np.uint32)
+
+
+def table_rows(table, ring_lo, c_off=0):
+    """{(campaign, bucket): count} of the non-zero cells of a campaign-major ring table
+    [rows][W] (cell (c, b mod W) holds bucket b of [ring_lo, ring_lo + W)); row i is
+    campaign c_off + i.  The layout of the device ring, the owned block and the truth table."""
+    t = np.asarray(table)
+    W = t.shape[-1]
+    t = t.reshape(-1, W)
+    cs, ss = np.nonzero(t)
+    buckets = ring_lo + ((ss.astype(np.int64) - ring_lo) % W)
+    return {(int(c) + c_off, int(b)): int(t[c, s]) for c, s, b in zip(cs, ss, buckets)}
+
+
+def ring_agreement(bases):
+    """The common ring base the ranks agree on (ysb_group_init / the first exchange): the
+    smallest base any rank holds (None: no rank has one yet)."""
+    known = [b for b in bases if b is not None]
+    return min(known) if known else None
+
+
+def exchange_mismatches(expected, per_rank):
+    """Post-exchange check: per_rank = [(owned_lo, owned_hi, {(campaign, bucket): count}), ...]
+    as every owner drained after the reduce-scatter.  Returns (cells whose summed count
+    differs from `expected`, ring rows an owner reported outside its campaign block, cells
+    compared).  Side-list rows (buckets outside the ring) are additive deltas any rank may
+    report, so a caller with out-of-ring events counts them apart."""
+    merged = {}
+    outside = 0
+    for lo, hi, rows in per_rank:
+        for (c, b), v in rows.items():
+            if not lo <= c < hi:
+                outside += 1
+            merged[(c, b)] = merged.get((c, b), 0) + v
+    keys = set(expected) | set(merged)
+    mism = sum(1 for k in keys if expected.get(k, 0) != merged.get(k, 0))
+    return mism, outside, len(keys)

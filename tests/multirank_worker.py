@@ -25,7 +25,8 @@ import torch.distributed as dist  # noqa: E402
 
 import golden_data as gd  # noqa: E402
 from oracle import oracle  # noqa: E402
-from ysb_amd import GenParams, owned_block, route_lines, shard_ads, split_batch  # noqa: E402
+from ysb_amd import (GenParams, exchange_mismatches, owned_block, ring_agreement, route_lines,  # noqa: E402
+                     shard_ads, split_batch, table_rows)
 
 W = 64   # ring width (power of two), like ysb_config.window_ring
 
@@ -40,13 +41,8 @@ def table_of(rows, c_pad, ring_lo):
 
 
 def rows_of_block(block, lo, ring_lo):
-    out = {}
-    for i, v in enumerate(block.tolist()):
-        if v:
-            c, cell = lo + i // W, i % W
-            b = ring_lo + ((cell - ring_lo) % W)
-            out[(c, b)] = v
-    return out
+    """The owner's drain of its block (the library's table layout: ysb_amd.table_rows)."""
+    return table_rows(block.numpy().reshape(-1, W), ring_lo, c_off=lo)
 
 
 def main():
@@ -78,15 +74,34 @@ def main():
         res["all_routed_here"] = bool((shard == rank).all())
         rows, st = oracle.run(oracle.AdMap(aids, base.ad_campaign_index()), raw, offs)
         res["lines"] = int(offs.size)
+    elif scenario == "skew":
+        # per-rank real-time streams with skew and late events (core.clj:166-174) that start
+        # 10 minutes apart: every rank auto-bases its ring differently (first bucket - W/8,
+        # ring_autobase_kernel) and rank 1's later buckets fall past the common ring
+        base = GenParams(seed=42, n_campaigns=20, ads_per_campaign=10, events_per_sec=1000)
+        _, aids = base.ids()
+        n_campaigns = 20
+        subset = shard_ads(aids, world)[rank]
+        g = GenParams(seed=42, event_stream=1 + rank, n_campaigns=20, ads_per_campaign=10, events_per_sec=1000,
+                      ad_subset=subset, with_skew=True, n_users=100, t0_ms=1_700_000_000_000 + rank * 600_000)
+        raw, offs = g.events_host(0, 20_000)
+        rows, st = oracle.run(oracle.AdMap(aids, base.ad_campaign_index()), raw, offs)
+        res["lines"] = int(offs.size)
     else:
         raise SystemExit("unknown scenario " + scenario)
 
-    # common ring base: the smallest bucket any rank saw
-    lo_b = torch.tensor([min((b for (_, b) in rows), default=2**62)], dtype=torch.int64)
-    dist.all_reduce(lo_b, op=dist.ReduceOp.MIN)
-    ring_lo = int(lo_b.item())
+    # ring-base agreement (ysb_group_init / the first exchange, ysb_capi.cpp agree_ring):
+    # each rank's auto-base is its first bucket - W/8; the common base is the smallest;
+    # a rank's rows the common ring cannot hold go to its exact side list (additive deltas)
+    my_base = min((b for (_, b) in rows), default=None)
+    my_base = None if my_base is None else my_base - W // 8
+    bases = [None] * world
+    dist.all_gather_object(bases, my_base)
+    ring_lo = ring_agreement(bases)
+    side = {k: v for k, v in rows.items() if not ring_lo <= k[1] < ring_lo + W}
+    in_ring = {k: v for k, v in rows.items() if k not in side}
     c_pad = (n_campaigns + world - 1) // world * world
-    table = table_of(rows, c_pad, ring_lo)
+    table = table_of(in_ring, c_pad, ring_lo)
     block = torch.zeros(c_pad // world * W, dtype=torch.int64)
     dist.reduce_scatter_tensor(block, table)
     lo, hi = owned_block(n_campaigns, rank, world)
@@ -97,9 +112,20 @@ def main():
     gathered = [None] * world
     dist.all_gather_object(gathered, {"local": [[c, b, n] for (c, b), n in rows.items()],
                                       "owned": [[c, b, n] for (c, b), n in owned.items()],
-                                      "block": [lo, hi], "stats": st})
+                                      "side": [[c, b, n] for (c, b), n in side.items()],
+                                      "block": [lo, hi], "stats": st, "base": my_base})
     if rank == 0:
         res["ranks"] = gathered
+        res["ring_lo"] = ring_lo
+        # bench.py's post-exchange check: the owners' rows (+ every rank's side deltas, any
+        # campaign) against the truth summed over ranks
+        expected = {}
+        for gi in gathered:
+            for c, b, n in gi["local"]:
+                expected[(c, b)] = expected.get((c, b), 0) + n
+        per = [(gi["block"][0], gi["block"][1], {(c, b): n for c, b, n in gi["owned"]}) for gi in gathered]
+        per += [(0, n_campaigns, {(c, b): n for c, b, n in gi["side"]}) for gi in gathered]
+        res["exchange"] = list(exchange_mismatches(expected, per))
     dist.barrier()
     dist.destroy_process_group()
     with open(out_path, "w") as f:

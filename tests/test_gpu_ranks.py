@@ -2,17 +2,22 @@
 RCCL refuses two ranks on one device, so the collective itself is not run here).
 
 Each rank's context is built exactly as bench.py builds it (its own generator stream
-over its shard of the shared ad ids, window_ring 1024, no explicit ring base), all on
-cuda:0.  What ysb_group_reduce_scatter needs before summing tables cell by cell is
-checked directly: every rank's ring starts at the same bucket (the exchange refuses
-otherwise, ysb_capi.cpp ysb_group_reduce_scatter), every rank counts exactly its
-generator truth, and the sum over ranks equals the campaign-major reduce-scatter
-result (owner blocks, ysb_group_owned's padding rule)."""
+over its shard of the shared ad ids, window_ring 1024, the ring base every rank derives
+from the shared t0), all on cuda:0.  What ysb_group_reduce_scatter needs before summing
+tables cell by cell is checked directly: every rank's ring starts at the same bucket
+(ysb_capi.cpp agree_ring would otherwise move a later-starting ring), every rank counts
+exactly its generator truth, and the sum over ranks equals the campaign-major
+reduce-scatter result (owner blocks, ysb_group_owned's padding rule).  A one-rank RCCL
+group runs bench.py's own post-exchange check (exchange_check) for real."""
+import os
+import sys
 from collections import Counter
 
 import pytest
 
 from ysb_amd import GenParams, YsbContext, owned_block, shard_ads
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 pytestmark = pytest.mark.gpu
 
@@ -36,7 +41,7 @@ def test_bench_ranks_share_ring_base_and_sum_to_truth(world):
     rings, tables, total_joined = [], [], 0
     for rank in range(world):
         g, aids, camp = rank_params(world, rank)
-        with YsbContext(device=0, n_campaigns=100, window_ring=1024,
+        with YsbContext(device=0, n_campaigns=100, window_ring=1024, ring_base_bucket=g.c.t0_ms // 10000 - 128,
                         max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
             ctx.load_ad_map(aids, camp)
             cap = n * g.max_line_bytes()
@@ -65,3 +70,38 @@ def test_bench_ranks_share_ring_base_and_sum_to_truth(world):
     assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
     owned = sum(v for (c, _), v in merged.items() for lo, hi in blocks if lo <= c < hi)
     assert owned == total_joined
+
+
+def test_one_rank_group_runs_bench_exchange_check():
+    """A real (one-rank) RCCL group: ysb_group_init agrees on the ring, the reduce-scatter
+    moves the table into the owned block, and bench.exchange_check -- the code the N-rank
+    run executes -- finds the owners' rows equal to the truth."""
+    import bench
+    g, aids, camp = rank_params(1, 0)
+    n = 3_000_000
+    with YsbContext(device=0, n_campaigns=100, window_ring=1024, max_batch_bytes=16 << 20,
+                    max_batch_events=1 << 16) as ctx:
+        ctx.load_ad_map(aids, camp)
+        ctx.group_init(0, 1, YsbContext.group_unique_id())
+        assert ctx.group_info() == (0, 1)
+        cap = n * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
+        nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+        segs = [(0, n, d_b, nb, d_o)]
+
+        def submit_all():
+            ctx.submit_device_segments([(d_b, nb, d_o, n)])
+        submit_all()
+        ctx.group_reduce_scatter()                       # first exchange: agrees on the ring
+        os.environ.pop("WORLD_SIZE", None)
+        d = bench.Dist(1)
+        chk = bench.exchange_check(d, ctx, g, segs, submit_all)
+        ex = chk["exchange"]
+        assert chk["truth_mismatched_cells"] == 0 and chk["truth_views"] == chk["counted_views"] > 0
+        assert ex["post_exchange_mismatched_cells"] == 0 and ex["owner_rows_outside_block"] == 0
+        assert ex["owned_views"] == ex["truth_views_summed"] == chk["truth_views"]
+        assert ex["rccl_ranks"] == [1] and ex["owned_blocks"] == [[0, 100]]
+        # after ysb_group_init, ring_advance is collective (one rank: trivially agreed)
+        lo, w = ctx.ring_range()
+        ctx.ring_advance(lo + 1)
+        assert ctx.ring_range() == (lo + 1, w)

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle
-from ysb_amd import GenParams, YsbContext
+from ysb_amd import YsbError, GenParams, YsbContext
 from ysb_amd.stream import SlotContext, StreamingOperator
 
 pytestmark = pytest.mark.gpu
@@ -146,6 +146,8 @@ def test_out_of_ring_cells_exact_through_side_map():
 
 
 def test_side_capacity_exhaustion_is_reported():
+    """Counts the device could not place (map AND fallback list full within one launch)
+    fail ysb_sync / ysb_drain with YSB_ERR_CAPACITY until ysb_reset: never silent."""
     g = GenParams(seed=9, n_campaigns=40, ads_per_campaign=5, events_per_sec=100)
     raw, offs = g.events_host(0, 80_000)
     _, aids = g.ids()
@@ -153,4 +155,32 @@ def test_side_capacity_exhaustion_is_reported():
                     max_batch_events=1 << 18) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         ctx.submit(raw, offs)
-        assert ctx.stats()["overflow_dropped"] > 0       # loud, never silent
+        with pytest.raises(YsbError) as e:
+            ctx.sync()
+        assert e.value.code == -4 and "lost" in str(e.value)
+        with pytest.raises(YsbError) as e:
+            ctx.drain()
+        assert e.value.code == -4
+        assert ctx.stats()["overflow_dropped"] > 0       # the stats stay readable
+        ctx.reset()
+        ctx.sync()                                       # cleared by the reset
+
+
+def test_side_map_spills_to_host_between_launches():
+    """A small out-of-ring map never fills across batches: ysb_sync empties it into the
+    exact host list once a quarter full, so many small batches stay exact."""
+    g = GenParams(seed=9, n_campaigns=40, ads_per_campaign=5, events_per_sec=100, with_skew=True)
+    raw, offs = g.events_host(0, 80_000)
+    rows, _ = oracle_rows(g, raw, offs)
+    _, aids = g.ids()
+    with YsbContext(n_campaigns=40, window_ring=16, overflow_capacity=512, max_batch_bytes=64 << 20,
+                    max_batch_events=1 << 18) as ctx:
+        ctx.load_ad_map(aids, g.ad_campaign_index())
+        step = 2000
+        for i in range(0, offs.size, step):
+            j = min(i + step, offs.size)
+            end = int(offs[j]) if j < offs.size else raw.size
+            ctx.submit(raw[offs[i]:end], offs[i:j] - offs[i], slot=(i // step) & 1)
+            ctx.sync()
+        assert ctx.stats()["overflow_dropped"] == 0
+        assert ctx.drain_buckets() == rows

@@ -89,6 +89,40 @@ def test_per_rank_generation_reduce_scatter(tmp_path):
     assert sum(sum(n for _, _, n in i["owned"]) for i in infos) == sum(i["stats"]["joined"] for i in infos)
 
 
+@pytest.mark.parametrize("scenario,world", [("route", 2), ("gen", 3), ("skew", 2), ("skew", 3)])
+def test_post_exchange_check(scenario, world, tmp_path):
+    """bench.py's N > 1 check (ysb_amd.exchange_mismatches): the owners' rows after the
+    reduce-scatter equal the truth summed over ranks, none outside its block."""
+    res = run_ranks(scenario, world, tmp_path)
+    mism, outside, cells = res[0]["exchange"]
+    assert mism == 0 and outside == 0 and cells > 0
+
+
+def test_skewed_ranks_agree_on_a_ring_base(tmp_path):
+    """Per-rank skewed streams auto-base differently; the agreement takes the smallest base
+    and the rows past the common ring travel as side deltas -- nothing is lost."""
+    res = run_ranks("skew", 2, tmp_path)
+    infos = res[0]["ranks"]
+    assert len(set(i["base"] for i in infos)) == 2           # the ranks disagreed ...
+    assert res[0]["ring_lo"] == min(i["base"] for i in infos)
+    assert sum(len(i["side"]) for i in infos) > 0            # ... and rank 1's late buckets moved out
+    tot = Counter()
+    for i in infos:
+        for c, b, n in i["owned"] + i["side"]:
+            tot[(c, b)] += n
+    assert dict(tot) == merged(infos, "local")
+
+
+def test_exchange_mismatches_detects_errors():
+    from ysb_amd import exchange_mismatches
+    exp = {(0, 5): 3, (1, 5): 2, (3, 6): 1}
+    ok = [(0, 2, {(0, 5): 3, (1, 5): 2}), (2, 4, {(3, 6): 1})]
+    assert exchange_mismatches(exp, ok) == (0, 0, 3)
+    bad = [(0, 2, {(0, 5): 3, (1, 5): 1}), (2, 4, {(3, 6): 1, (1, 5): 1})]
+    assert exchange_mismatches(exp, bad) == (0, 1, 3)        # the sum holds, one row in the wrong block
+    assert exchange_mismatches(exp, [(0, 4, {(0, 5): 3})])[0] == 2
+
+
 def test_owned_block_matches_padding_rule():
     for C in (1, 7, 100, 1_000_000):
         for N in (1, 2, 3, 8):

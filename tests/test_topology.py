@@ -159,6 +159,27 @@ def test_cpp_redis_writer_matches_python_writer(tmp_path):
         b.close()
 
 
+def test_cpp_redis_writer_many_rows(tmp_path):
+    """A config-3-sized flush (30k distinct (campaign, window) rows) is written in two
+    round trips and in linear time (the writer dedups its pending keys with sets)."""
+    camps = ["c%05d" % i for i in range(300)]
+    rows = [(c, 1700000000000 + 10000 * w, 1 + (c + w) % 5) for c in range(300) for w in range(100)]
+    csv = tmp_path / "rows.csv"
+    csv.write_text("campaign_id,window_ms,count\n" + "".join("%s,%d,%d\n" % (camps[c], w, n) for c, w, n in rows))
+    conf = write_conf(tmp_path, gd.path("gen_s7.jsonl"), gd.path("gen_s7.ad_to_campaign.txt"))
+    a = FakeRedis()
+    try:
+        out = last_json(run("--confPath", conf, "--sink", "redis:127.0.0.1:%d" % a.port, "--replay-rows", str(csv)))
+        assert out["rows"] == len(rows) and out["round_trips"] == 2
+        cli = RespClient("127.0.0.1", a.port)
+        for c, w, n in rows[::997]:
+            wid = cli.execute("HGET", camps[c], str(w))
+            assert int(cli.execute("HGET", wid, "seen_count")) == n
+        cli.close()
+    finally:
+        a.close()
+
+
 def test_parallel_source_on_a_large_file(tmp_path):
     """Blocks of >= 8 MiB take the multi-threaded pread + split path."""
     d = tmp_path / "gen"
