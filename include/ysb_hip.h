@@ -53,6 +53,10 @@ extern "C" {
                                    user_id|page_id|ad_id|ad_type|event_type|event_time
                                    (MockWindowedFlatMap, AdvertisingTopologyNative.java:
                                    197-226) instead of JSON                       */
+#define YSB_F_RECORD_COUNT 0x20u /* count joined views in record mode wherever possible (the
+                                   default: only for rings >= 1M cells and launches >= 1M
+                                   events without LDS window counters; ysb_path_time)  */
+#define YSB_F_NO_RECORD_COUNT 0x40u /* never: one global atomic per joined view             */
 #define YSB_F_SPARSE_FAST_JOIN 0x8u /* test hook: leave every other 36-byte key out of
                                    the fast-path cuckoo table, as a failed cuckoo
                                    placement would; its misses then take the
@@ -197,6 +201,10 @@ int         ysb_ring_advance(ysb_ctx* ctx, int64_t new_lo);
 /* With YSB_F_TIMING: total device time of the scan kernel launches (HIP events on
  * the compute stream) and the number of launches since the last call (resets). */
 int         ysb_kernel_time(ysb_ctx* ctx, double* total_ms, uint64_t* launches);
+/* The same launches' whole device sequence -- scan, general-path and (record mode)
+ * partition + count kernels -- as measured by the last ysb_kernel_time call (which
+ * collects both), and the launches so far that used record mode. */
+int         ysb_path_time(ysb_ctx* ctx, double* total_ms, uint64_t* launches, uint64_t* record_launches);
 /* The compute stream (hipStream_t) for callers that want to order work with it. */
 void*       ysb_stream(ysb_ctx* ctx);
 

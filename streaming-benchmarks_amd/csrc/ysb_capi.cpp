@@ -71,9 +71,21 @@ struct ysb_ctx {
     u32* d_off[2] = {nullptr, nullptr};
     hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_kdone[2] = {nullptr, nullptr};
     bool slot_busy[2] = {false, false};
-    // timing
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    // timing: per launch {before scan, after scan, after the last kernel of the launch}
+    std::vector<std::array<hipEvent_t, 3>> tev;
     size_t tev_used = 0;
+    double path_ms_acc = 0;                // ysb_path_time's share, collected by ysb_kernel_time
+    u64 path_launches_acc = 0;
+    // record mode (ysb_count.hip)
+    u32* d_rec = nullptr;
+    u64 rec_words = 0;
+    u32* d_rec_n = nullptr;
+    u64 rec_n_words = 0;
+    u32* d_part = nullptr;
+    u64 part_words = 0;
+    u32* d_runs = nullptr;
+    u64 runs_words = 0;
+    u64 rec_launches = 0;
     // group
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
@@ -173,7 +185,11 @@ static void destroy(ysb_ctx* c) {
         if (c->ev_h2d[s]) hipEventDestroy(c->ev_h2d[s]);
         if (c->ev_kdone[s]) hipEventDestroy(c->ev_kdone[s]);
     }
-    for (auto& p : c->tev) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+    for (auto& p : c->tev) for (hipEvent_t e : p) hipEventDestroy(e);
+    hipFree(c->d_rec);
+    hipFree(c->d_rec_n);
+    hipFree(c->d_part);
+    hipFree(c->d_runs);
     if (c->ev_ring) hipEventDestroy(c->ev_ring);
     if (c->s_comp) hipStreamDestroy(c->s_comp);
     if (c->s_copy) hipStreamDestroy(c->s_copy);
@@ -507,6 +523,72 @@ static void poll_ring(ysb_ctx* c) {
     }
 }
 
+// Grows a device u32 buffer to at least `words` (contents not kept).
+static int grow_u32(ysb_ctx* c, u32** buf, u64* have, u64 words) {
+    if (*have >= words) return YSB_OK;
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    hipFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    HIPCHK(c, hipMalloc(buf, words * 4));
+    *have = words;
+    return YSB_OK;
+}
+
+// Record mode (ysb_count.hip) for this launch: large count tables without LDS window
+// counters (configs[2]), where one global atomic per joined view is the bottleneck.
+// Auto: ring >= 1M cells and launch >= 1M events; YSB_F_RECORD_COUNT forces it on
+// wherever it is possible, YSB_F_NO_RECORD_COUNT off.
+static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
+    p.rec_on = 0;
+    const u32 W = c->cfg.window_ring;
+    const u64 cells = (u64)c->c_pad * W;
+    const bool force = (c->cfg.flags & YSB_F_RECORD_COUNT) != 0;
+    if ((c->cfg.flags & YSB_F_NO_RECORD_COUNT) || c->lds_wl || p.dyn_chunk || cells >= (1ull << 32) ||
+        W > (u32)REC_BLOCK_CELLS)
+        return YSB_OK;
+    if (!force && (cells < (1ull << 20) || n_events < (1ull << 20))) return YSB_OK;
+    r.ring_w = W;
+    r.w_log2 = log2u(W);
+    r.blk_shift = log2u(REC_BLOCK_CELLS / W);
+    r.c_pad = c->c_pad;
+    r.n_blocks = (u32)((c->c_pad + (1u << r.blk_shift) - 1) >> r.blk_shift);
+    const u32 sub = (r.n_blocks + REC_BINS_MAX - 1) / REC_BINS_MAX;
+    r.sub_log2 = log2u(sub);
+    if ((1u << r.sub_log2) > 4096u) return YSB_OK;
+    r.bins = (r.n_blocks + (1u << r.sub_log2) - 1) >> r.sub_log2;
+    r.grid = p.grid;
+    // lines one workgroup scans at most in this launch; ~1/3 are joined views on generator
+    // data; 3/4 of the lines spread over the bins leaves room for skew (a full sub-buffer
+    // sends the rest of its views to the atomics: slower, still exact)
+    u64 tiles = 0;
+    for (u32 i = 0; i < p.n_segs; ++i) tiles += p.seg[i].tiles_per_block + (p.seg[i].static_rem ? 1 : 0);
+    const u64 lines = tiles * TILE_LINES;
+    u64 cap = (lines * 3 / 4 + r.bins - 1) / r.bins;
+    cap = std::max<u64>(32, (cap + 31) / 32 * 32);
+    const u64 area = (u64)((r.grid + REC_QUARTERS - 1) / REC_QUARTERS) * cap;
+    const u64 part = (u64)r.bins * REC_QUARTERS * area;
+    if (cap > 0xFFFFFFFFull || part >= (1ull << 32)) return YSB_OK;
+    r.cap = (u32)cap;
+    int rc;
+    if ((rc = grow_u32(c, &c->d_rec, &c->rec_words, (u64)r.grid * r.bins * cap))) return rc;
+    if ((rc = grow_u32(c, &c->d_rec_n, &c->rec_n_words, (u64)r.grid * r.bins))) return rc;
+    if ((rc = grow_u32(c, &c->d_part, &c->part_words, part))) return rc;
+    if ((rc = grow_u32(c, &c->d_runs, &c->runs_words, (u64)r.n_blocks * REC_QUARTERS * 2))) return rc;
+    r.rec = c->d_rec;
+    r.rec_n = c->d_rec_n;
+    r.part = c->d_part;
+    r.runs = c->d_runs;
+    r.counts = c->d_counts;
+    p.rec_on = 1;
+    p.rec_bins = r.bins;
+    p.rec_shift = r.blk_shift + r.sub_log2;
+    p.rec_cap = r.cap;
+    p.rec = c->d_rec;
+    p.rec_n = c->d_rec_n;
+    return YSB_OK;
+}
+
 static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     if (!c->table_loaded) return fail(c, YSB_ERR_STATE, "ysb_load_ad_map has not been called");
     ysb_segment segs[MAX_SEGS];
@@ -555,16 +637,19 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     }
     // dynamic claims (off by default) count from zero in every launch
     if (p.dyn_chunk) HIPCHK(c, hipMemsetAsync(p.dyn_ctr, 0, 4 * MAX_SEGS, c->s_comp));
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    RecParams rp{};
+    int rc = plan_records(c, p, n, rp);
+    if (rc) return rc;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (c->cfg.flags & YSB_F_TIMING) {
         if (c->tev_used == c->tev.size()) {
-            hipEvent_t a, b;
-            HIPCHK(c, hipEventCreate(&a));
-            HIPCHK(c, hipEventCreate(&b));
-            c->tev.emplace_back(a, b);
+            std::array<hipEvent_t, 3> ev{};
+            for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
+            c->tev.push_back(ev);
         }
-        e0 = c->tev[c->tev_used].first;
-        e1 = c->tev[c->tev_used].second;
+        e0 = c->tev[c->tev_used][0];
+        e1 = c->tev[c->tev_used][1];
+        e2 = c->tev[c->tev_used][2];
         c->tev_used++;
         HIPCHK(c, hipEventRecord(e0, c->s_comp));
     }
@@ -573,6 +658,14 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     if (e1) HIPCHK(c, hipEventRecord(e1, c->s_comp));
     launch_defer(p, c->cus, c->s_comp);
     HIPCHK(c, hipGetLastError());
+    if (p.rec_on) {
+        launch_rec_partition(rp, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+        launch_rec_count(rp, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+        c->rec_launches++;
+    }
+    if (e2) HIPCHK(c, hipEventRecord(e2, c->s_comp));
     c->batches += nin;   // each segment counts as the batch it is
     return YSB_OK;
 }
@@ -922,15 +1015,27 @@ int ysb_kernel_time(ysb_ctx* c, double* total_ms, uint64_t* launches) {
     if (!c) return YSB_ERR_ARG;
     int rc = sync_streams(c);
     if (rc) return rc;
-    double t = 0;
+    double t = 0, tp = 0;
     for (size_t i = 0; i < c->tev_used; ++i) {
-        float ms = 0;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->tev[i].first, c->tev[i].second));
+        float ms = 0, mp = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->tev[i][0], c->tev[i][1]));
+        HIPCHK(c, hipEventElapsedTime(&mp, c->tev[i][0], c->tev[i][2]));
         t += ms;
+        tp += mp;
     }
     if (total_ms) *total_ms = t;
     if (launches) *launches = c->tev_used;
+    c->path_ms_acc = tp;
+    c->path_launches_acc = c->tev_used;
     c->tev_used = 0;
+    return YSB_OK;
+}
+
+int ysb_path_time(ysb_ctx* c, double* total_ms, uint64_t* launches, uint64_t* record_launches) {
+    if (!c) return YSB_ERR_ARG;
+    if (total_ms) *total_ms = c->path_ms_acc;
+    if (launches) *launches = c->path_launches_acc;
+    if (record_launches) *record_launches = c->rec_launches;
     return YSB_OK;
 }
 

@@ -121,7 +121,42 @@ struct ScanParams {
     u32* defer_count;           // [0] entries, reset by defer_kernel
     u32* defer_done;            // workgroup ticket of defer_kernel
     u32 defer_cap;
+    // Record mode (large count tables, no LDS window counters: configs[2]): a joined
+    // in-ring view is not an HBM atomic but a u32 record (its ring cell index) appended
+    // to the sub-buffer of (workgroup, campaign range); partition_kernel and
+    // count_kernel then sum the records per campaign block in LDS and add each touched
+    // ring cell once (RecParams).  A full sub-buffer falls back to the atomic.
+    u32 rec_on;
+    u32 rec_bins;               // level-1 bins (campaign >> rec_shift), <= REC_BINS_MAX
+    u32 rec_shift;
+    u32 rec_cap;                // records per (workgroup, bin) sub-buffer
+    u32* rec;                   // [grid][rec_bins][rec_cap]
+    u32* rec_n;                 // [grid][rec_bins] records written
 };
+
+// Record-mode pipeline after the scan (ysb_count.hip).  Level-2 bins ("blocks") are
+// L2C = 32768 / W campaigns, so a block's L2C x W cells fit one workgroup's LDS as u32.
+constexpr int REC_BINS_MAX = 64;      // level-1 bins (the scan's per-workgroup LDS cursors)
+constexpr int REC_BLOCK_CELLS = 32768;  // u32 LDS counters per count workgroup (128 KiB)
+constexpr int REC_QUARTERS = 4;       // partition workgroups per level-1 bin
+struct RecParams {
+    const u32* rec;             // the scan's sub-buffers
+    const u32* rec_n;
+    u32 grid;                   // scan workgroups
+    u32 bins;                   // level-1 bins
+    u32 cap;                    // records per sub-buffer
+    u32 sub_log2;               // level-2 blocks per level-1 bin = 1 << sub_log2
+    u32 blk_shift;              // block = campaign >> blk_shift (L2C = 1 << blk_shift)
+    u32 n_blocks;               // ceil(c_pad / L2C)
+    u32 ring_w;
+    u32 w_log2;
+    u32 c_pad;
+    u32* part;                  // partitioned records: [bins * QUARTERS][grid / QUARTERS * cap]
+    u32* runs;                  // [n_blocks][QUARTERS] {offset, count} into part
+    unsigned long long* counts; // the ring [c_pad][W]
+};
+void launch_rec_partition(const RecParams& r, hipStream_t s);
+void launch_rec_count(const RecParams& r, hipStream_t s);
 
 constexpr int N_STAMPS = 8;     // phases timed by the YSB_STAMPS diagnostic build
 

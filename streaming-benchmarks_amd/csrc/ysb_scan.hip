@@ -847,6 +847,10 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
     const u32 WL = P.lds_wl;
     const u32 ncells = WL ? P.n_campaigns * WL : 0u;
     for (u32 i = tid; i < ncells; i += SCAN_TPB) lcnt[i] = 0;
+    // record mode (no LDS window counters): the same LDS words are the cursors of this
+    // workgroup's level-1 record sub-buffers
+    if (P.rec_on)
+        for (u32 i = tid; i < P.rec_bins; i += SCAN_TPB) lcnt[i] = 0;
     // rebase requests of the LDS window (double-buffered by tile parity): the largest
     // bucket that fell ahead of the window, INT64_MIN = none
     if (tid < 2) misc64[tid] = INT64_MIN;
@@ -1028,7 +1032,20 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             }
         } else if (valid) {
 #ifndef YSB_DIAG_NO_COUNT
-            global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+            bool recorded = false;
+            if (P.rec_on) {   // record mode: the ring cell index into this workgroup's sub-buffer
+                const i64 rel = bucket - ring_lo;
+                if (ring_set && rel >= 0 && rel < (i64)P.ring_w) {
+                    const u32 bin = campaign >> P.rec_shift;
+                    const u32 pos = atomicAdd(&lcnt[bin], 1u);
+                    if (pos < P.rec_cap) {
+                        P.rec[((u64)blockIdx.x * P.rec_bins + bin) * P.rec_cap + pos] =
+                            campaign * P.ring_w + (u32)(bucket & (i64)(P.ring_w - 1));
+                        recorded = true;
+                    }
+                }
+            }
+            if (!recorded) global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
 #endif
         }
         STAMP(4);
@@ -1098,6 +1115,9 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             run_tiles();
         }
     }
+    if (P.rec_on)   // records per sub-buffer (a full one sent the rest to the atomics)
+        for (u32 i = tid; i < P.rec_bins; i += SCAN_TPB)
+            P.rec_n[(u64)blockIdx.x * P.rec_bins + i] = min(lcnt[i], P.rec_cap);
     if (n_run == 0) return;   // no segment has tiles for this workgroup (nothing touched)
 #ifdef YSB_STAMPS
     if (lane == 0) {

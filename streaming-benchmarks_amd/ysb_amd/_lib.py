@@ -23,6 +23,8 @@ YSB_F_REQUIRE_IP = 0x2
 YSB_F_NO_LDS_COUNT = 0x4
 YSB_F_SPARSE_FAST_JOIN = 0x8
 YSB_F_FORMAT_TBL = 0x10
+YSB_F_RECORD_COUNT = 0x20
+YSB_F_NO_RECORD_COUNT = 0x40
 INT64_MIN = -(1 << 63)
 UNIQUE_ID_BYTES = 128
 
@@ -86,6 +88,7 @@ SIGNATURES = {
     "ysb_ring_range": (_I, [_P, C.POINTER(_I64), C.POINTER(_U32)]),
     "ysb_ring_advance": (_I, [_P, _I64]),
     "ysb_kernel_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64)]),
+    "ysb_path_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_stream": (_P, [_P]),
     "ysb_device_alloc": (_I, [_P, _U64, C.POINTER(_P)]),
     "ysb_device_free": (_I, [_P, _P]),

@@ -24,7 +24,7 @@ class YsbContext:
     def __init__(self, device=0, n_campaigns=100, time_divisor_ms=10000, window_ring=1024,
                  max_batch_events=1 << 20, max_batch_bytes=256 << 20, ring_base_bucket=None,
                  overflow_capacity=1 << 20, timing=False, require_ip=False, lds_count=True,
-                 sparse_fast_join=False, input_format="json"):
+                 sparse_fast_join=False, input_format="json", record_count=None):
         L = lib()
         cfg = YsbConfig()
         L.ysb_config_default(C.byref(cfg))
@@ -38,7 +38,9 @@ class YsbContext:
         cfg.flags = ((_lib.YSB_F_TIMING if timing else 0) | (_lib.YSB_F_REQUIRE_IP if require_ip else 0)
                      | (0 if lds_count else _lib.YSB_F_NO_LDS_COUNT)
                      | (_lib.YSB_F_SPARSE_FAST_JOIN if sparse_fast_join else 0)
-                 | (_lib.YSB_F_FORMAT_TBL if input_format == "tbl" else 0))
+                 | (_lib.YSB_F_FORMAT_TBL if input_format == "tbl" else 0)
+                 | (0 if record_count is None else
+                    _lib.YSB_F_RECORD_COUNT if record_count else _lib.YSB_F_NO_RECORD_COUNT))
         if input_format not in ("json", "tbl"):
             raise ValueError("input_format must be 'json' or 'tbl'")
         h = C.c_void_p()
@@ -150,6 +152,14 @@ class YsbContext:
         t, k = C.c_double(), C.c_uint64()
         self._c(lib().ysb_kernel_time(self._h, C.byref(t), C.byref(k)))
         return t.value, k.value
+
+    def path_time(self):
+        """(total ms, launches, record-mode launches so far): the whole device sequence of
+        the launches the last kernel_time() call collected (scan + general path + record
+        mode's partition and count kernels)."""
+        t, k, r = C.c_double(), C.c_uint64(), C.c_uint64()
+        self._c(lib().ysb_path_time(self._h, C.byref(t), C.byref(k), C.byref(r)))
+        return t.value, k.value, r.value
 
     def stream(self):
         return lib().ysb_stream(self._h)

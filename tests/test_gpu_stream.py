@@ -108,6 +108,7 @@ def test_config3_large_tables_truth():
         st = ctx.stats()
         assert mism == 0 and truth == ring and st["join_misses"] == 0 and st["parse_errors"] == 0
         assert st["joined"] == st["views"] and st["views"] > n // 4
+        assert ctx.path_time()[2] == 1                   # counted in record mode (ysb_count.hip)
         rows = ctx.drain_buckets()
         assert sum(rows.values()) == truth
         # the first 20k events also through the CPU oracle, with the map entries they use

@@ -52,11 +52,12 @@ def submit_segments(ctx, segs, per_batch):
 
 
 def config3(args):
-    g = GenParams(seed=42, n_campaigns=1_000_000, ads_per_campaign=10, events_per_sec=100_000)
+    g = GenParams(seed=42, n_campaigns=args.campaigns, ads_per_campaign=10_000_000 // args.campaigns,
+                  events_per_sec=args.c3_rate)
     t = time.perf_counter()
     _, ab = g.ids_packed()
     # 100M events at 100k/s span 1000 s = 100 buckets: a 128-bucket ring holds them all
-    ctx = YsbContext(n_campaigns=1_000_000, window_ring=args.ring, timing=True, max_batch_bytes=1 << 20,
+    ctx = YsbContext(n_campaigns=args.campaigns, window_ring=args.ring, timing=True, max_batch_bytes=1 << 20,
                      max_batch_events=1 << 12)
     ctx.load_ad_map_packed(ab, g.ad_campaign_index_array())
     t_load = time.perf_counter() - t
@@ -90,7 +91,8 @@ def config3(args):
     st = ctx.stats()
     alg = (total_bytes + 4 * args.events) / (len(segs) if args.per_batch else 1)
     ach = alg / (kms / launches * 1e-3) / 1e9
-    return {"config": "configs[2]: 1M campaigns / 10M ads, %d events, W=%d" % (args.events, args.ring),
+    return {"config": "configs[2]: %d campaigns / 10M ads, %d events, W=%d, %d events/s of event time" % (
+                args.campaigns, args.events, args.ring, args.c3_rate),
             "events_per_s": round(args.events * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
             "batches_per_step": len(segs), "launches_per_step": len(segs) if args.per_batch else 1,
             "scan_avg_launch_ms": round(kms / launches, 4), "scan_alg_GBs": round(ach, 1),
@@ -304,6 +306,8 @@ def main():
     ap.add_argument("--seconds", type=int, default=10)
     ap.add_argument("--rate", type=int, default=1_000_000)
     ap.add_argument("--ring", type=int, default=128)
+    ap.add_argument("--campaigns", type=int, default=1_000_000, help="config3: campaigns (10M ads in all)")
+    ap.add_argument("--c3-rate", type=int, default=100_000, help="config3: events per second of event time")
     ap.add_argument("--batch-ms", type=int, default=100)
     ap.add_argument("--ooo-ms", type=int, default=100)
     args = ap.parse_args()
