@@ -175,10 +175,10 @@ class YsbContext:
 
     def h2d(self, d_dst, arr):
         arr = np.ascontiguousarray(arr)
-        self._c(lib().ysb_memcpy_h2d(self._h, C.c_void_p(d_dst), _ptr(arr), arr.nbytes))
+        self._c(lib().ysb_memcpy_h2d(self._h, C.c_void_p(int(d_dst)), _ptr(arr), arr.nbytes))
 
     def d2h(self, arr, d_src):
-        self._c(lib().ysb_memcpy_d2h(self._h, _ptr(arr), C.c_void_p(d_src), arr.nbytes))
+        self._c(lib().ysb_memcpy_d2h(self._h, _ptr(arr), C.c_void_p(int(d_src)), arr.nbytes))
         return arr
 
     # -- multi-GPU ------------------------------------------------------------------------

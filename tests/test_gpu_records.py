@@ -21,7 +21,7 @@ def counts(aids, camp, n_campaigns, raw, offs, record, ring=16, segments=1):
         else:
             d_b = ctx.device_alloc(raw.size + 64 * segments)
             d_o = ctx.device_alloc(4 * offs.size + 64)
-            cuts = np.linspace(0, offs.size, segments + 1).astype(int)
+            cuts = [int(x) for x in np.linspace(0, offs.size, segments + 1)]
             segs, pos = [], 0
             for a, b in zip(cuts[:-1], cuts[1:]):
                 lo = int(offs[a])
