@@ -555,9 +555,10 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     r.n_blocks = (u32)((c->c_pad + (1u << r.blk_shift) - 1) >> r.blk_shift);
     const u32 sub = (r.n_blocks + REC_BINS_MAX - 1) / REC_BINS_MAX;
     r.sub_log2 = log2u(sub);
-    if ((1u << r.sub_log2) > 4096u) return YSB_OK;
+    if ((1u << r.sub_log2) > (u32)REC_SUB_MAX) return YSB_OK;   // beyond 8 x 512 blocks: atomics
     r.bins = (r.n_blocks + (1u << r.sub_log2) - 1) >> r.sub_log2;
     r.grid = p.grid;
+    if ((r.grid + REC_QUARTERS - 1) / REC_QUARTERS > 128) return YSB_OK;   // REC_SLICE_MAX
     // lines one workgroup scans at most in this launch; ~1/3 are joined views on generator
     // data; 3/4 of the lines spread over the bins leaves room for skew (a full sub-buffer
     // sends the rest of its views to the atomics: slower, still exact)
@@ -566,10 +567,12 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     const u64 lines = tiles * TILE_LINES;
     u64 cap = (lines * 3 / 4 + r.bins - 1) / r.bins;
     cap = std::max<u64>(32, (cap + 31) / 32 * 32);
-    const u64 area = (u64)((r.grid + REC_QUARTERS - 1) / REC_QUARTERS) * cap;
+    // one (bin, slice) output area: the slice's sub-buffers plus a 32-record alignment pad per block
+    const u64 area = ((u64)((r.grid + REC_QUARTERS - 1) / REC_QUARTERS) * cap + 32ull * (1u << r.sub_log2) + 31) / 32 * 32;
     const u64 part = (u64)r.bins * REC_QUARTERS * area;
     if (cap > 0xFFFFFFFFull || part >= (1ull << 32)) return YSB_OK;
     r.cap = (u32)cap;
+    r.area = area;
     int rc;
     if ((rc = grow_u32(c, &c->d_rec, &c->rec_words, (u64)r.grid * r.bins * cap))) return rc;
     if ((rc = grow_u32(c, &c->d_rec_n, &c->rec_n_words, (u64)r.grid * r.bins))) return rc;
@@ -581,6 +584,7 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     r.runs = c->d_runs;
     r.counts = c->d_counts;
     p.rec_on = 1;
+    p.probe_serial = 1;   // the record-mode kernels are the HBM-table (serial probe) instantiations
     p.rec_bins = r.bins;
     p.rec_shift = r.blk_shift + r.sub_log2;
     p.rec_cap = r.cap;

@@ -8,11 +8,14 @@
 // atomics"), and config 3's 33M views per 100M events took 2.4 ms of a 6.9 ms launch.
 // Record mode sums them first:
 //
-//   scan_kernel   a joined in-ring view appends its ring cell index (u32) to the
-//                 sub-buffer of (its workgroup, campaign >> rec_shift) -- 64 level-1
-//                 bins, LDS cursors, plain stores that fill whole lines in L2;
-//   partition     per level-1 bin (x4 quarters of the scan workgroups): LDS histogram
-//                 over the bin's level-2 blocks, prefix, scatter into contiguous runs;
+//   scan_kernel   a joined in-ring view appends its ring cell index (u32) to a 64-record
+//                 LDS ring of its level-1 bin (campaign >> rec_shift, 8 bins); every full
+//                 32-record line goes to the (workgroup, bin) HBM sub-buffer as ONE 128-B
+//                 store (a partial-line store costs a memory write of its own: scattered
+//                 4-B stores were as slow as the atomics, tools/mb_scatter.hip);
+//   partition     per (level-1 bin, slice of the scan workgroups): LDS histogram over the
+//                 bin's level-2 blocks, 32-aligned runs, records staged per block in LDS
+//                 rings and written out as whole lines;
 //   count         per level-2 block (32768 / W campaigns, whose L2C x W cells are one
 //                 contiguous slab of the campaign-major ring): LDS u32 counters, then
 //                 every non-zero cell added to the ring ONCE with a plain load/add/store
@@ -25,35 +28,71 @@
 namespace ysb {
 
 constexpr int REC_TPB = 1024;
-constexpr u32 REC_SUB_MAX = 4096;   // level-2 blocks per level-1 bin (host keeps it below)
+constexpr int REC_WAVES = REC_TPB / 64;
+constexpr int REC_UNROLL = 8;        // records in flight per lane (loads issued together)
+constexpr u32 REC_NONE = 0xFFFFFFFFu;
 
+// One partition workgroup: level-1 bin b, the sub-buffers of scan workgroups
+// [w_lo, w_hi) (one of REC_QUARTERS slices).  Each wave walks its own sub-buffers (wave,
+// wave + 16, ...) 512 records per round, 8 loads in flight per lane.  Sweep 1 counts
+// the records per level-2 block; each block's run starts 32-record aligned in this
+// workgroup's output area.  Sweep 2 stages every record in its block's 64-record LDS ring
+// (a record arriving when its ring is full goes straight to its final slot) and after
+// every round each block's full 128-B lines are written out by one thread.
 __global__ __launch_bounds__(REC_TPB) void rec_partition_kernel(const RecParams R) {
+    __shared__ __attribute__((aligned(16))) u32 stage[REC_SUB_MAX * REC_RING];
     __shared__ u32 hist[REC_SUB_MAX];
+    __shared__ u32 boff[REC_SUB_MAX];
     __shared__ u32 cur[REC_SUB_MAX];
+    __shared__ u32 fl[REC_SUB_MAX];
+    __shared__ u32 rounds_sh;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u32 b = blockIdx.x / REC_QUARTERS, q = blockIdx.x % REC_QUARTERS;
     const u32 S = 1u << R.sub_log2;
-    for (u32 i = tid; i < S; i += REC_TPB) hist[i] = 0;
-    __syncthreads();
+    for (u32 i = tid; i < S; i += REC_TPB) { hist[i] = 0; cur[i] = 0; fl[i] = 0; }
+    if (tid == 0) rounds_sh = 0;
     const u32 w_lo = (u32)((u64)q * R.grid / REC_QUARTERS), w_hi = (u32)((u64)(q + 1) * R.grid / REC_QUARTERS);
     const u32 first_blk = b << R.sub_log2;
     const u32 sh = R.w_log2 + R.blk_shift;   // cell -> block
-    // sweep 1: level-2 histogram (one wave per sub-buffer)
-    for (u32 w = w_lo + wave; w < w_hi; w += REC_TPB / 64) {
-        const u64 sb = (u64)w * R.bins + b;
-        const u32 n = R.rec_n[sb];
-        const u32* src = R.rec + sb * R.cap;
-        for (u32 i = lane; i < n; i += 64) atomicAdd(&hist[(src[i] >> sh) - first_blk], 1u);
+    constexpr u32 CH = 64 * REC_UNROLL;      // records per wave and round
+    // this wave's rounds: its sub-buffers in chunks of CH
+    u32 my_rounds = 0;
+    for (u32 w = w_lo + wave; w < w_hi; w += REC_WAVES) my_rounds += (R.rec_n[(u64)w * R.bins + b] + CH - 1) / CH;
+    __syncthreads();
+    if (lane == 0) atomicMax(&rounds_sh, my_rounds);
+    // cursor over this wave's sub-buffers: (sub-buffer, offset)
+    u32 cw = w_lo + wave, coff = 0, cn = cw < w_hi ? R.rec_n[(u64)cw * R.bins + b] : 0u;
+    auto next_chunk = [&](u32 (&v)[REC_UNROLL]) {
+        while (cw < w_hi && coff >= cn) {
+            cw += REC_WAVES;
+            coff = 0;
+            cn = cw < w_hi ? R.rec_n[(u64)cw * R.bins + b] : 0u;
+        }
+        const u32* src = R.rec + ((u64)(cw < w_hi ? cw : w_lo) * R.bins + b) * R.cap;
+#pragma unroll
+        for (int u = 0; u < REC_UNROLL; ++u) {
+            const u32 i = coff + u * 64 + lane;
+            v[u] = (cw < w_hi && i < cn) ? src[i] : REC_NONE;
+        }
+        coff += CH;
+    };
+    // sweep 1: per-block histogram
+    for (u32 r = 0; r < my_rounds; ++r) {
+        u32 v[REC_UNROLL];
+        next_chunk(v);
+#pragma unroll
+        for (int u = 0; u < REC_UNROLL; ++u)
+            if (v[u] != REC_NONE) atomicAdd(&hist[(v[u] >> sh) - first_blk], 1u);
     }
     __syncthreads();
-    // exclusive prefix over the S blocks: wave 0, each lane a chunk
-    const u64 area = (u64)((R.grid + REC_QUARTERS - 1) / REC_QUARTERS) * R.cap;
-    const u64 base = ((u64)b * REC_QUARTERS + q) * area;
+    const u32 rounds = rounds_sh;
+    // block runs: 32-record aligned offsets in this workgroup's area
+    const u64 base = ((u64)b * REC_QUARTERS + q) * R.area;
     if (wave == 0) {
         const u32 per = (S + 63) / 64;
         const u32 k0 = min(S, lane * per), k1 = min(S, k0 + per);
         u32 sum = 0;
-        for (u32 k = k0; k < k1; ++k) sum += hist[k];
+        for (u32 k = k0; k < k1; ++k) sum += (hist[k] + 31u) & ~31u;
         u32 incl = sum;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -62,51 +101,132 @@ __global__ __launch_bounds__(REC_TPB) void rec_partition_kernel(const RecParams 
         }
         u32 run = incl - sum;
         for (u32 k = k0; k < k1; ++k) {
-            const u32 h = hist[k];
-            cur[k] = run;
+            boff[k] = run;
             const u32 blk = first_blk + k;
             if (blk < R.n_blocks) {
                 R.runs[((u64)blk * REC_QUARTERS + q) * 2] = (u32)(base + run);
-                R.runs[((u64)blk * REC_QUARTERS + q) * 2 + 1] = h;
+                R.runs[((u64)blk * REC_QUARTERS + q) * 2 + 1] = hist[k];
             }
-            run += h;
+            run += (hist[k] + 31u) & ~31u;
         }
     }
     __syncthreads();
-    // sweep 2: scatter into the blocks' runs
     u32* out = R.part + base;
-    for (u32 w = w_lo + wave; w < w_hi; w += REC_TPB / 64) {
-        const u64 sb = (u64)w * R.bins + b;
-        const u32 n = R.rec_n[sb];
-        const u32* src = R.rec + sb * R.cap;
-        for (u32 i = lane; i < n; i += 64) {
-            const u32 cell = src[i];
-            out[atomicAdd(&cur[(cell >> sh) - first_blk], 1u)] = cell;
+    // writes staged positions [fl, fl + n) of block k (n <= 32: one line or a tail)
+    auto write_line = [&](u32 k, u32 n) {
+        const u32 f = fl[k];
+        u32* dst = out + boff[k] + f;
+        const u32* src = stage + k * REC_RING;
+        if (n == 32 && (f & 31u) == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const u32 o = (f + 4 * j) & (REC_RING - 1);
+                reinterpret_cast<uint4*>(dst)[j] = make_uint4(src[o], src[o + 1], src[o + 2], src[o + 3]);
+            }
+        } else {
+            for (u32 j = 0; j < n; ++j) dst[j] = src[(f + j) & (REC_RING - 1)];
         }
+        fl[k] = f + n;
+    };
+    // sweep 2: stage + write full lines, every wave one chunk per round
+    cw = w_lo + wave;
+    coff = 0;
+    cn = cw < w_hi ? R.rec_n[(u64)cw * R.bins + b] : 0u;
+    for (u32 r = 0; r < rounds; ++r) {
+        if (r < my_rounds) {
+            u32 v[REC_UNROLL];
+            next_chunk(v);
+#pragma unroll
+            for (int u = 0; u < REC_UNROLL; ++u) {
+                if (v[u] == REC_NONE) continue;
+                const u32 k = (v[u] >> sh) - first_blk;
+                const u32 pos = atomicAdd(&cur[k], 1u);
+                if (pos - fl[k] < (u32)REC_RING) stage[k * REC_RING + (pos & (REC_RING - 1))] = v[u];
+                else out[boff[k] + pos] = v[u];   // its ring is full this round: straight to its slot
+            }
+        }
+        __syncthreads();
+        for (u32 k = tid; k < S; k += REC_TPB) {
+            const u32 f0 = fl[k], c = cur[k];
+            // staged this round: positions [f0, f0 + 64); beyond that they went direct
+            const u32 lines = min(c - f0, (u32)REC_RING) / 32;
+            for (u32 l = 0; l < lines; ++l) write_line(k, 32);
+            if (c - f0 > (u32)REC_RING) fl[k] = c;   // direct positions are written already
+        }
+        __syncthreads();
     }
+    for (u32 k = tid; k < S; k += REC_TPB)   // tails
+        if (cur[k] > fl[k]) write_line(k, cur[k] - fl[k]);
 }
 
+// One count workgroup: level-2 block j (campaigns [j*L2C, (j+1)*L2C), the slab of
+// L2C x W ring cells).  The block's QUARTERS runs flattened, 8 records per lane in flight
+// -> LDS u32 counters; then the slab is read, added to and written back whole (16-B
+// accesses, all issued before any is used: the sweep is a stream, not a chain of
+// dependent loads; whole lines written back, no partial-line writes).
 __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
     __shared__ __attribute__((aligned(16))) u32 cnt[REC_BLOCK_CELLS];
+    __shared__ u32 roff[REC_QUARTERS + 1];
+    __shared__ u32 rbeg[REC_QUARTERS];
     const u32 tid = threadIdx.x;
     const u32 j = blockIdx.x;
     const u32 c0 = j << R.blk_shift;
     const u32 nc = min(1u << R.blk_shift, R.c_pad - c0);
     const u32 cells = nc << R.w_log2;            // <= REC_BLOCK_CELLS, a multiple of 16
     for (u32 i = tid; i < cells / 4; i += REC_TPB) reinterpret_cast<uint4*>(cnt)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    const u32 base_cell = c0 << R.w_log2;
-    for (u32 q = 0; q < (u32)REC_QUARTERS; ++q) {
-        const u32 off = R.runs[((u64)j * REC_QUARTERS + q) * 2];
-        const u32 n = R.runs[((u64)j * REC_QUARTERS + q) * 2 + 1];
-        const u32* src = R.part + off;
-        for (u32 i = tid; i < n; i += REC_TPB) atomicAdd(&cnt[src[i] - base_cell], 1u);
+    if (tid < 64) {   // the runs' sizes, prefix
+        const u32 n = tid < (u32)REC_QUARTERS ? R.runs[((u64)j * REC_QUARTERS + tid) * 2 + 1] : 0u;
+        if (tid < (u32)REC_QUARTERS) rbeg[tid] = R.runs[((u64)j * REC_QUARTERS + tid) * 2];
+        u32 incl = n;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(incl, o, 64);
+            if ((int)tid >= o) incl += y;
+        }
+        if (tid < (u32)REC_QUARTERS) roff[tid] = incl - n;
+        if (tid == (u32)REC_QUARTERS - 1) roff[REC_QUARTERS] = incl;
     }
     __syncthreads();
-    unsigned long long* ring = R.counts + base_cell;
-    for (u32 i = tid; i < cells; i += REC_TPB) {
-        const u32 v = cnt[i];
-        if (v) ring[i] += v;
+    const u32 total = roff[REC_QUARTERS];
+    const u32 base_cell = c0 << R.w_log2;
+    for (u32 i0 = 0; i0 < total; i0 += REC_TPB * REC_UNROLL) {
+        u32 v[REC_UNROLL];
+#pragma unroll
+        for (int u = 0; u < REC_UNROLL; ++u) {
+            const u32 i = i0 + u * REC_TPB + tid;
+            v[u] = REC_NONE;
+            if (i < total) {
+                u32 qq = 0;
+                while (qq + 1 < (u32)REC_QUARTERS && roff[qq + 1] <= i) ++qq;
+                v[u] = R.part[rbeg[qq] + (i - roff[qq])];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < REC_UNROLL; ++u)
+            if (v[u] != REC_NONE) atomicAdd(&cnt[v[u] - base_cell], 1u);
+    }
+    __syncthreads();
+    // the slab: [base_cell, base_cell + cells) u64, as 16-B pairs
+    uint4* ring = reinterpret_cast<uint4*>(R.counts + base_cell);
+    const u32 pairs = cells / 2;
+    constexpr int SU = 8;
+    for (u32 p0 = 0; p0 < pairs; p0 += REC_TPB * SU) {
+        uint4 r[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+            const u32 p = p0 + u * REC_TPB + tid;
+            if (p < pairs) r[u] = ring[p];
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+            const u32 p = p0 + u * REC_TPB + tid;
+            if (p < pairs) {
+                const uint2 c = reinterpret_cast<const uint2*>(cnt)[p];
+                unsigned long long lo = ((unsigned long long)r[u].y << 32 | r[u].x) + c.x;
+                unsigned long long hi = ((unsigned long long)r[u].w << 32 | r[u].z) + c.y;
+                ring[p] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
+            }
+        }
     }
 }
 

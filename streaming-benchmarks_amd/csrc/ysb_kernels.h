@@ -44,7 +44,11 @@ constexpr int MAX_TILES_PER_BLOCK = YSB_MAX_TILES;   // tile bounds preloaded in
 
 // Per-input-format geometry of the scan kernel: tile capacity, prefetch registers and
 // the LDS carve (tile | slack | window counters | misc | tile bounds).
-template <bool TBL>
+// Record mode (REC): the window-counter area holds the record staging lines instead --
+// REC_BINS_MAX level-1 bins x a 64-record ring each (2 KiB).
+constexpr int REC_BINS_MAX = 8;       // level-1 bins of the scan's record staging
+constexpr int REC_RING = 64;          // staged records per bin (two 128-B lines)
+template <bool TBL, bool REC = false>
 struct Geom {
     static constexpr int WG_PER_CU = TBL ? YSB_TBL_WG_PER_CU : SCAN_WG_PER_CU;
     static constexpr int CAP = TILE_LINES * (TBL ? YSB_TBL_LINE_BYTES : YSB_TILE_LINE_BYTES);
@@ -52,7 +56,8 @@ struct Geom {
     static constexpr int CPT = (CHUNKS + SCAN_TPB - 1) / SCAN_TPB;   // 16-byte chunks per thread
     static constexpr int OFF_TILE = 0;
     static constexpr int OFF_LCNT = OFF_TILE + CAP + 64;             // 64 B slack for reads past a tile
-    static constexpr int OFF_MISC = OFF_LCNT + LCNT_CAP * 4;
+    static constexpr int LCNT_BYTES = REC ? REC_BINS_MAX * REC_RING * 4 : LCNT_CAP * 4;
+    static constexpr int OFF_MISC = OFF_LCNT + LCNT_BYTES;
     static constexpr int OFF_TB = OFF_MISC + 64;
     static constexpr int LDS = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
     static_assert(OFF_LCNT % 16 == 0 && OFF_MISC % 16 == 0 && OFF_TB % 16 == 0, "LDS carve must stay 16-byte aligned");
@@ -136,9 +141,12 @@ struct ScanParams {
 
 // Record-mode pipeline after the scan (ysb_count.hip).  Level-2 bins ("blocks") are
 // L2C = 32768 / W campaigns, so a block's L2C x W cells fit one workgroup's LDS as u32.
-constexpr int REC_BINS_MAX = 64;      // level-1 bins (the scan's per-workgroup LDS cursors)
+// Every stage writes whole 128-B lines from LDS staging: a partial-line store costs a
+// memory write of its own (the XCD L2s are write-through for stores), which made scattered
+// 4-B record stores as slow as the atomics they replace (tools/mb_scatter.hip).
 constexpr int REC_BLOCK_CELLS = 32768;  // u32 LDS counters per count workgroup (128 KiB)
-constexpr int REC_QUARTERS = 4;       // partition workgroups per level-1 bin
+constexpr int REC_QUARTERS = 32;      // partition workgroups per level-1 bin (each a slice of the scan workgroups)
+constexpr int REC_SUB_MAX = 512;      // level-2 blocks per level-1 bin (the partition's staging rings)
 struct RecParams {
     const u32* rec;             // the scan's sub-buffers
     const u32* rec_n;
@@ -151,7 +159,8 @@ struct RecParams {
     u32 ring_w;
     u32 w_log2;
     u32 c_pad;
-    u32* part;                  // partitioned records: [bins * QUARTERS][grid / QUARTERS * cap]
+    u64 area;                   // u32 words of one (bin, quarter) output area
+    u32* part;                  // partitioned records: [bins * QUARTERS][area], runs 32-record aligned
     u32* runs;                  // [n_blocks][QUARTERS] {offset, count} into part
     unsigned long long* counts; // the ring [c_pad][W]
 };

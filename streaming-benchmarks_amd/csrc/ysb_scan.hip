@@ -709,6 +709,15 @@ constexpr int AUX_NT = YSB_AUX_NT;
 #ifndef YSB_SETPRIO
 #define YSB_SETPRIO 1
 #endif
+#ifndef YSB_PROBE_NT
+#define YSB_PROBE_NT 0
+#endif
+
+__device__ __forceinline__ uint4 nt_load4(const uint4* p) {
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
 #ifndef YSB_PREFETCH_DEPTH
 #define YSB_PREFETCH_DEPTH 1
 #endif
@@ -819,13 +828,47 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #define STAMP(i) do { } while (0)
 #endif
 
-// SERIAL: probe the second cuckoo slot only after a first-slot miss (HBM-resident table);
-// a separate instantiation so the cache-resident configuration's code is untouched.
-// SERIAL: HBM-resident cuckoo table, second slot probed only after a first-slot miss.
-// TBL: the fork's .tbl rows (tbl_stage1/2) instead of JSON lines (canon_stage1/2).
-template <bool SERIAL, bool TBL>
+// Record mode: ring cell index -> (campaign, bucket) for the atomic fallback (a record the
+// workgroup's full HBM sub-buffer cannot take).
+__device__ __forceinline__ void rec_fallback(const ScanParams& P, u32 cell, i64 ring_lo, bool ring_set, Tally& tl) {
+    const u32 wl2 = 31u - (u32)__builtin_clz(P.ring_w);
+    const u32 c = cell >> wl2;
+    const i64 slot = (i64)(cell & (P.ring_w - 1));
+    const i64 b = ring_lo + ((slot - ring_lo) & (i64)(P.ring_w - 1));
+    global_add(P, ring_lo, ring_set, c, b, 1u, tl);
+}
+
+// Record mode: writes every staged full 32-record line (final: also the partial tails) of
+// the workgroup's level-1 bins to its HBM sub-buffers -- one 128-B store by lanes 0..31
+// per line.  rcur / rfl / the ring live in LDS, gcur in lane b of a VGPR; one wave.
+__device__ __forceinline__ void rec_flush_full(const ScanParams& P, u32* ring, u32* rcur, u32* rfl, u32& gcur,
+                                               int lane, i64 ring_lo, bool ring_set, bool final, Tally& tl) {
+    const u32 nb = P.rec_bins;
+    const u32 need = final ? 1u : 32u;
+    u64 full = __ballot(lane < (int)nb && rcur[lane] - rfl[lane] >= need);
+    while (full) {
+        const u32 b = (u32)__builtin_ctzll(full);
+        const u32 fl = rfl[b];
+        const u32 k = min(rcur[b] - fl, 32u);
+        const u32 g = (u32)__builtin_amdgcn_readlane((int)gcur, (int)b);
+        if ((u32)lane < k) {
+            const u32 v = ring[b * REC_RING + ((fl + lane) & (REC_RING - 1))];
+            if (g + k <= P.rec_cap) P.rec[((u64)blockIdx.x * nb + b) * P.rec_cap + g + lane] = v;
+            else rec_fallback(P, v, ring_lo, ring_set, tl);
+        }
+        if (g + k <= P.rec_cap && lane == (int)b) gcur = g + k;
+        if (lane == 0) rfl[b] = fl + k;
+        if (rcur[b] - (fl + k) < need) full &= full - 1;
+    }
+}
+
+// SERIAL: HBM-resident cuckoo table, second slot probed only after a first-slot miss (a
+// separate instantiation so the cache-resident configuration's code is untouched).
+// TBL: the fork's .tbl rows (tbl_stage1/2) instead of JSON lines (vocab_stage1/2).
+// REC: record mode (ysb_count.hip): in-ring joined views become ring-cell records.
+template <bool SERIAL, bool TBL, bool REC>
 __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<TBL>::WG_PER_CU * SCAN_TPB + 255) / 256))) void scan_kernel(const ScanParams P0) {
-    using G = Geom<TBL>;
+    using G = Geom<TBL, REC>;
     constexpr int CPT = G::CPT;
     extern __shared__ __attribute__((aligned(16))) u8 smem[];
     u32* tile32 = reinterpret_cast<u32*>(smem + G::OFF_TILE);
@@ -847,13 +890,17 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
     const u32 WL = P.lds_wl;
     const u32 ncells = WL ? P.n_campaigns * WL : 0u;
     for (u32 i = tid; i < ncells; i += SCAN_TPB) lcnt[i] = 0;
-    // record mode (no LDS window counters): the same LDS words are the cursors of this
-    // workgroup's level-1 record sub-buffers
-    if (P.rec_on)
-        for (u32 i = tid; i < P.rec_bins; i += SCAN_TPB) lcnt[i] = 0;
+    // record mode (no LDS window counters): the counter area holds a 64-record staging ring
+    // per level-1 bin (lcnt), the misc area the rings' cursors: rcur[b] = records staged,
+    // rfl[b] = records written out (multiples of 32 until the final flush); lane b of gcur
+    // = records of bin b in this workgroup's HBM sub-buffer
+    u32* rcur = reinterpret_cast<u32*>(misc64);
+    u32* rfl = rcur + REC_BINS_MAX;
+    u32 gcur = 0;
+    if (REC && tid < 2 * REC_BINS_MAX) rcur[tid] = 0;
     // rebase requests of the LDS window (double-buffered by tile parity): the largest
     // bucket that fell ahead of the window, INT64_MIN = none
-    if (tid < 2) misc64[tid] = INT64_MIN;
+    if (!REC && tid < 2) misc64[tid] = INT64_MIN;
 
     Tally tl{0, 0, 0, 0, 0, 0, 0};
     // Prefetch depth: tile t + PF_DEPTH is issued once tile t sits in LDS.  Depth 2 keeps
@@ -917,7 +964,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         }
         STAMP(0);
         __syncthreads();
-        if (tid == 0) misc64[par ^ 1] = INT64_MIN;   // every thread has read it
+        if (!REC && tid == 0) misc64[par ^ 1] = INT64_MIN;   // every thread has read it (REC: the ring cursors live there)
         STAMP(1);
 #ifdef YSB_DIAG_A_ONLY
         inf = t + PF_DEPTH < t_end ? tile_info<G::CAP>(P, t + PF_DEPTH, t_begin, tb) : none;
@@ -963,7 +1010,14 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         if (pend) {
             u32 ia, ib;
             cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
-            a0 = ct4[CSLOT_Q * (u64)ia]; a1 = ct4[CSLOT_Q * (u64)ia + 1]; a2 = ct4[CSLOT_Q * (u64)ia + 2];
+#if YSB_PROBE_NT
+            if constexpr (SERIAL) {   // HBM-resident table: the probe lines are never reused
+                a0 = nt_load4(&ct4[CSLOT_Q * (u64)ia]);
+                a1 = nt_load4(&ct4[CSLOT_Q * (u64)ia + 1]);
+                a2 = nt_load4(&ct4[CSLOT_Q * (u64)ia + 2]);
+            } else
+#endif
+            { a0 = ct4[CSLOT_Q * (u64)ia]; a1 = ct4[CSLOT_Q * (u64)ia + 1]; a2 = ct4[CSLOT_Q * (u64)ia + 2]; }
             ib_s = ib;
             if constexpr (!SERIAL) {
                 b0 = ct4[CSLOT_Q * (u64)ib]; b1 = ct4[CSLOT_Q * (u64)ib + 1]; b2 = ct4[CSLOT_Q * (u64)ib + 2];
@@ -987,6 +1041,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         // ---- Phase B2: join result ------------------------------------------------
         bool valid = false, dfr2 = false;
         u32 campaign = 0;
+#ifndef YSB_DIAG_NO_PROBE2
         if (SERIAL && pend) {   // the second slot only when the first does not hold the key
             const u32* k = ca.kw;
             const u32 da0 = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
@@ -995,6 +1050,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 b0 = ct4[CSLOT_Q * (u64)ib_s]; b1 = ct4[CSLOT_Q * (u64)ib_s + 1]; b2 = ct4[CSLOT_Q * (u64)ib_s + 2];
             }
         }
+#endif
         if (pend) {
             const u32* k = ca.kw;
             const u32 da = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
@@ -1020,6 +1076,8 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         if (P.ctable_partial) defer_append(P, dfr2, P.line_base + cur.first + li, lane);
         STAMP(3);
         // ---- count: LDS window counters; events outside go straight to the ring -----
+        bool rec_has = false;
+        u32 rec_bin = 0, rec_val = 0;
         if (WL) {
             if (valid) {
                 const i64 rel = bucket - lbase;
@@ -1032,21 +1090,32 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             }
         } else if (valid) {
 #ifndef YSB_DIAG_NO_COUNT
-            bool recorded = false;
-            if (P.rec_on) {   // record mode: the ring cell index into this workgroup's sub-buffer
+            if constexpr (REC) {
                 const i64 rel = bucket - ring_lo;
-                if (ring_set && rel >= 0 && rel < (i64)P.ring_w) {
-                    const u32 bin = campaign >> P.rec_shift;
-                    const u32 pos = atomicAdd(&lcnt[bin], 1u);
-                    if (pos < P.rec_cap) {
-                        P.rec[((u64)blockIdx.x * P.rec_bins + bin) * P.rec_cap + pos] =
-                            campaign * P.ring_w + (u32)(bucket & (i64)(P.ring_w - 1));
-                        recorded = true;
-                    }
+                if (ring_set && rel >= 0 && rel < (i64)P.ring_w) {   // in the ring: a record
+                    rec_has = true;
+                    rec_bin = campaign >> P.rec_shift;
+                    rec_val = campaign * P.ring_w + (u32)(bucket & (i64)(P.ring_w - 1));
+                } else {
+                    global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
                 }
+            } else {
+                global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
             }
-            if (!recorded) global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
 #endif
+        }
+        if constexpr (REC) {
+            // stage this tile's records, a 32-lane half at a time (a half adds <= 32 to a
+            // bin whose ring holds < 32 unwritten ones: the 64-record ring never overflows),
+            // each followed by writing out every full 128-B line
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                if (rec_has && (tid >> 5) == half) {
+                    const u32 pos = atomicAdd(&rcur[rec_bin], 1u);
+                    lcnt[rec_bin * REC_RING + (pos & (REC_RING - 1))] = rec_val;
+                }
+                rec_flush_full(P, lcnt, rcur, rfl, gcur, lane, ring_lo, ring_set, false, tl);
+            }
         }
         STAMP(4);
         __syncthreads();
@@ -1115,9 +1184,10 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             run_tiles();
         }
     }
-    if (P.rec_on)   // records per sub-buffer (a full one sent the rest to the atomics)
-        for (u32 i = tid; i < P.rec_bins; i += SCAN_TPB)
-            P.rec_n[(u64)blockIdx.x * P.rec_bins + i] = min(lcnt[i], P.rec_cap);
+    if constexpr (REC) {   // the staged tails (partial lines), then the records per sub-buffer
+        rec_flush_full(P, lcnt, rcur, rfl, gcur, lane, ring_lo, ring_set, true, tl);
+        if (tid < (int)P.rec_bins) P.rec_n[(u64)blockIdx.x * P.rec_bins + tid] = gcur;
+    }
     if (n_run == 0) return;   // no segment has tiles for this workgroup (nothing touched)
 #ifdef YSB_STAMPS
     if (lane == 0) {
@@ -1353,12 +1423,15 @@ void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s) {
 void launch_scan(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
     const dim3 g(p.grid), b(SCAN_TPB);
+    // record mode only with HBM-resident tables (large configurations: serial probes)
     if (p.tbl) {
-        if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, true>), g, b, Geom<true>::LDS, s, p);
-        else hipLaunchKernelGGL((scan_kernel<false, true>), g, b, Geom<true>::LDS, s, p);
+        if (p.rec_on) hipLaunchKernelGGL((scan_kernel<true, true, true>), g, b, (Geom<true, true>::LDS), s, p);
+        else if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, true, false>), g, b, Geom<true>::LDS, s, p);
+        else hipLaunchKernelGGL((scan_kernel<false, true, false>), g, b, Geom<true>::LDS, s, p);
     } else {
-        if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false>), g, b, Geom<false>::LDS, s, p);
-        else hipLaunchKernelGGL((scan_kernel<false, false>), g, b, Geom<false>::LDS, s, p);
+        if (p.rec_on) hipLaunchKernelGGL((scan_kernel<true, false, true>), g, b, (Geom<false, true>::LDS), s, p);
+        else if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false, false>), g, b, Geom<false>::LDS, s, p);
+        else hipLaunchKernelGGL((scan_kernel<false, false, false>), g, b, Geom<false>::LDS, s, p);
     }
 }
 
