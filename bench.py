@@ -315,7 +315,7 @@ def extras(args, device):
         segs = gen_segments(ctx, g, 100_000_000, 12_500_000)
         r = timed_extra("configs[2]: 100M JSON events, 1M campaigns x 10 ads (10M-ad join table and "
                         "1M x 128-bucket count ring in HBM)", ctx, g, segs, args.extra_steps, args.warmup,
-                        "ysb::scan_kernel<true, false>")
+                        "ysb::scan_kernel<true, false, true>")
         r["ad_map_load_s"] = round(load_s, 2)
         out["config3"] = r
         free_segments(ctx, segs)
@@ -328,9 +328,26 @@ def extras(args, device):
         segs = gen_segments(ctx, g, 100_000_000, 12_500_000)
         out["tbl"] = timed_extra("configs[1]'s 100M events as the fork's .tbl rows (MockWindowedFlatMap, "
                                  "AdvertisingTopologyNative.java:197-226)", ctx, g, segs, args.extra_steps,
-                                 args.warmup, "ysb::scan_kernel<false, true>")
+                                 args.warmup, "ysb::scan_kernel<false, true, false>")
         free_segments(ctx, segs)
     log("extras: tbl %.2f G events/s" % (out["tbl"]["events_per_s"] / 1e9))
+    # the same events as other producers would write them: off the vocabulary fast path,
+    # taken by the scan's canonical tiers (ysb_scan.hip canon_stage1/2)
+    from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP
+    for key, variant, what in (("tier2_random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
+                                "random dotted-quad ip_address and 8 ad_types (second tier)"),
+                               ("tier3_compact_json", GEN_COMPACT, "compact JSON, no space after ':' and ',' "
+                                                                   "(third tier)")):
+        g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, variant=variant)
+        _, aids = g.ids()
+        with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True,
+                        max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
+            ctx.load_ad_map(aids, g.ad_campaign_index())
+            segs = gen_segments(ctx, g, 100_000_000, args.segment)
+            out[key] = timed_extra("configs[1]'s 100M events, " + what, ctx, g, segs, args.extra_steps,
+                                   args.warmup, "ysb::scan_kernel<false, false, false>")
+            free_segments(ctx, segs)
+        log("extras: %s %.2f G events/s" % (key, out[key]["events_per_s"] / 1e9))
     return out
 
 
@@ -508,7 +525,7 @@ def main():
                        else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "ysb::scan_kernel<false, false>", "avg_launch_ms": round(avg_launch_ms, 4),
+                         "kernel": "ysb::scan_kernel<false, false, false>", "avg_launch_ms": round(avg_launch_ms, 4),
                          "alg_bytes_per_launch": int(alg_bytes_launch)},
             "cpu_baseline": cpu,
             "check": check,

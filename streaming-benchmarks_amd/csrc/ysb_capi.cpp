@@ -1229,11 +1229,13 @@ static GenSpec spec_of(const ysb_gen_params* p, const u32* subset) {
     s.subset = subset;
     s.n_pick = subset ? p->n_ad_subset : p->n_campaigns * p->ads_per_campaign;
     s.tbl = p->format == YSB_GEN_TBL;
+    s.variant = p->variant;
     return s;
 }
 
 static bool gen_ok(const ysb_gen_params* p) {
     return p && p->n_campaigns && p->ads_per_campaign && p->events_per_sec && p->format <= YSB_GEN_TBL &&
+           p->variant <= (YSB_GEN_RANDOM_IP | YSB_GEN_MORE_AD_TYPES | YSB_GEN_COMPACT) &&
            (!p->ad_subset || p->n_ad_subset) && (u64)p->n_campaigns * p->ads_per_campaign < (1ull << 32);
 }
 
@@ -1253,7 +1255,7 @@ int ysb_gen_ids(const ysb_gen_params* p, char* campaign_ids, char* ad_ids) {
     return YSB_OK;
 }
 
-uint64_t ysb_gen_max_line_bytes(const ysb_gen_params*) { return (u64)LINE_FIXED + 16 + 8 + 20; }
+uint64_t ysb_gen_max_line_bytes(const ysb_gen_params*) { return (u64)LINE_FIXED + 16 + 8 + 20 + 8; }
 
 int ysb_gen_events_host(const ysb_gen_params* p, uint64_t first, uint64_t n, uint8_t* out, uint64_t cap,
                         uint32_t* line_off, uint64_t* nbytes) {

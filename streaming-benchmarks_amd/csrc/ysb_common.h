@@ -76,9 +76,10 @@ enum { LEN_P0 = 13, LEN_P1 = 15, LEN_P2 = 13, LEN_P3 = 15, LEN_P4 = 18, LEN_P5 =
 enum { LINE_FIXED = LEN_P0 + LEN_P1 + LEN_P2 + LEN_P3 + LEN_P4 + LEN_P5 + LEN_P6 + 3 * 36 + 1 };  // 228
 
 YSB_HD const char* ad_type_str(u32 k) {
-    return k == 0 ? "banner" : k == 1 ? "modal" : k == 2 ? "sponsored-search" : k == 3 ? "mail" : "mobile";
+    return k == 0 ? "banner" : k == 1 ? "modal" : k == 2 ? "sponsored-search" : k == 3 ? "mail" : k == 4 ? "mobile"
+         : k == 5 ? "native-video" : k == 6 ? "interstitial" : "rewarded";
 }
-YSB_HD u32 ad_type_len(u32 k) { return k == 0 ? 6 : k == 1 ? 5 : k == 2 ? 16 : k == 3 ? 4 : 6; }
+YSB_HD u32 ad_type_len(u32 k) { return k == 0 ? 6 : k == 1 ? 5 : k == 2 ? 16 : k == 3 ? 4 : k == 4 ? 6 : k == 5 ? 12 : k == 6 ? 12 : 8; }
 YSB_HD const char* event_type_str(u32 k) { return k == 0 ? "view" : k == 1 ? "click" : "purchase"; }
 YSB_HD u32 event_type_len(u32 k) { return k == 0 ? 4 : k == 1 ? 5 : 8; }
 
@@ -93,7 +94,17 @@ struct GenSpec {
     const u32* subset;   // ad indices to draw from (nullptr: all)
     u32 n_pick;          // number of ads drawn from
     u32 tbl;             // 1: the fork's .tbl rows instead of JSON lines
+    u32 variant;         // GEN_V_* layout variants of the JSON lines (parity / tier tests)
 };
+
+// Off-vocabulary layouts of the same events (the generator's own stream is variant 0):
+// other producers' lines that the vocabulary fast path does not take.
+enum : u32 {
+    GEN_V_RANDOM_IP = 1u,      // ip_address a random dotted quad instead of "1.2.3.4"
+    GEN_V_MORE_AD_TYPES = 2u,  // ad_type one of 8 (adds native-video / interstitial / rewarded)
+    GEN_V_COMPACT = 4u,        // no space after ':' and ',' (compact JSON)
+};
+enum : u32 { S_IP = 9 };
 
 struct GenEvent {
     u32 ad, ad_type, event_type;
@@ -105,7 +116,7 @@ YSB_HD GenEvent gen_event(const GenSpec& s, u64 i) {
     u64 c = draw(stream_key(s.ev_seed, S_CHOICE), i);
     u32 idx = (u32)(((c >> 32) * (u64)s.n_pick) >> 32);   // rand-nth ads (core.clj:92)
     e.ad = s.subset ? s.subset[idx] : idx;
-    e.ad_type = (u32)(c & 0xFFFF) % 5u;                    // rand-nth ad-types (:93)
+    e.ad_type = (u32)(c & 0xFFFF) % ((s.variant & GEN_V_MORE_AD_TYPES) ? 8u : 5u);   // rand-nth ad-types (:93)
     e.event_type = (u32)((c >> 16) & 0xFFFF) % 3u;         // rand-nth event-types (:94)
     i64 t = s.t0_ms + (i64)((i * 1000ULL) / s.events_per_sec);   // (+ start-time (* n 10)) (:95)
     if (s.with_skew) {                                      // make-kafka-event-at (:166-174)
@@ -132,14 +143,83 @@ YSB_HD u32 dec_format(i64 v, char* out) {
     return n;
 }
 
-YSB_HD u32 gen_line_len(const GenSpec& s, const GenEvent& e) {
+// The random dotted quad of event i (GEN_V_RANDOM_IP): bytes of one draw.
+YSB_HD u32 gen_ip(const GenSpec& s, u64 i) { return (u32)draw(stream_key(s.ev_seed, S_IP), i); }
+YSB_HD u32 ip_len(u32 ip) {
+    u32 n = 3;   // the dots
+    for (int k = 0; k < 4; ++k) n += dec_len((i64)((ip >> (8 * k)) & 0xFF));
+    return n;
+}
+
+YSB_HD u32 gen_line_len(const GenSpec& s, u64 i, const GenEvent& e) {
     const u32 var = ad_type_len(e.ad_type) + event_type_len(e.event_type) + dec_len(e.time_ms);
-    return (s.tbl ? 3u * 36u + 5u + 1u : (u32)LINE_FIXED) + var;
+    if (s.tbl) return 3u * 36u + 5u + 1u + var;
+    u32 n = (u32)LINE_FIXED + var;
+    if (s.variant & GEN_V_RANDOM_IP) n += ip_len(gen_ip(s, i)) - 7u;
+    if (s.variant & GEN_V_COMPACT) n -= 13u;   // 7 ": " and 6 ", " lose their space
+    return n;
 }
 
 YSB_HD char* put_str(char* o, const char* s, u32 n) {
     for (u32 k = 0; k < n; ++k) o[k] = s[k];
     return o + n;
+}
+
+// A variant line (GEN_V_RANDOM_IP / GEN_V_COMPACT): the same seven keys in the same
+// order, the separators with or without their space, the ip a random dotted quad.
+YSB_HD u32 gen_line_write_variant(const GenSpec& s, u64 i, const GenEvent& e, char* out) {
+    const bool cp = (s.variant & GEN_V_COMPACT) != 0;
+    const char* sep = cp ? "\",\"" : "\", \"";       // between a value and the next key
+    const char* col = cp ? "\":\"" : "\": \"";       // between a key and its value
+    const u32 ls = cp ? 3u : 4u;
+    char* o = out;
+    u64 hi, lo;
+    *o++ = '{';
+    *o++ = '"';
+    o = put_str(o, "user_id", 7);
+    o = put_str(o, col, ls);
+    if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
+    else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);
+    uuid_format(hi, lo, o); o += 36;
+    o = put_str(o, sep, ls);
+    o = put_str(o, "page_id", 7);
+    o = put_str(o, col, ls);
+    if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_PAGE), i, &hi, &lo);
+    else uuid_words(stream_key(s.ev_seed, S_PAGE), draw(stream_key(s.ev_seed, S_PAGEPOOL), i) % s.n_users, &hi, &lo);
+    uuid_format(hi, lo, o); o += 36;
+    o = put_str(o, sep, ls);
+    o = put_str(o, "ad_id", 5);
+    o = put_str(o, col, ls);
+    uuid_words(stream_key(s.seed, S_AD), e.ad, &hi, &lo);
+    uuid_format(hi, lo, o); o += 36;
+    o = put_str(o, sep, ls);
+    o = put_str(o, "ad_type", 7);
+    o = put_str(o, col, ls);
+    o = put_str(o, ad_type_str(e.ad_type), ad_type_len(e.ad_type));
+    o = put_str(o, sep, ls);
+    o = put_str(o, "event_type", 10);
+    o = put_str(o, col, ls);
+    o = put_str(o, event_type_str(e.event_type), event_type_len(e.event_type));
+    o = put_str(o, sep, ls);
+    o = put_str(o, "event_time", 10);
+    o = put_str(o, col, ls);
+    o += dec_format(e.time_ms, o);
+    o = put_str(o, sep, ls);
+    o = put_str(o, "ip_address", 10);
+    o = put_str(o, col, ls);
+    if (s.variant & GEN_V_RANDOM_IP) {
+        const u32 ip = gen_ip(s, i);
+        for (int k = 0; k < 4; ++k) {
+            if (k) *o++ = '.';
+            o += dec_format((i64)((ip >> (8 * k)) & 0xFF), o);
+        }
+    } else {
+        o = put_str(o, "1.2.3.4", 7);
+    }
+    *o++ = '"';
+    *o++ = '}';
+    *o++ = '\n';
+    return (u32)(o - out);
 }
 
 // One event line, exactly the str of core.clj:90-96 plus the "\n" of :97; with s.tbl
@@ -169,6 +249,7 @@ YSB_HD u32 gen_line_write(const GenSpec& s, u64 i, const GenEvent& e, char* out)
         *o++ = '\n';
         return (u32)(o - out);
     }
+    if (s.variant & (GEN_V_RANDOM_IP | GEN_V_COMPACT)) return gen_line_write_variant(s, i, e, out);
     o = put_str(o, YSB_P0, LEN_P0);
     if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
     else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);

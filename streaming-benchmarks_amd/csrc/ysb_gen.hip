@@ -11,7 +11,7 @@ __global__ void gen_len_kernel(GenSpec s, u64 first, u64 n, u32* len, unsigned l
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     u32 l = 0;
     if (i < n) {
-        l = gen_line_len(s, gen_event(s, first + i));
+        l = gen_line_len(s, first + i, gen_event(s, first + i));
         len[i] = l;
     }
 #pragma unroll

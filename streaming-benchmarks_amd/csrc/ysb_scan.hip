@@ -288,16 +288,15 @@ __device__ __forceinline__ u32 cand_nib(u32 w) {
 // The line's first 164 bytes: structural bytes (compared) and the three UUID values
 // (scanned for candidates), as 41 little-endian words.
 constexpr int PREFIX_WORDS = 41;
-constexpr int TAIL_WORDS = 28;                  // raw dwords scanned for the tail's quotes
-constexpr int MAX_CANON_LEN = 164 + 4 * TAIL_WORDS - 3;   // 273: longest line the fast path takes
 struct PrefixTpl {
     u32 e[PREFIX_WORDS];   // expected structural bytes
     u32 m[PREFIX_WORDS];   // 0xFF per structural byte
     u32 v[PREFIX_WORDS];   // 0x80 per value byte
 };
-constexpr PrefixTpl make_prefix_tpl() {
+// The prefix up to the ad_type value: parts[0] UUID parts[1] UUID parts[2] UUID parts[3].
+constexpr PrefixTpl make_prefix_tpl(const char* p0, const char* p1, const char* p2, const char* p3) {
     PrefixTpl t{};
-    const char* parts[4] = {YSB_P0, YSB_P1, YSB_P2, YSB_P3};
+    const char* parts[4] = {p0, p1, p2, p3};
     int pos = 0;
     for (int k = 0; k < 4; ++k) {
         for (const char* q = parts[k]; *q; ++q, ++pos) {
@@ -309,47 +308,96 @@ constexpr PrefixTpl make_prefix_tpl() {
     }
     return t;
 }
+constexpr PrefixTpl make_prefix_tpl() { return make_prefix_tpl(YSB_P0, YSB_P1, YSB_P2, YSB_P3); }
+
+// Up to 20 expected bytes (a separator run) as 5 words + byte masks.
+struct SepTpl {
+    u32 e[5];
+    u32 m[5];
+};
+constexpr SepTpl make_sep(const char* str) {
+    SepTpl t{};
+    int pos = 0;
+    for (const char* q = str; *q; ++q, ++pos) {
+        t.e[pos >> 2] |= (u32)(u8)*q << (8 * (pos & 3));
+        t.m[pos >> 2] |= 0xFFu << (8 * (pos & 3));
+    }
+    return t;
+}
+__device__ __forceinline__ u32 sep_diff(const u32 (&w)[5], const SepTpl& t) {
+    u32 d = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        if (t.m[k]) d |= (w[k] ^ t.e[k]) & t.m[k];
+    return d;
+}
 
 struct CanonA {   // after the first LDS batch
-    u32 kw[9];     // ad_id bytes 113..148 (.tbl: 74..109)
+    u32 kw[9];     // the 36 ad_id bytes (.tbl: bytes 74..109)
     int e3, e4, e5, e6;   // closing quotes of ad_type, event_type, event_time, ip_address
                           // (.tbl: e3, e4 = the 4th and 5th '|'; e5, e6 = '|' bitmap of bytes 96..159)
+    int t0;        // line offset of the event_time value
 };
 
-// Stage 1: one batch of independent LDS reads -- the line's first 276 bytes as raw
-// dwords -- then register-only checks: the prefix template, the UUID values free of
-// candidates, and the tail's quote positions from a candidate bitmap of the raw tail
-// dwords.  False = not the generator's layout (deferred to the general path).
+// ---------------------------------------------------------------------------
+// Canonical tiers (lines the vocabulary path below does not take): the generator's seven
+// keys in its order with any string values -- other ip addresses, ad_types, event_types
+// or event_time lengths -- in two layouts, the generator's (": " and ", ", CP = false)
+// and compact JSON (":" and ",", CP = true).  Stage 1 reads the line's first 160-164
+// bytes and 28 more raw dwords: the prefix is compared with a template (structural bytes
+// exact, the three 36-byte UUID values shown free of '"', '\\' and control bytes), and
+// the tail's value ends are the next quote candidates of a SWAR bitmap; stage 2 compares
+// the three tail separators, the closing "}" and fetches event_type / event_time.  Every
+// byte up to '}' is compared or classified, so an accepted line parses exactly as
+// org.json parses it; anything else goes on to the general parser.
+// ---------------------------------------------------------------------------
+template <bool CP>
+struct CanonGeo {
+    static constexpr int PREFIX = CP ? 157 : 164;     // bytes before the ad_type value
+    static constexpr int PW = (PREFIX + 3) / 4;        // prefix words compared
+    static constexpr int TB = (PREFIX / 4) * 4;        // the tail bitmap starts at this (aligned) byte
+    static constexpr int TW = 28;                      // raw tail dwords scanned
+    static constexpr int MAXLEN = TB + 4 * TW - 3;     // longest line the tier takes
+    static constexpr int MINLEN = CP ? 207 : 220;
+    static constexpr int AD = CP ? 108 : 113;          // the ad_id value
+    static constexpr int SEP = CP ? 16 : 18;           // "<value>", "<key>": "<value>"
+};
+constexpr PrefixTpl make_compact_tpl() {
+    return make_prefix_tpl("{\"user_id\":\"", "\",\"page_id\":\"", "\",\"ad_id\":\"", "\",\"ad_type\":\"");
+}
+
+template <bool CP>
 __device__ __forceinline__ bool canon_stage1(const LdsSrc& src, int s, int e, CanonA& c) {
-    constexpr PrefixTpl T = make_prefix_tpl();
-    static_assert(T.e[0] == ('{' | ('"' << 8) | ('u' << 16) | ('s' << 24)), "prefix template");
+    using G = CanonGeo<CP>;
+    constexpr PrefixTpl T = CP ? make_compact_tpl() : make_prefix_tpl();
     const int L = e - s;
-    if (L < 220 || L > MAX_CANON_LEN) return false;
+    if (L < G::MINLEN || L > G::MAXLEN) return false;
     const int a = s >> 2;
     const u32 sb = (u32)(s & 3);
-    u32 P[PREFIX_WORDS + 1];
+    u32 P[G::PW + 1];
 #pragma unroll
-    for (int k = 0; k <= PREFIX_WORDS; ++k) P[k] = src.d[a + k];
-    u32 R[TAIL_WORDS];   // raw dwords from line offset 164 - sb (4-byte aligned)
+    for (int k = 0; k <= G::PW; ++k) P[k] = src.d[a + k];
+    u32 R[G::TW];   // raw dwords from line offset TB - sb
 #pragma unroll
-    for (int k = 0; k < TAIL_WORDS; ++k) R[k] = k == 0 ? P[PREFIX_WORDS] : src.d[a + PREFIX_WORDS + k];
+    for (int k = 0; k < G::TW; ++k) R[k] = src.d[a + G::TB / 4 + k];
     // prefix: XOR-accumulated compares and candidate flags; d == 0 <=> all hold
-    u32 d = 0, W[PREFIX_WORDS];
+    u32 d = 0, W[G::PW];
 #pragma unroll
-    for (int j = 0; j < PREFIX_WORDS; ++j) {
+    for (int j = 0; j < G::PW; ++j) {
         W[j] = __builtin_amdgcn_alignbyte(P[j + 1], P[j], sb);   // line bytes 4j..4j+3
         if (T.m[j] == 0xFFFFFFFFu) d |= W[j] ^ T.e[j];
         else if (T.m[j] != 0u) d |= (W[j] ^ T.e[j]) & T.m[j];
         if (T.v[j] != 0u) d |= cand_z(W[j]) & T.v[j];
     }
 #pragma unroll
-    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(W[29 + k], W[28 + k], 1u);   // bytes 113..148
-    // tail: candidate bitmap, bit i = line byte 164 - sb + i
+    for (int k = 0; k < 9; ++k)
+        c.kw[k] = __builtin_amdgcn_alignbyte(W[G::AD / 4 + k + 1], W[G::AD / 4 + k], (u32)(G::AD & 3));
+    // tail: candidate bitmap, bit i = line byte TB - sb + i
     u32 B[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int k = 0; k < TAIL_WORDS; ++k) B[k >> 3] |= cand_nib(R[k]) << (4 * (k & 7));
-    const int tb0 = 164 - (int)sb;
-    // first candidate at or after line offset p (164 <= p), via a 64-bit window
+    for (int k = 0; k < G::TW; ++k) B[k >> 3] |= cand_nib(R[k]) << (4 * (k & 7));
+    const int tb0 = G::TB - (int)sb;
+    // first candidate at or after line offset p (p >= tb0), via a 64-bit window
     auto nextq = [&](int p) -> int {
         const int q = p - tb0;
         const int k = q >> 5;
@@ -358,10 +406,11 @@ __device__ __forceinline__ bool canon_stage1(const LdsSrc& src, int s, int e, Ca
         const u64 w = (((u64)hi << 32) | lo) >> (q & 31);
         return w ? p + (int)__builtin_ctzll(w) : (1 << 20);
     };
-    c.e3 = nextq(164);            // end of ad_type
-    c.e4 = nextq(c.e3 + 18);      // end of event_type
-    c.e5 = nextq(c.e4 + 18);      // end of event_time
-    c.e6 = nextq(c.e5 + 18);      // end of ip_address
+    c.e3 = nextq(G::PREFIX);          // end of ad_type
+    c.e4 = nextq(c.e3 + G::SEP);      // end of event_type
+    c.e5 = nextq(c.e4 + G::SEP);      // end of event_time
+    c.e6 = nextq(c.e5 + G::SEP);      // end of ip_address
+    c.t0 = c.e4 + G::SEP;
     return d == 0u && c.e6 + 2 <= L;
 }
 
@@ -371,28 +420,29 @@ struct CanonB {   // after the second LDS batch
     int tlen;
 };
 
+
 // Stage 2: the variable tail -- the three separators, the closing "}", the event_type
 // value and the event_time digits -- in one batch of LDS reads.
+template <bool CP>
 __device__ __forceinline__ bool canon_stage2(const LdsSrc& src, int s, int e, const CanonA& a, CanonB& c) {
+    using G = CanonGeo<CP>;
+    constexpr SepTpl S4 = make_sep(CP ? "\",\"event_type\":\"" : "\", \"event_type\": \"");
+    constexpr SepTpl S5 = make_sep(CP ? "\",\"event_time\":\"" : "\", \"event_time\": \"");
+    constexpr SepTpl S6 = make_sep(CP ? "\",\"ip_address\":\"" : "\", \"ip_address\": \"");
     u32 t4[5], t5[5], t6[5], t7[1], ev[1];
     load_span(src, s + a.e3, t4);
     load_span(src, s + a.e4, t5);
     load_span(src, s + a.e5, t6);
     load_span(src, s + a.e6, t7);
-    load_span(src, s + a.e3 + 18, ev);
-    load_span(src, s + a.e4 + 18, c.td);
-    u32 d = (t4[0] ^ w4('"', ',', ' ', '"')) | (t4[1] ^ w4('e', 'v', 'e', 'n')) | (t4[2] ^ w4('t', '_', 't', 'y')) |
-            (t4[3] ^ w4('p', 'e', '"', ':')) | ((t4[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
-    d |= (t5[0] ^ w4('"', ',', ' ', '"')) | (t5[1] ^ w4('e', 'v', 'e', 'n')) | (t5[2] ^ w4('t', '_', 't', 'i')) |
-         (t5[3] ^ w4('m', 'e', '"', ':')) | ((t5[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
-    d |= (t6[0] ^ w4('"', ',', ' ', '"')) | (t6[1] ^ w4('i', 'p', '_', 'a')) | (t6[2] ^ w4('d', 'd', 'r', 'e')) |
-         (t6[3] ^ w4('s', 's', '"', ':')) | ((t6[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
+    load_span(src, s + a.e3 + G::SEP, ev);
+    load_span(src, s + a.t0, c.td);
+    u32 d = sep_diff(t4, S4) | sep_diff(t5, S5) | sep_diff(t6, S6);
     d |= (t7[0] & 0xFFFFu) ^ w4('"', '}', 0, 0);
     // org.json's JSONObject(String) stops at the closing '}': whatever follows it (normally
     // the '\n') is never read.
     if (d != 0u) return false;
-    c.view = (a.e4 - (a.e3 + 18) == 4) && ev[0] == VIEW_W;
-    c.tlen = a.e5 - (a.e4 + 18);
+    c.view = (a.e4 - (a.e3 + G::SEP) == 4) && ev[0] == VIEW_W;
+    c.tlen = a.e5 - a.t0;
     return true;
 }
 
@@ -416,10 +466,14 @@ __device__ __forceinline__ u32 swar_digits4(u32 w, u32& bad) {
 // (separators, keys, the event_type value, the ip value) and checks the 13 time bytes are
 // digits.  So every byte up to '}' is either compared or shown to be a UUID byte free of
 // '"', '\\' and control bytes or a digit: the line parses exactly as org.json parses
-// it.  No candidate scan of the tail.  Any other line is deferred to the general parser.
+// it.  No candidate scan of the tail.  A line it rejects tries the canonical tiers
+// (canon_stage1/2: other values, then compact JSON) before the general parser.
 // ---------------------------------------------------------------------------
 #ifndef YSB_VOCAB
 #define YSB_VOCAB 1
+#endif
+#ifndef YSB_CANON_TIERS
+#define YSB_CANON_TIERS 1
 #endif
 constexpr int VOC_WORDS = 50;            // line bytes 0..199
 constexpr int VOC_MIN_LEN = 248;         // 240 + shortest ad_type (4) + event_type (4)
@@ -462,6 +516,7 @@ __device__ __forceinline__ bool vocab_stage1(const LdsSrc& src, int s, int e, Ca
     c.e4 = c.e3 + 18 + Le;     // of event_type
     c.e5 = c.e4 + 18 + 13;     // of event_time
     c.e6 = c.e5 + 18 + 7;      // of ip_address
+    c.t0 = c.e4 + 18;
     return d == 0u && La != 0 && Le != 0 && c.e6 + 2 <= L;
 }
 
@@ -543,6 +598,7 @@ __device__ __forceinline__ bool tbl_stage1(const LdsSrc& src, int s, int e, Cano
     c.e4 = p4;
     c.e5 = (int)B[3];
     c.e6 = (int)B[4];
+    c.t0 = p4 + 1;
     return fixed && p4 + 2 <= L;
 }
 
@@ -973,17 +1029,19 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         return;
 #endif
         // ---- Phase B1: canonical parse from LDS; any other line is deferred -------
-        bool ok1 = false;
+        bool ok1 = false, elig = false;
         int ls = 0, le = 0;
         CanonA ca;
 #pragma unroll
         for (int k = 0; k < 9; ++k) ca.kw[k] = 0u;
+        ca.t0 = 0;
         if (li < cur.count && !cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
+            elig = true;
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
             else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1(lsrc, ls, le, ca);
-            else ok1 = canon_stage1(lsrc, ls, le, ca);
+            else ok1 = canon_stage1<false>(lsrc, ls, le, ca);
         }
         bool pend = false, dfr = false, tok = false;
         i64 bucket = 0;
@@ -993,9 +1051,30 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         if (li < cur.count) {
             if constexpr (TBL) ok2 = ok1 && tbl_stage2(lsrc, ls, le, ca, cb);
             else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2(lsrc, ls, le, ca, cb);
-            else ok2 = ok1 && canon_stage2(lsrc, ls, le, ca, cb);
-            dfr = !ok2;   // bad offsets, other layouts, escapes, over-size tiles
+            else ok2 = ok1 && canon_stage2<false>(lsrc, ls, le, ca, cb);
         }
+#if YSB_CANON_TIERS
+        if constexpr (!TBL && YSB_VOCAB != 0) {
+            // second and third tiers for the lanes the vocabulary path rejected (a branch
+            // no lane takes on the generator's own lines): any values in the generator's
+            // layout, then the same keys as compact JSON
+            if (elig && !ok2) {
+                CanonA c2;
+                CanonB b2;
+                b2.view = false;
+                bool t = canon_stage1<false>(lsrc, ls, le, c2) && canon_stage2<false>(lsrc, ls, le, c2, b2);
+                if (!t) t = canon_stage1<true>(lsrc, ls, le, c2) && canon_stage2<true>(lsrc, ls, le, c2, b2);
+                if (t) {
+                    ca = c2;
+                    cb = b2;
+                    ok2 = true;
+                }
+            }
+        }
+#else
+        (void)elig;
+#endif
+        dfr = li < cur.count && !ok2;   // bad offsets, other layouts, escapes, over-size tiles
         pend = ok2 && cb.view;                                             // EventFilterBolt
         // RedisJoinBolt's lookup (36-byte keys): both cuckoo slots, views only (a third
         // of the lanes: scattered loads cost address-unit time per lane), issued before
@@ -1027,7 +1106,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             tl.ev++;
             if (pend) {
                 tl.view++;
-                tok = canonical_bucket(lsrc, cb, ls + ca.e4 + (TBL ? 1 : 18), P, bucket);   // Long.parseLong
+                tok = canonical_bucket(lsrc, cb, ls + ca.t0, P, bucket);   // Long.parseLong
             }
         }
         defer_append(P, dfr, P.line_base + cur.first + li, lane);

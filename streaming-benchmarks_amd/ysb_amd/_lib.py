@@ -56,7 +56,7 @@ class YsbGenParams(C.Structure):
                 ("t0_ms", C.c_int64), ("events_per_sec", C.c_uint64), ("with_skew", C.c_uint32),
                 ("n_users", C.c_uint32), ("ad_subset", C.POINTER(C.c_uint32)), ("n_ad_subset", C.c_uint32),
                 ("event_stream", C.c_uint32),
-                ("format", C.c_uint32)]
+                ("format", C.c_uint32), ("variant", C.c_uint32)]
 
 
 _P = C.c_void_p

@@ -11,6 +11,8 @@ import numpy as np
 from ._lib import YsbGenParams, check, lib
 
 AD_TYPES = ("banner", "modal", "sponsored-search", "mail", "mobile")   # core.clj:68
+MORE_AD_TYPES = AD_TYPES + ("native-video", "interstitial", "rewarded")  # GEN_MORE_AD_TYPES
+GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_COMPACT = 1, 2, 4
 EVENT_TYPES = ("view", "click", "purchase")                            # core.clj:69
 
 
@@ -20,7 +22,7 @@ class GenParams:
 
     def __init__(self, seed=42, n_campaigns=100, ads_per_campaign=10, t0_ms=1_700_000_000_000,
                  events_per_sec=100_000, with_skew=False, n_users=0, ad_subset=None, event_stream=0,
-                 fmt="json"):
+                 fmt="json", variant=0):
         self.c = YsbGenParams()
         lib().ysb_gen_default(C.byref(self.c))
         self.c.seed = seed
@@ -34,6 +36,8 @@ class GenParams:
         if fmt not in ("json", "tbl"):
             raise ValueError("fmt must be 'json' or 'tbl'")
         self.c.format = 1 if fmt == "tbl" else 0   # YSB_GEN_TBL: the fork's .tbl rows
+        # variant: GEN_RANDOM_IP | GEN_MORE_AD_TYPES | GEN_COMPACT (off-vocabulary layouts)
+        self.c.variant = variant
         self._subset = None
         if ad_subset is not None:
             self._subset = np.ascontiguousarray(ad_subset, dtype=np.uint32)
