@@ -343,7 +343,7 @@ def extras(args, device):
         with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True,
                         max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
             ctx.load_ad_map(aids, g.ad_campaign_index())
-            segs = gen_segments(ctx, g, 100_000_000, args.segment)
+            segs = gen_segments(ctx, g, 100_000_000, 12_500_000)   # longer lines: 8 batches under 4 GiB
             out[key] = timed_extra("configs[1]'s 100M events, " + what, ctx, g, segs, args.extra_steps,
                                    args.warmup, "ysb::scan_kernel<false, false, false>")
             free_segments(ctx, segs)

@@ -1301,8 +1301,9 @@ int ysb_gen_events_device(ysb_ctx* c, const ysb_gen_params* p, uint64_t first, u
     int rc = upload_subset(c, p, &dsub);
     if (rc) return rc;
     const GenSpec s = spec_of(p, dsub);
-    hipError_t e = gen_events_device(s, first, n, d_out, std::min<u64>(cap, 0xFFFFFFFFull), d_off, nbytes, c->s_comp);
-    if (e == hipErrorInvalidValue && *nbytes > cap)
+    const u64 cap32 = std::min<u64>(cap, 0xFFFFFFFFull);   // u32 line offsets
+    hipError_t e = gen_events_device(s, first, n, d_out, cap32, d_off, nbytes, c->s_comp);
+    if (e == hipErrorInvalidValue && *nbytes > cap32)
         return fail(c, YSB_ERR_CAPACITY, "generator output %llu B exceeds cap %llu B (u32 offsets: <= 4 GiB per batch)",
                     (unsigned long long)*nbytes, (unsigned long long)cap);
     if (e != hipSuccess) return fail(c, YSB_ERR_HIP, "device generator: %s", hipGetErrorString(e));

@@ -26,7 +26,7 @@ static_assert(TILE_LINES >= 1 && TILE_LINES <= SCAN_TPB, "one line per lane at m
 #endif
 constexpr int SCAN_WG_PER_CU = YSB_WG_PER_CU; // resident scan workgroups per CU (LDS-bound)
 #ifndef YSB_TILE_LINE_BYTES
-#define YSB_TILE_LINE_BYTES 260
+#define YSB_TILE_LINE_BYTES 272
 #endif
 constexpr int TILE_CAP = TILE_LINES * YSB_TILE_LINE_BYTES;   // LDS bytes of one tile (per-line average cap)
 constexpr int TILE_CHUNKS = TILE_CAP / 16;    // 16-byte chunks per tile
