@@ -20,6 +20,9 @@ Here the operator:
   * follows the watermark with the device ring (ysb_ring_advance), keeping a lateness
     horizon (60 s of late events, core.clj:170) on the device.
 
+ShardedStreamingOperator drives N such slot pairs (one context per GPU) with one global
+watermark (configs[4]: "feeding double-buffered pinned batches to 8 GPUs").
+
 The context is duck-typed (slot_buffers / submit_raw / wait / sync / drain_rows /
 ring_advance / ring_range) so the host logic is testable on CPU with a stand-in.
 """
@@ -95,9 +98,57 @@ class SlotContext:
         self.ctx.ring_advance(lo)
 
 
+class WindowBook:
+    """Window bookkeeping of a flush: the windows seen, when the watermark closed each
+    (close latency), late deltas, and the running totals of everything written."""
+
+    def __init__(self, divisor):
+        self.d = divisor
+        self.seen_buckets = set()
+        self.closed = {}          # bucket -> close latency (ms), None for late-only windows
+        self.late_rows = 0        # deltas written for already-closed windows
+        self.totals = {}          # (campaign, bucket) -> count, everything written
+        self.rows_written = 0
+        self.flushed_wm = None    # watermark at the previous flush
+        self.first_wm = None      # watermark after the first batch
+
+    def account(self, rows, now, watermark):
+        d = self.d
+        for c, b, n in rows:
+            if b not in self.seen_buckets:
+                self.seen_buckets.add(b)
+                # first seen after the previous flush's watermark had passed its end:
+                # a window of late events only, not a window that closes (no latency)
+                ref = self.flushed_wm if self.flushed_wm is not None else self.first_wm
+                if ref is not None and (b + 1) * d <= ref:
+                    self.closed[b] = None
+            if b in self.closed:
+                self.late_rows += 1
+            self.totals[(c, b)] = self.totals.get((c, b), 0) + n
+        self.rows_written += len(rows)
+        if watermark is not None:
+            self.flushed_wm = watermark
+            for b in sorted(self.seen_buckets):
+                if b not in self.closed and (b + 1) * d <= watermark:
+                    self.closed[b] = now - (b + 1) * d
+
+    def open_windows(self):
+        return len([b for b in self.seen_buckets if b not in self.closed])
+
+    def latency_summary(self):
+        v = np.array(sorted(x for x in self.closed.values() if x is not None), dtype=np.float64)
+        late_only = sum(1 for x in self.closed.values() if x is None)
+        if v.size == 0:
+            return {"windows": 0, "late_only_windows": late_only}
+        return {"windows": int(v.size), "p50_ms": float(np.percentile(v, 50)),
+                "p99_ms": float(np.percentile(v, 99)), "max_ms": float(v.max()),
+                "late_only_windows": late_only}
+
+
 class StreamingOperator:
     def __init__(self, sctx, sink=None, batch_interval_ms=100, flush_interval_ms=1000,
-                 max_out_of_orderness_ms=100, lateness_horizon_ms=60_000, clock_ms=None):
+                 max_out_of_orderness_ms=100, lateness_horizon_ms=60_000, clock_ms=None,
+                 auto_flush=True):
         self.s = sctx
         self.sink = sink
         self.batch_interval_ms = batch_interval_ms
@@ -105,6 +156,7 @@ class StreamingOperator:
         self.ooo = max_out_of_orderness_ms
         self.horizon_buckets = -(-lateness_horizon_ms // sctx.divisor) + 1
         self.clock = clock_ms or (lambda: time.time() * 1000.0)
+        self.auto_flush = auto_flush   # False: a ShardedStreamingOperator flushes the shards
         self.slot = 0
         self.fill_bytes = 0
         self.fill_events = 0
@@ -112,17 +164,18 @@ class StreamingOperator:
         self.max_time = None
         self.watermark = None
         self.last_flush_ms = self.clock()
-        self.seen_buckets = set()
-        self.closed = {}          # bucket -> close latency (ms)
-        self.late_rows = 0        # deltas written for already-closed windows
+        self.book = WindowBook(sctx.divisor)
         self.events = 0
         self.batches = 0
-        self.rows_written = 0
         self.flushes = 0
-        self.totals = {}          # (campaign, bucket) -> count, everything written
         self.open_at_end = 0
-        self.flushed_wm = None    # watermark at the previous flush
-        self.first_wm = None      # watermark after the first batch
+
+    # the book's fields, as attributes of the operator (reports, tests)
+    seen_buckets = property(lambda self: self.book.seen_buckets)
+    closed = property(lambda self: self.book.closed)
+    late_rows = property(lambda self: self.book.late_rows)
+    totals = property(lambda self: self.book.totals)
+    rows_written = property(lambda self: self.book.rows_written)
 
     # -- filling -----------------------------------------------------------------------
     def free_space(self):
@@ -193,44 +246,30 @@ class StreamingOperator:
             wm = self.max_time - self.ooo
             closes = self.watermark is not None and wm // self.s.divisor > self.watermark // self.s.divisor
             if self.watermark is None:
-                self.first_wm = wm
+                self.book.first_wm = wm
             self.watermark = wm if self.watermark is None else max(self.watermark, wm)
-            if closes:
+            if closes and self.auto_flush:
                 self.flush()           # a window ended under the watermark: close it now
-        if self.clock() - self.last_flush_ms >= self.flush_interval_ms:
+        if self.auto_flush and self.clock() - self.last_flush_ms >= self.flush_interval_ms:
             self.flush()
+
+    def follow_ring(self, watermark):
+        """Moves the device ring behind the watermark, keeping the lateness horizon."""
+        rr = self.s.ring_range()
+        if rr is not None and watermark is not None:
+            target = watermark // self.s.divisor - self.horizon_buckets
+            if target > rr[0]:
+                self.s.ring_advance(target)
 
     def flush(self):
         now = self.clock()
         rows = self.s.drain_rows()
         self.flushes += 1
         self.last_flush_ms = now
-        d = self.s.divisor
-        for c, b, n in rows:
-            if b not in self.seen_buckets:
-                self.seen_buckets.add(b)
-                # first seen after the previous flush's watermark had passed its end:
-                # a window of late events only, not a window that closes (no latency)
-                ref = self.flushed_wm if self.flushed_wm is not None else self.first_wm
-                if ref is not None and (b + 1) * d <= ref:
-                    self.closed[b] = None
-            if b in self.closed:
-                self.late_rows += 1
-            self.totals[(c, b)] = self.totals.get((c, b), 0) + n
+        self.book.account(rows, now, self.watermark)
         if rows and self.sink is not None:
             self.sink([(c, b * self.s.divisor, n) for c, b, n in rows])
-        self.rows_written += len(rows)
-        if self.watermark is not None:
-            self.flushed_wm = self.watermark
-            for b in sorted(self.seen_buckets):
-                if b not in self.closed and (b + 1) * d <= self.watermark:
-                    self.closed[b] = now - (b + 1) * d
-            # follow the watermark with the device ring, keeping the lateness horizon
-            rr = self.s.ring_range()
-            if rr is not None:
-                target = self.watermark // d - self.horizon_buckets
-                if target > rr[0]:
-                    self.s.ring_advance(target)
+        self.follow_ring(self.watermark)
         return len(rows)
 
     def close(self):
@@ -239,14 +278,111 @@ class StreamingOperator:
         self.submit()
         self.s.sync()
         self.flush()
-        self.open_at_end = len([b for b in self.seen_buckets if b not in self.closed])
+        self.open_at_end = self.book.open_windows()
 
     # -- report ------------------------------------------------------------------------
     def latency_summary(self):
-        v = np.array(sorted(x for x in self.closed.values() if x is not None), dtype=np.float64)
-        late_only = sum(1 for x in self.closed.values() if x is None)
-        if v.size == 0:
-            return {"windows": 0, "late_only_windows": late_only}
-        return {"windows": int(v.size), "p50_ms": float(np.percentile(v, 50)),
-                "p99_ms": float(np.percentile(v, 99)), "max_ms": float(v.max()),
-                "late_only_windows": late_only}
+        return self.book.latency_summary()
+
+
+class ShardedStreamingOperator:
+    """configs[4] across GPUs: one double-buffered slot pair and context per GPU (shard),
+    events routed by ad_id hash (ysb_route_lines, the keyBy(0) of
+    AdvertisingTopologyNative.java:118 applied at the source) or produced per shard, and
+    ONE event-time watermark: the minimum over the shards' watermarks (Flink's watermark
+    at a keyed operator is the minimum over its input channels), reduced across processes
+    by `watermark_reduce` when the shards live in several ranks.  A window closes when the
+    global watermark passes its end; every shard then drains its deltas of it, and the
+    deltas go to the sink additively (HINCRBY, as parallel CampaignProcessor instances
+    write theirs: CampaignProcessorCommon.java:69-89) -- the streaming path needs no count
+    exchange.
+
+    Driven by tick(): submit every shard's open slot, reduce the watermark, flush on a
+    window close or every `flush_every` ticks (a tick count, so that ranks running in
+    lockstep take the same decisions and enter the same collectives)."""
+
+    def __init__(self, sctxs, sink=None, flush_every=10, max_out_of_orderness_ms=100,
+                 lateness_horizon_ms=60_000, clock_ms=None, watermark_reduce=None):
+        self.clock = clock_ms or (lambda: time.time() * 1000.0)
+        self.shards = [StreamingOperator(sc, sink=None, max_out_of_orderness_ms=max_out_of_orderness_ms,
+                                         lateness_horizon_ms=lateness_horizon_ms, clock_ms=self.clock,
+                                         auto_flush=False) for sc in sctxs]
+        self.n = len(self.shards)
+        self.d = sctxs[0].divisor
+        self.sink = sink
+        self.flush_every = flush_every
+        self.reduce = watermark_reduce
+        self.book = WindowBook(self.d)
+        self.watermark = None
+        self.ticks = 0
+        self.last_flush_tick = 0
+        self.flushes = 0
+        self.open_at_end = 0
+
+    totals = property(lambda self: self.book.totals)
+    events = property(lambda self: sum(s.events for s in self.shards))
+    batches = property(lambda self: sum(s.batches for s in self.shards))
+
+    # -- input ---------------------------------------------------------------------------
+    def append(self, raw, offs):
+        """Routes a host batch by ad_id hash over the local shards."""
+        from .group import route_lines, split_batch
+        if self.n == 1:
+            self.shards[0].append(raw, offs)
+            return
+        shard, _ = route_lines(raw, offs, self.n)
+        for r in range(self.n):
+            br, bo = split_batch(raw, offs, shard, r)
+            if bo.size:
+                self.shards[r].append(br, bo)
+
+    def append_shard(self, r, raw, offs):
+        self.shards[r].append(raw, offs)
+
+    def fill_with(self, r, producer):
+        self.shards[r].fill_with(producer)
+
+    # -- watermark / flush ----------------------------------------------------------------
+    def local_watermark(self):
+        wms = [s.watermark for s in self.shards if s.watermark is not None]
+        return min(wms) if len(wms) == self.n else None
+
+    def tick(self):
+        for s in self.shards:
+            s.submit()
+        self.ticks += 1
+        wm = self.local_watermark()
+        if self.reduce is not None:
+            wm = self.reduce(wm)            # min over ranks (None while any rank has none)
+        closes = False
+        if wm is not None:
+            if self.watermark is None:
+                self.book.first_wm = wm
+            closes = self.watermark is not None and wm // self.d > self.watermark // self.d
+            self.watermark = wm if self.watermark is None else max(self.watermark, wm)
+        if closes or self.ticks - self.last_flush_tick >= self.flush_every:
+            self.flush()
+
+    def flush(self):
+        now = self.clock()
+        rows = []
+        for s in self.shards:
+            rows.extend(s.s.drain_rows())
+        self.flushes += 1
+        self.last_flush_tick = self.ticks
+        self.book.account(rows, now, self.watermark)
+        if rows and self.sink is not None:
+            self.sink([(c, b * self.d, n) for c, b, n in rows])
+        for s in self.shards:
+            s.follow_ring(self.watermark)
+        return len(rows)
+
+    def close(self):
+        for s in self.shards:
+            s.submit()
+            s.s.sync()
+        self.flush()
+        self.open_at_end = self.book.open_windows()
+
+    def latency_summary(self):
+        return self.book.latency_summary()

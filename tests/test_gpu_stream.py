@@ -185,3 +185,57 @@ def test_side_map_spills_to_host_between_launches():
             ctx.sync()
         assert ctx.stats()["overflow_dropped"] == 0
         assert ctx.drain_buckets() == rows
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n", [2, 4])
+def test_sharded_streaming_n_contexts_exact(n):
+    """configs[4] rehearsal on one GPU: n contexts (one per would-be GPU), each with its
+    own pinned double-buffered slots fed by its ad_id shard's event stream (skew and late
+    events), one global watermark; the deltas equal the batch path's counts exactly."""
+    from ysb_amd import shard_ads
+    from ysb_amd.stream import ShardedStreamingOperator
+    base = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000)
+    _, aids = base.ids()
+    subsets = shard_ads(aids, n)
+    gens = [GenParams(seed=42, event_stream=1 + r, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000,
+                      ad_subset=subsets[r], with_skew=True, n_users=100, t0_ms=1_700_000_000_000)
+            for r in range(n)]
+    per_tick, ticks = 2000, 600                      # 20 ms of event time per tick, 12 s
+    ctxs = [YsbContext(n_campaigns=100, window_ring=16, max_batch_bytes=per_tick * 300,
+                       max_batch_events=per_tick * 2) for _ in range(n)]
+    for c in ctxs:
+        c.load_ad_map(aids, base.ad_campaign_index())
+    clk = [1_700_000_000_000.0]
+    op = ShardedStreamingOperator([SlotContext(c) for c in ctxs], clock_ms=lambda: clk[0], flush_every=50)
+    produced = [0] * n
+
+    def producer(r):
+        def fill(bv, ov, cap_b, cap_e):
+            raw, offs = gens[r].events_host(produced[r], per_tick)
+            bv[:raw.size] = raw
+            ov[:per_tick] = offs
+            produced[r] += per_tick
+            return raw.size, per_tick
+        return fill
+    for t in range(ticks):
+        clk[0] = 1_700_000_000_000 + (t + 1) * 20 + 5
+        for r in range(n):
+            op.fill_with(r, producer(r))
+        op.tick()
+    op.close()
+    ref = {}
+    for r in range(n):
+        raw, offs = gens[r].events_host(0, produced[r])
+        with YsbContext(n_campaigns=100, window_ring=64, max_batch_bytes=raw.size + 64,
+                        max_batch_events=offs.size + 1) as c2:
+            c2.load_ad_map(aids, base.ad_campaign_index())
+            c2.submit(raw, offs)
+            for k, v in c2.drain_buckets().items():
+                ref[k] = ref.get(k, 0) + v
+    for c in ctxs:
+        c.close()
+    assert op.totals == ref
+    assert op.events == n * per_tick * ticks
+    lat = op.latency_summary()
+    assert lat["windows"] >= 1 and lat["p99_ms"] < 1000

@@ -27,14 +27,15 @@ def free_port():
     return p
 
 
-def run_ranks(scenario, world, tmp_path):
+def run_ranks(scenario, world, tmp_path, worker="multirank_worker.py"):
     port = free_port()
     procs, outs = [], []
     for r in range(world):
         out = tmp_path / ("rank%d.json" % r)
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py"), scenario, str(out)],
+        args = [scenario, str(out)] if scenario else [str(out)]
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, worker)] + args,
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
         outs.append(out)
     logs = []
@@ -174,3 +175,15 @@ def test_dump_shards(tmp_path):
     from ysb_amd import ad_shard
     for r, lines in enumerate(parts):
         assert all(ad_shard(json.loads(ln)["ad_id"], 3) == r for ln in lines)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_streaming_ranks_share_one_watermark(world, tmp_path):
+    """configs[4] across processes: each rank streams its shard; the watermark is the
+    minimum over ranks (gloo all-reduce), so every rank closes the same windows at the
+    same tick, and each rank's deltas are exact for its shard."""
+    res = run_ranks(None, world, tmp_path, worker="stream_worker.py")[0]
+    assert len(res) == world and all(r["exact"] for r in res)
+    assert len(set(tuple(r["closed"]) for r in res)) == 1 and len(res[0]["closed"]) >= 2
+    assert len(set(r["watermark"] for r in res)) == 1
+    assert len(set(r["flushes"] for r in res)) == 1

@@ -187,3 +187,52 @@ def test_sharded_streaming_operators_share_one_redis():
         assert res and all(s == "CORRECT" for _, _, s, _ in res)
     finally:
         srv.close()
+
+
+def test_sharded_operator_global_watermark_exact():
+    """configs[4] host logic across 3 shards in one process: lines routed by ad_id hash,
+    one watermark = the minimum over the shards, windows closed on it, deltas additive."""
+    from ysb_amd.stream import ShardedStreamingOperator
+    g = GenParams(seed=31, n_campaigns=20, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
+                  t0_ms=1_700_000_000_000)
+    raw, offs = g.events_host(0, 45_000)               # 45 s of event time
+    clk = Clock(1_700_000_000_000.0)
+    shards = [OracleSlots(admap_gen(g), cap_bytes=1 << 18, cap_events=400) for _ in range(3)]
+    written = []
+    op = ShardedStreamingOperator(shards, sink=written.extend, clock_ms=clk, flush_every=10,
+                                  lateness_horizon_ms=20_000)
+    per = 100                                           # 100 ms of events per tick
+    for i in range(0, offs.size, per):
+        j = min(offs.size, i + per)
+        clk.t = 1_700_000_000_000 + j + 5
+        e = offs[j] if j < offs.size else raw.size
+        op.append(raw[offs[i]:e], (offs[i:j] - offs[i]).astype(np.uint32))
+        op.tick()
+    op.close()
+    ref, _ = oracle.run(admap_gen(g), raw, offs)
+    assert op.totals == ref
+    tot = {}
+    for c, w, n in written:
+        tot[(c, w // 10000)] = tot.get((c, w // 10000), 0) + n
+    assert tot == ref
+    assert all(s.events > 0 for s in op.shards) and op.events == offs.size
+    lat = op.latency_summary()
+    assert lat["windows"] >= 3 and 0 <= lat["p50_ms"] <= 100 + 5 + 100
+    # every shard's ring follows the one global watermark
+    assert all(s.advances and s.advances[-1] <= op.watermark // 10000 - op.shards[0].horizon_buckets
+               for s in shards)
+
+
+def test_sharded_operator_waits_for_every_shard():
+    """The global watermark is the minimum: a shard without data holds every window open."""
+    from ysb_amd.stream import ShardedStreamingOperator
+    g = GenParams(seed=31, n_campaigns=20, ads_per_campaign=10, events_per_sec=1000, t0_ms=1_700_000_000_000)
+    raw, offs = g.events_host(0, 30_000)
+    shards = [OracleSlots(admap_gen(g), cap_bytes=1 << 20, cap_events=4000) for _ in range(2)]
+    op = ShardedStreamingOperator(shards, clock_ms=Clock(0.0), flush_every=1000)
+    op.append_shard(0, raw, offs)
+    op.tick()
+    assert op.watermark is None and op.latency_summary()["windows"] == 0
+    op.append_shard(1, raw[:offs[1]], offs[:1])       # shard 1's first event: t0
+    op.tick()
+    assert op.watermark == 1_700_000_000_000 - 100

@@ -14,6 +14,9 @@
     python tools/bench_extra.py pcie [--batch-mb M] [--seconds S]
         host-staged throughput: pre-staged pinned double-buffered slots -> H2D copy
         stream -> scan kernel (PCIe-inclusive rate; never bench.py's value).
+    python tools/bench_extra.py stream_sharded --shards N [--rate R] [--seconds S]
+        configs[4] across N contexts (one per GPU; N contexts on one GPU when only one is
+        visible): per-shard real-time producers, one global watermark; p99 close latency.
     python tools/bench_extra.py stream [--rate R] [--seconds S]
         configs[4] on one GPU: a real-time producer (generator with skew and late
         events, core.clj:166-204) feeding the streaming operator; p50/p99 window-close
@@ -294,9 +297,91 @@ def stream(args):
             "exact_vs_batch_path": op.totals == ref, "rows": len(ref)}
 
 
+def stream_sharded(args):
+    """configs[4] with N shards: N contexts (one per GPU, round robin over the visible
+    devices; on a one-GPU box N contexts share it), each fed in real time by its ad_id
+    shard's producer (rate / N events per second each), one global watermark."""
+    from ysb_amd import shard_ads
+    from ysb_amd.stream import ShardedStreamingOperator, SlotContext
+    import ctypes as C
+    from ysb_amd._lib import lib as _l
+    n = args.shards
+    ndev = C.c_int(0)
+    try:
+        import torch
+        ndev.value = max(1, torch.cuda.device_count())
+    except Exception:
+        ndev.value = 1
+    rate = args.rate
+    t0_ms = (int(time.time() * 1000) // 10000 + 1) * 10000 - 2000
+    base = GenParams(seed=7, n_campaigns=100, ads_per_campaign=10, events_per_sec=rate)
+    _, aids = base.ids()
+    subsets = shard_ads(aids, n)
+    gens = [GenParams(seed=7, event_stream=1 + r, n_campaigns=100, ads_per_campaign=10, events_per_sec=rate // n,
+                      ad_subset=subsets[r], with_skew=True, n_users=100, t0_ms=t0_ms) for r in range(n)]
+    per_batch = max(1, rate // n * args.batch_ms // 1000)
+    cap_b = per_batch * gens[0].max_line_bytes() * 2
+    ctxs = [YsbContext(device=r % ndev.value, n_campaigns=100, window_ring=16, max_batch_bytes=cap_b,
+                       max_batch_events=per_batch * 2) for r in range(n)]
+    for c in ctxs:
+        c.load_ad_map(aids, base.ad_campaign_index())
+    wall0 = time.time() * 1000.0
+    clock_off = t0_ms - wall0
+    clock = lambda: time.time() * 1000.0 + clock_off   # noqa: E731
+    op = ShardedStreamingOperator([SlotContext(c) for c in ctxs], clock_ms=clock,
+                                  flush_every=max(1, 1000 // args.batch_ms), max_out_of_orderness_ms=args.ooo_ms)
+    n_total = rate // n * args.seconds
+    produced = [0] * n
+
+    def producer(r):
+        def fill(bv, ov, cap_bb, cap_e):
+            due = int((clock() - t0_ms) * (rate // n) / 1000)
+            m = min(cap_e, cap_bb // gens[r].max_line_bytes(), max(0, min(due, n_total) - produced[r]))
+            if m <= 0:
+                return 0, 0
+            raw, offs = gens[r].events_host(produced[r], m)
+            bv[:raw.size] = raw
+            ov[:m] = offs
+            produced[r] += m
+            return raw.size, m
+        return fill
+    last_tick = clock()
+    while min(produced) < n_total:
+        for r in range(n):
+            op.fill_with(r, producer(r))
+        if clock() - last_tick >= args.batch_ms:
+            op.tick()
+            last_tick = clock()
+        else:
+            time.sleep(0.001)
+    op.close()
+    ref = {}
+    for r in range(n):
+        with YsbContext(n_campaigns=100, window_ring=64) as c2:
+            c2.load_ad_map(aids, base.ad_campaign_index())
+            seg = 10_000_000
+            cap = seg * gens[r].max_line_bytes()
+            d_b, d_o = c2.device_alloc(cap), c2.device_alloc(4 * seg + 64)
+            for f in range(0, produced[r], seg):
+                m = min(seg, produced[r] - f)
+                nb = c2.gen_events_device(gens[r], f, m, d_b, cap, d_o)
+                c2.submit_device(d_b, nb, d_o, m)
+                c2.sync()
+            for k, v in c2.drain_buckets().items():
+                ref[k] = ref.get(k, 0) + v
+    for c in ctxs:
+        c.close()
+    return {"config": "configs[4] with %d shards (%d GPU(s) visible): real-time producers, %d events/s in all, "
+                      "skew +-50 ms, late p=1e-5 (core.clj:166-174); %d ms ticks, one global watermark"
+                      % (n, ndev.value, rate, args.batch_ms),
+            "shards": n, "devices": ndev.value, "events": op.events, "batches": op.batches, "flushes": op.flushes,
+            "window_close_latency": op.latency_summary(), "open_at_end": op.open_at_end,
+            "exact_vs_batch_path": op.totals == ref, "rows": len(ref)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["config3", "tbl", "general", "pcie", "stream"])
+    ap.add_argument("mode", choices=["config3", "tbl", "general", "pcie", "stream", "stream_sharded"])
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--segment", type=int, default=12_500_000)
     ap.add_argument("--steps", type=int, default=20)
@@ -310,8 +395,10 @@ def main():
     ap.add_argument("--c3-rate", type=int, default=100_000, help="config3: events per second of event time")
     ap.add_argument("--batch-ms", type=int, default=100)
     ap.add_argument("--ooo-ms", type=int, default=100)
+    ap.add_argument("--shards", type=int, default=2, help="stream_sharded: contexts (one per GPU)")
     args = ap.parse_args()
-    out = {"config3": config3, "tbl": tbl, "general": general, "pcie": pcie, "stream": stream}[args.mode](args)
+    out = {"config3": config3, "tbl": tbl, "general": general, "pcie": pcie, "stream": stream,
+           "stream_sharded": stream_sharded}[args.mode](args)
     print(json.dumps(out), flush=True)
 
 
