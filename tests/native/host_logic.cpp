@@ -38,11 +38,14 @@ int main() {
     s.seed = 5; s.n_campaigns = 100; s.ads_per_campaign = 10; s.t0_ms = -123456789; s.events_per_sec = 3;
     s.n_pick = 1000;
     char line[400];
-    for (u32 tbl = 0; tbl < 2; ++tbl) {   // JSON lines and .tbl rows
-        s.tbl = tbl;
-        for (u64 i = 0; i < 5000; ++i) {
-            GenEvent e = gen_event(s, i);
-            CHECK(gen_line_len(s, e) == gen_line_write(s, i, e, line));
+    for (u32 tbl = 0; tbl < 2; ++tbl) {   // JSON lines and .tbl rows, every layout variant
+        for (u32 v = 0; v < 8; ++v) {
+            s.tbl = tbl;
+            s.variant = v;
+            for (u64 i = 0; i < 5000; ++i) {
+                GenEvent e = gen_event(s, i);
+                CHECK(gen_line_len(s, i, e) == gen_line_write(s, i, e, line));
+            }
         }
     }
     std::printf("%s\n", fails ? "FAILED" : "OK");
