@@ -1086,7 +1086,16 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         // HBM lines per view at the price of a dependent load for the few others.
         uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, a2 = a0, b0 = a0, b1 = a0, b2 = a0;
         u32 ib_s = 0;
+#ifdef YSB_DIAG_NO_PROBE
+        if (pend) {   // diagnostic build: the first slot "holds" the key, campaign from its bytes
+            a0 = make_uint4(ca.kw[0], ca.kw[1], ca.kw[2], ca.kw[3]);
+            a1 = make_uint4(ca.kw[4], ca.kw[5], ca.kw[6], ca.kw[7]);
+            a2 = make_uint4(ca.kw[8], ca.kw[0] % P.n_campaigns, 0, 0);
+        }
+        if (false) {
+#else
         if (pend) {
+#endif
             u32 ia, ib;
             cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
 #if YSB_PROBE_NT
@@ -1183,6 +1192,9 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             }
 #endif
         }
+#ifdef YSB_DIAG_NO_REC
+        rec_has = false;   // diagnostic build: views found and parsed, never counted
+#endif
         if constexpr (REC) {
             // stage this tile's records, a 32-lane half at a time (a half adds <= 32 to a
             // bin whose ring holds < 32 unwritten ones: the 64-record ring never overflows),

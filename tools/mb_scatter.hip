@@ -71,6 +71,19 @@ __global__ __launch_bounds__(64) void k(const unsigned char* __restrict__ buf, u
             const uint4 a = p[0], b = p[1], c = p[2];
             acc += a.x ^ b.y ^ c.z;
         }
+        if (MODE == 8) {   // the same 21 x 48 B as ONE instruction: lanes 3r..3r+2 load view r's parts
+            const u32 r = lane / 3, part = lane % 3;
+            if (lane < 63) {
+                const u64 hr = mix(t * 64 + r);
+                const uint4 a = probe_tab[4 * (hr & probe_mask) + part];
+                acc += a.x ^ a.y;
+            }
+        }
+        if (MODE == 9 && act) {   // 2 loads (32 B) per view
+            const uint4* p = probe_tab + 4 * (h & probe_mask);
+            const uint4 a = p[0], b = p[1];
+            acc += a.x ^ b.y;
+        }
         if (MODE == 7) {
             if (pprobe) acc += pa.x ^ pb.y ^ pc.z;
             pprobe = act;
@@ -133,7 +146,8 @@ int main(int argc, char** argv) {
     hipEventCreate(&b);
     const char* names[] = {"stream only", "u64 atomics, 1 GiB", "u32 scattered stores, 1 GiB",
                            "LDS-staged 128-B record lines", "u64 atomics deferred one tile",
-                           "u64 atomics, 16 MiB", "48-B probes, same tile", "48-B probes, next tile"};
+                           "u64 atomics, 16 MiB", "48-B probes, same tile", "48-B probes, next tile",
+                           "48-B probes as one 63-lane load", "32-B probes (2 loads)"};
     int only = argc > 1 ? atoi(argv[1]) : -1;
     if (only == 6) {   // probe cost vs table size
         for (u64 sz : {1ull << 26, 1ull << 24, 1ull << 22, 1ull << 21, 1ull << 20}) {
@@ -151,7 +165,8 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    for (int mode = 0; mode < 8; ++mode) {
+    for (int mode = 0; mode < 10; ++mode) {
+        if (only >= 0 && mode != only && !(only == 100 && (mode == 0 || mode == 6 || mode == 8 || mode == 9))) continue;
         float best = 1e9;
         for (int rep = 0; rep < 6; ++rep) {
             hipEventRecord(a);
@@ -159,6 +174,7 @@ int main(int argc, char** argv) {
             switch (mode) {
                 case 0: L(0); break; case 1: L(1); break; case 2: L(2); break; case 3: L(3); break;
                 case 4: L(4); break; case 5: L(5); break; case 6: L(6); break; case 7: L(7); break;
+                case 8: L(8); break; case 9: L(9); break;
             }
             hipEventRecord(b);
             hipEventSynchronize(b);
