@@ -68,6 +68,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-check", action="store_true", help="skip the generator-truth check")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[2] / .tbl extra measurements")
     ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--stream-seconds", type=int, default=22,
+                    help="extras: seconds of real-time sharded streaming (configs[4]); 0 skips it")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and set up torch.distributed, then stop before any GPU call")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -348,6 +350,14 @@ def extras(args, device):
                                    args.warmup, "ysb::scan_kernel<false, false, false>")
             free_segments(ctx, segs)
         log("extras: %s %.2f G events/s" % (key, out[key]["events_per_s"] / 1e9))
+    if args.stream_seconds > 0:
+        # configs[4]: real-time producers into double-buffered pinned slots of 2 contexts
+        # (2 shards; on a one-GPU box both on it), one global watermark, p99 close latency
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_extra
+        ns = argparse.Namespace(shards=2, rate=1_000_000, seconds=args.stream_seconds, batch_ms=20, ooo_ms=100)
+        out["stream_sharded"] = bench_extra.stream_sharded(ns)
+        log("extras: stream %s" % json.dumps(out["stream_sharded"]["window_close_latency"]))
     return out
 
 

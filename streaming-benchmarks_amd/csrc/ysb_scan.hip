@@ -1058,7 +1058,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             // second and third tiers for the lanes the vocabulary path rejected (a branch
             // no lane takes on the generator's own lines): any values in the generator's
             // layout, then the same keys as compact JSON
-            if (elig && !ok2) {
+            if (__builtin_expect(elig && !ok2, 0)) {
                 CanonA c2;
                 CanonB b2;
                 b2.view = false;
