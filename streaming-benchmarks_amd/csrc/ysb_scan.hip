@@ -472,6 +472,9 @@ __device__ __forceinline__ u32 swar_digits4(u32 w, u32& bad) {
 #ifndef YSB_VOCAB
 #define YSB_VOCAB 1
 #endif
+#ifndef YSB_FLAT_TIER
+#define YSB_FLAT_TIER 1   // flat objects in any key order: in the scan (fourth tier) and the deferred-line kernel
+#endif
 #ifndef YSB_CANON_TIERS
 #define YSB_CANON_TIERS 1
 #endif
@@ -629,13 +632,10 @@ __device__ __forceinline__ bool tbl_stage2(const LdsSrc& src, int s, int e, cons
 // Per-thread tallies go to st[].
 struct Tally { u32 ev, view, join, miss, perr, terr, oor; };
 
-// The general path (lines that are not in the generator's layout).
+// A parsed event's filter, join and bucket (the bolts after DeserializeBolt).
 template <class S>
-__device__ __forceinline__ bool process_line(const S& src, int s, int e, const ScanParams& P,
-                                             Tally& t, u32& campaign, i64& bucket) {
-    Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
-    t.ev++;
-    if (!parse_line(src, s, e, P.require_mask, ad, et, tm)) { t.perr++; return false; }
+__device__ __forceinline__ bool finish_line(const S& src, const Span& ad, const Span& et, const Span& tm,
+                                            const ScanParams& P, Tally& t, u32& campaign, i64& bucket) {
     if (!span_is_view(src, et)) return false;                // EventFilterBolt
     t.view++;
     u32 kw[KEY_WORDS];
@@ -648,6 +648,146 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
     if (!span_long(src, tm, tv)) { t.terr++; return false; }   // CampaignProcessorCommon :58
     campaign = (u32)c;
     bucket = div_trunc(tv, P.div);
+    return true;
+}
+
+// The general path (lines that are not in the generator's layout).
+template <class S>
+__device__ __forceinline__ bool process_line(const S& src, int s, int e, const ScanParams& P,
+                                             Tally& t, u32& campaign, i64& bucket) {
+    Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
+    t.ev++;
+    if (!parse_line(src, s, e, P.require_mask, ad, et, tm)) { t.perr++; return false; }
+    return finish_line(src, ad, et, tm, P, t, campaign, bucket);
+}
+
+// ---- the general path's flat tier --------------------------------------------------------
+// A flat object of plain double-quoted string pairs whose keys are all DeserializeBolt's
+// -- in any order, with any whitespace nextClean skips, ',' or ';' between pairs and a
+// separator allowed before '}' -- is decided here with word-at-a-time string scans over
+// the staged line instead of org.json's character machine.  On exactly this subset the
+// steps are JSONObject(JSONTokener)'s: nextClean '{'; per pair nextClean -> '"' ->
+// nextString, nextClean ':', nextClean '"' -> nextString, putOnce; nextClean ',' | ';'
+// (then '}' closes) | '}' (org.json 20180813 JSONObject.java constructor).  Anything
+// else -- another key, a repeated key, a value that is not a plain string, a quote other
+// than '"', an escape, a control byte or NUL, a missing field -- returns false having
+// counted nothing, and parse_line decides the line.
+__device__ __forceinline__ u32 zero_bytes(u32 x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
+
+// The next byte > ' ' at or after p (its position; c = the byte), or -1 if the end of
+// the line or a NUL comes first.  Four bytes per step; of the two flag sets the lowest
+// flagged byte is exact (a false flag only sits above a true one: zero_bytes' borrow
+// above a zero byte, the +0x5F carry above a byte >= 0xA1, itself flagged by its top bit).
+template <class S>
+__device__ __forceinline__ int ft_clean(const S& src, int p, int e, u32& c) {
+    for (; p < e; p += 4) {
+        const u32 x = src.load4(p);
+        const u32 z = (((x + 0x5F5F5F5Fu) | x) & 0x80808080u) | zero_bytes(x);
+        if (z != 0u) {
+            const int k = __builtin_ctz(z) >> 3;
+            c = (x >> (8 * k)) & 0xFFu;
+            return (p + k < e && c != 0u) ? p + k : -1;
+        }
+    }
+    return -1;
+}
+
+// The closing '"' of a string whose content starts at p, or -1 if a backslash, a control
+// byte or the end of the line comes first (lowest flagged byte exact, as above).  16
+// bytes per step: four independent LDS words (may read up to 15 bytes past e; a flag
+// there is rejected by the at < e test).
+__device__ __forceinline__ u32 ft_flags(u32 w) {
+    return zero_bytes(w ^ 0x22222222u) | zero_bytes(w ^ 0x5C5C5C5Cu) | zero_bytes(w & 0xE0E0E0E0u);
+}
+template <class S>
+__device__ __forceinline__ int ft_string_end(const S& src, int p, int e) {
+    int q = p & ~3;
+    u32 first = 0xFFFFFFFFu << ((p & 3) << 3);
+    for (;;) {
+        u32 w[4], z[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = src.d[(q >> 2) + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[k] = ft_flags(w[k]);
+        z[0] &= first;
+        u32 zz = 0, ww = 0;
+        int base = 0;
+#pragma unroll
+        for (int k = 3; k >= 0; --k)
+            if (z[k] != 0u) { zz = z[k]; ww = w[k]; base = 4 * k; }
+        if (zz != 0u) {
+            const int bi = __builtin_ctz(zz) >> 3;
+            const int at = q + base + bi;
+            return (at < e && ((ww >> (8 * bi)) & 0xFFu) == '"') ? at : -1;
+        }
+        q += 16;
+        first = 0xFFFFFFFFu;
+        if (q >= e) return -1;
+    }
+}
+
+// true: the line is a flat object of the subset above with every field of `require` (and
+// the three the topology reads); ad / et / tm = the values' spans
+template <class S>
+__device__ __forceinline__ bool flat_parse(const S& src, int s, int e, u32 require, Span& ad, Span& et, Span& tm) {
+    u32 c = 0;
+    int p = ft_clean(src, s, e, c);
+    if (p < 0 || c != '{') return false;
+    u32 seen = 0;
+    for (;;) {
+        p = ft_clean(src, p + 1, e, c);                       // a key, or '}'
+        if (p < 0) return false;
+        if (c == '}') break;                                  // {} or a separator before '}'
+        if (c != '"') return false;
+        const int ke = ft_string_end(src, p + 1, e);
+        if (ke < 0) return false;
+        const u32 id = match_key_raw(src, p + 1, ke - p - 1);
+        if (id == 0u || (seen & id) != 0u) return false;      // another key, or a repeat
+        seen |= id;
+        p = ft_clean(src, ke + 1, e, c);
+        if (p < 0 || c != ':') return false;
+        p = ft_clean(src, p + 1, e, c);
+        if (p < 0 || c != '"') return false;
+        const int ve = ft_string_end(src, p + 1, e);
+        if (ve < 0) return false;
+        const Span sp{p + 1, ve, 0};
+        if (id == K_AD) ad = sp;
+        else if (id == K_ETYPE) et = sp;
+        else if (id == K_ETIME) tm = sp;
+        p = ft_clean(src, ve + 1, e, c);
+        if (p < 0) return false;
+        if (c == '}') break;
+        if (c != ',' && c != ';') return false;
+    }
+    const u32 need = require | K_AD | K_ETYPE | K_ETIME;
+    return (seen & need) == need;
+}
+
+// The scan kernel's fourth tier: a flat line whose ad_id is 36 plain bytes, in the form
+// the canonical tiers hand on (key words, event_time offset and first 20 bytes, view).
+// Other ad_id lengths go to the deferred-line kernel (its table lookup takes any key).
+template <class S>
+__device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 require, CanonA& a, CanonB& b) {
+    Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
+    if (!flat_parse(src, ls, le, require, ad, et, tm) || ad.e - ad.s != 36) return false;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a.kw[k] = src.load4(ad.s + 4 * k);
+    a.t0 = tm.s - ls;
+    b.tlen = tm.e - tm.s;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) b.td[k] = 4 * k < b.tlen ? src.load4(tm.s + 4 * k) : 0u;
+    b.view = et.e - et.s == 4 && src.load4(et.s) == VIEW_W;
+    return true;
+}
+
+// The deferred-line kernel's use: true = decided here (ok = counted); false = nothing
+// counted, parse it in full.
+__device__ __forceinline__ bool flat_line(const LdsSrc3& src, int s, int e, const ScanParams& P, Tally& t,
+                                          u32& campaign, i64& bucket, bool& ok) {
+    Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
+    if (!flat_parse(src, s, e, P.require_mask, ad, et, tm)) return false;
+    t.ev++;
+    ok = finish_line(src, ad, et, tm, P, t, campaign, bucket);
     return true;
 }
 
@@ -1062,8 +1202,18 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 CanonA c2;
                 CanonB b2;
                 b2.view = false;
-                bool t = canon_stage1<false>(lsrc, ls, le, c2) && canon_stage2<false>(lsrc, ls, le, c2, b2);
-                if (!t) t = canon_stage1<true>(lsrc, ls, le, c2) && canon_stage2<true>(lsrc, ls, le, c2, b2);
+                // both canonical layouts open with {"user_id": then ' ' or '"' (byte 11)
+                const u32 h2 = lsrc.load4(ls + 8);
+                const bool up = lsrc.load4(ls) == w4('{', '"', 'u', 's') && lsrc.load4(ls + 4) == w4('e', 'r', '_', 'i') &&
+                                (h2 & 0xFFFFFFu) == (w4('d', '"', ':', 0) & 0xFFFFFFu);
+                bool t = false;
+                if (up && (h2 >> 24) == ' ')
+                    t = canon_stage1<false>(lsrc, ls, le, c2) && canon_stage2<false>(lsrc, ls, le, c2, b2);
+                else if (up && (h2 >> 24) == '"')
+                    t = canon_stage1<true>(lsrc, ls, le, c2) && canon_stage2<true>(lsrc, ls, le, c2, b2);
+#if YSB_FLAT_TIER
+                if (!t) t = flat_tier(lsrc, ls, le, P.require_mask, c2, b2);   // any key order / spacing
+#endif
                 if (t) {
                     ca = c2;
                     cb = b2;
@@ -1361,6 +1511,8 @@ __device__ __forceinline__ bool process_tbl_line(const S& src, int s, int e, con
 constexpr int DEFER_TPB = YSB_DEFER_TPB;
 constexpr int DEFER_REGION_DW = 81;                       // per-lane LDS region (odd: bank spread)
 constexpr int DEFER_STAGE_MAX = 4 * DEFER_REGION_DW - 16 - 16;   // line bytes staged (+ align, slack)
+constexpr int DEFER_CHUNKS = (15 + DEFER_STAGE_MAX + 15) / 16;   // 16-B chunks a staged line can span
+static_assert(4 * DEFER_CHUNKS + 1 <= DEFER_REGION_DW, "staged chunks + the slack word fit the region");
 
 __global__ __launch_bounds__(DEFER_TPB) void defer_kernel(const ScanParams P0) {
     __shared__ u32 stage[DEFER_TPB * DEFER_REGION_DW];
@@ -1396,25 +1548,39 @@ __global__ __launch_bounds__(DEFER_TPB) void defer_kernel(const ScanParams P0) {
         const int sh = (int)(ls - a16), len = (int)(le - ls);
         if (len <= DEFER_STAGE_MAX) {
             const int nch = (sh + len + 15) >> 4;
-            for (int k = 0; k < nch; ++k) {
+            // every chunk's load issued before any is stored (one memory latency per line,
+            // not one per chunk); P.bytes is 16-byte aligned
+            uint4 v[DEFER_CHUNKS];
+#pragma unroll
+            for (int k = 0; k < DEFER_CHUNKS; ++k) {
                 const u64 at = a16 + 16ull * (u64)k;
-                uint4 v;
-                if (at + 16 <= P.nbytes) {
-                    v = *reinterpret_cast<const uint4*>(P.bytes + at);   // P.bytes is 16-byte aligned
-                } else {                                               // the batch's last chunk: bytes, zeros past it
-                    u32 w[4] = {0u, 0u, 0u, 0u};
-                    for (int b = 0; b < 16 && at + b < P.nbytes; ++b) w[b >> 2] |= (u32)P.bytes[at + b] << (8 * (b & 3));
-                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                v[k] = (k < nch && at + 16 <= P.nbytes) ? *reinterpret_cast<const uint4*>(P.bytes + at)
+                                                        : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int k = 0; k < DEFER_CHUNKS; ++k) {
+                if (k < nch) {
+                    region[4 * k] = v[k].x;
+                    region[4 * k + 1] = v[k].y;
+                    region[4 * k + 2] = v[k].z;
+                    region[4 * k + 3] = v[k].w;
                 }
-                region[4 * k] = v.x;
-                region[4 * k + 1] = v.y;
-                region[4 * k + 2] = v.z;
-                region[4 * k + 3] = v.w;
+            }
+            const u64 last = a16 + 16ull * (u64)(nch - 1);
+            if (last + 16 > P.nbytes) {                        // the batch's last chunk: bytes, zeros past it
+                for (int b = 0; b < 16; ++b) {
+                    const u32 x = last + b < P.nbytes ? (u32)P.bytes[last + b] : 0u;
+                    if ((b & 3) == 0) region[4 * (nch - 1) + (b >> 2)] = 0u;
+                    region[4 * (nch - 1) + (b >> 2)] |= x << (8 * (b & 3));
+                }
             }
             region[4 * nch] = 0u;                           // slack for word reads past the end
             const LdsSrc3 lsrc{(lds_u32*)region};
-            ok = P.tbl ? process_tbl_line(lsrc, sh, sh + len, P, tl, campaign, bucket)
-                       : process_line(lsrc, sh, sh + len, P, tl, campaign, bucket);
+            if (P.tbl) ok = process_tbl_line(lsrc, sh, sh + len, P, tl, campaign, bucket);
+#if YSB_FLAT_TIER
+            else if (flat_line(lsrc, sh, sh + len, P, tl, campaign, bucket, ok)) {}
+#endif
+            else ok = process_line(lsrc, sh, sh + len, P, tl, campaign, bucket);
         } else {
             const GlbSrc gsrc{P.bytes + ls, le - ls};
             ok = P.tbl ? process_tbl_line(gsrc, 0, len, P, tl, campaign, bucket)

@@ -404,3 +404,92 @@ def test_vocabulary_fast_path_edges_match_oracle():
         out.append(ln)
     _oracle_vs_gpu(out, False)
     _oracle_vs_gpu(out, True, lds=False)
+
+
+def _flat_lines(seed, n):
+    """Generator events re-laid as flat objects: keys in a random order, whitespace and
+    ',' / ';' separators as nextClean sees them, a separator before '}' -- the general
+    path's flat tier -- plus, in about a third of the lines, one change that must send the
+    line to org.json's full machine (a repeated / unknown / missing key, a non-string or
+    single-quoted value, an escape, a control byte, NUL, a missing ':' ...)."""
+    raw, offs = gd.events("gen_s7")
+    bounds = list(offs) + [len(raw)]
+    import json
+    evs = [json.loads(raw[bounds[i]:bounds[i + 1]]) for i in range(len(offs))]
+    rng = np.random.default_rng(seed)
+    ws = ["", "", " ", "  ", "\t", "\x01", "\x1f ", "\r\n"]
+    times = ["1700000000000", "-5", "+17", "01700000000000", "9223372036854775807", "9223372036854775808", "1e3", ""]
+    out = []
+    for i in range(n):
+        ev = dict(evs[i % len(evs)])
+        if rng.random() < 0.2:
+            ev["event_time"] = times[int(rng.integers(len(times)))]
+        if rng.random() < 0.2:
+            ev["event_type"] = ["view", "click", "View", "view "][int(rng.integers(4))]
+        keys = list(ev)
+        rng.shuffle(keys)
+        pairs = [[k, v] for k, v in ((k, ev[k]) for k in keys)]
+        mut = int(rng.integers(30))
+        w = lambda: ws[int(rng.integers(len(ws)))]
+        def q(s):
+            return '"' + s + '"'
+        parts = None
+        if mut == 0:
+            pairs.append(list(pairs[int(rng.integers(len(pairs)))]))          # repeated key
+        elif mut == 1:
+            pairs.insert(int(rng.integers(len(pairs) + 1)), ["extra", "x"])   # another key
+        elif mut == 2:
+            del pairs[int(rng.integers(len(pairs)))]                           # missing key
+        elif mut == 3:
+            j = int(rng.integers(len(pairs)))
+            parts = (j, "value", "'" + pairs[j][1] + "'")                     # single-quoted value
+        elif mut == 4:
+            j = int(rng.integers(len(pairs)))
+            parts = (j, "value", pairs[j][1] or "1")                          # unquoted value
+        elif mut == 5:
+            j = int(rng.integers(len(pairs)))
+            parts = (j, "key", q(pairs[j][0][:1] + "\\u00" + "%02x" % ord(pairs[j][0][1]) + pairs[j][0][2:]))
+        elif mut == 6:
+            j = int(rng.integers(len(pairs)))
+            parts = (j, "value", q(pairs[j][1][:2] + "\\/" + pairs[j][1][2:]))
+        elif mut == 7:
+            j = int(rng.integers(len(pairs)))
+            parts = (j, "value", q(pairs[j][1][:1] + ["\x00", "\r", "\x02", "\x7f"][int(rng.integers(4))] + pairs[j][1][1:]))
+        elif mut == 8:
+            j = int(rng.integers(len(pairs)))
+            parts = (j, "sep", "=")                                             # no ':'
+        elif mut == 9:
+            j = int(rng.integers(len(pairs)))
+            parts = (j, "value", '{"a": "b"}')                                  # nested value
+        body = []
+        for j, (k, v) in enumerate(pairs):
+            ks, vs, sep = q(k), q(v), ":"
+            if parts and parts[0] == j:
+                if parts[1] == "value":
+                    vs = parts[2]
+                elif parts[1] == "key":
+                    ks = parts[2]
+                else:
+                    sep = parts[2]
+            body.append(w() + ks + w() + sep + w() + vs + w())
+        sepc = [",", ";"]
+        line = w() + "{" + "".join(b + (sepc[int(rng.integers(2))] if j + 1 < len(body) else "")
+                                   for j, b in enumerate(body))
+        if rng.random() < 0.2:
+            line += sepc[int(rng.integers(2))] + w()                            # separator before '}'
+        line += "}"
+        if mut == 10:
+            line += ["x", " {", "}", "\x00junk"][int(rng.integers(4))]           # after '}': not read
+        elif mut == 11:
+            line = line[: int(rng.integers(len(line)))]                          # truncated
+        out.append(line.encode("utf-8") + b"\n")
+    return out
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_flat_tier_matches_oracle(seed):
+    """The general path's flat tier (ysb_scan.hip flat_line) and its hand-offs to the
+    org.json machine: every counter and count equals the C oracle's."""
+    lines = _flat_lines(seed, 6000)
+    _oracle_vs_gpu(lines, False)
+    _oracle_vs_gpu(lines, True)

@@ -159,12 +159,21 @@ def general(args):
     _, aids = g.ids()
     n = min(args.events, 4_000_000)
     raw, offs = g.events_host(0, n)
-    data = raw.tobytes().replace(b'": "', b'":"')            # not the generator's layout any more
+    data = raw.tobytes()
+    if args.shape == "compact":      # '":"': the scan's compact tier takes these
+        data = data.replace(b'": "', b'":"')
+    elif args.shape == "reorder":    # page_id before user_id: no scan tier, the general path's flat tier
+        data = data.replace(b'{"user_id": ', b'{"XXXX_id": ').replace(b', "page_id": ', b', "user_id": ')
+        data = data.replace(b'{"XXXX_id": ', b'{"page_id": ')
+    elif args.shape == "spaced":     # '" : "': the flat tier too
+        data = data.replace(b'": "', b'" : "')
+    elif args.shape == "escaped":    # a \u escape in every key: org.json's full machine
+        data = data.replace(b'"ad_id"', b'"ad_\\u0069d"')
     offs2 = np.zeros(n, dtype=np.uint32)
     nl = np.flatnonzero(np.frombuffer(data, dtype=np.uint8) == 0x0A)
     offs2[1:] = (nl[:-1] + 1).astype(np.uint32)
-    ctx = YsbContext(n_campaigns=100, window_ring=1024, timing=True, max_batch_bytes=16 << 20,
-                     max_batch_events=1 << 16)
+    ctx = YsbContext(n_campaigns=100, window_ring=1024, timing=True, max_batch_bytes=args.batch_mb << 20,
+                     max_batch_events=(args.batch_mb << 20) // 200)
     ctx.load_ad_map(aids, g.ad_campaign_index())
     d_b, d_o = ctx.device_alloc(len(data) + 64), ctx.device_alloc(4 * n + 64)
     ctx.h2d(d_b, np.frombuffer(data, dtype=np.uint8))
@@ -172,18 +181,22 @@ def general(args):
     ctx.submit_device(d_b, len(data), d_o, n)
     ctx.sync()
     ctx.reset()
+    ctx.kernel_time()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.submit_device(d_b, len(data), d_o, n)
     ctx.sync()
     el = time.perf_counter() - t0
+    ctx.kernel_time()
+    dev_ms, launches, _ = ctx.path_time()
     ctx.reset()
     ctx.submit_device(d_b, len(data), d_o, n)
     got = ctx.drain_buckets()
     st = ctx.stats()
     rows, ost = orc.run(orc.AdMap(aids, g.ad_campaign_index()), data, offs2.tolist(), threads=8)
-    return {"config": "%d generator events without the space after ':' (all through the general parser)" % n,
+    return {"config": "%d generator events, shape %s" % (n, args.shape),
             "events_per_s": round(n * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
+            "device_ms_per_step": round(dev_ms / max(1, args.steps), 3), "launches": launches,
             "deferred": st["deferred"], "exact_vs_oracle": got == rows and all(st[k] == v for k, v in ost.items())}
 
 
@@ -395,6 +408,8 @@ def main():
     ap.add_argument("--c3-rate", type=int, default=100_000, help="config3: events per second of event time")
     ap.add_argument("--batch-ms", type=int, default=100)
     ap.add_argument("--ooo-ms", type=int, default=100)
+    ap.add_argument("--shape", default="reorder", choices=["generator", "compact", "reorder", "spaced", "escaped"],
+                    help="general: how the generator's lines are re-laid")
     ap.add_argument("--shards", type=int, default=2, help="stream_sharded: contexts (one per GPU)")
     args = ap.parse_args()
     out = {"config3": config3, "tbl": tbl, "general": general, "pcie": pcie, "stream": stream,
