@@ -430,7 +430,9 @@ def main():
 
     ctx = YsbContext(device=d.local, n_campaigns=100, window_ring=W, timing=True, ring_base_bucket=ring_base,
                      max_batch_bytes=16 << 20, max_batch_events=1 << 16)
-    ctx.load_ad_map(aids, camp)
+    # N > 1: the input is sharded by ad_id hash, so each rank holds only its shard of the
+    # join table; the post-exchange check proves nothing is missed
+    ctx.load_ad_map(aids, camp, shard=(d.rank, d.world) if d.world > 1 else None)
     if d.world > 1:
         uid = d.bcast_bytes(YsbContext.group_unique_id() if d.rank == 0 else None)
         ctx.group_init(d.rank, d.world, uid)

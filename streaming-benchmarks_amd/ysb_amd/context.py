@@ -71,9 +71,22 @@ class YsbContext:
         return check(rc, self._h)
 
     # -- join table --------------------------------------------------------------------
-    def load_ad_map(self, ad_ids, campaign_idx):
-        """ad_ids: sequence of str/bytes; campaign_idx: matching campaign indices."""
+    def load_ad_map(self, ad_ids, campaign_idx, shard=None):
+        """ad_ids: sequence of str/bytes; campaign_idx: matching campaign indices.
+
+        shard = (rank, nranks): load only the ads of this rank's ad_id-hash shard
+        (ysb_ad_shard) -- the join table sharded 1/N per GPU for
+        input that is pre-sharded by the same hash (bench.py's ranks, ysb_gen_dump_shards);
+        an event of another shard's ad is then a join miss, as the reference drops it."""
         keys = [a.encode() if isinstance(a, str) else bytes(a) for a in ad_ids]
+        if shard is not None:
+            from .generator import ad_shard
+            rank, nranks = shard
+            if not 0 <= rank < nranks:
+                raise ValueError("shard rank out of range")
+            pick = [i for i, k in enumerate(keys) if ad_shard(k, nranks) == rank]
+            campaign_idx = [campaign_idx[i] for i in pick]
+            keys = [keys[i] for i in pick]
         n = len(keys)
         arr = (C.c_char_p * max(n, 1))(*keys)
         lens = (C.c_uint32 * max(n, 1))(*[len(k) for k in keys])

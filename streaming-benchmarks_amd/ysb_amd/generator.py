@@ -107,8 +107,8 @@ def json_to_tbl(raw, offs):
     return out[:nb.value], oo[:offs.size]
 
 
-def ad_shard(ad_id: str, nranks: int) -> int:
-    b = ad_id.encode()
+def ad_shard(ad_id, nranks: int) -> int:
+    b = ad_id.encode() if isinstance(ad_id, str) else bytes(ad_id)
     return int(lib().ysb_ad_shard(b, len(b), nranks))
 
 

@@ -43,7 +43,8 @@ def test_bench_ranks_share_ring_base_and_sum_to_truth(world):
         g, aids, camp = rank_params(world, rank)
         with YsbContext(device=0, n_campaigns=100, window_ring=1024, ring_base_bucket=g.c.t0_ms // 10000 - 128,
                         max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
-            ctx.load_ad_map(aids, camp)
+            # bench.py: each rank loads only its ad_id-hash shard of the join table
+            ctx.load_ad_map(aids, camp, shard=(rank, world))
             cap = n * g.max_line_bytes()
             d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
             nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
@@ -105,3 +106,28 @@ def test_one_rank_group_runs_bench_exchange_check():
         lo, w = ctx.ring_range()
         ctx.ring_advance(lo + 1)
         assert ctx.ring_range() == (lo + 1, w)
+
+
+def test_sharded_join_table_misses_other_shards_ads():
+    """A rank's sharded table joins exactly its own shard's ads: another rank's events are
+    join misses (dropped, as RedisJoinBolt drops an unknown ad), its own all join."""
+    world = 4
+    n = 200_000
+    g0, aids, camp = rank_params(world, 0)
+    g1, _, _ = rank_params(world, 1)
+    with YsbContext(device=0, n_campaigns=100, window_ring=1024, ring_base_bucket=g0.c.t0_ms // 10000 - 128,
+                    max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
+        ctx.load_ad_map(aids, camp, shard=(0, world))
+        cap = n * g0.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
+        nb = ctx.gen_events_device(g1, 0, n, d_b, cap, d_o)   # rank 1's events
+        ctx.submit_device_segments([(d_b, nb, d_o, n)])
+        ctx.sync()
+        st = ctx.stats()
+        assert st["joined"] == 0 and st["join_misses"] == st["views"] > 0
+        ctx.reset()
+        nb = ctx.gen_events_device(g0, 0, n, d_b, cap, d_o)   # its own
+        ctx.submit_device_segments([(d_b, nb, d_o, n)])
+        ctx.sync()
+        st = ctx.stats()
+        assert st["join_misses"] == 0 and st["joined"] == st["views"] > 0
