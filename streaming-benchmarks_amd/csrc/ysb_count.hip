@@ -206,24 +206,38 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
             if (v[u] != REC_NONE) atomicAdd(&cnt[v[u] - base_cell], 1u);
     }
     __syncthreads();
-    // the slab: [base_cell, base_cell + cells) u64, as 16-B pairs
+    // the slab: [base_cell, base_cell + cells) u64, as 16-B pairs; 8 consecutive threads
+    // cover one 128-B line, and a line none of whose 16 cells was counted is neither read
+    // nor written (the ring slots this launch's buckets do not reach: ~a fifth of the slab
+    // for 100 live buckets of 128), so every store is still a whole line
     uint4* ring = reinterpret_cast<uint4*>(R.counts + base_cell);
-    const u32 pairs = cells / 2;
+    const u32 pairs = cells / 2;   // a multiple of 8
     constexpr int SU = 8;
     for (u32 p0 = 0; p0 < pairs; p0 += REC_TPB * SU) {
+        uint2 c[SU];
+        bool live[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+            const u32 p = p0 + u * REC_TPB + tid;
+            c[u] = p < pairs ? reinterpret_cast<const uint2*>(cnt)[p] : make_uint2(0u, 0u);
+            u32 any = c[u].x | c[u].y;
+            any |= __shfl_xor(any, 1, 64);
+            any |= __shfl_xor(any, 2, 64);
+            any |= __shfl_xor(any, 4, 64);
+            live[u] = p < pairs && any != 0u;
+        }
         uint4 r[SU];
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
             const u32 p = p0 + u * REC_TPB + tid;
-            if (p < pairs) r[u] = ring[p];
+            if (live[u]) r[u] = ring[p];
         }
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
             const u32 p = p0 + u * REC_TPB + tid;
-            if (p < pairs) {
-                const uint2 c = reinterpret_cast<const uint2*>(cnt)[p];
-                unsigned long long lo = ((unsigned long long)r[u].y << 32 | r[u].x) + c.x;
-                unsigned long long hi = ((unsigned long long)r[u].w << 32 | r[u].z) + c.y;
+            if (live[u]) {
+                unsigned long long lo = ((unsigned long long)r[u].y << 32 | r[u].x) + c[u].x;
+                unsigned long long hi = ((unsigned long long)r[u].w << 32 | r[u].z) + c[u].y;
                 ring[p] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
             }
         }

@@ -77,3 +77,20 @@ def test_record_mode_multi_segment_launch(big_map, ring):
     exp, _ = oracle.run(oracle.AdMap(aids, camp), raw, offs)
     rows, _, nrec = counts(aids, camp, 200_000, raw, offs, record=True, ring=ring, segments=5)
     assert nrec == 1 and rows == exp
+
+
+@pytest.mark.timeout(300)
+def test_record_mode_flat_tier_lines(big_map):
+    """Lines in another key order (the scan's flat tier) counted in record mode: the flat
+    tier hands the same key words / time / view flag on, so counts equal the oracle's."""
+    g, aids, raw, offs = big_map
+    camp = g.ad_campaign_index()
+    data = raw.tobytes()
+    data = data.replace(b'{"user_id": ', b'{"XXXX_id": ').replace(b', "page_id": ', b', "user_id": ')
+    data = data.replace(b'{"XXXX_id": ', b'{"page_id": ')
+    raw2 = np.frombuffer(data, dtype=np.uint8)
+    exp, est = oracle.run(oracle.AdMap(aids, camp), raw2, offs)
+    rows, st, nrec = counts(aids, camp, 200_000, raw2, offs, record=True)
+    assert nrec == 1 and rows == exp and st["deferred"] == 0
+    for k, v in est.items():
+        assert st[k] == v, k
