@@ -34,7 +34,8 @@ struct ysb_ctx {
     u32* d_table = nullptr;
     u64 table_slots = 0;
     u32* d_ctable = nullptr;   // 36-byte-key cuckoo table
-    u64 ctable_slots = 0;
+    u64 ctable_slots = 0;      // slots, or buckets when ctable_buckets
+    bool ctable_buckets = false; // HBM-resident table: 3-entry 128-B buckets (CB_*), serial probes
     CuckooSeed cseed{};
     bool ctable_partial = false;
     bool table_loaded = false;
@@ -380,6 +381,13 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
     }
     u64 cslots = 64;
     while (cslots < 4 * keys36.size()) cslots <<= 1;
+    // tables far beyond the L2s (32 MiB) go to HBM per probe: bucket layout
+    const bool buckets = cslots * CSLOT_WORDS * 4 > (64ull << 20);
+    if (buckets) {
+        cslots = 64;
+        while (cslots < 2 * keys36.size()) cslots <<= 1;
+    }
+    const u32 unit = buckets ? CB_WORDS : CSLOT_WORDS;
     std::vector<u32> ct;
     CuckooSeed cs{};
     u64 seed = 0x5EEDC0FFEEULL;
@@ -394,10 +402,56 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         }
         seed = mix64(seed + (u64)attempt + cslots);
         cs = cuckoo_seed(seed);
-        ct.assign(cslots * CSLOT_WORDS, 0);
-        for (u64 s = 0; s < cslots; ++s) ct[s * CSLOT_WORDS + CSLOT_CAMP] = EMPTY_SLOT;
+        ct.assign(cslots * unit, 0);
         const u32 cm = (u32)(cslots - 1);
         bool ok = true;
+        if (buckets) {
+            for (u64 s = 0; s < cslots; ++s)
+                for (u32 e = 0; e < CB_ENTRIES; ++e) ct[s * CB_WORDS + e * CB_STRIDE + CKEY_WORDS] = EMPTY_SLOT;
+            u64 rng = seed;
+            for (const auto& kv : keys36) {
+                Key36 k = kv.first;
+                u32 camp = kv.second;
+                u32 a, b;
+                cuckoo_slots36(k.data(), cs, cm, &a, &b);
+                u32 pos = a;
+                bool placed = false;
+                for (int kicks = 0; kicks <= 500 && !placed; ++kicks) {
+                    // the first bucket while it has room; the second only when the first is full
+                    for (u32 cand : {pos, pos == a ? b : a}) {
+                        u32* bk = &ct[(u64)cand * CB_WORDS];
+                        for (u32 e = 0; e < CB_ENTRIES && !placed; ++e)
+                            if (bk[e * CB_STRIDE + CKEY_WORDS] == EMPTY_SLOT) {
+                                std::memcpy(bk + e * CB_STRIDE, k.data(), 36);
+                                bk[e * CB_STRIDE + CKEY_WORDS] = camp;
+                                placed = true;
+                            }
+                        if (placed || kicks > 0) break;   // an evicted key tries only its other bucket
+                    }
+                    if (placed) break;
+                    // both full: evict a random entry of pos, which keeps pos full
+                    rng = mix64(rng + 1);
+                    const u32 e = (u32)(rng % CB_ENTRIES);
+                    u32* en = &ct[(u64)pos * CB_WORDS + e * CB_STRIDE];
+                    Key36 ok_;
+                    std::memcpy(ok_.data(), en, 36);
+                    const u32 oc = en[CKEY_WORDS];
+                    std::memcpy(en, k.data(), 36);
+                    en[CKEY_WORDS] = camp;
+                    k = ok_;
+                    camp = oc;
+                    u32 oa, ob;
+                    cuckoo_slots36(k.data(), cs, cm, &oa, &ob);
+                    pos = (pos == oa) ? ob : oa;   // the evicted key's other bucket
+                    a = oa;
+                    b = ob;
+                }
+                if (!placed) { ok = false; if (!partial) break; }
+            }
+            if (ok || partial) break;
+            continue;
+        }
+        for (u64 s = 0; s < cslots; ++s) ct[s * CSLOT_WORDS + CSLOT_CAMP] = EMPTY_SLOT;
         for (const auto& kv : keys36) {
             Key36 k = kv.first;
             u32 camp = kv.second;
@@ -437,6 +491,7 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
     }
     HIPCHK(c, hipMemcpy(c->d_ctable, ct.data(), ct.size() * 4, hipMemcpyHostToDevice));
     c->cseed = cs;
+    c->ctable_buckets = buckets;
     c->ctable_partial = partial;
     c->table_loaded = true;
     return YSB_OK;
@@ -459,8 +514,8 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     p.ctable_mask = (u32)(c->ctable_slots - 1);
     p.cseed = c->cseed;
     p.ctable_partial = c->ctable_partial ? 1u : 0u;
-    // tables far beyond the L2s (32 MiB) go to HBM per probe: serial slots halve the lines
-    p.probe_serial = c->ctable_slots * CSLOT_WORDS * 4 > (64ull << 20) ? 1u : 0u;
+    // HBM-resident table: buckets, the second one read only after a miss in a full first
+    p.probe_serial = c->ctable_buckets ? 1u : 0u;
     p.n_campaigns = c->cfg.n_campaigns;
     p.counts = c->d_counts;
     p.ring_w = c->cfg.window_ring;
@@ -544,8 +599,9 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     const u32 W = c->cfg.window_ring;
     const u64 cells = (u64)c->c_pad * W;
     const bool force = (c->cfg.flags & YSB_F_RECORD_COUNT) != 0;
+    // (the record-mode kernels are the HBM-table instantiations: bucket-layout join table)
     if ((c->cfg.flags & YSB_F_NO_RECORD_COUNT) || c->lds_wl || p.dyn_chunk || cells >= (1ull << 32) ||
-        W > (u32)REC_BLOCK_CELLS)
+        W > (u32)REC_BLOCK_CELLS || !c->ctable_buckets)
         return YSB_OK;
     if (!force && (cells < (1ull << 20) || n_events < (1ull << 20))) return YSB_OK;
     r.ring_w = W;
@@ -584,7 +640,6 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     r.runs = c->d_runs;
     r.counts = c->d_counts;
     p.rec_on = 1;
-    p.probe_serial = 1;   // the record-mode kernels are the HBM-table (serial probe) instantiations
     p.rec_bins = r.bins;
     p.rec_shift = r.blk_shift + r.sub_log2;
     p.rec_cap = r.cap;

@@ -311,6 +311,14 @@ YSB_HD u32 key_hash(const u32* w, u32 len) {
 #define YSB_CSLOT_WORDS 16
 #endif
 enum : u32 { CSLOT_WORDS = YSB_CSLOT_WORDS, CKEY_WORDS = 9, CSLOT_CAMP = 9, CSLOT_Q = YSB_CSLOT_WORDS / 4 };
+// HBM-resident tables (beyond the L2s: configs[2]'s 10M ads) use BUCKETS instead: 128 B =
+// 3 entries of [9 key words, campaign] at a 10-word stride (+ 2 spare words).  A key goes
+// to its first bucket while that has a free entry, to its second only when the first is
+// full (cuckoo eviction keeps a full bucket full), so a lookup reads one 128-B line and
+// reads the second bucket only when the key is not in a FULL first bucket -- at 2 buckets
+// per key ~0.1 % of keys instead of the ~8 % a one-key slot table leaves in its second
+// slot, each of which cost the whole wave a dependent HBM round trip.
+enum : u32 { CB_WORDS = 32, CB_ENTRIES = 3, CB_STRIDE = 10, CB_Q = CB_WORDS / 4 };
 
 struct CuckooSeed {
     u32 s[CKEY_WORDS];   // additive salts of the XOR fold

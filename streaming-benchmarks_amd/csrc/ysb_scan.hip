@@ -905,14 +905,30 @@ constexpr int AUX_NT = YSB_AUX_NT;
 #ifndef YSB_SETPRIO
 #define YSB_SETPRIO 1
 #endif
-#ifndef YSB_PROBE_NT
-#define YSB_PROBE_NT 0
-#endif
 
-__device__ __forceinline__ uint4 nt_load4(const uint4* p) {
-    typedef u32 v4u __attribute__((ext_vector_type(4)));
-    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
-    return make_uint4(v[0], v[1], v[2], v[3]);
+// The campaign of key k in a 128-B bucket (EMPTY_SLOT: not there); full = all three
+// entries taken (only then may the key sit in its second bucket)
+__device__ __forceinline__ u32 bucket_find(const uint4 (&q)[CB_Q], const u32* k, bool& full) {
+    u32 w[CB_WORDS];
+#pragma unroll
+    for (int j = 0; j < (int)CB_Q; ++j) {
+        w[4 * j] = q[j].x;
+        w[4 * j + 1] = q[j].y;
+        w[4 * j + 2] = q[j].z;
+        w[4 * j + 3] = q[j].w;
+    }
+    u32 found = EMPTY_SLOT;
+    full = true;
+#pragma unroll
+    for (int e = 0; e < (int)CB_ENTRIES; ++e) {
+        u32 d = 0;
+#pragma unroll
+        for (int j = 0; j < (int)CKEY_WORDS; ++j) d |= w[e * CB_STRIDE + j] ^ k[j];
+        const u32 c = w[e * CB_STRIDE + CKEY_WORDS];
+        if (c == EMPTY_SLOT) full = false;
+        else if (d == 0u) found = c;
+    }
+    return found;
 }
 #ifndef YSB_PREFETCH_DEPTH
 #define YSB_PREFETCH_DEPTH 1
@@ -1226,21 +1242,26 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
 #endif
         dfr = li < cur.count && !ok2;   // bad offsets, other layouts, escapes, over-size tiles
         pend = ok2 && cb.view;                                             // EventFilterBolt
-        // RedisJoinBolt's lookup (36-byte keys): both cuckoo slots, views only (a third
-        // of the lanes: scattered loads cost address-unit time per lane), issued before
-        // the time parse and the next tile's prefetch so their latency hides under both
-        // and waiting for them never waits for the prefetch.
-        // Cache-resident table (config 2): both slots at once.  HBM-resident table
-        // (config 3, P.probe_serial): the second slot only after the first missed -- the
-        // build places almost every key in its first slot, so this halves the random
-        // HBM lines per view at the price of a dependent load for the few others.
+        // RedisJoinBolt's lookup (36-byte keys), views only (a third of the lanes:
+        // scattered loads cost address-unit time per lane), issued before the time parse
+        // and the next tile's prefetch so their latency hides under both and waiting for
+        // them never waits for the prefetch.
+        // Cache-resident table (config 2): both cuckoo slots at once.  HBM-resident table
+        // (config 3, SERIAL): the key's first 128-B bucket; the second only when the key
+        // is not in a full first bucket (ysb_common.h CB_*), ~0.1 % of the keys.
         uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, a2 = a0, b0 = a0, b1 = a0, b2 = a0;
+        uint4 q[CB_Q];
+#pragma unroll
+        for (int j = 0; j < (int)CB_Q; ++j) q[j] = a0;
         u32 ib_s = 0;
 #ifdef YSB_DIAG_NO_PROBE
-        if (pend) {   // diagnostic build: the first slot "holds" the key, campaign from its bytes
+        if (pend) {   // diagnostic build: the first slot / entry "holds" the key, campaign from its bytes
             a0 = make_uint4(ca.kw[0], ca.kw[1], ca.kw[2], ca.kw[3]);
             a1 = make_uint4(ca.kw[4], ca.kw[5], ca.kw[6], ca.kw[7]);
             a2 = make_uint4(ca.kw[8], ca.kw[0] % P.n_campaigns, 0, 0);
+            q[0] = a0;
+            q[1] = a1;
+            q[2] = a2;
         }
         if (false) {
 #else
@@ -1248,16 +1269,12 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
 #endif
             u32 ia, ib;
             cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
-#if YSB_PROBE_NT
-            if constexpr (SERIAL) {   // HBM-resident table: the probe lines are never reused
-                a0 = nt_load4(&ct4[CSLOT_Q * (u64)ia]);
-                a1 = nt_load4(&ct4[CSLOT_Q * (u64)ia + 1]);
-                a2 = nt_load4(&ct4[CSLOT_Q * (u64)ia + 2]);
-            } else
-#endif
-            { a0 = ct4[CSLOT_Q * (u64)ia]; a1 = ct4[CSLOT_Q * (u64)ia + 1]; a2 = ct4[CSLOT_Q * (u64)ia + 2]; }
-            ib_s = ib;
-            if constexpr (!SERIAL) {
+            if constexpr (SERIAL) {
+#pragma unroll
+                for (int j = 0; j < (int)CB_Q; ++j) q[j] = ct4[CB_Q * (u64)ia + j];
+                ib_s = ib;
+            } else {
+                a0 = ct4[CSLOT_Q * (u64)ia]; a1 = ct4[CSLOT_Q * (u64)ia + 1]; a2 = ct4[CSLOT_Q * (u64)ia + 2];
                 b0 = ct4[CSLOT_Q * (u64)ib]; b1 = ct4[CSLOT_Q * (u64)ib + 1]; b2 = ct4[CSLOT_Q * (u64)ib + 2];
             }
         }
@@ -1279,23 +1296,26 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         // ---- Phase B2: join result ------------------------------------------------
         bool valid = false, dfr2 = false;
         u32 campaign = 0;
-#ifndef YSB_DIAG_NO_PROBE2
-        if (SERIAL && pend) {   // the second slot only when the first does not hold the key
-            const u32* k = ca.kw;
-            const u32 da0 = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
-                            (a1.y ^ k[5]) | (a1.z ^ k[6]) | (a1.w ^ k[7]) | (a2.x ^ k[8]);
-            if (da0 != 0u || a2.y == EMPTY_SLOT) {
-                b0 = ct4[CSLOT_Q * (u64)ib_s]; b1 = ct4[CSLOT_Q * (u64)ib_s + 1]; b2 = ct4[CSLOT_Q * (u64)ib_s + 2];
-            }
-        }
-#endif
         if (pend) {
             const u32* k = ca.kw;
-            const u32 da = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
-                           (a1.y ^ k[5]) | (a1.z ^ k[6]) | (a1.w ^ k[7]) | (a2.x ^ k[8]);
-            const u32 db = (b0.x ^ k[0]) | (b0.y ^ k[1]) | (b0.z ^ k[2]) | (b0.w ^ k[3]) | (b1.x ^ k[4]) |
-                           (b1.y ^ k[5]) | (b1.z ^ k[6]) | (b1.w ^ k[7]) | (b2.x ^ k[8]);
-            const u32 ci = (da == 0u && a2.y != EMPTY_SLOT) ? a2.y : (db == 0u ? b2.y : EMPTY_SLOT);
+            u32 ci;
+            if constexpr (SERIAL) {
+                bool full;
+                ci = bucket_find(q, k, full);
+#ifndef YSB_DIAG_NO_PROBE2
+                if (ci == EMPTY_SLOT && full) {   // the second bucket
+#pragma unroll
+                    for (int j = 0; j < (int)CB_Q; ++j) q[j] = ct4[CB_Q * (u64)ib_s + j];
+                    ci = bucket_find(q, k, full);
+                }
+#endif
+            } else {
+                const u32 da = (a0.x ^ k[0]) | (a0.y ^ k[1]) | (a0.z ^ k[2]) | (a0.w ^ k[3]) | (a1.x ^ k[4]) |
+                               (a1.y ^ k[5]) | (a1.z ^ k[6]) | (a1.w ^ k[7]) | (a2.x ^ k[8]);
+                const u32 db = (b0.x ^ k[0]) | (b0.y ^ k[1]) | (b0.z ^ k[2]) | (b0.w ^ k[3]) | (b1.x ^ k[4]) |
+                               (b1.y ^ k[5]) | (b1.z ^ k[6]) | (b1.w ^ k[7]) | (b2.x ^ k[8]);
+                ci = (da == 0u && a2.y != EMPTY_SLOT) ? a2.y : (db == 0u ? b2.y : EMPTY_SLOT);
+            }
             if (ci == EMPTY_SLOT) {
                 if (P.ctable_partial) {   // the key may be one the cuckoo build left out
                     dfr2 = true;

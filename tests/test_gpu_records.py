@@ -94,3 +94,38 @@ def test_record_mode_flat_tier_lines(big_map):
     assert nrec == 1 and rows == exp and st["deferred"] == 0
     for k, v in est.items():
         assert st[k] == v, k
+
+
+@pytest.fixture(scope="module")
+def huge_map():
+    g = GenParams(seed=13, n_campaigns=600_000, ads_per_campaign=2, events_per_sec=1000)
+    _, aids = g.ids()
+    raw, offs = g.events_host(0, 200_000)
+    return g, aids, raw, offs
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("record", [True, False])
+def test_bucket_table_sparse_and_misses(huge_map, record):
+    """The HBM-resident (bucket-layout) cuckoo table: 1.2M ads, a tenth of them missing
+    from the map (join misses, dropped) and every other remaining key left out of the
+    table (as a failed placement would: their views take the general path) -- counts and
+    counters equal the oracle's, in record and in atomic mode."""
+    g, aids, raw, offs = huge_map
+    camp = g.ad_campaign_index()
+    keep = [i for i in range(len(aids)) if i % 10 != 3]
+    a2, c2 = [aids[i] for i in keep], [camp[i] for i in keep]
+    exp, est = oracle.run(oracle.AdMap(a2, c2), raw, offs)
+    with YsbContext(n_campaigns=600_000, window_ring=16, record_count=record, sparse_fast_join=True,
+                    max_batch_bytes=raw.size + 64, max_batch_events=offs.size + 1, timing=True) as ctx:
+        ctx.load_ad_map(a2, c2)
+        ctx.submit(raw, offs)
+        rows = ctx.drain_buckets()
+        st = ctx.stats()
+        ctx.kernel_time()
+        nrec = ctx.path_time()[2]
+    assert nrec == (1 if record else 0)
+    assert st["deferred"] > 0 and st["join_misses"] > 0
+    assert rows == exp
+    for k, v in est.items():
+        assert st[k] == v, k

@@ -13,6 +13,8 @@
 //   mode 5: u64 atomicAdd into a random cell of a 16 MiB table
 //   mode 6: 48-B random reads of a 4 GiB table, consumed in the same tile (probe)
 //   mode 7: like 6, consumed one tile later (pipelined probe)
+//   mode 10: 128-B bucket reads (one 128-B line per probe); 11: 48-B probes plus, for 1 in
+//   13 lanes, a dependent second probe (serial cuckoo); 12: 64-B probes
 //
 //   hipcc --offload-arch=gfx950 -O3 -o mb_scatter tools/mb_scatter.hip && ./mb_scatter
 #include <hip/hip_runtime.h>
@@ -84,6 +86,29 @@ __global__ __launch_bounds__(64) void k(const unsigned char* __restrict__ buf, u
             const uint4 a = p[0], b = p[1];
             acc += a.x ^ b.y;
         }
+        if (MODE == 10 && act) {   // a 128-B bucket: 8 x 16 B of one 128-B line
+            const uint4* p = probe_tab + 8 * (h & (probe_mask >> 1));
+            uint4 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = p[q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc += v[q].x ^ v[q].w;
+        }
+        if (MODE == 11 && act) {   // 48-B probe, then (1 in 13 lanes) a dependent second one
+            const uint4* p = probe_tab + 4 * (h & probe_mask);
+            const uint4 a = p[0], b = p[1], c = p[2];
+            acc += a.x ^ b.y ^ c.z;
+            if ((h >> 40) % 13 == 0) {
+                const uint4* p2 = probe_tab + 4 * (((h >> 20) ^ a.x) & probe_mask);
+                const uint4 a2 = p2[0], b2 = p2[1], c2 = p2[2];
+                acc += a2.x ^ b2.y ^ c2.z;
+            }
+        }
+        if (MODE == 12 && act) {   // 64-B probe: 4 x 16 B of one 64-B slot
+            const uint4* p = probe_tab + 4 * (h & probe_mask);
+            const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+            acc += a.x ^ b.y ^ c.z ^ d.w;
+        }
         if (MODE == 7) {
             if (pprobe) acc += pa.x ^ pb.y ^ pc.z;
             pprobe = act;
@@ -147,7 +172,9 @@ int main(int argc, char** argv) {
     const char* names[] = {"stream only", "u64 atomics, 1 GiB", "u32 scattered stores, 1 GiB",
                            "LDS-staged 128-B record lines", "u64 atomics deferred one tile",
                            "u64 atomics, 16 MiB", "48-B probes, same tile", "48-B probes, next tile",
-                           "48-B probes as one 63-lane load", "32-B probes (2 loads)"};
+                           "48-B probes as one 63-lane load", "32-B probes (2 loads)",
+                           "128-B bucket probes (8 loads)", "48-B probes + 1/13 dependent 2nd",
+                           "64-B probes (4 loads)"};
     int only = argc > 1 ? atoi(argv[1]) : -1;
     if (only == 6) {   // probe cost vs table size
         for (u64 sz : {1ull << 26, 1ull << 24, 1ull << 22, 1ull << 21, 1ull << 20}) {
@@ -165,8 +192,9 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    for (int mode = 0; mode < 10; ++mode) {
-        if (only >= 0 && mode != only && !(only == 100 && (mode == 0 || mode == 6 || mode == 8 || mode == 9))) continue;
+    for (int mode = 0; mode < 13; ++mode) {
+        if (only >= 0 && mode != only && !(only == 100 && (mode == 0 || mode == 6 || mode == 8 || mode == 9)) &&
+            !(only == 101 && (mode == 0 || mode == 6 || mode >= 10))) continue;
         float best = 1e9;
         for (int rep = 0; rep < 6; ++rep) {
             hipEventRecord(a);
@@ -174,7 +202,8 @@ int main(int argc, char** argv) {
             switch (mode) {
                 case 0: L(0); break; case 1: L(1); break; case 2: L(2); break; case 3: L(3); break;
                 case 4: L(4); break; case 5: L(5); break; case 6: L(6); break; case 7: L(7); break;
-                case 8: L(8); break; case 9: L(9); break;
+                case 8: L(8); break; case 9: L(9); break; case 10: L(10); break; case 11: L(11); break;
+                case 12: L(12); break;
             }
             hipEventRecord(b);
             hipEventSynchronize(b);
