@@ -1050,28 +1050,20 @@ __device__ __forceinline__ void rec_fallback(const ScanParams& P, u32 cell, i64 
     global_add(P, ring_lo, ring_set, c, b, 1u, tl);
 }
 
-// Record mode: writes every staged full 32-record line (final: also the partial tails) of
-// the workgroup's level-1 bins to its HBM sub-buffers -- one 128-B store by lanes 0..31
-// per line.  rcur / rfl / the ring live in LDS, gcur in lane b of a VGPR; one wave.
-__device__ __forceinline__ void rec_flush_full(const ScanParams& P, u32* ring, u32* rcur, u32* rfl, u32& gcur,
-                                               int lane, i64 ring_lo, bool ring_set, bool final, Tally& tl) {
-    const u32 nb = P.rec_bins;
-    const u32 need = final ? 1u : 32u;
-    u64 full = __ballot(lane < (int)nb && rcur[lane] - rfl[lane] >= need);
-    while (full) {
-        const u32 b = (u32)__builtin_ctzll(full);
-        const u32 fl = rfl[b];
-        const u32 k = min(rcur[b] - fl, 32u);
-        const u32 g = (u32)__builtin_amdgcn_readlane((int)gcur, (int)b);
-        if ((u32)lane < k) {
-            const u32 v = ring[b * REC_RING + ((fl + lane) & (REC_RING - 1))];
-            if (g + k <= P.rec_cap) P.rec[((u64)blockIdx.x * nb + b) * P.rec_cap + g + lane] = v;
-            else rec_fallback(P, v, ring_lo, ring_set, tl);
-        }
-        if (g + k <= P.rec_cap && lane == (int)b) gcur = g + k;
-        if (lane == 0) rfl[b] = fl + k;
-        if (rcur[b] - (fl + k) < need) full &= full - 1;
+// Record mode: writes n (<= 32) staged records of bin b, ring positions [fl, fl + n), to
+// the workgroup's HBM sub-buffer of the bin -- one store by lanes 0..n-1, a whole 128-B
+// line when n = 32 -- or, once that sub-buffer is full, to the ring atomics (slower,
+// exact).  Lane b of gcur = records in bin b's sub-buffer; one wave.
+__device__ __forceinline__ void rec_write(const ScanParams& P, const u32* ring, u32 b, u32 fl, u32 n, u32& gcur,
+                                          int lane, i64 ring_lo, bool ring_set, Tally& tl) {
+    const u32 g = (u32)__builtin_amdgcn_readlane((int)gcur, (int)b);
+    const bool fits = g + n <= P.rec_cap;
+    if ((u32)lane < n) {
+        const u32 v = ring[b * REC_RING + ((fl + (u32)lane) & (REC_RING - 1))];
+        if (fits) P.rec[((u64)blockIdx.x * P.rec_bins + b) * P.rec_cap + g + (u32)lane] = v;
+        else rec_fallback(P, v, ring_lo, ring_set, tl);
     }
+    if (fits && lane == (int)b) gcur = g + n;
 }
 
 // SERIAL: HBM-resident cuckoo table, second slot probed only after a first-slot miss (a
@@ -1103,13 +1095,11 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
     const u32 ncells = WL ? P.n_campaigns * WL : 0u;
     for (u32 i = tid; i < ncells; i += SCAN_TPB) lcnt[i] = 0;
     // record mode (no LDS window counters): the counter area holds a 64-record staging ring
-    // per level-1 bin (lcnt), the misc area the rings' cursors: rcur[b] = records staged,
-    // rfl[b] = records written out (multiples of 32 until the final flush); lane b of gcur
-    // = records of bin b in this workgroup's HBM sub-buffer
+    // per level-1 bin (lcnt), the misc area the rings' cursors rcur[b] = records staged;
+    // lane b of gcur = records of bin b in this workgroup's HBM sub-buffer
     u32* rcur = reinterpret_cast<u32*>(misc64);
-    u32* rfl = rcur + REC_BINS_MAX;
     u32 gcur = 0;
-    if (REC && tid < 2 * REC_BINS_MAX) rcur[tid] = 0;
+    if (REC && tid < REC_BINS_MAX) rcur[tid] = 0;
     // rebase requests of the LDS window (double-buffered by tile parity): the largest
     // bucket that fell ahead of the window, INT64_MIN = none
     if (!REC && tid < 2) misc64[tid] = INT64_MIN;
@@ -1367,15 +1357,25 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
 #endif
         if constexpr (REC) {
             // stage this tile's records, a 32-lane half at a time (a half adds <= 32 to a
-            // bin whose ring holds < 32 unwritten ones: the 64-record ring never overflows),
-            // each followed by writing out every full 128-B line
+            // bin whose ring holds < 32 unwritten ones: the 64-record ring never overflows);
+            // the lane whose record takes position 32k + 31 completed line k of its bin
+            // and has it written out (no cursor reads: one LDS round trip per half)
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
-                if (rec_has && (tid >> 5) == half) {
-                    const u32 pos = atomicAdd(&rcur[rec_bin], 1u);
+                const bool mine = rec_has && (tid >> 5) == half;
+                u32 pos = 0;
+                if (mine) {
+                    pos = atomicAdd(&rcur[rec_bin], 1u);
                     lcnt[rec_bin * REC_RING + (pos & (REC_RING - 1))] = rec_val;
                 }
-                rec_flush_full(P, lcnt, rcur, rfl, gcur, lane, ring_lo, ring_set, false, tl);
+                unsigned long long done = __ballot(mine && (pos & 31u) == 31u);
+                while (done) {
+                    const int src = (int)__builtin_ctzll(done);
+                    done &= done - 1;
+                    const u32 b = (u32)__builtin_amdgcn_readlane((int)rec_bin, src);
+                    const u32 p = (u32)__builtin_amdgcn_readlane((int)pos, src);
+                    rec_write(P, lcnt, b, p - 31u, 32u, gcur, lane, ring_lo, ring_set, tl);
+                }
             }
         }
         STAMP(4);
@@ -1446,7 +1446,11 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         }
     }
     if constexpr (REC) {   // the staged tails (partial lines), then the records per sub-buffer
-        rec_flush_full(P, lcnt, rcur, rfl, gcur, lane, ring_lo, ring_set, true, tl);
+        // the tails: the records after each bin's last complete line
+        for (u32 b = 0; b < P.rec_bins; ++b) {
+            const u32 staged = rcur[b], n = staged & 31u;
+            if (n) rec_write(P, lcnt, b, staged - n, n, gcur, lane, ring_lo, ring_set, tl);
+        }
         if (tid < (int)P.rec_bins) P.rec_n[(u64)blockIdx.x * P.rec_bins + tid] = gcur;
     }
     if (n_run == 0) return;   // no segment has tiles for this workgroup (nothing touched)
