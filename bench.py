@@ -336,7 +336,9 @@ def extras(args, device):
     # the same events as other producers would write them: off the vocabulary fast path,
     # taken by the scan's canonical tiers (ysb_scan.hip canon_stage1/2)
     from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP
-    for key, variant, what in (("tier2_random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
+    for key, variant, what in (("random_ip", GEN_RANDOM_IP, "random dotted-quad ip_address (the vocabulary "
+                                                           "path's generic ip value)"),
+                               ("tier2_random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
                                 "random dotted-quad ip_address and 8 ad_types (second tier)"),
                                ("tier3_compact_json", GEN_COMPACT, "compact JSON, no space after ':' and ',' "
                                                                    "(third tier)")):

@@ -414,6 +414,61 @@ __device__ __forceinline__ bool canon_stage1(const LdsSrc& src, int s, int e, Ca
     return d == 0u && c.e6 + 2 <= L;
 }
 
+// ---- word-at-a-time byte scans (the vocabulary path's ip value, the flat tier) -------------
+__device__ __forceinline__ u32 zero_bytes(u32 x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
+
+// The next byte > ' ' at or after p (its position; c = the byte), or -1 if the end of
+// the line or a NUL comes first.  Four bytes per step; of the two flag sets the lowest
+// flagged byte is exact (a false flag only sits above a true one: zero_bytes' borrow
+// above a zero byte, the +0x5F carry above a byte >= 0xA1, itself flagged by its top bit).
+template <class S>
+__device__ __forceinline__ int ft_clean(const S& src, int p, int e, u32& c) {
+    for (; p < e; p += 4) {
+        const u32 x = src.load4(p);
+        const u32 z = (((x + 0x5F5F5F5Fu) | x) & 0x80808080u) | zero_bytes(x);
+        if (z != 0u) {
+            const int k = __builtin_ctz(z) >> 3;
+            c = (x >> (8 * k)) & 0xFFu;
+            return (p + k < e && c != 0u) ? p + k : -1;
+        }
+    }
+    return -1;
+}
+
+// The closing '"' of a string whose content starts at p, or -1 if a backslash, a control
+// byte or the end of the line comes first (lowest flagged byte exact, as above).  16
+// bytes per step: four independent LDS words (may read up to 15 bytes past e; a flag
+// there is rejected by the at < e test).
+__device__ __forceinline__ u32 ft_flags(u32 w) {
+    return zero_bytes(w ^ 0x22222222u) | zero_bytes(w ^ 0x5C5C5C5Cu) | zero_bytes(w & 0xE0E0E0E0u);
+}
+template <class S>
+__device__ __forceinline__ int ft_string_end(const S& src, int p, int e) {
+    int q = p & ~3;
+    u32 first = 0xFFFFFFFFu << ((p & 3) << 3);
+    for (;;) {
+        u32 w[4], z[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = src.d[(q >> 2) + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[k] = ft_flags(w[k]);
+        z[0] &= first;
+        u32 zz = 0, ww = 0;
+        int base = 0;
+#pragma unroll
+        for (int k = 3; k >= 0; --k)
+            if (z[k] != 0u) { zz = z[k]; ww = w[k]; base = 4 * k; }
+        if (zz != 0u) {
+            const int bi = __builtin_ctz(zz) >> 3;
+            const int at = q + base + bi;
+            return (at < e && ((ww >> (8 * bi)) & 0xFFu) == '"') ? at : -1;
+        }
+        q += 16;
+        first = 0xFFFFFFFFu;
+        if (q >= e) return -1;
+    }
+}
+
 struct CanonB {   // after the second LDS batch
     bool view;
     u32 td[5];     // event_time bytes (first 20)
@@ -534,9 +589,11 @@ __device__ __forceinline__ bool vocab_stage2(const LdsSrc& src, int s, int e, co
             (t4[3] ^ w4('p', 'e', '"', ':')) | ((t4[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
     d |= (t5[0] ^ w4('"', ',', ' ', '"')) | (t5[1] ^ w4('e', 'v', 'e', 'n')) | (t5[2] ^ w4('t', '_', 't', 'i')) |
          (t5[3] ^ w4('m', 'e', '"', ':')) | ((t5[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
-    d |= (t6[0] ^ w4('"', ',', ' ', '"')) | (t6[1] ^ w4('i', 'p', '_', 'a')) | (t6[2] ^ w4('d', 'd', 'r', 'e')) |
-         (t6[3] ^ w4('s', 's', '"', ':')) | (t6[4] ^ w4(' ', '"', '1', '.')) | (t6[5] ^ w4('2', '.', '3', '.')) |
-         ((t6[6] & 0xFFFFFFu) ^ w4('4', '"', '}', 0));
+    const u32 dkey = (t6[0] ^ w4('"', ',', ' ', '"')) | (t6[1] ^ w4('i', 'p', '_', 'a')) |
+                     (t6[2] ^ w4('d', 'd', 'r', 'e')) | (t6[3] ^ w4('s', 's', '"', ':')) |
+                     ((t6[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
+    const u32 dip = ((t6[4] >> 16) ^ (w4('1', '.', 0, 0))) | (t6[5] ^ w4('2', '.', '3', '.')) |
+                    ((t6[6] & 0xFFFFFFu) ^ w4('4', '"', '}', 0));
     // the event_type value: exactly the one its first byte named
     const int Le = a.e4 - a.e3 - 18;
     const bool etok = Le == 4   ? ev[0] == w4('v', 'i', 'e', 'w')
@@ -551,7 +608,14 @@ __device__ __forceinline__ bool vocab_stage2(const LdsSrc& src, int s, int e, co
     c.view = Le == 4;
     c.tlen = 13;
     // org.json's JSONObject(String) stops at the closing '}': what follows is never read.
-    return d == 0u && etok && bad == 0u;
+    const bool pre = d == 0u && dkey == 0u && etok && bad == 0u;
+    if (__builtin_expect(pre && dip != 0u, 0)) {
+        // another ip address (a branch the generator's lines never take): any plain string
+        // value -- no quote, backslash or control byte before its closing quote -- then '}'
+        const int q = ft_string_end(src, s + a.e5 + 18, e);
+        return q >= 0 && q + 1 < e && src.b(q + 1) == '}';
+    }
+    return pre && dip == 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -672,60 +736,6 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
 // else -- another key, a repeated key, a value that is not a plain string, a quote other
 // than '"', an escape, a control byte or NUL, a missing field -- returns false having
 // counted nothing, and parse_line decides the line.
-__device__ __forceinline__ u32 zero_bytes(u32 x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
-
-// The next byte > ' ' at or after p (its position; c = the byte), or -1 if the end of
-// the line or a NUL comes first.  Four bytes per step; of the two flag sets the lowest
-// flagged byte is exact (a false flag only sits above a true one: zero_bytes' borrow
-// above a zero byte, the +0x5F carry above a byte >= 0xA1, itself flagged by its top bit).
-template <class S>
-__device__ __forceinline__ int ft_clean(const S& src, int p, int e, u32& c) {
-    for (; p < e; p += 4) {
-        const u32 x = src.load4(p);
-        const u32 z = (((x + 0x5F5F5F5Fu) | x) & 0x80808080u) | zero_bytes(x);
-        if (z != 0u) {
-            const int k = __builtin_ctz(z) >> 3;
-            c = (x >> (8 * k)) & 0xFFu;
-            return (p + k < e && c != 0u) ? p + k : -1;
-        }
-    }
-    return -1;
-}
-
-// The closing '"' of a string whose content starts at p, or -1 if a backslash, a control
-// byte or the end of the line comes first (lowest flagged byte exact, as above).  16
-// bytes per step: four independent LDS words (may read up to 15 bytes past e; a flag
-// there is rejected by the at < e test).
-__device__ __forceinline__ u32 ft_flags(u32 w) {
-    return zero_bytes(w ^ 0x22222222u) | zero_bytes(w ^ 0x5C5C5C5Cu) | zero_bytes(w & 0xE0E0E0E0u);
-}
-template <class S>
-__device__ __forceinline__ int ft_string_end(const S& src, int p, int e) {
-    int q = p & ~3;
-    u32 first = 0xFFFFFFFFu << ((p & 3) << 3);
-    for (;;) {
-        u32 w[4], z[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = src.d[(q >> 2) + k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) z[k] = ft_flags(w[k]);
-        z[0] &= first;
-        u32 zz = 0, ww = 0;
-        int base = 0;
-#pragma unroll
-        for (int k = 3; k >= 0; --k)
-            if (z[k] != 0u) { zz = z[k]; ww = w[k]; base = 4 * k; }
-        if (zz != 0u) {
-            const int bi = __builtin_ctz(zz) >> 3;
-            const int at = q + base + bi;
-            return (at < e && ((ww >> (8 * bi)) & 0xFFu) == '"') ? at : -1;
-        }
-        q += 16;
-        first = 0xFFFFFFFFu;
-        if (q >= e) return -1;
-    }
-}
-
 // true: the line is a flat object of the subset above with every field of `require` (and
 // the three the topology reads); ad / et / tm = the values' spans
 template <class S>
