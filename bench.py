@@ -333,15 +333,14 @@ def extras(args, device):
                                  args.warmup, "ysb::scan_kernel<false, true, false>")
         free_segments(ctx, segs)
     log("extras: tbl %.2f G events/s" % (out["tbl"]["events_per_s"] / 1e9))
-    # the same events as other producers would write them: off the vocabulary fast path,
-    # taken by the scan's canonical tiers (ysb_scan.hip canon_stage1/2)
+    # the same events as other producers would write them: other ip / ad_type values (the
+    # vocabulary path's generic-value branches) and compact JSON (the scan's third tier)
     from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP
-    for key, variant, what in (("random_ip", GEN_RANDOM_IP, "random dotted-quad ip_address (the vocabulary "
-                                                           "path's generic ip value)"),
-                               ("tier2_random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
-                                "random dotted-quad ip_address and 8 ad_types (second tier)"),
-                               ("tier3_compact_json", GEN_COMPACT, "compact JSON, no space after ':' and ',' "
-                                                                   "(third tier)")):
+    for key, variant, what in (("random_ip", GEN_RANDOM_IP, "random dotted-quad ip_address"),
+                               ("random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
+                                "random dotted-quad ip_address and 8 ad_types"),
+                               ("compact_json", GEN_COMPACT, "compact JSON, no space after ':' and ',' "
+                                                             "(third tier)")):
         g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, variant=variant)
         _, aids = g.ids()
         with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True,

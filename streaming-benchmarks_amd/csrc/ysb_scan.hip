@@ -567,8 +567,18 @@ __device__ __forceinline__ bool vocab_stage1(const LdsSrc& src, int s, int e, Ca
              W[44] == w4('a', 'r', 'c', 'h'))
         La = 16;
     // event_type's first byte at 164 + La + 18 (bytes 186 / 187 / 188 / 198)
-    const u32 et0 = La == 4 ? (W[46] >> 16) & 0xFFu : La == 5 ? W[46] >> 24 : La == 6 ? W[47] & 0xFFu
-                                                                                    : (W[49] >> 16) & 0xFFu;
+    u32 et0 = La == 4 ? (W[46] >> 16) & 0xFFu : La == 5 ? W[46] >> 24 : La == 6 ? W[47] & 0xFFu
+                                                                              : (W[49] >> 16) & 0xFFu;
+    if (__builtin_expect(La == 0 && d == 0u, 0)) {
+        // another ad_type (a branch the generator's lines never take): any plain string
+        // value -- no quote, backslash or control byte before its closing quote; stage 2
+        // checks everything after that quote as for the five
+        const int q = ft_string_end(src, s + 164, e);
+        if (q > s + 164 && q - s - 164 <= 64) {
+            La = q - s - 164;
+            et0 = src.b(q + 18);
+        }
+    }
     const int Le = et0 == 'v' ? 4 : et0 == 'c' ? 5 : et0 == 'p' ? 8 : 0;
     c.e3 = 164 + La;           // closing quote of ad_type
     c.e4 = c.e3 + 18 + Le;     // of event_type

@@ -83,3 +83,40 @@ def test_tier_mixed_with_off_template_lines():
     for k, v in est.items():
         assert st[k] == v, k
     assert 0 < st["deferred"] <= 1000
+
+
+def test_canonical_tier_other_event_types_and_times():
+    """Lines in the generator's layout whose event_type is none of the three or whose
+    event_time is not 13 digits (the vocabulary path names both from closed sets) go to
+    the canonical tier, not to the general path: exact, nothing deferred."""
+    g = GenParams(seed=31, n_campaigns=40, ads_per_campaign=10, events_per_sec=1000,
+                  variant=GEN_RANDOM_IP | GEN_MORE_AD_TYPES)
+    _, aids = g.ids()
+    raw, offs = g.events_host(0, 60_000)
+    lines = bytes(raw).split(b"\n")[:-1]
+    ets = [b'"impression"', b'"View"', b'"views"', b'""']
+    out = []
+    for i, ln in enumerate(lines):
+        if i % 2 == 0:
+            for et in (b'"view"', b'"click"', b'"purchase"'):
+                ln = ln.replace(b'"event_type": ' + et, b'"event_type": ' + ets[(i // 2) % 4])
+        if i % 3 == 0:
+            j = ln.index(b'"event_time": "') + 15
+            k = ln.index(b'"', j)
+            t = ln[j:k]
+            ln = ln[:j] + [t + b"1", t[:-2], b"-" + t, t[:5] + b"x" + t[6:], b"0" + t][(i // 3) % 5] + ln[k:]
+        out.append(ln)
+    data = b"\n".join(out) + b"\n"
+    offs2 = np.zeros(len(out), dtype=np.uint32)
+    offs2[1:] = np.cumsum([len(x) + 1 for x in out[:-1]])
+    exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), data, offs2)
+    with YsbContext(n_campaigns=40, window_ring=256, max_batch_bytes=len(data) + 64,
+                    max_batch_events=len(out) + 1) as ctx:
+        ctx.load_ad_map(aids, g.ad_campaign_index())
+        ctx.submit(data, offs2)
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+    assert got == exp
+    for k, v in est.items():
+        assert st[k] == v, k
+    assert st["deferred"] == 0 and st["time_errors"] > 0

@@ -1,4 +1,4 @@
 set -e
 cd /root/repo
-mkdir -p gpurun_out/ip2; rm -f gpurun_out/ip2/*
-timeout -k 10 400 python bench.py --steps 20 --warmup 10 --no-cpu > gpurun_out/ip2/bench.json 2> gpurun_out/ip2/bench.err
+mkdir -p gpurun_out/ip4; rm -f gpurun_out/ip4/*
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tiers.py > gpurun_out/ip4/tests.log 2>&1
