@@ -534,12 +534,54 @@ __device__ __forceinline__ u32 swar_digits4(u32 w, u32& bad) {
 #define YSB_CANON_TIERS 1
 #endif
 constexpr int VOC_WORDS = 50;            // line bytes 0..199
-constexpr int VOC_MIN_LEN = 248;         // 240 + shortest ad_type (4) + event_type (4)
 
+// Expected bytes [from, to) of str as N words + byte masks (compile time).
+template <int N>
+struct WordTpl {
+    u32 e[N];
+    u32 m[N];
+};
+template <int N>
+constexpr WordTpl<N> make_words(const char* str, int from, int to) {
+    WordTpl<N> t{};
+    for (int pos = from; pos < to; ++pos) {
+        t.e[pos >> 2] |= (u32)(u8)str[pos] << (8 * (pos & 3));
+        t.m[pos >> 2] |= 0xFFu << (8 * (pos & 3));
+    }
+    return t;
+}
+template <int N>
+__device__ __forceinline__ u32 words_diff(const u32 (&w)[N], const WordTpl<N>& t) {
+    u32 d = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (t.m[k] == 0xFFFFFFFFu) d |= w[k] ^ t.e[k];
+        else if (t.m[k] != 0u) d |= (w[k] ^ t.e[k]) & t.m[k];
+    }
+    return d;
+}
+// bytes POS..POS+3 / byte POS of the line from its aligned words W (compile-time POS)
+template <int POS, int N>
+__device__ __forceinline__ u32 word_at(const u32 (&W)[N]) {
+    if constexpr ((POS & 3) == 0) return W[POS >> 2];
+    else return __builtin_amdgcn_alignbyte(W[(POS >> 2) + 1], W[POS >> 2], (u32)(POS & 3));
+}
+template <int POS, int N>
+__device__ __forceinline__ u32 byte_at(const u32 (&W)[N]) {
+    return (W[POS >> 2] >> (8 * (POS & 3))) & 0xFFu;
+}
+
+// The vocabulary path for the generator's layout (CP = false: ": " and ", ") and the same
+// keys as compact JSON (CP = true: ":" and ",", the third tier's lines).
+template <bool CP>
 __device__ __forceinline__ bool vocab_stage1(const LdsSrc& src, int s, int e, CanonA& c) {
-    constexpr PrefixTpl T = make_prefix_tpl();
+    using G = CanonGeo<CP>;
+    constexpr PrefixTpl T = CP ? make_compact_tpl() : make_prefix_tpl();
+    constexpr int PF = G::PREFIX, SEP = G::SEP, AD = G::AD;
+    constexpr int MINLEN = PF + 4 + 4 + 3 * SEP + 13 + 7 + 2;   // shortest ad_type and event_type
+    static_assert(PF + 16 + SEP < 4 * VOC_WORDS, "the event_type's first byte is among the words read");
     const int L = e - s;
-    if (L < VOC_MIN_LEN) return false;
+    if (L < MINLEN) return false;
     const int a = s >> 2;
     const u32 sb = (u32)(s & 3);
     u32 P[VOC_WORDS + 1];
@@ -549,63 +591,67 @@ __device__ __forceinline__ bool vocab_stage1(const LdsSrc& src, int s, int e, Ca
 #pragma unroll
     for (int j = 0; j < VOC_WORDS; ++j) W[j] = __builtin_amdgcn_alignbyte(P[j + 1], P[j], sb);   // bytes 4j..4j+3
 #pragma unroll
-    for (int j = 0; j < PREFIX_WORDS; ++j) {
+    for (int j = 0; j < G::PW; ++j) {
         if (T.m[j] == 0xFFFFFFFFu) d |= W[j] ^ T.e[j];
         else if (T.m[j] != 0u) d |= (W[j] ^ T.e[j]) & T.m[j];
         if (T.v[j] != 0u) d |= cand_z(W[j]) & T.v[j];
     }
 #pragma unroll
-    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(W[29 + k], W[28 + k], 1u);   // bytes 113..148
-    // ad_type at byte 164, exactly one of the five
-    const u32 a0 = W[41], a1 = W[42];
+    for (int k = 0; k < 9; ++k)   // the ad_id bytes
+        c.kw[k] = __builtin_amdgcn_alignbyte(W[(AD >> 2) + 1 + k], W[(AD >> 2) + k], (u32)(AD & 3));
+    // ad_type at byte PF, exactly one of the five
+    const u32 a0 = word_at<PF>(W), a1 = word_at<PF + 4>(W);
     int La = 0;
     if (a0 == w4('b', 'a', 'n', 'n') && (a1 & 0xFFFFu) == w4('e', 'r', 0, 0)) La = 6;
     else if (a0 == w4('m', 'a', 'i', 'l')) La = 4;
     else if (a0 == w4('m', 'o', 'd', 'a') && (a1 & 0xFFu) == 'l') La = 5;
     else if (a0 == w4('m', 'o', 'b', 'i') && (a1 & 0xFFFFu) == w4('l', 'e', 0, 0)) La = 6;
-    else if (a0 == w4('s', 'p', 'o', 'n') && a1 == w4('s', 'o', 'r', 'e') && W[43] == w4('d', '-', 's', 'e') &&
-             W[44] == w4('a', 'r', 'c', 'h'))
+    else if (a0 == w4('s', 'p', 'o', 'n') && a1 == w4('s', 'o', 'r', 'e') && word_at<PF + 8>(W) == w4('d', '-', 's', 'e') &&
+             word_at<PF + 12>(W) == w4('a', 'r', 'c', 'h'))
         La = 16;
-    // event_type's first byte at 164 + La + 18 (bytes 186 / 187 / 188 / 198)
-    u32 et0 = La == 4 ? (W[46] >> 16) & 0xFFu : La == 5 ? W[46] >> 24 : La == 6 ? W[47] & 0xFFu
-                                                                              : (W[49] >> 16) & 0xFFu;
+    // event_type's first byte at PF + La + SEP
+    u32 et0 = La == 4   ? byte_at<PF + 4 + SEP>(W)
+              : La == 5 ? byte_at<PF + 5 + SEP>(W)
+              : La == 6 ? byte_at<PF + 6 + SEP>(W)
+                        : byte_at<PF + 16 + SEP>(W);
     if (__builtin_expect(La == 0 && d == 0u, 0)) {
         // another ad_type (a branch the generator's lines never take): any plain string
         // value -- no quote, backslash or control byte before its closing quote; stage 2
         // checks everything after that quote as for the five
-        const int q = ft_string_end(src, s + 164, e);
-        if (q > s + 164 && q - s - 164 <= 64) {
-            La = q - s - 164;
-            et0 = src.b(q + 18);
+        const int q = ft_string_end(src, s + PF, e);
+        if (q > s + PF && q - s - PF <= 64) {
+            La = q - s - PF;
+            et0 = src.b(q + SEP);
         }
     }
     const int Le = et0 == 'v' ? 4 : et0 == 'c' ? 5 : et0 == 'p' ? 8 : 0;
-    c.e3 = 164 + La;           // closing quote of ad_type
-    c.e4 = c.e3 + 18 + Le;     // of event_type
-    c.e5 = c.e4 + 18 + 13;     // of event_time
-    c.e6 = c.e5 + 18 + 7;      // of ip_address
-    c.t0 = c.e4 + 18;
+    c.e3 = PF + La;            // closing quote of ad_type
+    c.e4 = c.e3 + SEP + Le;    // of event_type
+    c.e5 = c.e4 + SEP + 13;    // of event_time
+    c.e6 = c.e5 + SEP + 7;     // of ip_address
+    c.t0 = c.e4 + SEP;
     return d == 0u && La != 0 && Le != 0 && c.e6 + 2 <= L;
 }
 
+template <bool CP>
 __device__ __forceinline__ bool vocab_stage2(const LdsSrc& src, int s, int e, const CanonA& a, CanonB& c) {
+    using G = CanonGeo<CP>;
+    constexpr int SEP = G::SEP;
+    constexpr WordTpl<5> S4 = make_words<5>(CP ? "\",\"event_type\":\"" : "\", \"event_type\": \"", 0, SEP);
+    constexpr WordTpl<5> S5 = make_words<5>(CP ? "\",\"event_time\":\"" : "\", \"event_time\": \"", 0, SEP);
+    constexpr const char* TAIL = CP ? "\",\"ip_address\":\"1.2.3.4\"}" : "\", \"ip_address\": \"1.2.3.4\"}";
+    constexpr WordTpl<7> S6 = make_words<7>(TAIL, 0, SEP);              // the key
+    constexpr WordTpl<7> IP = make_words<7>(TAIL, SEP, SEP + 9);        // 1.2.3.4"}
     u32 t4[5], ev[2], t5[5], t6[7];
     load_span(src, s + a.e3, t4);
-    load_span(src, s + a.e3 + 18, ev);
+    load_span(src, s + a.e3 + SEP, ev);
     load_span(src, s + a.e4, t5);
-    load_span(src, s + a.e4 + 18, c.td);
+    load_span(src, s + a.e4 + SEP, c.td);
     load_span(src, s + a.e5, t6);
-    u32 d = (t4[0] ^ w4('"', ',', ' ', '"')) | (t4[1] ^ w4('e', 'v', 'e', 'n')) | (t4[2] ^ w4('t', '_', 't', 'y')) |
-            (t4[3] ^ w4('p', 'e', '"', ':')) | ((t4[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
-    d |= (t5[0] ^ w4('"', ',', ' ', '"')) | (t5[1] ^ w4('e', 'v', 'e', 'n')) | (t5[2] ^ w4('t', '_', 't', 'i')) |
-         (t5[3] ^ w4('m', 'e', '"', ':')) | ((t5[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
-    const u32 dkey = (t6[0] ^ w4('"', ',', ' ', '"')) | (t6[1] ^ w4('i', 'p', '_', 'a')) |
-                     (t6[2] ^ w4('d', 'd', 'r', 'e')) | (t6[3] ^ w4('s', 's', '"', ':')) |
-                     ((t6[4] & 0xFFFFu) ^ w4(' ', '"', 0, 0));
-    const u32 dip = ((t6[4] >> 16) ^ (w4('1', '.', 0, 0))) | (t6[5] ^ w4('2', '.', '3', '.')) |
-                    ((t6[6] & 0xFFFFFFu) ^ w4('4', '"', '}', 0));
+    const u32 d = words_diff(t4, S4) | words_diff(t5, S5);
+    const u32 dkey = words_diff(t6, S6), dip = words_diff(t6, IP);
     // the event_type value: exactly the one its first byte named
-    const int Le = a.e4 - a.e3 - 18;
+    const int Le = a.e4 - a.e3 - SEP;
     const bool etok = Le == 4   ? ev[0] == w4('v', 'i', 'e', 'w')
                       : Le == 5 ? (ev[0] == w4('c', 'l', 'i', 'c') && (ev[1] & 0xFFu) == 'k')
                                 : (ev[0] == w4('p', 'u', 'r', 'c') && ev[1] == w4('h', 'a', 's', 'e'));
@@ -622,7 +668,7 @@ __device__ __forceinline__ bool vocab_stage2(const LdsSrc& src, int s, int e, co
     if (__builtin_expect(pre && dip != 0u, 0)) {
         // another ip address (a branch the generator's lines never take): any plain string
         // value -- no quote, backslash or control byte before its closing quote -- then '}'
-        const int q = ft_string_end(src, s + a.e5 + 18, e);
+        const int q = ft_string_end(src, s + a.e5 + SEP, e);
         return q >= 0 && q + 1 < e && src.b(q + 1) == '}';
     }
     return pre && dip == 0u;
@@ -1206,7 +1252,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
-            else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1(lsrc, ls, le, ca);
+            else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1<false>(lsrc, ls, le, ca);
             else ok1 = canon_stage1<false>(lsrc, ls, le, ca);
         }
         bool pend = false, dfr = false, tok = false;
@@ -1216,7 +1262,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         bool ok2 = false;
         if (li < cur.count) {
             if constexpr (TBL) ok2 = ok1 && tbl_stage2(lsrc, ls, le, ca, cb);
-            else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2(lsrc, ls, le, ca, cb);
+            else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2<false>(lsrc, ls, le, ca, cb);
             else ok2 = ok1 && canon_stage2<false>(lsrc, ls, le, ca, cb);
         }
 #if YSB_CANON_TIERS
@@ -1235,8 +1281,10 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 bool t = false;
                 if (up && (h2 >> 24) == ' ')
                     t = canon_stage1<false>(lsrc, ls, le, c2) && canon_stage2<false>(lsrc, ls, le, c2, b2);
-                else if (up && (h2 >> 24) == '"')
-                    t = canon_stage1<true>(lsrc, ls, le, c2) && canon_stage2<true>(lsrc, ls, le, c2, b2);
+                else if (up && (h2 >> 24) == '"') {   // compact JSON: its vocabulary path, then its canonical tier
+                    t = vocab_stage1<true>(lsrc, ls, le, c2) && vocab_stage2<true>(lsrc, ls, le, c2, b2);
+                    if (!t) t = canon_stage1<true>(lsrc, ls, le, c2) && canon_stage2<true>(lsrc, ls, le, c2, b2);
+                }
 #if YSB_FLAT_TIER
                 if (!t) t = flat_tier(lsrc, ls, le, P.require_mask, c2, b2);   // any key order / spacing
 #endif
