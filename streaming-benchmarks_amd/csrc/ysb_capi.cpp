@@ -87,6 +87,14 @@ struct ysb_ctx {
     u32* d_runs = nullptr;
     u64 runs_words = 0;
     u64 rec_launches = 0;
+    // record mode counts into a u32 delta ring with the u64 ring's layout; fold_delta adds
+    // it to the u64 ring before anything reads that, and before delta_bound (events
+    // counted into delta since the last fold, an upper bound of any cell's delta) could
+    // reach 2^32
+    u32* d_delta = nullptr;
+    u64 delta_cells = 0;
+    u64 delta_bound = 0;
+    u64 delta_limit = 1ull << 32;   // YSB_DELTA_FOLD_EVENTS lowers it (test hook: frequent folds)
     // group
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
@@ -189,6 +197,7 @@ static void destroy(ysb_ctx* c) {
     for (auto& p : c->tev) for (hipEvent_t e : p) hipEventDestroy(e);
     hipFree(c->d_rec);
     hipFree(c->d_rec_n);
+    hipFree(c->d_delta);
     hipFree(c->d_part);
     hipFree(c->d_runs);
     if (c->ev_ring) hipEventDestroy(c->ev_ring);
@@ -237,6 +246,10 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->cus = prop.multiProcessorCount;
     // scan schedule overrides (timing experiments): YSB_DYN_PCT=0 -> all static
     if (const char* e = getenv("YSB_DYN_PCT")) c->dyn_pct = (u32)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("YSB_DELTA_FOLD_EVENTS")) {
+        const u64 v = strtoull(e, nullptr, 10);
+        if (v > 0 && v < c->delta_limit) c->delta_limit = v;
+    }
     if (const char* e = getenv("YSB_DYN_CHUNK")) c->dyn_chunk = (u32)strtoul(e, nullptr, 10);
     if (hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking) != hipSuccess) {
@@ -590,6 +603,15 @@ static int grow_u32(ysb_ctx* c, u32** buf, u64* have, u64 words) {
     return YSB_OK;
 }
 
+// The delta ring into the u64 ring (queued on the compute stream), delta cleared.
+static int fold_delta(ysb_ctx* c) {
+    if (!c->d_delta || c->delta_bound == 0) return YSB_OK;
+    launch_fold(c->d_counts, c->d_delta, c->delta_cells, c->s_comp);
+    HIPCHK(c, hipGetLastError());
+    c->delta_bound = 0;
+    return YSB_OK;
+}
+
 // Record mode (ysb_count.hip) for this launch: large count tables without LDS window
 // counters (configs[2]), where one global atomic per joined view is the bottleneck.
 // Auto: ring >= 1M cells and launch >= 1M events; YSB_F_RECORD_COUNT forces it on
@@ -634,11 +656,25 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     if ((rc = grow_u32(c, &c->d_rec_n, &c->rec_n_words, (u64)r.grid * r.bins))) return rc;
     if ((rc = grow_u32(c, &c->d_part, &c->part_words, part))) return rc;
     if ((rc = grow_u32(c, &c->d_runs, &c->runs_words, (u64)r.n_blocks * REC_QUARTERS * 2))) return rc;
+    if (c->delta_cells != cells) {   // the delta ring: the u64 ring's layout, zeroed
+        if ((rc = fold_delta(c))) return rc;
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        hipFree(c->d_delta);
+        c->d_delta = nullptr;
+        c->delta_cells = 0;
+        HIPCHK(c, hipMalloc(&c->d_delta, cells * 4));
+        HIPCHK(c, hipMemset(c->d_delta, 0, cells * 4));
+        c->delta_cells = cells;
+    }
+    // no delta cell may wrap: fold first if this launch's events could take the views
+    // added since the last fold to 2^32
+    if (c->delta_bound + n_events >= c->delta_limit && (rc = fold_delta(c))) return rc;
+    c->delta_bound += n_events;
+    r.delta = c->d_delta;
     r.rec = c->d_rec;
     r.rec_n = c->d_rec_n;
     r.part = c->d_part;
     r.runs = c->d_runs;
-    r.counts = c->d_counts;
     p.rec_on = 1;
     p.rec_bins = r.bins;
     p.rec_shift = r.blk_shift + r.sub_log2;
@@ -907,6 +943,8 @@ static int pull_side_list(ysb_ctx* c) {
 // Non-zero ring cells of buckets [blo, bhi) (rank-local table + owned block), compacted
 // on the device (two passes: count, then rows), added to `into`; clear zeroes them.
 static int ring_rows(ysb_ctx* c, i64 blo, i64 bhi, bool clear, std::map<std::pair<u32, i64>, u64>& into) {
+    int frc = fold_delta(c);
+    if (frc) return frc;
     if (!c->ring_known) return YSB_OK;
     const u32 W = c->cfg.window_ring;
     const i64 lo = c->ring_lo;
@@ -1046,6 +1084,8 @@ int ysb_reset(ysb_ctx* c) {
     if (rc) return rc;
     const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
     HIPCHK(c, hipMemset(c->d_counts, 0, cells * 8));
+    if (c->d_delta) HIPCHK(c, hipMemset(c->d_delta, 0, c->delta_cells * 4));
+    c->delta_bound = 0;
     if (c->d_owned) HIPCHK(c, hipMemset(c->d_owned, 0, cells / c->nranks * 8));
     if (c->d_truth) HIPCHK(c, hipMemset(c->d_truth, 0, cells * 8));
     if (c->d_truth_out) HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
@@ -1185,7 +1225,12 @@ int ysb_group_init(ysb_ctx* c, int rank, int nranks, const uint8_t uid[YSB_UNIQU
     // pad campaigns to a multiple of nranks; keep the current counts
     const u32 cp = (c->cfg.n_campaigns + nranks - 1) / nranks * nranks;
     if (cp != c->c_pad) {
+        int frc = fold_delta(c);   // the delta ring has the old layout: fold it, drop it
+        if (frc) return frc;
         HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        hipFree(c->d_delta);
+        c->d_delta = nullptr;
+        c->delta_cells = 0;
         unsigned long long* old = c->d_counts;
         const u64 W = c->cfg.window_ring;
         c->d_counts = nullptr;
@@ -1220,6 +1265,8 @@ int ysb_group_reduce_scatter(ysb_ctx* c) {
         int rc = agree_ring(c);
         if (rc) return rc;
     }
+    int frc = fold_delta(c);
+    if (frc) return frc;
     const u64 per = (u64)c->c_pad / c->nranks * c->cfg.window_ring;
     ncclResult_t r = ncclReduceScatter(c->d_counts, c->d_rs_tmp, per, ncclUint64, ncclSum, c->comm, c->s_comp);
     if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
@@ -1393,6 +1440,8 @@ int ysb_truth_compare(ysb_ctx* c, uint64_t* mismatched, uint64_t* truth_total, u
     if (!c) return YSB_ERR_ARG;
     if (!c->d_truth) return fail(c, YSB_ERR_STATE, "no truth accumulated");
     HIPCHK(c, hipSetDevice(c->device));
+    int frc = fold_delta(c);
+    if (frc) return frc;
     HIPCHK(c, hipMemsetAsync(c->d_cmp, 0, 32, c->s_comp));
     launch_compare(c->d_truth, c->d_counts, (u64)c->c_pad * c->cfg.window_ring, c->d_cmp, c->s_comp);
     unsigned long long r[3], outside = 0;

@@ -18,12 +18,18 @@
 //                 rings and written out as whole lines;
 //   count         per level-2 block (32768 / W campaigns, whose L2C x W cells are one
 //                 contiguous slab of the campaign-major ring): LDS u32 counters, then
-//                 every non-zero cell added to the ring ONCE with a plain load/add/store
-//                 (the block's slab belongs to this workgroup alone; consecutive lanes
-//                 take consecutive cells, so the loads and stores coalesce).
+//                 every counted line of cells added ONCE with a plain load/add/store to
+//                 the u32 DELTA ring (the block's slab belongs to this workgroup alone;
+//                 consecutive lanes take consecutive cells, so the loads and stores
+//                 coalesce) -- half the bytes of the u64 ring's read-modify-write;
+//   fold          before anything reads the u64 ring (drain, ring advance, exchange,
+//                 truth compare) and before the views added since the last fold could
+//                 reach 2^32 (so no delta cell can wrap), delta is added to the ring and
+//                 cleared (ysb_capi.cpp fold_delta).
 //
 // Exact: the same additions, reordered (integer sums commute).
 #include "ysb_kernels.h"
+#include <algorithm>
 
 namespace ysb {
 
@@ -206,46 +212,67 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
             if (v[u] != REC_NONE) atomicAdd(&cnt[v[u] - base_cell], 1u);
     }
     __syncthreads();
-    // the slab: [base_cell, base_cell + cells) u64, as 16-B pairs; 8 consecutive threads
-    // cover one 128-B line, and a line none of whose 16 cells was counted is neither read
-    // nor written (the ring slots this launch's buckets do not reach: ~a fifth of the slab
-    // for 100 live buckets of 128), so every store is still a whole line
-    uint4* ring = reinterpret_cast<uint4*>(R.counts + base_cell);
-    const u32 pairs = cells / 2;   // a multiple of 8
+    // the slab of the delta ring: [base_cell, base_cell + cells) u32, as 16-B quads; 8
+    // consecutive threads cover one 128-B line, and a line none of whose 32 cells was
+    // counted is neither read nor written (the ring slots this launch's buckets do not
+    // reach), so every store is still a whole line.  No cell wraps: the host folds the
+    // delta ring into the u64 ring before 2^32 views can have been added to it.
+    uint4* dr = reinterpret_cast<uint4*>(R.delta + base_cell);
+    const u32 quads = cells / 4;   // a multiple of 4 (cells: of 16); lines of 8 quads
     constexpr int SU = 8;
-    for (u32 p0 = 0; p0 < pairs; p0 += REC_TPB * SU) {
-        uint2 c[SU];
+    for (u32 p0 = 0; p0 < quads; p0 += REC_TPB * SU) {
+        uint4 c[SU];
         bool live[SU];
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
             const u32 p = p0 + u * REC_TPB + tid;
-            c[u] = p < pairs ? reinterpret_cast<const uint2*>(cnt)[p] : make_uint2(0u, 0u);
-            u32 any = c[u].x | c[u].y;
+            c[u] = p < quads ? reinterpret_cast<const uint4*>(cnt)[p] : make_uint4(0u, 0u, 0u, 0u);
+            u32 any = c[u].x | c[u].y | c[u].z | c[u].w;
             any |= __shfl_xor(any, 1, 64);
             any |= __shfl_xor(any, 2, 64);
             any |= __shfl_xor(any, 4, 64);
-            live[u] = p < pairs && any != 0u;
+            live[u] = p < quads && any != 0u;
         }
         uint4 r[SU];
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
             const u32 p = p0 + u * REC_TPB + tid;
-            if (live[u]) r[u] = ring[p];
+            if (live[u]) r[u] = dr[p];
         }
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
             const u32 p = p0 + u * REC_TPB + tid;
-            if (live[u]) {
-                unsigned long long lo = ((unsigned long long)r[u].y << 32 | r[u].x) + c[u].x;
-                unsigned long long hi = ((unsigned long long)r[u].w << 32 | r[u].z) + c[u].y;
-                ring[p] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
-            }
+            if (live[u]) dr[p] = make_uint4(r[u].x + c[u].x, r[u].y + c[u].y, r[u].z + c[u].z, r[u].w + c[u].w);
         }
+    }
+}
+
+// counts[i] += delta[i], delta[i] = 0 for every cell (4 per thread; all-zero quads skipped)
+__global__ __launch_bounds__(256) void fold_kernel(unsigned long long* counts, u32* delta, u64 quads) {
+    for (u64 q = (u64)blockIdx.x * 256 + threadIdx.x; q < quads; q += (u64)gridDim.x * 256) {
+        const uint4 d = reinterpret_cast<const uint4*>(delta)[q];
+        if ((d.x | d.y | d.z | d.w) == 0u) continue;
+        ulonglong2* c2 = reinterpret_cast<ulonglong2*>(counts + 4 * q);
+        ulonglong2 a = c2[0], b = c2[1];
+        a.x += d.x;
+        a.y += d.y;
+        b.x += d.z;
+        b.y += d.w;
+        c2[0] = a;
+        c2[1] = b;
+        reinterpret_cast<uint4*>(delta)[q] = make_uint4(0u, 0u, 0u, 0u);
     }
 }
 
 void launch_rec_partition(const RecParams& r, hipStream_t s) {
     hipLaunchKernelGGL(rec_partition_kernel, dim3(r.bins * REC_QUARTERS), dim3(REC_TPB), 0, s, r);
+}
+
+void launch_fold(unsigned long long* counts, u32* delta, u64 cells, hipStream_t s) {
+    const u64 quads = cells / 4;   // cells: c_pad * W, W a power of two >= 16
+    if (!quads) return;
+    const u64 blocks = std::min<u64>((quads + 255) / 256, 65536);
+    hipLaunchKernelGGL(fold_kernel, dim3((u32)blocks), dim3(256), 0, s, counts, delta, quads);
 }
 
 void launch_rec_count(const RecParams& r, hipStream_t s) {

@@ -162,10 +162,11 @@ struct RecParams {
     u64 area;                   // u32 words of one (bin, quarter) output area
     u32* part;                  // partitioned records: [bins * QUARTERS][area], runs 32-record aligned
     u32* runs;                  // [n_blocks][QUARTERS] {offset, count} into part
-    unsigned long long* counts; // the ring [c_pad][W]
+    u32* delta;                 // the u32 delta ring [c_pad][W], folded into the u64 ring before it is read
 };
 void launch_rec_partition(const RecParams& r, hipStream_t s);
 void launch_rec_count(const RecParams& r, hipStream_t s);
+void launch_fold(unsigned long long* counts, u32* delta, u64 cells, hipStream_t s);
 
 constexpr int N_STAMPS = 8;     // phases timed by the YSB_STAMPS diagnostic build
 

@@ -129,3 +129,49 @@ def test_bucket_table_sparse_and_misses(huge_map, record):
     assert rows == exp
     for k, v in est.items():
         assert st[k] == v, k
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fold_events", [None, "50000"])
+def test_record_delta_ring_folds(big_map, monkeypatch, fold_events):
+    """Record mode counts into a u32 delta ring folded into the u64 ring before anything
+    reads it and before 2^32 events could have been counted into it.  Eight launches
+    back to back with a stats read and a drain-with-clear in between -- with the default
+    bound (folds only at the drains) and with a bound of 50k events (a fold before every
+    launch) -- equal the oracle."""
+    if fold_events:
+        monkeypatch.setenv("YSB_DELTA_FOLD_EVENTS", fold_events)
+    g, aids, raw, offs = big_map
+    camp = g.ad_campaign_index()
+    n = offs.size
+    cuts = [int(x) for x in np.linspace(0, n, 9)]
+    with YsbContext(n_campaigns=200_000, window_ring=16, record_count=True, timing=True,
+                    max_batch_bytes=raw.size + 64, max_batch_events=n + 1) as ctx:
+        ctx.load_ad_map(aids, camp)
+        d_b = ctx.device_alloc(raw.size + 64 * 9)
+        d_o = ctx.device_alloc(4 * n + 64)
+        chunks, pos = [], 0
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            lo = int(offs[a])
+            hi = int(offs[b]) if b < n else raw.size
+            ctx.h2d(d_b + pos, raw[lo:hi])
+            ctx.h2d(d_o + 4 * a, (offs[a:b] - lo).astype(np.uint32))
+            chunks.append((d_b + pos, hi - lo, d_o + 4 * a, b - a))
+            pos += (hi - lo + 15) // 16 * 16
+        got = {}
+
+        def add(rows):
+            for k, v in rows.items():
+                got[k] = got.get(k, 0) + v
+        for ch in chunks[:3]:
+            ctx.submit_device(*ch)
+        assert ctx.stats()["events"] == cuts[3]
+        for ch in chunks[3:5]:
+            ctx.submit_device(*ch)
+        add(ctx.drain_buckets(clear=True))
+        for ch in chunks[5:]:
+            ctx.submit_device(*ch)
+        add(ctx.drain_buckets(clear=True))
+        assert ctx.path_time()[2] == 8
+    exp, _ = oracle.run(oracle.AdMap(aids, camp), raw, offs)
+    assert got == exp
