@@ -440,10 +440,28 @@ struct OjTok {
     }
 };
 
+// Advances t.p over bytes nextString only steps over -- neither the quote q, a backslash
+// nor a byte below ' ' (NUL, CR, LF and the other control bytes the per-byte loop below
+// decides) -- four at a time.
+template <class S>
+__device__ __forceinline__ void oj_skip_plain(OjTok<S>& t, int q) {
+    const u32 qq = (u32)q * 0x01010101u;
+    while (t.p + 4 <= t.e) {
+        const u32 x = t.src.load4(t.p);
+        const u32 z = zero_bytes(x ^ qq) | zero_bytes(x ^ 0x5C5C5C5Cu) | zero_bytes(x & 0xE0E0E0E0u);
+        if (z != 0u) {
+            t.p += (int)(__builtin_ctz(z) >> 3);
+            return;
+        }
+        t.p += 4;
+    }
+}
+
 // nextString after the opening quote q: validates up to the closing quote.
 template <class S>
 __device__ __forceinline__ bool oj_string(OjTok<S>& t, int q, int& esc) {
     for (;;) {
+        oj_skip_plain(t, q);
         int c = t.next();
         if (c < 0 || c == '\n' || c == '\r') return false;                // Unterminated string
         if (c == q) return true;

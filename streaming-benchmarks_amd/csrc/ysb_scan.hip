@@ -112,6 +112,9 @@ __device__ __forceinline__ u32 match_key_raw(const S& src, int s, int len) {
     return 0u;
 }
 
+// bytes of x that are zero (exact for the lowest one: a false flag only sits above a true one)
+__device__ __forceinline__ u32 zero_bytes(u32 x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
+
 }  // namespace ysb
 
 #include "ysb_orgjson.h"
@@ -415,7 +418,6 @@ __device__ __forceinline__ bool canon_stage1(const LdsSrc& src, int s, int e, Ca
 }
 
 // ---- word-at-a-time byte scans (the vocabulary path's ip value, the flat tier) -------------
-__device__ __forceinline__ u32 zero_bytes(u32 x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
 
 // The next byte > ' ' at or after p (its position; c = the byte), or -1 if the end of
 // the line or a NUL comes first.  Four bytes per step; of the two flag sets the lowest
