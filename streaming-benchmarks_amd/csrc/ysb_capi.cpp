@@ -401,6 +401,15 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         while (cslots < 2 * keys36.size()) cslots <<= 1;
     }
     const u32 unit = buckets ? CB_WORDS : CSLOT_WORDS;
+    std::vector<u32> kw, cv;   // bucket layout: the keys as words, their campaigns
+    if (buckets) {
+        kw.resize(keys36.size() * CKEY_WORDS);
+        cv.resize(keys36.size());
+        for (size_t i = 0; i < keys36.size(); ++i) {
+            std::memcpy(&kw[i * CKEY_WORDS], keys36[i].first.data(), 36);
+            cv[i] = keys36[i].second;
+        }
+    }
     std::vector<u32> ct;
     CuckooSeed cs{};
     u64 seed = 0x5EEDC0FFEEULL;
@@ -419,48 +428,9 @@ int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         const u32 cm = (u32)(cslots - 1);
         bool ok = true;
         if (buckets) {
-            for (u64 s = 0; s < cslots; ++s)
-                for (u32 e = 0; e < CB_ENTRIES; ++e) ct[s * CB_WORDS + e * CB_STRIDE + CKEY_WORDS] = EMPTY_SLOT;
-            u64 rng = seed;
-            for (const auto& kv : keys36) {
-                Key36 k = kv.first;
-                u32 camp = kv.second;
-                u32 a, b;
-                cuckoo_slots36(k.data(), cs, cm, &a, &b);
-                u32 pos = a;
-                bool placed = false;
-                for (int kicks = 0; kicks <= 500 && !placed; ++kicks) {
-                    // the first bucket while it has room; the second only when the first is full
-                    for (u32 cand : {pos, pos == a ? b : a}) {
-                        u32* bk = &ct[(u64)cand * CB_WORDS];
-                        for (u32 e = 0; e < CB_ENTRIES && !placed; ++e)
-                            if (bk[e * CB_STRIDE + CKEY_WORDS] == EMPTY_SLOT) {
-                                std::memcpy(bk + e * CB_STRIDE, k.data(), 36);
-                                bk[e * CB_STRIDE + CKEY_WORDS] = camp;
-                                placed = true;
-                            }
-                        if (placed || kicks > 0) break;   // an evicted key tries only its other bucket
-                    }
-                    if (placed) break;
-                    // both full: evict a random entry of pos, which keeps pos full
-                    rng = mix64(rng + 1);
-                    const u32 e = (u32)(rng % CB_ENTRIES);
-                    u32* en = &ct[(u64)pos * CB_WORDS + e * CB_STRIDE];
-                    Key36 ok_;
-                    std::memcpy(ok_.data(), en, 36);
-                    const u32 oc = en[CKEY_WORDS];
-                    std::memcpy(en, k.data(), 36);
-                    en[CKEY_WORDS] = camp;
-                    k = ok_;
-                    camp = oc;
-                    u32 oa, ob;
-                    cuckoo_slots36(k.data(), cs, cm, &oa, &ob);
-                    pos = (pos == oa) ? ob : oa;   // the evicted key's other bucket
-                    a = oa;
-                    b = ob;
-                }
-                if (!placed) { ok = false; if (!partial) break; }
-            }
+            const u64 homeless = cuckoo_build_buckets(kw.data(), cv.data(), keys36.size(), cs, cslots, seed, partial,
+                                                      ct.data());
+            ok = homeless == 0;
             if (ok || partial) break;
             continue;
         }

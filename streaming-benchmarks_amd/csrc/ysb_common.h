@@ -348,6 +348,81 @@ YSB_HD void cuckoo_slots36(const u32* w, const CuckooSeed& cs, u32 mask, u32* a,
 }
 
 #if !defined(__HIP_DEVICE_COMPILE__)
+// Host build of the bucket-layout table (ysb_load_ad_map): key i (9 words) with campaign
+// camp[i] into nb buckets (ct: nb * CB_WORDS words, cleared here).  A key goes to its
+// first bucket while that has a free entry, else to its second; with both full it takes a
+// random entry of the bucket it is headed for (which so stays full) and the evicted key
+// tries only its other bucket.  So a key sits in its second bucket only while its first
+// is full -- the probe's rule.  Returns the keys left out (keep_going: placement goes on
+// without them, a partial table; else it stops at the first).
+static inline u64 cuckoo_build_buckets(const u32* keys, const u32* camp, u64 n, const CuckooSeed& cs, u64 nb,
+                                       u64 seed, bool keep_going, u32* ct) {
+    for (u64 i = 0; i < nb * CB_WORDS; ++i) ct[i] = 0;
+    for (u64 b = 0; b < nb; ++b)
+        for (u32 e = 0; e < CB_ENTRIES; ++e) ct[b * CB_WORDS + e * CB_STRIDE + CKEY_WORDS] = EMPTY_SLOT;
+    const u32 mask = (u32)(nb - 1);
+    u64 rng = seed, homeless = 0;
+    for (u64 i = 0; i < n; ++i) {
+        u32 k[CKEY_WORDS];
+        for (u32 j = 0; j < CKEY_WORDS; ++j) k[j] = keys[i * CKEY_WORDS + j];
+        u32 c = camp[i];
+        u32 a, b;
+        cuckoo_slots36(k, cs, mask, &a, &b);
+        u32 pos = a;
+        bool placed = false;
+        for (int kicks = 0; kicks <= 500 && !placed; ++kicks) {
+            const u32 cands[2] = {pos, pos == a ? b : a};
+            for (int ci = 0; ci < (kicks == 0 ? 2 : 1) && !placed; ++ci) {
+                u32* bk = &ct[(u64)cands[ci] * CB_WORDS];
+                for (u32 e = 0; e < CB_ENTRIES && !placed; ++e)
+                    if (bk[e * CB_STRIDE + CKEY_WORDS] == EMPTY_SLOT) {
+                        for (u32 j = 0; j < CKEY_WORDS; ++j) bk[e * CB_STRIDE + j] = k[j];
+                        bk[e * CB_STRIDE + CKEY_WORDS] = c;
+                        placed = true;
+                    }
+            }
+            if (placed) break;
+            rng = mix64(rng + 1);
+            u32* en = &ct[(u64)pos * CB_WORDS + (u32)(rng % CB_ENTRIES) * CB_STRIDE];
+            for (u32 j = 0; j < CKEY_WORDS; ++j) {
+                const u32 t = en[j];
+                en[j] = k[j];
+                k[j] = t;
+            }
+            const u32 oc = en[CKEY_WORDS];
+            en[CKEY_WORDS] = c;
+            c = oc;
+            cuckoo_slots36(k, cs, mask, &a, &b);
+            pos = (pos == a) ? b : a;   // the evicted key's other bucket
+        }
+        if (!placed) {
+            ++homeless;
+            if (!keep_going) return homeless;
+        }
+    }
+    return homeless;
+}
+
+// Host restatement of the scan's bucket probe (ysb_scan.hip bucket_find + the second
+// bucket after a miss in a full first one): the campaign, or EMPTY_SLOT.
+static inline u32 cuckoo_lookup_buckets(const u32* ct, u64 nb, const CuckooSeed& cs, const u32* k) {
+    u32 a, b;
+    cuckoo_slots36(k, cs, (u32)(nb - 1), &a, &b);
+    for (int round = 0; round < 2; ++round) {
+        const u32* bk = &ct[(u64)(round ? b : a) * CB_WORDS];
+        bool full = true;
+        for (u32 e = 0; e < CB_ENTRIES; ++e) {
+            const u32 c = bk[e * CB_STRIDE + CKEY_WORDS];
+            if (c == EMPTY_SLOT) { full = false; continue; }
+            bool eq = true;
+            for (u32 j = 0; j < CKEY_WORDS; ++j) eq &= bk[e * CB_STRIDE + j] == k[j];
+            if (eq) return c;
+        }
+        if (!full) return EMPTY_SLOT;
+    }
+    return EMPTY_SLOT;
+}
+
 static inline CuckooSeed cuckoo_seed(u64 seed) {
     CuckooSeed cs;
     for (u32 k = 0; k < CKEY_WORDS; ++k) {

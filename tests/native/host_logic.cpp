@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <vector>
 #include "ysb_common.h"
 
 using namespace ysb;
@@ -46,6 +47,38 @@ int main() {
                 GenEvent e = gen_event(s, i);
                 CHECK(gen_line_len(s, i, e) == gen_line_write(s, i, e, line));
             }
+        }
+    }
+    // bucket-layout cuckoo table: every placed key is found by the probe's rule, a key in
+    // its second bucket only while its first is full, and absent keys are not found
+    for (u64 nb : {16384ull, 8192ull}) {   // load 41 % and 81 % of the entries
+        const u64 n = 20000;
+        std::vector<u32> keys(n * CKEY_WORDS), camp(n), ct(nb * CB_WORDS);
+        std::mt19937_64 kr(nb);
+        for (auto& w : keys) w = (u32)kr();
+        for (u64 i = 0; i < n; ++i) camp[i] = (u32)(i % 1000);
+        const CuckooSeed cs = cuckoo_seed(77 + nb);
+        const u64 homeless = cuckoo_build_buckets(keys.data(), camp.data(), n, cs, nb, 99, true, ct.data());
+        CHECK(homeless == 0);
+        u64 second = 0;
+        for (u64 i = 0; i < n; ++i) {
+            const u32* k = &keys[i * CKEY_WORDS];
+            CHECK(cuckoo_lookup_buckets(ct.data(), nb, cs, k) == camp[i]);
+            u32 a, b;
+            cuckoo_slots36(k, cs, (u32)(nb - 1), &a, &b);
+            bool in_a = false, a_full = true;
+            for (u32 e = 0; e < CB_ENTRIES; ++e) {
+                const u32* en = &ct[(u64)a * CB_WORDS + e * CB_STRIDE];
+                if (en[CKEY_WORDS] == EMPTY_SLOT) a_full = false;
+                else if (std::memcmp(en, k, 36) == 0) in_a = true;
+            }
+            if (!in_a) { CHECK(a_full); ++second; }
+        }
+        if (nb == 16384) CHECK(second < n / 20);
+        for (int t = 0; t < 2000; ++t) {   // keys not in the table
+            u32 k[CKEY_WORDS];
+            for (auto& w : k) w = (u32)kr();
+            CHECK(cuckoo_lookup_buckets(ct.data(), nb, cs, k) == EMPTY_SLOT);
         }
     }
     std::printf("%s\n", fails ? "FAILED" : "OK");
