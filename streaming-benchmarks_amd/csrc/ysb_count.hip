@@ -195,6 +195,27 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
     __syncthreads();
     const u32 total = roff[REC_QUARTERS];
     const u32 base_cell = c0 << R.w_log2;
+    // the slab of the delta ring: [base_cell, base_cell + cells) u32, as 16-B quads; 8
+    // consecutive threads cover one 128-B line; quads <= REC_TPB * SU, so each thread
+    // holds at most SU of them.  No cell wraps: the host folds the delta ring into the
+    // u64 ring before 2^32 views can have been added to it.
+    uint4* dr = reinterpret_cast<uint4*>(R.delta + base_cell);
+    const u32 quads = cells / 4;   // a multiple of 4 (cells: of 16); lines of 8 quads
+    constexpr int SU = REC_BLOCK_CELLS / 4 / REC_TPB;
+    static_assert(SU * REC_TPB * 4 == REC_BLOCK_CELLS, "one slab quad set per thread");
+    // Dense block (at least one record per 16 cells: nearly every line is counted): the
+    // whole slab is read up front, its round trip under the record loads and LDS atomics,
+    // and written back whole.  Sparse block: after the counts, only the lines holding a
+    // count are read and written (the ring slots this launch's buckets do not reach).
+    const bool dense = (u64)total * 16u >= cells;
+    uint4 r[SU];
+    if (dense) {
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+            const u32 p = u * REC_TPB + tid;
+            r[u] = p < quads ? dr[p] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
     for (u32 i0 = 0; i0 < total; i0 += REC_TPB * REC_UNROLL) {
         u32 v[REC_UNROLL];
 #pragma unroll
@@ -212,38 +233,38 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
             if (v[u] != REC_NONE) atomicAdd(&cnt[v[u] - base_cell], 1u);
     }
     __syncthreads();
-    // the slab of the delta ring: [base_cell, base_cell + cells) u32, as 16-B quads; 8
-    // consecutive threads cover one 128-B line, and a line none of whose 32 cells was
-    // counted is neither read nor written (the ring slots this launch's buckets do not
-    // reach), so every store is still a whole line.  No cell wraps: the host folds the
-    // delta ring into the u64 ring before 2^32 views can have been added to it.
-    uint4* dr = reinterpret_cast<uint4*>(R.delta + base_cell);
-    const u32 quads = cells / 4;   // a multiple of 4 (cells: of 16); lines of 8 quads
-    constexpr int SU = 8;
-    for (u32 p0 = 0; p0 < quads; p0 += REC_TPB * SU) {
-        uint4 c[SU];
-        bool live[SU];
+    if (dense) {
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
-            const u32 p = p0 + u * REC_TPB + tid;
-            c[u] = p < quads ? reinterpret_cast<const uint4*>(cnt)[p] : make_uint4(0u, 0u, 0u, 0u);
-            u32 any = c[u].x | c[u].y | c[u].z | c[u].w;
-            any |= __shfl_xor(any, 1, 64);
-            any |= __shfl_xor(any, 2, 64);
-            any |= __shfl_xor(any, 4, 64);
-            live[u] = p < quads && any != 0u;
+            const u32 p = u * REC_TPB + tid;
+            if (p < quads) {
+                const uint4 c = reinterpret_cast<const uint4*>(cnt)[p];
+                dr[p] = make_uint4(r[u].x + c.x, r[u].y + c.y, r[u].z + c.z, r[u].w + c.w);
+            }
         }
-        uint4 r[SU];
+        return;
+    }
+    uint4 c[SU];
+    bool live[SU];
 #pragma unroll
-        for (int u = 0; u < SU; ++u) {
-            const u32 p = p0 + u * REC_TPB + tid;
-            if (live[u]) r[u] = dr[p];
-        }
+    for (int u = 0; u < SU; ++u) {
+        const u32 p = u * REC_TPB + tid;
+        c[u] = p < quads ? reinterpret_cast<const uint4*>(cnt)[p] : make_uint4(0u, 0u, 0u, 0u);
+        u32 any = c[u].x | c[u].y | c[u].z | c[u].w;
+        any |= __shfl_xor(any, 1, 64);
+        any |= __shfl_xor(any, 2, 64);
+        any |= __shfl_xor(any, 4, 64);
+        live[u] = p < quads && any != 0u;
+    }
 #pragma unroll
-        for (int u = 0; u < SU; ++u) {
-            const u32 p = p0 + u * REC_TPB + tid;
-            if (live[u]) dr[p] = make_uint4(r[u].x + c[u].x, r[u].y + c[u].y, r[u].z + c[u].z, r[u].w + c[u].w);
-        }
+    for (int u = 0; u < SU; ++u) {
+        const u32 p = u * REC_TPB + tid;
+        if (live[u]) r[u] = dr[p];
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+        const u32 p = u * REC_TPB + tid;
+        if (live[u]) dr[p] = make_uint4(r[u].x + c[u].x, r[u].y + c[u].y, r[u].z + c[u].z, r[u].w + c[u].w);
     }
 }
 

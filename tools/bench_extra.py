@@ -86,6 +86,7 @@ def config3(args):
     ctx.sync()
     el = time.perf_counter() - t0
     kms, launches = ctx.kernel_time()
+    pms, _, _ = ctx.path_time()
     ctx.reset()
     submit_segments(ctx, segs, args.per_batch)
     for (f, n, d_b, nb, d_o) in segs:
@@ -98,7 +99,8 @@ def config3(args):
                 args.campaigns, args.events, args.ring, args.c3_rate),
             "events_per_s": round(args.events * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
             "batches_per_step": len(segs), "launches_per_step": len(segs) if args.per_batch else 1,
-            "scan_avg_launch_ms": round(kms / launches, 4), "scan_alg_GBs": round(ach, 1),
+            "scan_avg_launch_ms": round(kms / launches, 4), "path_avg_ms": round(pms / launches, 4),
+            "scan_alg_GBs": round(ach, 1),
             "hbm_frac": round(ach / HBM_PEAK_GBS, 4), "ad_map_load_s": round(t_load, 2),
             "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
                       "join_misses": st["join_misses"], "parse_errors": st["parse_errors"],
@@ -134,6 +136,7 @@ def tbl(args):
     ctx.sync()
     el = time.perf_counter() - t0
     kms, launches = ctx.kernel_time()
+    pms, _, _ = ctx.path_time()
     ctx.reset()
     submit_segments(ctx, segs, args.per_batch)
     for (f, n, d_b, nb, d_o) in segs:
@@ -146,7 +149,8 @@ def tbl(args):
             "tbl_bytes_per_event": round(total_bytes / args.events, 3),
             "events_per_s": round(args.events * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
             "batches_per_step": len(segs), "launches_per_step": len(segs) if args.per_batch else 1,
-            "scan_avg_launch_ms": round(kms / launches, 4), "scan_alg_GBs": round(ach, 1),
+            "scan_avg_launch_ms": round(kms / launches, 4), "path_avg_ms": round(pms / launches, 4),
+            "scan_alg_GBs": round(ach, 1),
             "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
             "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
                       "join_misses": st["join_misses"], "parse_errors": st["parse_errors"],
