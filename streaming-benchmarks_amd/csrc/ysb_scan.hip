@@ -686,6 +686,9 @@ __device__ __forceinline__ bool vocab_stage2(const LdsSrc& src, int s, int e, co
 // other row is deferred to process_tbl_line.  Same two-batch shape as the JSON path.
 // ---------------------------------------------------------------------------
 constexpr int TBL_WORDS = 40;                          // bytes 0..159 of the line
+#ifndef YSB_TBL_ZCMP
+#define YSB_TBL_ZCMP 1
+#endif
 constexpr int TBL_MIN_LEN = 116, TBL_MAX_LEN = 4 * TBL_WORDS;
 
 // Per byte, bit 7 set if the byte may be '|' (SWAR has-zero of w ^ '|'); the lowest flag
@@ -706,6 +709,27 @@ __device__ __forceinline__ bool tbl_stage1(const LdsSrc& src, int s, int e, Cano
     for (int k = 0; k <= TBL_WORDS; ++k) P[k] = src.d[a + k];
     u32 W[TBL_WORDS];
     u32 B[5] = {0u, 0u, 0u, 0u, 0u};   // bit i = line byte i may be '|'
+#if YSB_TBL_ZCMP
+    // bytes 0..95: the '|' flags of each word compared with the only pattern a generator
+    // row has there -- '|' at 36 and 73 (word 9 byte 0, word 18 byte 1), no other byte
+    // flagged (a false flag above a true '|' only rejects the line); no bitmap is packed
+    u32 dz = 0;
+#pragma unroll
+    for (int j = 0; j < TBL_WORDS; ++j) {
+        W[j] = __builtin_amdgcn_alignbyte(P[j + 1], P[j], sb);   // line bytes 4j..4j+3
+        if (j < 24) {
+            const u32 t = W[j] ^ 0x7C7C7C7Cu;
+            const u32 z = ((t - 0x01010101u) & ~t) & 0x80808080u;
+            dz |= j == 9 ? z ^ 0x80u : j == 18 ? z ^ 0x8000u : z;
+        } else {
+            B[j >> 3] |= bar_nib(W[j]) << (4 * (j & 7));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(W[19 + k], W[18 + k], 2u);   // bytes 74..109
+    // the first three '|' exactly at 36, 73, 110 (each the lowest flag of its word: true)
+    const bool fixed = dz == 0u && (B[3] & 0x7FFFu) == (1u << 14);
+#else
 #pragma unroll
     for (int j = 0; j < TBL_WORDS; ++j) {
         W[j] = __builtin_amdgcn_alignbyte(P[j + 1], P[j], sb);   // line bytes 4j..4j+3
@@ -715,6 +739,7 @@ __device__ __forceinline__ bool tbl_stage1(const LdsSrc& src, int s, int e, Cano
     for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(W[19 + k], W[18 + k], 2u);   // bytes 74..109
     // the first three '|' exactly at 36, 73, 110 (each the lowest flag of its word: true)
     const bool fixed = B[0] == 0u && B[1] == (1u << 4) && B[2] == (1u << 9) && (B[3] & 0x7FFFu) == (1u << 14);
+#endif
     const u64 hi = ((u64)B[4] << 32) | (B[3] & ~0x7FFFu);   // bytes 96..159, above 110
     const int p3 = hi ? 96 + (int)__builtin_ctzll(hi) : (1 << 20);
     const u64 hi2 = hi & (hi - 1);
