@@ -314,7 +314,7 @@ def extras(args, device):
                     max_batch_bytes=1 << 20, max_batch_events=1 << 12) as ctx:
         ctx.load_ad_map_packed(ab, g.ad_campaign_index_array())
         load_s = time.perf_counter() - t
-        segs = gen_segments(ctx, g, 100_000_000, 12_500_000)
+        segs = gen_segments(ctx, g, 100_000_000, 16_666_667)   # 6 batches, as the headline
         r = timed_extra("configs[2]: 100M JSON events, 1M campaigns x 10 ads (10M-ad join table and "
                         "1M x 128-bucket count ring in HBM)", ctx, g, segs, args.extra_steps, args.warmup,
                         "ysb::scan_kernel<true, false, true>")
@@ -327,7 +327,7 @@ def extras(args, device):
     with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True, input_format="tbl",
                     max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
-        segs = gen_segments(ctx, g, 100_000_000, 12_500_000)
+        segs = gen_segments(ctx, g, 100_000_000, 25_000_000)   # 4 batches of ~3.5 GB (rows ~140 B)
         out["tbl"] = timed_extra("configs[1]'s 100M events as the fork's .tbl rows (MockWindowedFlatMap, "
                                  "AdvertisingTopologyNative.java:197-226)", ctx, g, segs, args.extra_steps,
                                  args.warmup, "ysb::scan_kernel<false, true, false>")
