@@ -367,6 +367,44 @@ def test_tbl_mutations_match_oracle(seed):
     _oracle_vs_gpu(out, False, lds=False, fmt="tbl", ad_map=amap)
 
 
+@pytest.mark.parametrize("seed", [3, 4])
+def test_tbl_vocabulary_edges_match_oracle(seed):
+    """The .tbl fast path names ad_type / event_type from the generator's sets and wants 13
+    digits to the row's end: rows with near-miss values (other lengths, one byte off, a
+    '|' inside, other time lengths, signs) take the bitmap branch or the deferred path --
+    every counter equals the C oracle's."""
+    g = GenParams(seed=9, n_campaigns=10, ads_per_campaign=10, fmt="tbl", events_per_sec=1000)
+    _, aids = g.ids()
+    amap = (aids, list(g.ad_campaign_index()))
+    raw, offs = g.events_host(0, 3000)
+    raw = raw.tobytes()
+    bounds = list(offs) + [len(raw)]
+    rows = [raw[bounds[i]:bounds[i + 1]] for i in range(len(offs))]
+    ad_types = [b"banner", b"modal", b"sponsored-search", b"mail", b"mobile", b"banners", b"mai", b"mobilE",
+                b"sponsored-searcX", b"sponsored-search-2", b"", b"x", b"b|nner", b"modal}", b"maiL"]
+    ev_types = [b"view", b"click", b"purchase", b"vie", b"views", b"clic", b"clickk", b"purchas", b"purchasee",
+                b"View", b"", b"v|ew"]
+    rng = np.random.default_rng(seed)
+    out = []
+    for r in rows:
+        f = r[:-1].split(b"|")
+        k = int(rng.integers(6))
+        if k == 1:
+            f[3] = ad_types[int(rng.integers(len(ad_types)))]
+        elif k == 2:
+            f[4] = ev_types[int(rng.integers(len(ev_types)))]
+        elif k == 3:
+            t = f[5]
+            f[5] = [t[:-1], t + b"7", b"-" + t[1:], b"+" + t[1:], t[:6] + b"|" + t[7:], t[:12] + b" ",
+                    t[:12] + b"/"][int(rng.integers(7))]
+        elif k == 4:
+            f[3] = ad_types[int(rng.integers(len(ad_types)))]
+            f[4] = ev_types[int(rng.integers(len(ev_types)))]
+        out.append(b"|".join(f) + b"\n")
+    _oracle_vs_gpu(out, False, fmt="tbl", ad_map=amap)
+    _oracle_vs_gpu(out, False, lds=False, fmt="tbl", ad_map=amap)
+
+
 def test_vocabulary_fast_path_edges_match_oracle():
     """Generator-layout lines whose ad_type / event_type / event_time / ip_address leave
     the generator's vocabulary (or hide a quote / backslash / control byte in it) must
