@@ -336,19 +336,24 @@ def extras(args, device):
     # the same events as other producers would write them: other ip / ad_type values (the
     # vocabulary path's generic-value branches) and compact JSON (the scan's third tier)
     from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP
-    for key, variant, what in (("random_ip", GEN_RANDOM_IP, "random dotted-quad ip_address"),
-                               ("random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
-                                "random dotted-quad ip_address and 8 ad_types"),
-                               ("compact_json", GEN_COMPACT, "compact JSON, no space after ':' and ',' "
-                                                             "(third tier)")):
+    for key, variant, cf, what in (("random_ip", GEN_RANDOM_IP, False, "random dotted-quad ip_address"),
+                                   ("random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES, False,
+                                    "random dotted-quad ip_address and 8 ad_types"),
+                                   ("compact_json", GEN_COMPACT, True,
+                                    "compact JSON, no space after ':' and ',' (layout hint YSB_F_COMPACT_FIRST: "
+                                    "the compact layout's vocabulary path first)"),
+                                   ("compact_json_no_hint", GEN_COMPACT, False,
+                                    "compact JSON without the layout hint (the generator layout tried first, "
+                                    "the compact one as the third tier)")):
         g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, variant=variant)
         _, aids = g.ids()
         with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True,
-                        max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
+                        max_batch_bytes=16 << 20, max_batch_events=1 << 16, compact_first=cf) as ctx:
             ctx.load_ad_map(aids, g.ad_campaign_index())
-            segs = gen_segments(ctx, g, 100_000_000, 12_500_000)   # longer lines: 8 batches under 4 GiB
+            # lines up to ~280 B: 7 batches keep each under the 4 GiB of u32 offsets
+            segs = gen_segments(ctx, g, 100_000_000, 14_285_715)
             out[key] = timed_extra("configs[1]'s 100M events, " + what, ctx, g, segs, args.extra_steps,
-                                   args.warmup, "ysb::scan_kernel<false, false, false>")
+                                   args.warmup, "ysb::scan_kernel<false, false, false%s>" % (", true" if cf else ""))
             free_segments(ctx, segs)
         log("extras: %s %.2f G events/s" % (key, out[key]["events_per_s"] / 1e9))
     if args.stream_seconds > 0:

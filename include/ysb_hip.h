@@ -57,6 +57,12 @@ extern "C" {
                                    default: only for rings >= 1M cells and launches >= 1M
                                    events without LDS window counters; ysb_path_time)  */
 #define YSB_F_NO_RECORD_COUNT 0x40u /* never: one global atomic per joined view             */
+#define YSB_F_COMPACT_FIRST 0x80u /* layout hint: JSON lines are expected as compact JSON
+                                   ({"user_id":"...","page_id":...} -- no space after ':'
+                                   or ','); the scan tries that layout first and the
+                                   generator's (core.clj:90-96) as a later tier.  Counts
+                                   are identical either way; only the speed differs.
+                                   Cache-resident join tables only (ignored otherwise). */
 #define YSB_F_SPARSE_FAST_JOIN 0x8u /* test hook: leave every other 36-byte key out of
                                    the fast-path cuckoo table, as a failed cuckoo
                                    placement would; its misses then take the

@@ -1163,7 +1163,9 @@ __device__ __forceinline__ void rec_write(const ScanParams& P, const u32* ring, 
 // separate instantiation so the cache-resident configuration's code is untouched).
 // TBL: the fork's .tbl rows (tbl_stage1/2) instead of JSON lines (vocab_stage1/2).
 // REC: record mode (ysb_count.hip): in-ring joined views become ring-cell records.
-template <bool SERIAL, bool TBL, bool REC>
+// CPF: compact JSON first (YSB_F_COMPACT_FIRST): the compact layout's vocabulary path is
+// the first stage and the generator layout a later tier (the same tiers, reordered).
+template <bool SERIAL, bool TBL, bool REC, bool CPF = false>
 __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<TBL>::WG_PER_CU * SCAN_TPB + 255) / 256))) void scan_kernel(const ScanParams P0) {
     using G = Geom<TBL, REC>;
     constexpr int CPT = G::CPT;
@@ -1279,7 +1281,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
-            else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1<false>(lsrc, ls, le, ca);
+            else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1<CPF>(lsrc, ls, le, ca);
             else ok1 = canon_stage1<false>(lsrc, ls, le, ca);
         }
         bool pend = false, dfr = false, tok = false;
@@ -1289,7 +1291,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         bool ok2 = false;
         if (li < cur.count) {
             if constexpr (TBL) ok2 = ok1 && tbl_stage2(lsrc, ls, le, ca, cb);
-            else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2<false>(lsrc, ls, le, ca, cb);
+            else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2<CPF>(lsrc, ls, le, ca, cb);
             else ok2 = ok1 && canon_stage2<false>(lsrc, ls, le, ca, cb);
         }
 #if YSB_CANON_TIERS
@@ -1306,11 +1308,20 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 const bool up = lsrc.load4(ls) == w4('{', '"', 'u', 's') && lsrc.load4(ls + 4) == w4('e', 'r', '_', 'i') &&
                                 (h2 & 0xFFFFFFu) == (w4('d', '"', ':', 0) & 0xFFFFFFu);
                 bool t = false;
+                if constexpr (CPF) {   // the generator layout: its vocabulary path, then its canonical tier
+                    if (up && (h2 >> 24) == ' ') {
+                        t = vocab_stage1<false>(lsrc, ls, le, c2) && vocab_stage2<false>(lsrc, ls, le, c2, b2);
+                        if (!t) t = canon_stage1<false>(lsrc, ls, le, c2) && canon_stage2<false>(lsrc, ls, le, c2, b2);
+                    } else if (up && (h2 >> 24) == '"') {
+                        t = canon_stage1<true>(lsrc, ls, le, c2) && canon_stage2<true>(lsrc, ls, le, c2, b2);
+                    }
+                } else {
                 if (up && (h2 >> 24) == ' ')
                     t = canon_stage1<false>(lsrc, ls, le, c2) && canon_stage2<false>(lsrc, ls, le, c2, b2);
                 else if (up && (h2 >> 24) == '"') {   // compact JSON: its vocabulary path, then its canonical tier
                     t = vocab_stage1<true>(lsrc, ls, le, c2) && vocab_stage2<true>(lsrc, ls, le, c2, b2);
                     if (!t) t = canon_stage1<true>(lsrc, ls, le, c2) && canon_stage2<true>(lsrc, ls, le, c2, b2);
+                }
                 }
 #if YSB_FLAT_TIER
                 if (!t) t = flat_tier(lsrc, ls, le, P.require_mask, c2, b2);   // any key order / spacing
@@ -1807,6 +1818,7 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
     } else {
         if (p.rec_on) hipLaunchKernelGGL((scan_kernel<true, false, true>), g, b, (Geom<false, true>::LDS), s, p);
         else if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false, false>), g, b, Geom<false>::LDS, s, p);
+        else if (p.compact_first) hipLaunchKernelGGL((scan_kernel<false, false, false, true>), g, b, Geom<false>::LDS, s, p);
         else hipLaunchKernelGGL((scan_kernel<false, false, false>), g, b, Geom<false>::LDS, s, p);
     }
 }

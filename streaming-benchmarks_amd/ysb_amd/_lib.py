@@ -25,6 +25,7 @@ YSB_F_SPARSE_FAST_JOIN = 0x8
 YSB_F_FORMAT_TBL = 0x10
 YSB_F_RECORD_COUNT = 0x20
 YSB_F_NO_RECORD_COUNT = 0x40
+YSB_F_COMPACT_FIRST = 0x80
 INT64_MIN = -(1 << 63)
 UNIQUE_ID_BYTES = 128
 

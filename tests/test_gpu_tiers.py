@@ -1,7 +1,8 @@
 """GPU: the canonical tiers of the scan kernel -- lines the vocabulary fast path rejects
 (other ip addresses, ad_types, event_types, event_time lengths; compact JSON) parsed in
 the scan itself instead of the general path -- exact against the CPU oracle (org.json's
-grammar restated) and the generator truth, with nothing deferred."""
+grammar restated) and the generator truth, with nothing deferred; and the same with the
+compact-first layout hint (YSB_F_COMPACT_FIRST: the tiers reordered)."""
 import numpy as np
 import pytest
 
@@ -14,15 +15,16 @@ VARIANTS = [GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
             GEN_COMPACT | GEN_RANDOM_IP, GEN_COMPACT | GEN_RANDOM_IP | GEN_MORE_AD_TYPES]
 
 
+@pytest.mark.parametrize("compact_first", [False, True])
 @pytest.mark.parametrize("variant", VARIANTS)
-def test_tier_lines_exact_and_not_deferred(variant):
+def test_tier_lines_exact_and_not_deferred(variant, compact_first):
     g = GenParams(seed=23, n_campaigns=50, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
                   variant=variant)
     _, aids = g.ids()
     raw, offs = g.events_host(0, 150_000)
     exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), raw, offs)
     with YsbContext(n_campaigns=50, window_ring=256, max_batch_bytes=raw.size + 64,
-                    max_batch_events=offs.size + 1) as ctx:
+                    max_batch_events=offs.size + 1, compact_first=compact_first) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         ctx.submit(raw, offs)
         got = ctx.drain_buckets()
@@ -33,13 +35,15 @@ def test_tier_lines_exact_and_not_deferred(variant):
     assert st["deferred"] == 0                # every line taken by a scan tier
 
 
-@pytest.mark.parametrize("variant", [GEN_RANDOM_IP | GEN_MORE_AD_TYPES, GEN_COMPACT | GEN_RANDOM_IP])
-def test_tier_device_generator_truth(variant):
+@pytest.mark.parametrize("variant,compact_first", [(GEN_RANDOM_IP | GEN_MORE_AD_TYPES, False),
+                                                   (GEN_COMPACT | GEN_RANDOM_IP, False),
+                                                   (GEN_COMPACT | GEN_RANDOM_IP, True), (0, True)])
+def test_tier_device_generator_truth(variant, compact_first):
     g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000, variant=variant)
     _, aids = g.ids()
     n = 4_000_000
     hraw, _ = g.events_host(0, 20_000)
-    with YsbContext(n_campaigns=100, window_ring=1024) as ctx:
+    with YsbContext(n_campaigns=100, window_ring=1024, compact_first=compact_first) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         cap = n * g.max_line_bytes()
         d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
@@ -54,7 +58,8 @@ def test_tier_device_generator_truth(variant):
     assert st["deferred"] == 0 and st["parse_errors"] == 0 and st["join_misses"] == 0
 
 
-def test_tier_mixed_with_off_template_lines():
+@pytest.mark.parametrize("compact_first", [False, True])
+def test_tier_mixed_with_off_template_lines(compact_first):
     """Tier lines, vocabulary lines and general-path lines (whitespace, escapes, other key
     orders) interleaved in one batch: still exactly the oracle."""
     g0 = GenParams(seed=5, n_campaigns=20, ads_per_campaign=5, events_per_sec=100)
@@ -74,7 +79,7 @@ def test_tier_mixed_with_off_template_lines():
     offs = np.zeros(len(lines), dtype=np.uint32)
     offs[1:] = np.cumsum([len(x) + 1 for x in lines[:-1]])
     exp, est = oracle.run(oracle.AdMap(aids, g0.ad_campaign_index()), data, offs)
-    with YsbContext(n_campaigns=20, window_ring=64) as ctx:
+    with YsbContext(n_campaigns=20, window_ring=64, compact_first=compact_first) as ctx:
         ctx.load_ad_map(aids, g0.ad_campaign_index())
         ctx.submit(data, offs)
         got = ctx.drain_buckets()
@@ -85,7 +90,8 @@ def test_tier_mixed_with_off_template_lines():
     assert 0 < st["deferred"] <= 1000
 
 
-def test_canonical_tier_other_event_types_and_times():
+@pytest.mark.parametrize("compact_first", [False, True])
+def test_canonical_tier_other_event_types_and_times(compact_first):
     """Lines in the generator's layout whose event_type is none of the three or whose
     event_time is not 13 digits (the vocabulary path names both from closed sets) go to
     the canonical tier, not to the general path: exact, nothing deferred."""
@@ -111,7 +117,7 @@ def test_canonical_tier_other_event_types_and_times():
     offs2[1:] = np.cumsum([len(x) + 1 for x in out[:-1]])
     exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), data, offs2)
     with YsbContext(n_campaigns=40, window_ring=256, max_batch_bytes=len(data) + 64,
-                    max_batch_events=len(out) + 1) as ctx:
+                    max_batch_events=len(out) + 1, compact_first=compact_first) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         ctx.submit(data, offs2)
         got = ctx.drain_buckets()
