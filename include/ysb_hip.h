@@ -63,6 +63,12 @@ extern "C" {
                                    generator's (core.clj:90-96) as a later tier.  Counts
                                    are identical either way; only the speed differs.
                                    Cache-resident join tables only (ignored otherwise). */
+#define YSB_F_FLAT_FIRST 0x100u /* layout hint: JSON lines are flat objects in any key
+                                   order or spacing (another producer's serializer); the
+                                   scan parses every line with its flat-object tier first
+                                   (generator-layout lines too, a little slower than their
+                                   own path).  Counts are identical; takes precedence over
+                                   YSB_F_COMPACT_FIRST.  Cache-resident join tables only. */
 #define YSB_F_SPARSE_FAST_JOIN 0x8u /* test hook: leave every other 36-byte key out of
                                    the fast-path cuckoo table, as a failed cuckoo
                                    placement would; its misses then take the

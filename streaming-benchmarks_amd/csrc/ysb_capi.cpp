@@ -499,7 +499,7 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     p.ctable_partial = c->ctable_partial ? 1u : 0u;
     // HBM-resident table: buckets, the second one read only after a miss in a full first
     p.probe_serial = c->ctable_buckets ? 1u : 0u;
-    p.compact_first = (c->cfg.flags & YSB_F_COMPACT_FIRST) ? 1u : 0u;
+    p.layout = (c->cfg.flags & YSB_F_FLAT_FIRST) ? 2u : (c->cfg.flags & YSB_F_COMPACT_FIRST) ? 1u : 0u;
     p.n_campaigns = c->cfg.n_campaigns;
     p.counts = c->d_counts;
     p.ring_w = c->cfg.window_ring;

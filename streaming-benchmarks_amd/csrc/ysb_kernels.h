@@ -137,7 +137,7 @@ struct ScanParams {
     u32 rec_cap;                // records per (workgroup, bin) sub-buffer
     u32* rec;                   // [grid][rec_bins][rec_cap]
     u32* rec_n;                 // [grid][rec_bins] records written
-    u32 compact_first;          // 1: YSB_F_COMPACT_FIRST (the compact-JSON instantiation)
+    u32 layout;                 // JSON layout tried first: 0 generator, 1 YSB_F_COMPACT_FIRST, 2 YSB_F_FLAT_FIRST
 };
 
 // Record-mode pipeline after the scan (ysb_count.hip).  Level-2 bins ("blocks") are

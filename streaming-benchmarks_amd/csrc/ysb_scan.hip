@@ -423,8 +423,22 @@ __device__ __forceinline__ bool canon_stage1(const LdsSrc& src, int s, int e, Ca
 // the line or a NUL comes first.  Four bytes per step; of the two flag sets the lowest
 // flagged byte is exact (a false flag only sits above a true one: zero_bytes' borrow
 // above a zero byte, the +0x5F carry above a byte >= 0xA1, itself flagged by its top bit).
-template <class S>
+template <class S, bool FAST = false>
 __device__ __forceinline__ int ft_clean(const S& src, int p, int e, u32& c) {
+    if constexpr (FAST) {
+        // the first four bytes outside the loop: nearly every call ends there, and the
+        // loop becomes a region the wave skips when no lane needs it
+        if (p < e) {
+            const u32 x = src.load4(p);
+            const u32 z = (((x + 0x5F5F5F5Fu) | x) & 0x80808080u) | zero_bytes(x);
+            if (z != 0u) {
+                const int k = __builtin_ctz(z) >> 3;
+                c = (x >> (8 * k)) & 0xFFu;
+                return (p + k < e && c != 0u) ? p + k : -1;
+            }
+            p += 4;
+        }
+    }
     for (; p < e; p += 4) {
         const u32 x = src.load4(p);
         const u32 z = (((x + 0x5F5F5F5Fu) | x) & 0x80808080u) | zero_bytes(x);
@@ -821,14 +835,17 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
 // counted nothing, and parse_line decides the line.
 // true: the line is a flat object of the subset above with every field of `require` (and
 // the three the topology reads); ad / et / tm = the values' spans
-template <class S>
+// FAST (the flat-first instantiation only): the whitespace skips' first step outside their
+// loops, and the id values (ad / user / page) checked as 36-byte UUIDs in one step before
+// the string scan -- the same decisions, fewer divergent loop trips.
+template <class S, bool FAST = false>
 __device__ __forceinline__ bool flat_parse(const S& src, int s, int e, u32 require, Span& ad, Span& et, Span& tm) {
     u32 c = 0;
-    int p = ft_clean(src, s, e, c);
+    int p = ft_clean<S, FAST>(src, s, e, c);
     if (p < 0 || c != '{') return false;
     u32 seen = 0;
     for (;;) {
-        p = ft_clean(src, p + 1, e, c);                       // a key, or '}'
+        p = ft_clean<S, FAST>(src, p + 1, e, c);             // a key, or '}'
         if (p < 0) return false;
         if (c == '}') break;                                  // {} or a separator before '}'
         if (c != '"') return false;
@@ -837,17 +854,26 @@ __device__ __forceinline__ bool flat_parse(const S& src, int s, int e, u32 requi
         const u32 id = match_key_raw(src, p + 1, ke - p - 1);
         if (id == 0u || (seen & id) != 0u) return false;      // another key, or a repeat
         seen |= id;
-        p = ft_clean(src, ke + 1, e, c);
+        p = ft_clean<S, FAST>(src, ke + 1, e, c);
         if (p < 0 || c != ':') return false;
-        p = ft_clean(src, p + 1, e, c);
+        p = ft_clean<S, FAST>(src, p + 1, e, c);
         if (p < 0 || c != '"') return false;
-        const int ve = ft_string_end(src, p + 1, e);
+        int ve = -1;
+        if constexpr (FAST) {
+            if (id & (K_AD | K_USER | K_PAGE)) {   // 36 plain bytes and the closing quote
+                u32 f = 0;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) f |= ft_flags(src.load4(p + 1 + 4 * k));
+                if (f == 0u && p + 37 < e && src.b(p + 37) == '"') ve = p + 37;
+            }
+        }
+        if (ve < 0) ve = ft_string_end(src, p + 1, e);
         if (ve < 0) return false;
         const Span sp{p + 1, ve, 0};
         if (id == K_AD) ad = sp;
         else if (id == K_ETYPE) et = sp;
         else if (id == K_ETIME) tm = sp;
-        p = ft_clean(src, ve + 1, e, c);
+        p = ft_clean<S, FAST>(src, ve + 1, e, c);
         if (p < 0) return false;
         if (c == '}') break;
         if (c != ',' && c != ';') return false;
@@ -859,10 +885,10 @@ __device__ __forceinline__ bool flat_parse(const S& src, int s, int e, u32 requi
 // The scan kernel's fourth tier: a flat line whose ad_id is 36 plain bytes, in the form
 // the canonical tiers hand on (key words, event_time offset and first 20 bytes, view).
 // Other ad_id lengths go to the deferred-line kernel (its table lookup takes any key).
-template <class S>
+template <class S, bool FAST = false>
 __device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 require, CanonA& a, CanonB& b) {
     Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
-    if (!flat_parse(src, ls, le, require, ad, et, tm) || ad.e - ad.s != 36) return false;
+    if (!flat_parse<S, FAST>(src, ls, le, require, ad, et, tm) || ad.e - ad.s != 36) return false;
 #pragma unroll
     for (int k = 0; k < 9; ++k) a.kw[k] = src.load4(ad.s + 4 * k);
     a.t0 = tm.s - ls;
@@ -1163,9 +1189,12 @@ __device__ __forceinline__ void rec_write(const ScanParams& P, const u32* ring, 
 // separate instantiation so the cache-resident configuration's code is untouched).
 // TBL: the fork's .tbl rows (tbl_stage1/2) instead of JSON lines (vocab_stage1/2).
 // REC: record mode (ysb_count.hip): in-ring joined views become ring-cell records.
-// CPF: compact JSON first (YSB_F_COMPACT_FIRST): the compact layout's vocabulary path is
-// the first stage and the generator layout a later tier (the same tiers, reordered).
-template <bool SERIAL, bool TBL, bool REC, bool CPF = false>
+// LAY: the JSON layout tried first (the same grammar and counts; only the order of the
+// tiers differs).  0: the generator's (the default); 1, compact JSON first
+// (YSB_F_COMPACT_FIRST): the compact layout's vocabulary path is the first stage and the
+// generator layout a later tier; 2, any key order (YSB_F_FLAT_FIRST): the flat tier is the
+// only stage (every line a canonical tier takes, it takes too), with its FAST steps.
+template <bool SERIAL, bool TBL, bool REC, int LAY = 0>
 __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<TBL>::WG_PER_CU * SCAN_TPB + 255) / 256))) void scan_kernel(const ScanParams P0) {
     using G = Geom<TBL, REC>;
     constexpr int CPT = G::CPT;
@@ -1276,26 +1305,28 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
 #pragma unroll
         for (int k = 0; k < 9; ++k) ca.kw[k] = 0u;
         ca.t0 = 0;
+        CanonB cb;
+        cb.view = false;
         if (li < cur.count && !cur.oversize && my_off >= cur.s0 && my_end >= my_off && my_end <= cur.e) {
             elig = true;
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
-            else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1<CPF>(lsrc, ls, le, ca);
+            else if constexpr (LAY == 2) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb);
+            else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1<LAY == 1>(lsrc, ls, le, ca);
             else ok1 = canon_stage1<false>(lsrc, ls, le, ca);
         }
         bool pend = false, dfr = false, tok = false;
         i64 bucket = 0;
-        CanonB cb;
-        cb.view = false;
         bool ok2 = false;
         if (li < cur.count) {
             if constexpr (TBL) ok2 = ok1 && tbl_stage2(lsrc, ls, le, ca, cb);
-            else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2<CPF>(lsrc, ls, le, ca, cb);
+            else if constexpr (LAY == 2) ok2 = ok1;
+            else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2<LAY == 1>(lsrc, ls, le, ca, cb);
             else ok2 = ok1 && canon_stage2<false>(lsrc, ls, le, ca, cb);
         }
 #if YSB_CANON_TIERS
-        if constexpr (!TBL && YSB_VOCAB != 0) {
+        if constexpr (!TBL && YSB_VOCAB != 0 && LAY != 2) {
             // second and third tiers for the lanes the vocabulary path rejected (a branch
             // no lane takes on the generator's own lines): any values in the generator's
             // layout, then the same keys as compact JSON
@@ -1308,7 +1339,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 const bool up = lsrc.load4(ls) == w4('{', '"', 'u', 's') && lsrc.load4(ls + 4) == w4('e', 'r', '_', 'i') &&
                                 (h2 & 0xFFFFFFu) == (w4('d', '"', ':', 0) & 0xFFFFFFu);
                 bool t = false;
-                if constexpr (CPF) {   // the generator layout: its vocabulary path, then its canonical tier
+                if constexpr (LAY == 1) {   // the generator layout: its vocabulary path, then its canonical tier
                     if (up && (h2 >> 24) == ' ') {
                         t = vocab_stage1<false>(lsrc, ls, le, c2) && vocab_stage2<false>(lsrc, ls, le, c2, b2);
                         if (!t) t = canon_stage1<false>(lsrc, ls, le, c2) && canon_stage2<false>(lsrc, ls, le, c2, b2);
@@ -1818,7 +1849,8 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
     } else {
         if (p.rec_on) hipLaunchKernelGGL((scan_kernel<true, false, true>), g, b, (Geom<false, true>::LDS), s, p);
         else if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false, false>), g, b, Geom<false>::LDS, s, p);
-        else if (p.compact_first) hipLaunchKernelGGL((scan_kernel<false, false, false, true>), g, b, Geom<false>::LDS, s, p);
+        else if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<false, false, false, 1>), g, b, Geom<false>::LDS, s, p);
+        else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<false, false, false, 2>), g, b, Geom<false>::LDS, s, p);
         else hipLaunchKernelGGL((scan_kernel<false, false, false>), g, b, Geom<false>::LDS, s, p);
     }
 }

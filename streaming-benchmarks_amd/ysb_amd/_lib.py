@@ -26,6 +26,7 @@ YSB_F_FORMAT_TBL = 0x10
 YSB_F_RECORD_COUNT = 0x20
 YSB_F_NO_RECORD_COUNT = 0x40
 YSB_F_COMPACT_FIRST = 0x80
+YSB_F_FLAT_FIRST = 0x100
 INT64_MIN = -(1 << 63)
 UNIQUE_ID_BYTES = 128
 

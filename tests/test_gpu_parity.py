@@ -246,7 +246,7 @@ def test_tbl_generated_stream_vs_oracle():
             assert s[k] == v, k
 
 
-def _oracle_vs_gpu(lines, require_ip, lds=True, fmt="json", ad_map=None):
+def _oracle_vs_gpu(lines, require_ip, lds=True, fmt="json", ad_map=None, **ctx_kw):
     """Submits the lines as one batch; on a mismatch, bisects to the first line whose
     GPU counters differ from the C oracle's (for the failure message)."""
     ads, camp = ad_map or gd.ad_arrays()
@@ -255,7 +255,7 @@ def _oracle_vs_gpu(lines, require_ip, lds=True, fmt="json", ad_map=None):
     def run_gpu(ls):
         raw = b"".join(ls)
         offs = np.cumsum([0] + [len(x) for x in ls[:-1]]).tolist()
-        with make_ctx(ads=(ads, camp), require_ip=require_ip, lds_count=lds, input_format=fmt) as ctx:
+        with make_ctx(ads=(ads, camp), require_ip=require_ip, lds_count=lds, input_format=fmt, **ctx_kw) as ctx:
             ctx.submit(raw, offs, slot=0)
             rows = ctx.drain_buckets()
             st = ctx.stats()
@@ -531,3 +531,6 @@ def test_flat_tier_matches_oracle(seed):
     lines = _flat_lines(seed, 6000)
     _oracle_vs_gpu(lines, False)
     _oracle_vs_gpu(lines, True)
+    # the flat-first instantiation (YSB_F_FLAT_FIRST: the flat tier is the scan's only stage)
+    _oracle_vs_gpu(lines, False, flat_first=True)
+    _oracle_vs_gpu(lines, True, flat_first=True)

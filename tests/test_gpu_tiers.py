@@ -2,7 +2,8 @@
 (other ip addresses, ad_types, event_types, event_time lengths; compact JSON) parsed in
 the scan itself instead of the general path -- exact against the CPU oracle (org.json's
 grammar restated) and the generator truth, with nothing deferred; and the same with the
-compact-first layout hint (YSB_F_COMPACT_FIRST: the tiers reordered)."""
+layout hints (YSB_F_COMPACT_FIRST: the tiers reordered; YSB_F_FLAT_FIRST: the flat-object
+tier as the only stage)."""
 import numpy as np
 import pytest
 
@@ -15,16 +16,16 @@ VARIANTS = [GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
             GEN_COMPACT | GEN_RANDOM_IP, GEN_COMPACT | GEN_RANDOM_IP | GEN_MORE_AD_TYPES]
 
 
-@pytest.mark.parametrize("compact_first", [False, True])
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first"])
 @pytest.mark.parametrize("variant", VARIANTS)
-def test_tier_lines_exact_and_not_deferred(variant, compact_first):
+def test_tier_lines_exact_and_not_deferred(variant, hint):
     g = GenParams(seed=23, n_campaigns=50, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
                   variant=variant)
     _, aids = g.ids()
     raw, offs = g.events_host(0, 150_000)
     exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), raw, offs)
     with YsbContext(n_campaigns=50, window_ring=256, max_batch_bytes=raw.size + 64,
-                    max_batch_events=offs.size + 1, compact_first=compact_first) as ctx:
+                    max_batch_events=offs.size + 1, **({hint: True} if hint else {})) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         ctx.submit(raw, offs)
         got = ctx.drain_buckets()
@@ -35,15 +36,15 @@ def test_tier_lines_exact_and_not_deferred(variant, compact_first):
     assert st["deferred"] == 0                # every line taken by a scan tier
 
 
-@pytest.mark.parametrize("variant,compact_first", [(GEN_RANDOM_IP | GEN_MORE_AD_TYPES, False),
-                                                   (GEN_COMPACT | GEN_RANDOM_IP, False),
-                                                   (GEN_COMPACT | GEN_RANDOM_IP, True), (0, True)])
-def test_tier_device_generator_truth(variant, compact_first):
+@pytest.mark.parametrize("variant,hint", [(GEN_RANDOM_IP | GEN_MORE_AD_TYPES, None), (GEN_COMPACT | GEN_RANDOM_IP, None),
+                                          (GEN_COMPACT | GEN_RANDOM_IP, "compact_first"), (0, "compact_first"),
+                                          (GEN_RANDOM_IP | GEN_MORE_AD_TYPES, "flat_first"), (0, "flat_first")])
+def test_tier_device_generator_truth(variant, hint):
     g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000, variant=variant)
     _, aids = g.ids()
     n = 4_000_000
     hraw, _ = g.events_host(0, 20_000)
-    with YsbContext(n_campaigns=100, window_ring=1024, compact_first=compact_first) as ctx:
+    with YsbContext(n_campaigns=100, window_ring=1024, **({hint: True} if hint else {})) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         cap = n * g.max_line_bytes()
         d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
@@ -58,8 +59,8 @@ def test_tier_device_generator_truth(variant, compact_first):
     assert st["deferred"] == 0 and st["parse_errors"] == 0 and st["join_misses"] == 0
 
 
-@pytest.mark.parametrize("compact_first", [False, True])
-def test_tier_mixed_with_off_template_lines(compact_first):
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first"])
+def test_tier_mixed_with_off_template_lines(hint):
     """Tier lines, vocabulary lines and general-path lines (whitespace, escapes, other key
     orders) interleaved in one batch: still exactly the oracle."""
     g0 = GenParams(seed=5, n_campaigns=20, ads_per_campaign=5, events_per_sec=100)
@@ -79,7 +80,7 @@ def test_tier_mixed_with_off_template_lines(compact_first):
     offs = np.zeros(len(lines), dtype=np.uint32)
     offs[1:] = np.cumsum([len(x) + 1 for x in lines[:-1]])
     exp, est = oracle.run(oracle.AdMap(aids, g0.ad_campaign_index()), data, offs)
-    with YsbContext(n_campaigns=20, window_ring=64, compact_first=compact_first) as ctx:
+    with YsbContext(n_campaigns=20, window_ring=64, **({hint: True} if hint else {})) as ctx:
         ctx.load_ad_map(aids, g0.ad_campaign_index())
         ctx.submit(data, offs)
         got = ctx.drain_buckets()
@@ -90,8 +91,8 @@ def test_tier_mixed_with_off_template_lines(compact_first):
     assert 0 < st["deferred"] <= 1000
 
 
-@pytest.mark.parametrize("compact_first", [False, True])
-def test_canonical_tier_other_event_types_and_times(compact_first):
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first"])
+def test_canonical_tier_other_event_types_and_times(hint):
     """Lines in the generator's layout whose event_type is none of the three or whose
     event_time is not 13 digits (the vocabulary path names both from closed sets) go to
     the canonical tier, not to the general path: exact, nothing deferred."""
@@ -117,7 +118,7 @@ def test_canonical_tier_other_event_types_and_times(compact_first):
     offs2[1:] = np.cumsum([len(x) + 1 for x in out[:-1]])
     exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), data, offs2)
     with YsbContext(n_campaigns=40, window_ring=256, max_batch_bytes=len(data) + 64,
-                    max_batch_events=len(out) + 1, compact_first=compact_first) as ctx:
+                    max_batch_events=len(out) + 1, **({hint: True} if hint else {})) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         ctx.submit(data, offs2)
         got = ctx.drain_buckets()

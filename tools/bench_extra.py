@@ -177,7 +177,8 @@ def general(args):
     nl = np.flatnonzero(np.frombuffer(data, dtype=np.uint8) == 0x0A)
     offs2[1:] = (nl[:-1] + 1).astype(np.uint32)
     ctx = YsbContext(n_campaigns=100, window_ring=1024, timing=True, max_batch_bytes=args.batch_mb << 20,
-                     max_batch_events=(args.batch_mb << 20) // 200)
+                     max_batch_events=(args.batch_mb << 20) // 200, compact_first=args.hint == "compact",
+                     flat_first=args.hint == "flat")
     ctx.load_ad_map(aids, g.ad_campaign_index())
     d_b, d_o = ctx.device_alloc(len(data) + 64), ctx.device_alloc(4 * n + 64)
     ctx.h2d(d_b, np.frombuffer(data, dtype=np.uint8))
@@ -198,7 +199,7 @@ def general(args):
     got = ctx.drain_buckets()
     st = ctx.stats()
     rows, ost = orc.run(orc.AdMap(aids, g.ad_campaign_index()), data, offs2.tolist(), threads=8)
-    return {"config": "%d generator events, shape %s" % (n, args.shape),
+    return {"config": "%d generator events, shape %s, layout hint %s" % (n, args.shape, args.hint),
             "events_per_s": round(n * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
             "device_ms_per_step": round(dev_ms / max(1, args.steps), 3), "launches": launches,
             "deferred": st["deferred"], "exact_vs_oracle": got == rows and all(st[k] == v for k, v in ost.items())}
@@ -415,6 +416,8 @@ def main():
     ap.add_argument("--shape", default="reorder", choices=["generator", "compact", "reorder", "spaced", "escaped"],
                     help="general: how the generator's lines are re-laid")
     ap.add_argument("--shards", type=int, default=2, help="stream_sharded: contexts (one per GPU)")
+    ap.add_argument("--hint", default="none", choices=["none", "compact", "flat"],
+                    help="general: layout hint (YSB_F_COMPACT_FIRST / YSB_F_FLAT_FIRST)")
     args = ap.parse_args()
     out = {"config3": config3, "tbl": tbl, "general": general, "pcie": pcie, "stream": stream,
            "stream_sharded": stream_sharded}[args.mode](args)
