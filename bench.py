@@ -317,7 +317,7 @@ def extras(args, device):
         segs = gen_segments(ctx, g, 100_000_000, 16_666_667)   # 6 batches, as the headline
         r = timed_extra("configs[2]: 100M JSON events, 1M campaigns x 10 ads (10M-ad join table and "
                         "1M x 128-bucket count ring in HBM)", ctx, g, segs, args.extra_steps, args.warmup,
-                        "ysb::scan_kernel<true, false, true>")
+                        "ysb::scan_kernel<true, false, true, 0>")
         r["ad_map_load_s"] = round(load_s, 2)
         out["config3"] = r
         free_segments(ctx, segs)
@@ -330,7 +330,7 @@ def extras(args, device):
         segs = gen_segments(ctx, g, 100_000_000, 25_000_000)   # 4 batches of ~3.5 GB (rows ~140 B)
         out["tbl"] = timed_extra("configs[1]'s 100M events as the fork's .tbl rows (MockWindowedFlatMap, "
                                  "AdvertisingTopologyNative.java:197-226)", ctx, g, segs, args.extra_steps,
-                                 args.warmup, "ysb::scan_kernel<false, true, false>")
+                                 args.warmup, "ysb::scan_kernel<false, true, false, 0>")
         free_segments(ctx, segs)
     log("extras: tbl %.2f G events/s" % (out["tbl"]["events_per_s"] / 1e9))
     # the same events as other producers would write them: other ip / ad_type values (the
@@ -353,7 +353,7 @@ def extras(args, device):
             # lines up to ~280 B: 7 batches keep each under the 4 GiB of u32 offsets
             segs = gen_segments(ctx, g, 100_000_000, 14_285_715)
             out[key] = timed_extra("configs[1]'s 100M events, " + what, ctx, g, segs, args.extra_steps,
-                                   args.warmup, "ysb::scan_kernel<false, false, false%s>" % (", true" if cf else ""))
+                                   args.warmup, "ysb::scan_kernel<false, false, false, %d>" % (1 if cf else 0))
             free_segments(ctx, segs)
         log("extras: %s %.2f G events/s" % (key, out[key]["events_per_s"] / 1e9))
     if args.stream_seconds > 0:
@@ -543,7 +543,7 @@ def main():
                        else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "ysb::scan_kernel<false, false, false>", "avg_launch_ms": round(avg_launch_ms, 4),
+                         "kernel": "ysb::scan_kernel<false, false, false, 0>", "avg_launch_ms": round(avg_launch_ms, 4),
                          "alg_bytes_per_launch": int(alg_bytes_launch)},
             "cpu_baseline": cpu,
             "check": check,
