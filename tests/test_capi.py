@@ -124,3 +124,15 @@ def test_ad_shard_is_stable_and_balanced():
             assert 0 <= s < n and s == ad_shard(a, n)
             counts[s] += 1
         assert min(counts) > 1000 / n * 0.7
+
+
+def test_config_flags_match_the_header():
+    """Every YSB_F_* flag the header defines has the same value in the ctypes mirror, and
+    no two flags share a bit."""
+    src = open(HEADER).read()
+    flags = {m.group(1): int(m.group(2), 16) for m in re.finditer(r"^#define (YSB_F_\w+)\s+0x([0-9a-fA-F]+)u", src, re.M)}
+    assert "YSB_F_COMPACT_FIRST" in flags and "YSB_F_FLAT_FIRST" in flags
+    for name, v in flags.items():
+        assert getattr(_lib, name) == v, name
+    vals = list(flags.values())
+    assert all(v & (v - 1) == 0 for v in vals) and len(set(vals)) == len(vals)
