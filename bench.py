@@ -129,6 +129,16 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # this rank's GPU: LOCAL_RANK, unless the launcher left each process fewer visible
+        # devices (e.g. one per rank through HIP_VISIBLE_DEVICES): then the k-th visible one
+        self.device = self.local
+        try:
+            import torch
+            nvis = torch.cuda.device_count()   # counts devices without initialising one
+            if 0 < nvis <= self.local:
+                self.device = self.local % nvis
+        except Exception:
+            pass
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
@@ -188,7 +198,7 @@ def dry_run(d, args):
     stop-the-others path: the remaining ranks would wait in the gather forever)."""
     if os.environ.get("YSB_BENCH_FAIL_RANK") == str(d.rank):
         sys.exit(3)
-    info = {"rank": d.rank, "local_rank": d.local, "world": d.world, "pid": os.getpid(),
+    info = {"rank": d.rank, "local_rank": d.local, "device": d.device, "world": d.world, "pid": os.getpid(),
             "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")),
             "events_per_gpu": args.events}
     allinfo = d.gather(info)
@@ -434,7 +444,7 @@ def main():
     else:
         g = base
 
-    ctx = YsbContext(device=d.local, n_campaigns=100, window_ring=W, timing=True, ring_base_bucket=ring_base,
+    ctx = YsbContext(device=d.device, n_campaigns=100, window_ring=W, timing=True, ring_base_bucket=ring_base,
                      max_batch_bytes=16 << 20, max_batch_events=1 << 16)
     # N > 1: the input is sharded by ad_id hash, so each rank holds only its shard of the
     # join table; the post-exchange check proves nothing is missed
@@ -465,18 +475,18 @@ def main():
 
     # torch's own CUDA context is created here, before the warmup: created between warmup
     # and timing it idles the GPU ~1.5 s and the first timed steps run at ramping clocks
-    torch_sync(d.local)
+    torch_sync(d.device)
     for _ in range(args.warmup):
         step()
     ctx.sync()
     ctx.kernel_time()   # discard warmup launches
-    torch_sync(d.local)
+    torch_sync(d.device)
     d.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     ctx.sync()
-    torch_sync(d.local)
+    torch_sync(d.device)
     d.barrier()
     el = d.max(time.perf_counter() - t0)
     kms, launches = ctx.kernel_time()
@@ -522,7 +532,7 @@ def main():
     if d.world == 1 and not args.no_extras:
         free_segments(ctx, segs)
         ctx.close()
-        extra = extras(args, d.local)
+        extra = extras(args, d.device)
 
     if d.rank == 0:
         out = {

@@ -364,6 +364,7 @@ def stream_sharded(args):
             return raw.size, m
         return fill
     last_tick = clock()
+    last_log = time.time()
     while min(produced) < n_total:
         for r in range(n):
             op.fill_with(r, producer(r))
@@ -372,6 +373,10 @@ def stream_sharded(args):
             last_tick = clock()
         else:
             time.sleep(0.001)
+        if time.time() - last_log >= 30:   # progress (a long run stays visibly alive)
+            last_log = time.time()
+            log("stream_sharded: %.0f s, %d events, %d flushes" % (last_log - wall0 / 1000.0, sum(produced),
+                                                                    op.flushes))
     op.close()
     ref = {}
     for r in range(n):
