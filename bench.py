@@ -345,7 +345,7 @@ def extras(args, device):
     log("extras: tbl %.2f G events/s" % (out["tbl"]["events_per_s"] / 1e9))
     # the same events as other producers would write them: other ip / ad_type values (the
     # vocabulary path's generic-value branches) and compact JSON (the scan's third tier)
-    from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP
+    from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER
     for key, variant, cf, what in (("random_ip", GEN_RANDOM_IP, False, "random dotted-quad ip_address"),
                                    ("random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES, False,
                                     "random dotted-quad ip_address and 8 ad_types"),
@@ -354,16 +354,24 @@ def extras(args, device):
                                     "the compact layout's vocabulary path first)"),
                                    ("compact_json_no_hint", GEN_COMPACT, False,
                                     "compact JSON without the layout hint (the generator layout tried first, "
-                                    "the compact one as the third tier)")):
+                                    "the compact one as the third tier)"),
+                                   ("reordered_keys", GEN_REORDER, "flat",
+                                    "the keys in another order (ad_type, event_time, ad_id, ip_address, user_id, "
+                                    "event_type, page_id), layout hint YSB_F_FLAT_FIRST: the flat-object tier first"),
+                                   ("reordered_keys_no_hint", GEN_REORDER, False,
+                                    "the keys in another order without the layout hint (the scan's fourth tier, "
+                                    "after the vocabulary path fails)")):
         g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, variant=variant)
         _, aids = g.ids()
         with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True,
-                        max_batch_bytes=16 << 20, max_batch_events=1 << 16, compact_first=cf) as ctx:
+                        max_batch_bytes=16 << 20, max_batch_events=1 << 16, compact_first=cf is True,
+                        flat_first=cf == "flat") as ctx:
             ctx.load_ad_map(aids, g.ad_campaign_index())
             # lines up to ~280 B: 7 batches keep each under the 4 GiB of u32 offsets
             segs = gen_segments(ctx, g, 100_000_000, 14_285_715)
             out[key] = timed_extra("configs[1]'s 100M events, " + what, ctx, g, segs, args.extra_steps,
-                                   args.warmup, "ysb::scan_kernel<false, false, false, %d>" % (1 if cf else 0))
+                                   args.warmup, "ysb::scan_kernel<false, false, false, %d>"
+                                   % (2 if cf == "flat" else 1 if cf else 0))
             free_segments(ctx, segs)
         log("extras: %s %.2f G events/s" % (key, out[key]["events_per_s"] / 1e9))
     if args.stream_seconds > 0:

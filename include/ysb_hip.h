@@ -283,9 +283,10 @@ typedef struct ysb_gen_params {
     uint32_t format;            /* YSB_GEN_JSON (core.clj:90-97 lines) or YSB_GEN_TBL (the
                                    fork's .tbl rows of the same events, :197-226)       */
     uint32_t variant;           /* 0: the generator's own lines; YSB_GEN_RANDOM_IP /
-                                   YSB_GEN_MORE_AD_TYPES / YSB_GEN_COMPACT: the same events
-                                   as other producers would write them (a random dotted-quad
-                                   ip_address, 8 ad_types, no space after ':' and ',') --
+                                   YSB_GEN_MORE_AD_TYPES / YSB_GEN_COMPACT / YSB_GEN_REORDER:
+                                   the same events as other producers would write them (a
+                                   random dotted-quad ip_address, 8 ad_types, no space after
+                                   ':' and ',', the keys in another fixed order) --
                                    lines the vocabulary fast path does not take; the views,
                                    ads and times (and so the truth) are unchanged except that
                                    YSB_GEN_MORE_AD_TYPES draws the ad_type from 8           */
@@ -295,6 +296,7 @@ typedef struct ysb_gen_params {
 #define YSB_GEN_RANDOM_IP     1u
 #define YSB_GEN_MORE_AD_TYPES 2u
 #define YSB_GEN_COMPACT       4u
+#define YSB_GEN_REORDER       8u
 
 void        ysb_gen_default(ysb_gen_params* p);
 /* Campaign and ad UUIDs, 36 bytes each, no separators (ad a -> campaign a / ads_per_campaign). */

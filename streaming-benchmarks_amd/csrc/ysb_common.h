@@ -103,6 +103,7 @@ enum : u32 {
     GEN_V_RANDOM_IP = 1u,      // ip_address a random dotted quad instead of "1.2.3.4"
     GEN_V_MORE_AD_TYPES = 2u,  // ad_type one of 8 (adds native-video / interstitial / rewarded)
     GEN_V_COMPACT = 4u,        // no space after ':' and ',' (compact JSON)
+    GEN_V_REORDER = 8u,        // the seven pairs in another (fixed) key order
 };
 enum : u32 { S_IP = 9 };
 
@@ -165,56 +166,74 @@ YSB_HD char* put_str(char* o, const char* s, u32 n) {
     return o + n;
 }
 
-// A variant line (GEN_V_RANDOM_IP / GEN_V_COMPACT): the same seven keys in the same
-// order, the separators with or without their space, the ip a random dotted quad.
+// A variant line (GEN_V_RANDOM_IP / GEN_V_COMPACT / GEN_V_REORDER): the same seven keys,
+// in the generator's order or (GEN_V_REORDER) in the order ad_type, event_time, ad_id,
+// ip_address, user_id, event_type, page_id; the separators with or without their space;
+// the ip a random dotted quad.  Same pieces, so gen_line_len holds for every variant.
 YSB_HD u32 gen_line_write_variant(const GenSpec& s, u64 i, const GenEvent& e, char* out) {
     const bool cp = (s.variant & GEN_V_COMPACT) != 0;
     const char* sep = cp ? "\",\"" : "\", \"";       // between a value and the next key
     const char* col = cp ? "\":\"" : "\": \"";       // between a key and its value
     const u32 ls = cp ? 3u : 4u;
+    const u32 order_gen[7] = {0, 1, 2, 3, 4, 5, 6};
+    const u32 order_re[7] = {3, 5, 2, 6, 0, 4, 1};
+    const u32* order = (s.variant & GEN_V_REORDER) ? order_re : order_gen;
     char* o = out;
     u64 hi, lo;
     *o++ = '{';
     *o++ = '"';
-    o = put_str(o, "user_id", 7);
-    o = put_str(o, col, ls);
-    if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
-    else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);
-    uuid_format(hi, lo, o); o += 36;
-    o = put_str(o, sep, ls);
-    o = put_str(o, "page_id", 7);
-    o = put_str(o, col, ls);
-    if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_PAGE), i, &hi, &lo);
-    else uuid_words(stream_key(s.ev_seed, S_PAGE), draw(stream_key(s.ev_seed, S_PAGEPOOL), i) % s.n_users, &hi, &lo);
-    uuid_format(hi, lo, o); o += 36;
-    o = put_str(o, sep, ls);
-    o = put_str(o, "ad_id", 5);
-    o = put_str(o, col, ls);
-    uuid_words(stream_key(s.seed, S_AD), e.ad, &hi, &lo);
-    uuid_format(hi, lo, o); o += 36;
-    o = put_str(o, sep, ls);
-    o = put_str(o, "ad_type", 7);
-    o = put_str(o, col, ls);
-    o = put_str(o, ad_type_str(e.ad_type), ad_type_len(e.ad_type));
-    o = put_str(o, sep, ls);
-    o = put_str(o, "event_type", 10);
-    o = put_str(o, col, ls);
-    o = put_str(o, event_type_str(e.event_type), event_type_len(e.event_type));
-    o = put_str(o, sep, ls);
-    o = put_str(o, "event_time", 10);
-    o = put_str(o, col, ls);
-    o += dec_format(e.time_ms, o);
-    o = put_str(o, sep, ls);
-    o = put_str(o, "ip_address", 10);
-    o = put_str(o, col, ls);
-    if (s.variant & GEN_V_RANDOM_IP) {
-        const u32 ip = gen_ip(s, i);
-        for (int k = 0; k < 4; ++k) {
-            if (k) *o++ = '.';
-            o += dec_format((i64)((ip >> (8 * k)) & 0xFF), o);
+    for (u32 k = 0; k < 7; ++k) {
+        if (k) o = put_str(o, sep, ls);
+        switch (order[k]) {
+        case 0:
+            o = put_str(o, "user_id", 7);
+            o = put_str(o, col, ls);
+            if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
+            else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);
+            uuid_format(hi, lo, o); o += 36;
+            break;
+        case 1:
+            o = put_str(o, "page_id", 7);
+            o = put_str(o, col, ls);
+            if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_PAGE), i, &hi, &lo);
+            else uuid_words(stream_key(s.ev_seed, S_PAGE), draw(stream_key(s.ev_seed, S_PAGEPOOL), i) % s.n_users, &hi, &lo);
+            uuid_format(hi, lo, o); o += 36;
+            break;
+        case 2:
+            o = put_str(o, "ad_id", 5);
+            o = put_str(o, col, ls);
+            uuid_words(stream_key(s.seed, S_AD), e.ad, &hi, &lo);
+            uuid_format(hi, lo, o); o += 36;
+            break;
+        case 3:
+            o = put_str(o, "ad_type", 7);
+            o = put_str(o, col, ls);
+            o = put_str(o, ad_type_str(e.ad_type), ad_type_len(e.ad_type));
+            break;
+        case 4:
+            o = put_str(o, "event_type", 10);
+            o = put_str(o, col, ls);
+            o = put_str(o, event_type_str(e.event_type), event_type_len(e.event_type));
+            break;
+        case 5:
+            o = put_str(o, "event_time", 10);
+            o = put_str(o, col, ls);
+            o += dec_format(e.time_ms, o);
+            break;
+        default:
+            o = put_str(o, "ip_address", 10);
+            o = put_str(o, col, ls);
+            if (s.variant & GEN_V_RANDOM_IP) {
+                const u32 ip = gen_ip(s, i);
+                for (int q = 0; q < 4; ++q) {
+                    if (q) *o++ = '.';
+                    o += dec_format((i64)((ip >> (8 * q)) & 0xFF), o);
+                }
+            } else {
+                o = put_str(o, "1.2.3.4", 7);
+            }
+            break;
         }
-    } else {
-        o = put_str(o, "1.2.3.4", 7);
     }
     *o++ = '"';
     *o++ = '}';
@@ -249,7 +268,7 @@ YSB_HD u32 gen_line_write(const GenSpec& s, u64 i, const GenEvent& e, char* out)
         *o++ = '\n';
         return (u32)(o - out);
     }
-    if (s.variant & (GEN_V_RANDOM_IP | GEN_V_COMPACT)) return gen_line_write_variant(s, i, e, out);
+    if (s.variant & (GEN_V_RANDOM_IP | GEN_V_COMPACT | GEN_V_REORDER)) return gen_line_write_variant(s, i, e, out);
     o = put_str(o, YSB_P0, LEN_P0);
     if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
     else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);

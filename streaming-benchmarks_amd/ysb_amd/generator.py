@@ -12,7 +12,7 @@ from ._lib import YsbGenParams, check, lib
 
 AD_TYPES = ("banner", "modal", "sponsored-search", "mail", "mobile")   # core.clj:68
 MORE_AD_TYPES = AD_TYPES + ("native-video", "interstitial", "rewarded")  # GEN_MORE_AD_TYPES
-GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_COMPACT = 1, 2, 4
+GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_COMPACT, GEN_REORDER = 1, 2, 4, 8
 EVENT_TYPES = ("view", "click", "purchase")                            # core.clj:69
 
 
@@ -36,7 +36,7 @@ class GenParams:
         if fmt not in ("json", "tbl"):
             raise ValueError("fmt must be 'json' or 'tbl'")
         self.c.format = 1 if fmt == "tbl" else 0   # YSB_GEN_TBL: the fork's .tbl rows
-        # variant: GEN_RANDOM_IP | GEN_MORE_AD_TYPES | GEN_COMPACT (off-vocabulary layouts)
+        # variant: GEN_RANDOM_IP | GEN_MORE_AD_TYPES | GEN_COMPACT | GEN_REORDER (off-vocabulary layouts)
         self.c.variant = variant
         self._subset = None
         if ad_subset is not None:

@@ -8,12 +8,13 @@ import numpy as np
 import pytest
 
 from oracle import oracle
-from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GenParams, YsbContext
+from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER, GenParams, YsbContext
 
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_RANDOM_IP | GEN_MORE_AD_TYPES, GEN_COMPACT,
-            GEN_COMPACT | GEN_RANDOM_IP, GEN_COMPACT | GEN_RANDOM_IP | GEN_MORE_AD_TYPES]
+            GEN_COMPACT | GEN_RANDOM_IP, GEN_COMPACT | GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
+            GEN_REORDER, GEN_REORDER | GEN_COMPACT | GEN_RANDOM_IP]
 
 
 @pytest.mark.parametrize("hint", [None, "compact_first", "flat_first"])
@@ -38,7 +39,8 @@ def test_tier_lines_exact_and_not_deferred(variant, hint):
 
 @pytest.mark.parametrize("variant,hint", [(GEN_RANDOM_IP | GEN_MORE_AD_TYPES, None), (GEN_COMPACT | GEN_RANDOM_IP, None),
                                           (GEN_COMPACT | GEN_RANDOM_IP, "compact_first"), (0, "compact_first"),
-                                          (GEN_RANDOM_IP | GEN_MORE_AD_TYPES, "flat_first"), (0, "flat_first")])
+                                          (GEN_RANDOM_IP | GEN_MORE_AD_TYPES, "flat_first"), (0, "flat_first"),
+                                          (GEN_REORDER, None), (GEN_REORDER | GEN_RANDOM_IP, "flat_first")])
 def test_tier_device_generator_truth(variant, hint):
     g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000, variant=variant)
     _, aids = g.ids()

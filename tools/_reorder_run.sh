@@ -1,0 +1,9 @@
+set -e
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out/reo; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tiers.py tests/test_generator.py > $OUT/tests.log 2>&1
+echo tests ok
+timeout -k 10 500 python -u bench.py --no-cpu --stream-seconds 0 > $OUT/bench.json 2> $OUT/bench.err
+python3 -c "
+import json;d=json.load(open('$OUT/bench.json'));print(d['value']/1e9, d['roofline']['frac'])
+for k,e in d['extras'].items(): print(k, round(e.get('events_per_s',0)/1e9,3), e.get('avg_launch_ms'), e.get('hbm_frac'), e.get('check',{}).get('truth_mismatched_cells'), e.get('check',{}).get('deferred'))"
