@@ -835,6 +835,109 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
 // counted nothing, and parse_line decides the line.
 // true: the line is a flat object of the subset above with every field of `require` (and
 // the three the topology reads); ad / et / tm = the values' spans
+// The flat-first instantiation's parser of the same subset (flat_parse below decides every
+// line identically): a key is one of DeserializeBolt's seven, so it is named by its first
+// four bytes and its remaining bytes and closing quote compared in place (any other key,
+// or one with an escape, fails the compare as it fails match_key_raw); the separators
+// `": "` / `":"` after a key and `", "` / `","` / `}` after a value are compared in place,
+// any other spacing takes the ft_clean scans; the id values are checked as 36-byte UUIDs
+// in one step.  Positions read past e are never accepted (each fast compare checks the
+// bytes it uses are < e).
+template <class S>
+__device__ __forceinline__ bool flat_parse_fast(const S& src, int s, int e, u32 require, Span& ad, Span& et,
+                                                Span& tm) {
+    u32 c = 0;
+    int p = ft_clean<S, true>(src, s, e, c);
+    if (p < 0 || c != '{') return false;
+    p = ft_clean<S, true>(src, p + 1, e, c);             // the first key, or '}'
+    if (p < 0) return false;
+    u32 seen = 0;
+    if (c != '}') {
+        if (c != '"') return false;
+        int kq = p;                                       // the next key's opening quote
+        for (;;) {
+            const u32 k0 = src.load4(kq + 1);
+            u32 id = 0;
+            int kl = 0;
+            if (k0 == w4('a', 'd', '_', 'i')) {
+                kl = 5;
+                id = src.b(kq + 5) == 'd' ? K_AD : 0u;
+            } else if (k0 == w4('u', 's', 'e', 'r')) {
+                kl = 7;
+                id = src.load4(kq + 4) == w4('r', '_', 'i', 'd') ? K_USER : 0u;
+            } else if (k0 == w4('p', 'a', 'g', 'e')) {
+                kl = 7;
+                id = src.load4(kq + 4) == w4('e', '_', 'i', 'd') ? K_PAGE : 0u;
+            } else if (k0 == w4('a', 'd', '_', 't')) {
+                kl = 7;
+                id = src.load4(kq + 4) == w4('t', 'y', 'p', 'e') ? K_ADTYPE : 0u;
+            } else if (k0 == w4('e', 'v', 'e', 'n')) {
+                kl = 10;
+                const u32 k1 = src.load4(kq + 5), k2 = src.load4(kq + 7);
+                id = (k1 == w4('t', '_', 't', 'y') && k2 == w4('t', 'y', 'p', 'e'))   ? K_ETYPE
+                     : (k1 == w4('t', '_', 't', 'i') && k2 == w4('t', 'i', 'm', 'e')) ? K_ETIME
+                                                                                        : 0u;
+            } else if (k0 == w4('i', 'p', '_', 'a')) {
+                kl = 10;
+                id = (src.load4(kq + 5) == w4('d', 'd', 'r', 'e') && src.load4(kq + 7) == w4('r', 'e', 's', 's')) ? K_IP
+                                                                                                                 : 0u;
+            }
+            const int ke = kq + 1 + kl;                   // the key's closing quote
+            if (id == 0u || (seen & id) != 0u || ke >= e || src.b(ke) != '"') return false;
+            seen |= id;
+            // ':' and the value's opening quote
+            int vq;
+            const u32 w = src.load4(ke + 1);
+            if ((w & 0xFFFFFFu) == (w4(':', ' ', '"', 0) & 0xFFFFFFu) && ke + 3 < e) {
+                vq = ke + 3;
+            } else if ((w & 0xFFFFu) == (w4(':', '"', 0, 0) & 0xFFFFu) && ke + 2 < e) {
+                vq = ke + 2;
+            } else {
+                p = ft_clean<S, true>(src, ke + 1, e, c);
+                if (p < 0 || c != ':') return false;
+                p = ft_clean<S, true>(src, p + 1, e, c);
+                if (p < 0 || c != '"') return false;
+                vq = p;
+            }
+            int ve = -1;
+            if (id & (K_AD | K_USER | K_PAGE)) {          // 36 plain bytes and the closing quote
+                u32 f = 0;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) f |= ft_flags(src.load4(vq + 1 + 4 * k));
+                if (f == 0u && vq + 37 < e && src.b(vq + 37) == '"') ve = vq + 37;
+            }
+            if (ve < 0) ve = ft_string_end(src, vq + 1, e);
+            if (ve < 0) return false;
+            const Span sp{vq + 1, ve, 0};
+            if (id == K_AD) ad = sp;
+            else if (id == K_ETYPE) et = sp;
+            else if (id == K_ETIME) tm = sp;
+            // ', "' / ',"' and the next key, or '}'
+            const u32 x = src.load4(ve + 1);
+            if ((x & 0xFFFFFFu) == (w4(',', ' ', '"', 0) & 0xFFFFFFu) && ve + 3 < e) {
+                kq = ve + 3;
+                continue;
+            }
+            if ((x & 0xFFFFu) == (w4(',', '"', 0, 0) & 0xFFFFu) && ve + 2 < e) {
+                kq = ve + 2;
+                continue;
+            }
+            if ((x & 0xFFu) == '}' && ve + 1 < e) break;
+            p = ft_clean<S, true>(src, ve + 1, e, c);
+            if (p < 0) return false;
+            if (c == '}') break;
+            if (c != ',' && c != ';') return false;
+            p = ft_clean<S, true>(src, p + 1, e, c);     // the next key, or '}' after a separator
+            if (p < 0) return false;
+            if (c == '}') break;
+            if (c != '"') return false;
+            kq = p;
+        }
+    }
+    const u32 need = require | K_AD | K_ETYPE | K_ETIME;
+    return (seen & need) == need;
+}
+
 // FAST (the flat-first instantiation only): the whitespace skips' first step outside their
 // loops, and the id values (ad / user / page) checked as 36-byte UUIDs in one step before
 // the string scan -- the same decisions, fewer divergent loop trips.
@@ -888,7 +991,10 @@ __device__ __forceinline__ bool flat_parse(const S& src, int s, int e, u32 requi
 template <class S, bool FAST = false>
 __device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 require, CanonA& a, CanonB& b) {
     Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
-    if (!flat_parse<S, FAST>(src, ls, le, require, ad, et, tm) || ad.e - ad.s != 36) return false;
+    bool okp;
+    if constexpr (FAST) okp = flat_parse_fast(src, ls, le, require, ad, et, tm);
+    else okp = flat_parse<S, FAST>(src, ls, le, require, ad, et, tm);
+    if (!okp || ad.e - ad.s != 36) return false;
 #pragma unroll
     for (int k = 0; k < 9; ++k) a.kw[k] = src.load4(ad.s + 4 * k);
     a.t0 = tm.s - ls;
