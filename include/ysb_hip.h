@@ -69,6 +69,11 @@ extern "C" {
                                    (generator-layout lines too, a little slower than their
                                    own path).  Counts are identical; takes precedence over
                                    YSB_F_COMPACT_FIRST.  Cache-resident join tables only. */
+#define YSB_F_LAYOUT_AUTO 0x200u /* layout hint read from the data: ysb_submit picks the
+                                   instantiation from the first line of the batch it is
+                                   handed (the generator's layout, compact JSON, or the
+                                   flat-object tier first); device batches keep the flags.
+                                   Counts are identical whichever runs. */
 #define YSB_F_SPARSE_FAST_JOIN 0x8u /* test hook: leave every other 36-byte key out of
                                    the fast-path cuckoo table, as a failed cuckoo
                                    placement would; its misses then take the

@@ -36,6 +36,7 @@ struct ysb_ctx {
     u32* d_ctable = nullptr;   // 36-byte-key cuckoo table
     u64 ctable_slots = 0;      // slots, or buckets when ctable_buckets
     bool ctable_buckets = false; // HBM-resident table: 3-entry 128-B buckets (CB_*), serial probes
+    int submit_layout = -1;      // YSB_F_LAYOUT_AUTO: the layout ysb_submit read off the slot's first line
     CuckooSeed cseed{};
     bool ctable_partial = false;
     bool table_loaded = false;
@@ -500,6 +501,7 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     // HBM-resident table: buckets, the second one read only after a miss in a full first
     p.probe_serial = c->ctable_buckets ? 1u : 0u;
     p.layout = (c->cfg.flags & YSB_F_FLAT_FIRST) ? 2u : (c->cfg.flags & YSB_F_COMPACT_FIRST) ? 1u : 0u;
+    if (c->submit_layout >= 0) p.layout = (u32)c->submit_layout;
     p.n_campaigns = c->cfg.n_campaigns;
     p.counts = c->d_counts;
     p.ring_w = c->cfg.window_ring;
@@ -736,6 +738,20 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     return YSB_OK;
 }
 
+// The JSON layout of a batch's first line: 0 the generator's ({"user_id": "...), 1 compact
+// ({"user_id":"...), 2 anything else (the flat-object tier first).
+static int sniff_layout(const uint8_t* bytes, u64 nbytes, const u32* off, u64 n) {
+    const u64 s = off[0];
+    const u64 e = n > 1 ? (u64)off[1] : nbytes;
+    if (s >= e || e > nbytes) return 0;
+    static const char gen[] = "{\"user_id\": \"";
+    static const char cpt[] = "{\"user_id\":\"";
+    const u64 len = e - s;
+    if (len >= sizeof(gen) - 1 && std::memcmp(bytes + s, gen, sizeof(gen) - 1) == 0) return 0;
+    if (len >= sizeof(cpt) - 1 && std::memcmp(bytes + s, cpt, sizeof(cpt) - 1) == 0) return 1;
+    return 2;
+}
+
 static int ensure_slots(ysb_ctx* c) {
     if (c->h_bytes[0]) return YSB_OK;
     HIPCHK(c, hipSetDevice(c->device));
@@ -779,7 +795,11 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
     HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
     HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_h2d[slot], 0));
     const ysb_segment sg{c->d_bytes[slot], nbytes, c->d_off[slot], n};
+    // YSB_F_LAYOUT_AUTO: the scan instantiation named by the batch's first line, which
+    // the host holds in the pinned slot (counts are the same whichever runs)
+    if ((c->cfg.flags & YSB_F_LAYOUT_AUTO) && n) c->submit_layout = sniff_layout(c->h_bytes[slot], nbytes, c->h_off[slot], n);
     rc = enqueue_scan(c, &sg, 1);
+    c->submit_layout = -1;
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev_kdone[slot], c->s_comp));
     return YSB_OK;

@@ -27,6 +27,7 @@ YSB_F_RECORD_COUNT = 0x20
 YSB_F_NO_RECORD_COUNT = 0x40
 YSB_F_COMPACT_FIRST = 0x80
 YSB_F_FLAT_FIRST = 0x100
+YSB_F_LAYOUT_AUTO = 0x200
 INT64_MIN = -(1 << 63)
 UNIQUE_ID_BYTES = 128
 

@@ -25,7 +25,7 @@ class YsbContext:
                  max_batch_events=1 << 20, max_batch_bytes=256 << 20, ring_base_bucket=None,
                  overflow_capacity=1 << 20, timing=False, require_ip=False, lds_count=True,
                  sparse_fast_join=False, input_format="json", record_count=None, compact_first=False,
-                 flat_first=False):
+                 flat_first=False, layout_auto=False):
         L = lib()
         cfg = YsbConfig()
         L.ysb_config_default(C.byref(cfg))
@@ -42,6 +42,7 @@ class YsbContext:
                  | (_lib.YSB_F_FORMAT_TBL if input_format == "tbl" else 0)
                  | (_lib.YSB_F_COMPACT_FIRST if compact_first else 0)
                  | (_lib.YSB_F_FLAT_FIRST if flat_first else 0)
+                 | (_lib.YSB_F_LAYOUT_AUTO if layout_auto else 0)
                  | (0 if record_count is None else
                     _lib.YSB_F_RECORD_COUNT if record_count else _lib.YSB_F_NO_RECORD_COUNT))
         if input_format not in ("json", "tbl"):

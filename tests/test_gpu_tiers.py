@@ -3,7 +3,8 @@
 the scan itself instead of the general path -- exact against the CPU oracle (org.json's
 grammar restated) and the generator truth, with nothing deferred; and the same with the
 layout hints (YSB_F_COMPACT_FIRST: the tiers reordered; YSB_F_FLAT_FIRST: the flat-object
-tier as the only stage)."""
+tier as the only stage; YSB_F_LAYOUT_AUTO: the instantiation named by each host batch's
+first line)."""
 import numpy as np
 import pytest
 
@@ -17,7 +18,7 @@ VARIANTS = [GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
             GEN_REORDER, GEN_REORDER | GEN_COMPACT | GEN_RANDOM_IP]
 
 
-@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first"])
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "layout_auto"])
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_tier_lines_exact_and_not_deferred(variant, hint):
     g = GenParams(seed=23, n_campaigns=50, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
@@ -61,7 +62,7 @@ def test_tier_device_generator_truth(variant, hint):
     assert st["deferred"] == 0 and st["parse_errors"] == 0 and st["join_misses"] == 0
 
 
-@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first"])
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "layout_auto"])
 def test_tier_mixed_with_off_template_lines(hint):
     """Tier lines, vocabulary lines and general-path lines (whitespace, escapes, other key
     orders) interleaved in one batch: still exactly the oracle."""
@@ -93,7 +94,7 @@ def test_tier_mixed_with_off_template_lines(hint):
     assert 0 < st["deferred"] <= 1000
 
 
-@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first"])
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "layout_auto"])
 def test_canonical_tier_other_event_types_and_times(hint):
     """Lines in the generator's layout whose event_type is none of the three or whose
     event_time is not 13 digits (the vocabulary path names both from closed sets) go to
@@ -129,3 +130,32 @@ def test_canonical_tier_other_event_types_and_times(hint):
     for k, v in est.items():
         assert st[k] == v, k
     assert st["deferred"] == 0 and st["time_errors"] > 0
+
+
+@pytest.mark.parametrize("variant", [0, GEN_COMPACT, GEN_REORDER, GEN_REORDER | GEN_COMPACT | GEN_RANDOM_IP])
+def test_layout_auto_host_batches_exact(variant):
+    """YSB_F_LAYOUT_AUTO over host batches whose layouts change from batch to batch (each
+    batch's first line names the instantiation; a batch of mixed layouts still counts
+    exactly): the oracle's counts."""
+    g = GenParams(seed=41, n_campaigns=30, ads_per_campaign=10, events_per_sec=1000, variant=variant)
+    g0 = GenParams(seed=42, n_campaigns=30, ads_per_campaign=10, events_per_sec=1000)
+    _, aids = g.ids()
+    a, _ = g.events_host(0, 6000)
+    b, _ = g0.events_host(0, 6000)
+    la, lb = bytes(a).split(b"\n")[:-1], bytes(b).split(b"\n")[:-1]
+    batches = [la[:2000], lb[:2000], la[2000:4000] + lb[2000:3000], lb[3000:4000] + la[4000:6000]]
+    exp_rows, exp_st = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()),
+                                  b"".join(b"\n".join(x) + b"\n" for x in batches),
+                                  np.cumsum([0] + [len(ln) + 1 for x in batches for ln in x][:-1]).astype(np.uint32))
+    with YsbContext(n_campaigns=30, window_ring=64, max_batch_bytes=1 << 22, max_batch_events=1 << 14,
+                    layout_auto=True) as ctx:
+        ctx.load_ad_map(aids, g.ad_campaign_index())
+        for k, x in enumerate(batches):
+            data = b"\n".join(x) + b"\n"
+            offs = np.cumsum([0] + [len(ln) + 1 for ln in x[:-1]]).astype(np.uint32)
+            ctx.submit(data, offs, slot=k & 1)
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+    assert got == exp_rows
+    for k, v in exp_st.items():
+        assert st[k] == v, k

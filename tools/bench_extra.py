@@ -157,6 +157,49 @@ def tbl(args):
                       "time_errors": st["time_errors"], "out_of_ring": st["out_of_ring"]}}
 
 
+def general_host(args, ctx, g, aids, data, offs2, n):
+    """The general-path workload as host batches of <= --batch-mb through the pinned slots
+    (ysb_submit), so YSB_F_LAYOUT_AUTO can read each batch's first line; the rate is the
+    device path's (kernel time), the PCIe copies aside."""
+    from oracle import oracle as orc
+    ctx.load_ad_map(aids, g.ad_campaign_index())
+    cap = args.batch_mb << 20
+    batches, i = [], 0
+    ends = np.append(offs2[1:].astype(np.int64), len(data))
+    while i < n:
+        j = int(np.searchsorted(ends, int(offs2[i]) + cap, side="right"))
+        j = max(j, i + 1)
+        j = min(j, i + ((args.batch_mb << 20) // 200))
+        base = int(offs2[i])
+        batches.append((data[base:int(ends[j - 1])], (offs2[i:j] - base).astype(np.uint32)))
+        i = j
+
+    def step():
+        for k, (b, o) in enumerate(batches):
+            ctx.submit(b, o, slot=k & 1)
+    step()
+    ctx.sync()
+    ctx.reset()
+    ctx.kernel_time()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    el = time.perf_counter() - t0
+    ctx.kernel_time()
+    dev_ms, launches, _ = ctx.path_time()
+    ctx.reset()
+    step()
+    got = ctx.drain_buckets()
+    st = ctx.stats()
+    rows, ost = orc.run(orc.AdMap(aids, g.ad_campaign_index()), data, offs2.tolist(), threads=8)
+    return {"config": "%d generator events, shape %s, layout hint auto, %d host batches" % (n, args.shape, len(batches)),
+            "events_per_s_device": round(n * args.steps / (dev_ms * 1e-3), 1),
+            "events_per_s_pcie_inclusive": round(n * args.steps / el, 1),
+            "device_ms_per_step": round(dev_ms / max(1, args.steps), 3), "launches": launches,
+            "deferred": st["deferred"], "exact_vs_oracle": got == rows and all(st[k] == v for k, v in ost.items())}
+
+
 def general(args):
     from oracle import oracle as orc   # the checker (test infrastructure), not the measured path
     g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000)
@@ -178,7 +221,9 @@ def general(args):
     offs2[1:] = (nl[:-1] + 1).astype(np.uint32)
     ctx = YsbContext(n_campaigns=100, window_ring=1024, timing=True, max_batch_bytes=args.batch_mb << 20,
                      max_batch_events=(args.batch_mb << 20) // 200, compact_first=args.hint == "compact",
-                     flat_first=args.hint == "flat")
+                     flat_first=args.hint == "flat", layout_auto=args.hint == "auto")
+    if args.hint == "auto":   # YSB_F_LAYOUT_AUTO acts on host batches: the pinned slots
+        return general_host(args, ctx, g, aids, data, offs2, n)
     ctx.load_ad_map(aids, g.ad_campaign_index())
     d_b, d_o = ctx.device_alloc(len(data) + 64), ctx.device_alloc(4 * n + 64)
     ctx.h2d(d_b, np.frombuffer(data, dtype=np.uint8))
@@ -421,8 +466,8 @@ def main():
     ap.add_argument("--shape", default="reorder", choices=["generator", "compact", "reorder", "spaced", "escaped"],
                     help="general: how the generator's lines are re-laid")
     ap.add_argument("--shards", type=int, default=2, help="stream_sharded: contexts (one per GPU)")
-    ap.add_argument("--hint", default="none", choices=["none", "compact", "flat"],
-                    help="general: layout hint (YSB_F_COMPACT_FIRST / YSB_F_FLAT_FIRST)")
+    ap.add_argument("--hint", default="none", choices=["none", "compact", "flat", "auto"],
+                    help="general: layout hint (YSB_F_COMPACT_FIRST / YSB_F_FLAT_FIRST / YSB_F_LAYOUT_AUTO, host batches)")
     args = ap.parse_args()
     out = {"config3": config3, "tbl": tbl, "general": general, "pcie": pcie, "stream": stream,
            "stream_sharded": stream_sharded}[args.mode](args)
