@@ -364,7 +364,9 @@ void GpuAdCampaignOperator::open() {
     cfg.max_ads = map_.ads.size();
     cfg.max_batch_bytes = o_.batchBytes;
     cfg.max_batch_events = o_.batchEvents;
-    cfg.flags = (o_.tbl ? YSB_F_FORMAT_TBL : 0u) | (o_.requireIp ? YSB_F_REQUIRE_IP : 0u);
+    // the replay file's producer is not known here: each host batch picks its scan from its
+    // first line (YSB_F_LAYOUT_AUTO; the counts do not depend on it)
+    cfg.flags = (o_.tbl ? YSB_F_FORMAT_TBL : 0u) | (o_.requireIp ? YSB_F_REQUIRE_IP : 0u) | YSB_F_LAYOUT_AUTO;
     if (ysb_open(&ctx_, o_.device, &cfg) != YSB_OK)
         throw std::runtime_error(std::string("ysb_open: ") + ysb_last_error(nullptr));
     // RedisJoinBolt(Map) (:443-448): the whole map on the device
