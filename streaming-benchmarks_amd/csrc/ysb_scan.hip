@@ -1018,6 +1018,12 @@ __device__ __forceinline__ bool flat_line(const LdsSrc3& src, int s, int e, cons
 
 // Long.parseLong of a canonical line's event_time, then the bucket.  13 unsigned digits
 // (epoch milliseconds 2001..2286) take a SWAR path; any other form the general one.
+// FASTDIV (the .tbl instantiations, VALU-bound): with the reference's 10 s windows the
+// bucket of a 13-digit time comes from its digit groups in 32-bit arithmetic,
+// t / 10^4 = g0 * 10^5 + g1 * 10 + (g2 * 10 + d12) / 10^4 (exact: t >= 0, the first two
+// terms of t are multiples of 10^4, and the result is below 10^9), instead of building the
+// 64-bit t and a 64-bit magic-number division.
+template <bool FASTDIV = false>
 __device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, const CanonB& b, int tms, const ScanParams& P,
                                                  i64& bucket) {
     i64 tv;
@@ -1027,6 +1033,12 @@ __device__ __forceinline__ bool canonical_bucket(const LdsSrc& src, const CanonB
         const u32 g0 = swar_digits4(b.td[0], bad), g1 = swar_digits4(b.td[1], bad), g2 = swar_digits4(b.td[2], bad);
         const u32 d12 = (b.td[3] & 0xFFu) - '0';
         bad |= d12 > 9u;
+        if constexpr (FASTDIV) {
+            if (P.div.d == 10000 && bad == 0u) {
+                bucket = (i64)(g0 * 100000u + g1 * 10u + (g2 * 10u + d12) / 10000u);
+                return true;
+            }
+        }
         tv = (i64)(((u64)(g0 * 10000u + g1) * 10000u + g2) * 10u + d12);
         ok = bad == 0u;
     }
@@ -1515,7 +1527,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             tl.ev++;
             if (pend) {
                 tl.view++;
-                tok = canonical_bucket(lsrc, cb, ls + ca.t0, P, bucket);   // Long.parseLong
+                tok = canonical_bucket<TBL>(lsrc, cb, ls + ca.t0, P, bucket);   // Long.parseLong
             }
         }
         defer_append(P, dfr, P.line_base + cur.first + li, lane);
