@@ -549,6 +549,9 @@ __device__ __forceinline__ u32 swar_digits4(u32 w, u32& bad) {
 #ifndef YSB_CANON_TIERS
 #define YSB_CANON_TIERS 1
 #endif
+#ifndef YSB_FLAT_FAST_TIER4
+#define YSB_FLAT_FAST_TIER4 0   // A/B only: flat_parse_fast as the default kernel's fourth tier
+#endif
 constexpr int VOC_WORDS = 50;            // line bytes 0..199
 
 // Expected bytes [from, to) of str as N words + byte masks (compile time).
@@ -1473,7 +1476,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 }
                 }
 #if YSB_FLAT_TIER
-                if (!t) t = flat_tier(lsrc, ls, le, P.require_mask, c2, b2);   // any key order / spacing
+                if (!t) t = flat_tier<LdsSrc, YSB_FLAT_FAST_TIER4 != 0>(lsrc, ls, le, P.require_mask, c2, b2);   // any key order / spacing
 #endif
                 if (t) {
                     ca = c2;
