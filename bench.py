@@ -68,8 +68,13 @@ def parse_args(argv=None):
     ap.add_argument("--no-check", action="store_true", help="skip the generator-truth check")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[2] / .tbl extra measurements")
     ap.add_argument("--extra-steps", type=int, default=20)
-    ap.add_argument("--stream-seconds", type=int, default=22,
-                    help="extras: seconds of real-time sharded streaming (configs[4]); 0 skips it")
+    ap.add_argument("--stream-seconds", type=int, default=125,
+                    help="extras: seconds of real-time sharded streaming (configs[4]; 125 s closes >= 10 windows); "
+                         "0 skips it")
+    ap.add_argument("--c3-events", type=int, default=100_000_000,
+                    help="extras at N > 1: events per GPU of the configs[2]-table leg (1M campaigns / 10M ads)")
+    ap.add_argument("--layout-fixed", action="store_true",
+                    help="A/B: no first-line layout sampling of the device batches (YSB_F_LAYOUT_FIXED)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and set up torch.distributed, then stop before any GPU call")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -312,11 +317,33 @@ def timed_extra(name, ctx, g, segs, steps, warmup, kernel):
                       "overflow_dropped": st["overflow_dropped"]}}
 
 
+def guarded(out, key, fn):
+    """One extra measurement: its result, or {"error": ...} -- a failing extra never costs the
+    headline line."""
+    try:
+        out[key] = fn()
+    except Exception as e:   # noqa: BLE001 (recorded in the line, the headline still prints)
+        import traceback
+        log("extras: %s failed: %s" % (key, traceback.format_exc()))
+        out[key] = {"error": "%s: %s" % (type(e).__name__, e)}
+
+
 def extras(args, device):
-    """configs[2] (1M campaigns / 10M ads: join and count tables in HBM) and configs[1]'s
-    events as the fork's .tbl rows, each timed like the headline (one launch per step)."""
-    from ysb_amd import GenParams, YsbContext
+    """configs[2] (1M campaigns / 10M ads: join and count tables in HBM), configs[1]'s
+    events as the fork's .tbl rows and in other producers' layouts, each timed like the
+    headline (one launch per step), and configs[4]'s sharded streaming.  Each leg is
+    guarded: a failure is recorded as {"error": ...} under its key."""
     out = {}
+    guarded(out, "config3", lambda: extra_config3(args, device))
+    guarded(out, "tbl", lambda: extra_tbl(args, device))
+    extra_layouts(args, device, out)
+    if args.stream_seconds > 0:
+        guarded(out, "stream_sharded", lambda: extra_stream(args))
+    return out
+
+
+def extra_config3(args, device):
+    from ysb_amd import GenParams, YsbContext
     t = time.perf_counter()
     g = GenParams(seed=42, n_campaigns=1_000_000, ads_per_campaign=10, events_per_sec=args.rate)
     _, ab = g.ids_packed()
@@ -329,23 +356,33 @@ def extras(args, device):
                         "1M x 128-bucket count ring in HBM)", ctx, g, segs, args.extra_steps, args.warmup,
                         "ysb::scan_kernel<true, false, true, 0>")
         r["ad_map_load_s"] = round(load_s, 2)
-        out["config3"] = r
         free_segments(ctx, segs)
-    log("extras: config3 %.2f G events/s" % (out["config3"]["events_per_s"] / 1e9))
+    log("extras: config3 %.2f G events/s" % (r["events_per_s"] / 1e9))
+    return r
+
+
+def extra_tbl(args, device):
+    from ysb_amd import GenParams, YsbContext
     g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, fmt="tbl")
     _, aids = g.ids()
     with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True, input_format="tbl",
                     max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         segs = gen_segments(ctx, g, 100_000_000, 25_000_000)   # 4 batches of ~3.5 GB (rows ~140 B)
-        out["tbl"] = timed_extra("configs[1]'s 100M events as the fork's .tbl rows (MockWindowedFlatMap, "
-                                 "AdvertisingTopologyNative.java:197-226)", ctx, g, segs, args.extra_steps,
-                                 args.warmup, "ysb::scan_kernel<false, true, false, 0>")
+        r = timed_extra("configs[1]'s 100M events as the fork's .tbl rows (MockWindowedFlatMap, "
+                        "AdvertisingTopologyNative.java:197-226)", ctx, g, segs, args.extra_steps,
+                        args.warmup, "ysb::scan_kernel<false, true, false, 0>")
         free_segments(ctx, segs)
-    log("extras: tbl %.2f G events/s" % (out["tbl"]["events_per_s"] / 1e9))
-    # the same events as other producers would write them: other ip / ad_type values (the
-    # vocabulary path's generic-value branches) and compact JSON (the scan's third tier)
-    from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER
+    log("extras: tbl %.2f G events/s" % (r["events_per_s"] / 1e9))
+    return r
+
+
+def extra_layouts(args, device, out):
+    """The same events as other producers would write them: other ip / ad_type values (the
+    vocabulary path's generic-value branches), compact JSON and another key order -- with
+    the layout read from each batch's first line (the default), with an explicit hint, and
+    (_fixed) with neither."""
+    from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER, GenParams, YsbContext
     for key, variant, cf, what in (("random_ip", GEN_RANDOM_IP, False, "random dotted-quad ip_address"),
                                    ("random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES, False,
                                     "random dotted-quad ip_address and 8 ad_types"),
@@ -353,36 +390,161 @@ def extras(args, device):
                                     "compact JSON, no space after ':' and ',' (layout hint YSB_F_COMPACT_FIRST: "
                                     "the compact layout's vocabulary path first)"),
                                    ("compact_json_no_hint", GEN_COMPACT, False,
-                                    "compact JSON without the layout hint (the generator layout tried first, "
-                                    "the compact one as the third tier)"),
+                                    "compact JSON without a hint (the layout read from each batch's first line)"),
                                    ("reordered_keys", GEN_REORDER, "flat",
                                     "the keys in another order (ad_type, event_time, ad_id, ip_address, user_id, "
                                     "event_type, page_id), layout hint YSB_F_FLAT_FIRST: the flat-object tier first"),
                                    ("reordered_keys_no_hint", GEN_REORDER, False,
-                                    "the keys in another order without the layout hint (the scan's fourth tier, "
-                                    "after the vocabulary path fails)")):
-        g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, variant=variant)
-        _, aids = g.ids()
-        with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True,
-                        max_batch_bytes=16 << 20, max_batch_events=1 << 16, compact_first=cf is True,
-                        flat_first=cf == "flat") as ctx:
-            ctx.load_ad_map(aids, g.ad_campaign_index())
-            # lines up to ~280 B: 7 batches keep each under the 4 GiB of u32 offsets
-            segs = gen_segments(ctx, g, 100_000_000, 14_285_715)
-            out[key] = timed_extra("configs[1]'s 100M events, " + what, ctx, g, segs, args.extra_steps,
-                                   args.warmup, "ysb::scan_kernel<false, false, false, %d>"
-                                   % (2 if cf == "flat" else 1 if cf else 0))
+                                    "the keys in another order without a hint (the layout read from each batch's "
+                                    "first line)"),
+                                   ("reordered_keys_fixed", GEN_REORDER, "fixed",
+                                    "the keys in another order with the layout fixed to the generator's "
+                                    "(YSB_F_LAYOUT_FIXED: the scan's fourth tier, after the vocabulary path fails)")):
+        def one(key=key, variant=variant, cf=cf, what=what):
+            g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, variant=variant)
+            _, aids = g.ids()
+            with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True,
+                            max_batch_bytes=16 << 20, max_batch_events=1 << 16, compact_first=cf is True,
+                            flat_first=cf == "flat", layout_auto=cf != "fixed") as ctx:
+                ctx.load_ad_map(aids, g.ad_campaign_index())
+                # lines up to ~280 B: 7 batches keep each under the 4 GiB of u32 offsets
+                segs = gen_segments(ctx, g, 100_000_000, 14_285_715)
+                r = timed_extra("configs[1]'s 100M events, " + what, ctx, g, segs, args.extra_steps,
+                                args.warmup, None)
+                lay = ctx.launch_info()["layout"]
+                r["kernel"] = "ysb::scan_kernel<false, false, false, %d>" % lay
+                free_segments(ctx, segs)
+            log("extras: %s %.2f G events/s" % (key, r["events_per_s"] / 1e9))
+            return r
+        guarded(out, key, one)
+
+
+def extra_stream(args):
+    # configs[4]: real-time producers into double-buffered pinned slots of 2 contexts
+    # (2 shards; on a one-GPU box both on it), one global watermark, p50 / p99 close latency
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_extra
+    ns = argparse.Namespace(shards=2, rate=1_000_000, seconds=args.stream_seconds, batch_ms=20, ooo_ms=100)
+    r = bench_extra.stream_sharded(ns)
+    log("extras: stream %s" % json.dumps(r["window_close_latency"]))
+    return r
+
+
+def config3_ranks(args, d):
+    """configs[2]'s tables at N > 1 (configs[3]'s layout with 1M campaigns / 10M ads): each
+    rank loads its 1/N ad_id-hash shard of the 10M-ad table (ysb_load_ad_map_packed_shard),
+    scans args.c3_events of its own shard's events per step in record mode (W = 128), and
+    every step ends with the range-limited exchange (only the buckets holding counts, in the
+    narrowest cell width).  After timing: one more pass with the generator truth, one
+    exchange, and the linear checksums (ysb_group_checksum): for every owner block r,
+    owned(r) + SUM over ranks pending(r) == SUM over ranks truth(r) (mod 2^64) -- moving no
+    table between ranks."""
+    from ysb_amd import GenParams, YsbContext, shard_packed
+    t = time.perf_counter()
+    C3 = 1_000_000
+    base = GenParams(seed=42, n_campaigns=C3, ads_per_campaign=10, events_per_sec=args.rate)
+    _, ab = base.ids_packed()
+    subset = np.nonzero(shard_packed(ab, d.world) == d.rank)[0].astype(np.uint32)
+    g = GenParams(seed=42, event_stream=1 + d.rank, n_campaigns=C3, ads_per_campaign=10, events_per_sec=args.rate,
+                  ad_subset=subset)
+    W = 128
+    # phase 1 is rank-local (no collective): a failure anywhere is agreed on before any rank
+    # enters a collective, so every rank skips the leg together instead of waiting forever
+    ctx, segs, err = None, [], None
+    try:
+        ctx = YsbContext(device=d.device, n_campaigns=C3, window_ring=W, timing=True,
+                         ring_base_bucket=g.c.t0_ms // 10000 - W // 8, max_batch_bytes=1 << 20,
+                         max_batch_events=1 << 12, layout_auto=not args.layout_fixed)
+        ctx.load_ad_map_packed(ab, base.ad_campaign_index_array(), shard=(d.rank, d.world))
+        del ab
+        segs = gen_segments(ctx, g, args.c3_events, 16_666_667)
+    except Exception as e:   # noqa: BLE001
+        err = "rank %d: %s: %s" % (d.rank, type(e).__name__, e)
+    errs = [x for x in d.gather(err) if x]
+    if errs:
+        if ctx is not None:
             free_segments(ctx, segs)
-        log("extras: %s %.2f G events/s" % (key, out[key]["events_per_s"] / 1e9))
-    if args.stream_seconds > 0:
-        # configs[4]: real-time producers into double-buffered pinned slots of 2 contexts
-        # (2 shards; on a one-GPU box both on it), one global watermark, p99 close latency
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        import bench_extra
-        ns = argparse.Namespace(shards=2, rate=1_000_000, seconds=args.stream_seconds, batch_ms=20, ooo_ms=100)
-        out["stream_sharded"] = bench_extra.stream_sharded(ns)
-        log("extras: stream %s" % json.dumps(out["stream_sharded"]["window_close_latency"]))
-    return out
+            ctx.close()
+        raise RuntimeError("; ".join(errs))
+    try:
+        uid = d.bcast_bytes(YsbContext.group_unique_id() if d.rank == 0 else None)
+        ctx.group_init(d.rank, d.world, uid)
+        load_s = time.perf_counter() - t
+        sub = [(d_b, nb, d_o, n) for (_, n, d_b, nb, d_o) in segs]
+
+        def step():
+            ctx.submit_device_segments(sub)
+            ctx.group_reduce_scatter()
+        for _ in range(args.warmup):
+            step()
+        ctx.sync()
+        ctx.kernel_time()
+        ctx.exchange_info(reset=True)
+        torch_sync(d.device)
+        d.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.extra_steps):
+            step()
+        ctx.sync()
+        torch_sync(d.device)
+        d.barrier()
+        el = d.max(time.perf_counter() - t0)
+        kms, launches = ctx.kernel_time()
+        pms, _, nrec = ctx.path_time()
+        x = ctx.exchange_info(reset=True)
+        # the check: one more pass, its truth, one exchange, the checksums
+        ctx.reset()
+        ctx.submit_device_segments(sub)
+        for (f, n, _, _, _) in segs:
+            ctx.truth_accumulate(g, f, n)
+        ctx.sync()
+        mism, truth, ring = ctx.truth_compare()
+        tsum = ctx.checksum("truth", d.world)
+        st = ctx.stats()
+        ctx.group_reduce_scatter()
+        own = ctx.checksum("owned")[0]
+        pend = ctx.checksum("pending", d.world)
+        xi = ctx.exchange_info(reset=True)
+        events = sum(s[1] for s in segs)
+        nbytes = sum(s[3] for s in segs)
+        per = d.gather({"tsum": tsum, "own": own, "pend": pend, "mism": mism, "truth": truth, "ring": ring,
+                        "misses": st["join_misses"], "foreign": st["foreign_shard"], "perr": st["parse_errors"],
+                        "oor": st["out_of_ring"], "chk_width": xi["last_width"], "chk_buckets": xi["last_buckets"]})
+        free_segments(ctx, segs)
+    finally:
+        ctx.close()
+    if d.rank != 0:
+        return None
+    M = (1 << 64) - 1
+    bad_blocks = 0
+    for r in range(d.world):
+        want = sum(p["tsum"][r] for p in per) & M
+        got = (per[r]["own"] + sum(p["pend"][r] for p in per)) & M
+        bad_blocks += want != got
+    alg = (nbytes + 4 * events)
+    path = pms / max(launches, 1)
+    ach = alg / (path * 1e-3) / 1e9
+    steps = args.extra_steps
+    return {"workload": "configs[2]'s tables at N = %d: %dM JSON events per GPU, 1M campaigns x 10 ads (each rank "
+                        "1/%d of the 10M-ad join table), W = 128, range-limited RCCL exchange every step"
+                        % (d.world, events // 1_000_000, d.world),
+            "n_gpus": d.world, "events_per_gpu": events, "bytes_per_event": round(nbytes / events, 3),
+            "events_per_s": round(events * d.world * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
+            "avg_launch_ms": round(kms / max(launches, 1), 4), "avg_path_ms": round(path, 4),
+            "record_mode": nrec > 0, "alg_GBs_per_gpu": round(ach, 1), "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
+            "ad_map_load_s": round(load_s, 2),
+            "exchange": {"ms_per_step": round(x["ms"] / max(x["exchanges"], 1), 4),
+                         "bytes_per_step_per_gpu": x["bytes"] // max(x["exchanges"], 1),
+                         "buckets": x["last_buckets"], "cell_bytes": x["last_width"],
+                         "whole_ring_u64_bytes": x["full_ring_bytes"],
+                         "note": "ms: HIP events around plan, all-reduce(max), read-back, pack, reduce-scatter, "
+                                 "unpack on the compute stream, per step"},
+            "check": {"checksum_blocks_mismatched": bad_blocks, "blocks": d.world,
+                      "truth_mismatched_cells": sum(p["mism"] for p in per),
+                      "truth_views": sum(p["truth"] for p in per), "counted_views": sum(p["ring"] for p in per),
+                      "join_misses": sum(p["misses"] for p in per), "foreign_shard": sum(p["foreign"] for p in per),
+                      "parse_errors": sum(p["perr"] for p in per), "out_of_ring": sum(p["oor"] for p in per),
+                      "check_exchange_cell_bytes": per[0]["chk_width"]}}
 
 
 def exchange_check(d, ctx, g, segs, submit_all):
@@ -453,7 +615,7 @@ def main():
         g = base
 
     ctx = YsbContext(device=d.device, n_campaigns=100, window_ring=W, timing=True, ring_base_bucket=ring_base,
-                     max_batch_bytes=16 << 20, max_batch_events=1 << 16)
+                     max_batch_bytes=16 << 20, max_batch_events=1 << 16, layout_auto=not args.layout_fixed)
     # N > 1: the input is sharded by ad_id hash, so each rank holds only its shard of the
     # join table; the post-exchange check proves nothing is missed
     ctx.load_ad_map(aids, camp, shard=(d.rank, d.world) if d.world > 1 else None)
@@ -488,6 +650,8 @@ def main():
         step()
     ctx.sync()
     ctx.kernel_time()   # discard warmup launches
+    if d.world > 1:
+        ctx.exchange_info(reset=True)
     torch_sync(d.device)
     d.barrier()
     t0 = time.perf_counter()
@@ -498,6 +662,8 @@ def main():
     d.barrier()
     el = d.max(time.perf_counter() - t0)
     kms, launches = ctx.kernel_time()
+    xinfo = ctx.exchange_info(reset=True) if d.world > 1 else None
+    layout_run = ctx.launch_info()["layout"]
 
     events_all = args.events * d.world * args.steps
     value = events_all / el
@@ -537,10 +703,14 @@ def main():
         cpu = cpu_baseline(ctx, s0[2], s0[4], s0[3], s0[1], aids, camp, args.cpu_sample, args.cpu_seconds)
 
     extra = None
-    if d.world == 1 and not args.no_extras:
+    if not args.no_extras:
         free_segments(ctx, segs)
         ctx.close()
-        extra = extras(args, d.device)
+        if d.world == 1:
+            extra = extras(args, d.device)
+        else:
+            extra = {}
+            guarded(extra, "config3", lambda: config3_ranks(args, d))
 
     if d.rank == 0:
         out = {
@@ -561,11 +731,17 @@ def main():
                        else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "ysb::scan_kernel<false, false, false, 0>", "avg_launch_ms": round(avg_launch_ms, 4),
+                         "kernel": "ysb::scan_kernel<false, false, false, %d>" % layout_run,
+                         "avg_launch_ms": round(avg_launch_ms, 4),
                          "alg_bytes_per_launch": int(alg_bytes_launch)},
             "cpu_baseline": cpu,
             "check": check,
         }
+        if xinfo is not None:
+            out["exchange"] = {"ms_per_step": round(xinfo["ms"] / max(xinfo["exchanges"], 1), 4),
+                               "bytes_per_step_per_gpu": xinfo["bytes"] // max(xinfo["exchanges"], 1),
+                               "buckets": xinfo["last_buckets"], "cell_bytes": xinfo["last_width"],
+                               "whole_ring_u64_bytes": xinfo["full_ring_bytes"]}
         if extra is not None:
             out["extras"] = extra
         print(json.dumps(out), flush=True)

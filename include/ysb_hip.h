@@ -26,7 +26,12 @@
 extern "C" {
 #endif
 
-#define YSB_ABI_VERSION 1
+/* 2: ysb_stats.foreign_shard, YSB_F_STRICT, ysb_load_ad_map(_packed)_shard, the
+ *    range-limited exchange (ysb_group_exchange_info / ysb_exchange_plan),
+ *    ysb_group_checksum, layout selection on by default (YSB_F_LAYOUT_FIXED turns it off),
+ *    ysb_sync's sticky YSB_ERR_CAPACITY, the collective ysb_ring_advance after
+ *    ysb_group_init, ysb_gen_params.variant */
+#define YSB_ABI_VERSION 2
 
 /* status codes */
 #define YSB_OK            0
@@ -55,7 +60,12 @@ extern "C" {
                                    197-226) instead of JSON                       */
 #define YSB_F_RECORD_COUNT 0x20u /* count joined views in record mode wherever possible (the
                                    default: only for rings >= 1M cells and launches >= 1M
-                                   events without LDS window counters; ysb_path_time)  */
+                                   events without LDS window counters; ysb_path_time).
+                                   Record mode needs the HBM-resident join table (the
+                                   bucket layout ysb_load_ad_map builds for tables beyond
+                                   64 MB): with a cache-resident table the flag has no
+                                   effect.  ysb_path_time's record_launches tells which
+                                   launches used it.                                    */
 #define YSB_F_NO_RECORD_COUNT 0x40u /* never: one global atomic per joined view             */
 #define YSB_F_COMPACT_FIRST 0x80u /* layout hint: JSON lines are expected as compact JSON
                                    ({"user_id":"...","page_id":...} -- no space after ':'
@@ -69,11 +79,29 @@ extern "C" {
                                    (generator-layout lines too, a little slower than their
                                    own path).  Counts are identical; takes precedence over
                                    YSB_F_COMPACT_FIRST.  Cache-resident join tables only. */
-#define YSB_F_LAYOUT_AUTO 0x200u /* layout hint read from the data: ysb_submit picks the
-                                   instantiation from the first line of the batch it is
-                                   handed (the generator's layout, compact JSON, or the
-                                   flat-object tier first); device batches keep the flags.
-                                   Counts are identical whichever runs. */
+#define YSB_F_LAYOUT_AUTO 0x200u /* (the default since ABI 2; the bit is accepted and
+                                   ignored) layout read from the data: every submit picks
+                                   the scan instantiation from the first line of each batch
+                                   -- host batches from the pinned slot, device batches from
+                                   a <= 64-byte device-to-host sample per segment -- the
+                                   generator's layout, compact JSON, or the flat-object
+                                   tier first.  Counts are identical whichever runs.  The
+                                   explicit hints above take precedence.  Cache-resident
+                                   join tables only (the HBM-table and record-mode
+                                   instantiations keep the generator layout first). */
+#define YSB_F_LAYOUT_FIXED 0x800u /* no layout sampling: the generator's layout first (or
+                                   the explicit hint); device batches are then never read
+                                   by the host before their launch */
+#define YSB_F_STRICT 0x400u      /* ysb_sync (and the calls built on it) return YSB_ERR_DATA
+                                   once a record the reference would have thrown on was seen
+                                   (parse_errors / time_errors: JSONObject / getString /
+                                   Long.parseLong exceptions fail the Flink task,
+                                   AdvertisingTopologyNative.java:263-272,
+                                   CampaignProcessorCommon.java:58) or a view whose ad_id
+                                   belongs to another rank's shard (foreign_shard: input
+                                   routed by another hash than the join table's).  Sticky
+                                   until ysb_reset; the counts of the other records stay
+                                   exact and readable through ysb_stats_get. */
 #define YSB_F_SPARSE_FAST_JOIN 0x8u /* test hook: leave every other 36-byte key out of
                                    the fast-path cuckoo table, as a failed cuckoo
                                    placement would; its misses then take the
@@ -113,6 +141,9 @@ typedef struct ysb_stats {
     uint64_t overflow_dropped; /* side-list entries lost for lack of capacity (must be 0) */
     uint64_t batches;      /* submits                                                */
     uint64_t deferred;     /* lines the fast path handed to the general tokenizer    */
+    uint64_t foreign_shard; /* views dropped on a map miss whose ad_id belongs to another
+                              rank's shard (ysb_load_ad_map_shard): mis-routed input, not a
+                              miss of the reference's map; join_misses excludes them      */
 } ysb_stats;
 
 /* One (campaign, window) delta: the unit the Redis writer HINCRBYs into
@@ -150,6 +181,19 @@ int         ysb_load_ad_map(ysb_ctx* ctx, const char* const* ad_ids,
  * loads 10M ads this way). */
 int         ysb_load_ad_map_packed(ysb_ctx* ctx, const char* keys, uint32_t key_len,
                                    const uint32_t* campaign_idx, uint64_t n);
+/* The join table sharded 1/nranks per GPU: of the n entries only
+ * those with ysb_ad_shard(ad_id, nranks) == rank are loaded, and the context remembers its
+ * shard.  A view whose ad_id misses the table is then classified on the miss path only:
+ * an ad of another shard counts as foreign_shard (input routed by another hash -- with
+ * YSB_F_STRICT ysb_sync fails with YSB_ERR_DATA), any other as a join miss that the
+ * reference's RedisJoinBolt would drop too (AdvertisingTopologyNative.java:443-448,
+ * 465-467).  nranks = 1 is ysb_load_ad_map. */
+int         ysb_load_ad_map_shard(ysb_ctx* ctx, const char* const* ad_ids,
+                                  const uint32_t* ad_id_lens, const uint32_t* campaign_idx,
+                                  uint64_t n, uint32_t rank, uint32_t nranks);
+int         ysb_load_ad_map_packed_shard(ysb_ctx* ctx, const char* keys, uint32_t key_len,
+                                         const uint32_t* campaign_idx, uint64_t n,
+                                         uint32_t rank, uint32_t nranks);
 
 /* ---- batches --------------------------------------------------------------------
  * A batch is n_events JSON lines packed back to back in `bytes`; line i spans
@@ -185,10 +229,14 @@ typedef struct ysb_segment {
 } ysb_segment;
 int         ysb_submit_device_segments(ysb_ctx* ctx, const ysb_segment* segs, uint32_t n_segs);
 /* Wait for every submitted batch.  YSB_ERR_CAPACITY if joined views were lost because
- * the out-of-ring map and its fallback list (overflow_capacity) both filled within one
- * launch (stats.overflow_dropped > 0): counts are then not exact, and every ysb_sync /
- * ysb_drain reports it until ysb_reset.  Between launches the map is emptied into the
- * exact host-side list once it is a quarter full, so it never fills across batches. */
+ * the out-of-ring map and its fallback list (overflow_capacity) both filled (stats.
+ * overflow_dropped > 0): counts are then not exact, and every ysb_sync / ysb_drain reports
+ * it until ysb_reset.  The map is emptied into the exact host-side list once it is a
+ * quarter full: here, and at every submit from its fill level after the launch before
+ * the previous one (read without waiting).  So a chain of submits without ysb_sync loses
+ * counts only if ONE or two launches fill the map from below a quarter to full
+ * (overflow_capacity distinct out-of-ring cells).  With YSB_F_STRICT, YSB_ERR_DATA once a
+ * record the reference would have thrown on (or a foreign-shard view) was seen. */
 int         ysb_sync(ysb_ctx* ctx);
 
 /* ---- results ------------------------------------------------------------------------
@@ -211,7 +259,9 @@ int         ysb_ring_range(ysb_ctx* ctx, int64_t* lo, uint32_t* width);
  * Counts of buckets leaving the ring move to the exact host-side list and are reported
  * by later drains; events of buckets outside the new range keep going to the side list.
  * Replaces the LRU eviction of old buckets (LRUHashMap(10), CampaignProcessorCommon.java:37,
- * LRUHashMap.java:18-19) without its loss of counts.  Single-rank contexts only. */
+ * LRUHashMap.java:18-19) without its loss of counts.  After ysb_group_init this is a
+ * collective: every rank calls it with the same new_lo (YSB_ERR_ARG on every rank if they
+ * differ). */
 int         ysb_ring_advance(ysb_ctx* ctx, int64_t new_lo);
 
 /* ---- measurement -------------------------------------------------------------------- */
@@ -222,6 +272,17 @@ int         ysb_kernel_time(ysb_ctx* ctx, double* total_ms, uint64_t* launches);
  * partition + count kernels -- as measured by the last ysb_kernel_time call (which
  * collects both), and the launches so far that used record mode. */
 int         ysb_path_time(ysb_ctx* ctx, double* total_ms, uint64_t* launches, uint64_t* record_launches);
+/* The scan instantiation the last launch ran: the JSON layout tried first (0 the
+ * generator's, 1 compact JSON, 2 the flat-object tier; what layout sampling or a hint
+ * chose), record-mode counting, the HBM-resident join table (bucket layout, serial
+ * probes), the .tbl format -- each 0 or 1. */
+typedef struct ysb_launch_desc {
+    uint32_t layout;
+    uint32_t record_mode;
+    uint32_t hbm_table;
+    uint32_t tbl;
+} ysb_launch_desc;
+int         ysb_launch_info(ysb_ctx* ctx, ysb_launch_desc* out);
 /* The compute stream (hipStream_t) for callers that want to order work with it. */
 void*       ysb_stream(ysb_ctx* ctx);
 
@@ -244,9 +305,47 @@ int         ysb_group_unique_id(uint8_t uid[YSB_UNIQUE_ID_BYTES]);
  * After ysb_group_init, ysb_ring_advance is collective too (same new_lo on every rank). */
 int         ysb_group_init(ysb_ctx* ctx, int rank, int nranks,
                            const uint8_t uid[YSB_UNIQUE_ID_BYTES]);
-/* Asynchronous on the compute stream; sums the ring tables into the owner rank.
- * Every rank's ring part is consumed (zeroed) by the call. */
+/* Collective: sums the ranks' pending counts (everything counted since the previous call)
+ * into the owner ranks' tables and zeroes them.  Range-limited, like the reference's keyed
+ * shuffle, which carries only the touched (campaign, window) pairs: per ring bucket the
+ * largest pending count on any rank is agreed by one W-element all-reduce(max) (the call's
+ * only wait for the device), and only the buckets holding a count travel, as a dense
+ * [C_pad][buckets] array of the narrowest cell width that cannot wrap in the sum (1 byte
+ * while nranks * max <= 255, else 4, else 8) through one ncclReduceScatter.  The rest is
+ * asynchronous on the compute stream.  Record mode's u8 delta ring is read directly (no
+ * fold): configs[2]'s 1M campaigns x 100 live buckets move 100 MB per rank and exchange
+ * instead of the whole 1 GB u64 ring. */
 int         ysb_group_reduce_scatter(ysb_ctx* ctx);
+/* Exchange accounting: exchanges run, reduce-scatter input bytes this rank contributed,
+ * device time of the exchanges (HIP events on the compute stream around plan, all-reduce,
+ * read-back, pack, reduce-scatter and unpack), the last exchange's bucket count and cell
+ * width (0: nothing was pending), and what one whole-ring u64 exchange would move.
+ * reset != 0 zeroes the totals after reading them. */
+typedef struct ysb_exchange_info {
+    uint64_t exchanges;
+    uint64_t bytes;
+    double   ms;
+    uint32_t last_buckets;
+    uint32_t last_width;
+    uint64_t full_ring_bytes;
+} ysb_exchange_info;
+int         ysb_group_exchange_info(ysb_ctx* ctx, ysb_exchange_info* out, int reset);
+/* The plan every rank derives from the all-reduced per-bucket maxima (host function):
+ * slots[0..*n_slots) = the ring slots with slot_max > 0, ascending; *width = the cell width
+ * above.  YSB_ERR_CAPACITY if nranks * max does not fit 64 bits. */
+int         ysb_exchange_plan(const uint64_t* slot_max, uint32_t W, uint32_t nranks, uint32_t* slots,
+                              uint32_t* n_slots, uint32_t* width);
+/* Linear checksums for a multi-rank check that moves no tables (sum over cells of count x
+ * an odd 64-bit weight of (campaign, bucket), mod 2^64, so checksums add like the tables):
+ *   YSB_SUM_TRUTH_BLOCKS   out[r], r < nranks: the generator truth's cells of owner block r
+ *   YSB_SUM_PENDING_BLOCKS out[r], r < nranks: this rank's pending (not yet exchanged) cells
+ *   YSB_SUM_OWNED          out[0]: this rank's owned table (its block, after exchanges)
+ * After ysb_group_reduce_scatter on every rank: OWNED of rank r + SUM over ranks of
+ * PENDING[r] == SUM over ranks of TRUTH[r]. */
+#define YSB_SUM_TRUTH_BLOCKS   0
+#define YSB_SUM_PENDING_BLOCKS 1
+#define YSB_SUM_OWNED          2
+int         ysb_group_checksum(ysb_ctx* ctx, int what, uint32_t nranks, uint64_t* out);
 int         ysb_group_owned(ysb_ctx* ctx, uint32_t* campaign_lo, uint32_t* campaign_hi);
 /* The communicator as RCCL sees it (ncclCommUserRank / ncclCommCount): a check that the
  * exchange really spans the ranks the launcher started. */
@@ -261,8 +360,10 @@ int         ysb_group_block(uint32_t n_campaigns, int rank, int nranks, uint32_t
 /* Host router for batches that are not pre-sharded: out_shard[i] = ysb_ad_shard of the
  * raw bytes of line i's top-level "ad_id" string (generator lines: bytes 113..148;
  * other layouts: a key scan); lines without one go to shard 0.  shard_counts (nranks
- * entries, may be NULL) receives the lines per shard.  Any deterministic routing is
- * exact because every rank loads the whole ad map; this one balances by ad. */
+ * entries, may be NULL) receives the lines per shard.  Routing must match the join table:
+ * with a sharded table (ysb_load_ad_map_shard) only this hash is exact -- a view routed
+ * elsewhere misses and is counted as foreign_shard (an error under YSB_F_STRICT); with the
+ * whole map on every rank (ysb_load_ad_map) any deterministic routing is exact. */
 int         ysb_route_lines(const uint8_t* bytes, uint64_t nbytes, const uint32_t* line_off,
                             uint64_t n, uint32_t nranks, uint32_t* out_shard,
                             uint64_t* shard_counts);

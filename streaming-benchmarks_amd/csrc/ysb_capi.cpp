@@ -36,10 +36,17 @@ struct ysb_ctx {
     u32* d_ctable = nullptr;   // 36-byte-key cuckoo table
     u64 ctable_slots = 0;      // slots, or buckets when ctable_buckets
     bool ctable_buckets = false; // HBM-resident table: 3-entry 128-B buckets (CB_*), serial probes
-    int submit_layout = -1;      // YSB_F_LAYOUT_AUTO: the layout ysb_submit read off the slot's first line
+    int submit_layout = -1;      // the layout a submit read off its batch's first line (-1: the flags')
+    ysb_launch_desc last_launch{};   // the instantiation of the last launch
+    u8* h_sample = nullptr;      // pinned: device batches' first-line samples
+    u32* h_used = nullptr;       // pinned: the out-of-ring map's fill level after a launch ...
+    hipEvent_t ev_used = nullptr; // ... readable once this has completed
+    bool used_pending = false;
+    hipStream_t s_aux = nullptr; // the samples' copies
     CuckooSeed cseed{};
     bool ctable_partial = false;
     bool table_loaded = false;
+    u32 shard_rank = 0, shard_n = 1;      // the join table's shard (ysb_load_ad_map_shard)
     // counts
     u32 c_pad = 0;                        // campaigns padded to the group size
     unsigned long long* d_counts = nullptr;   // [c_pad][W]
@@ -88,18 +95,35 @@ struct ysb_ctx {
     u32* d_runs = nullptr;
     u64 runs_words = 0;
     u64 rec_launches = 0;
-    // record mode counts into a u32 delta ring with the u64 ring's layout; fold_delta adds
-    // it to the u64 ring before anything reads that, and before delta_bound (events
-    // counted into delta since the last fold, an upper bound of any cell's delta) could
-    // reach 2^32
-    u32* d_delta = nullptr;
+    // record mode counts into a saturating u8 delta ring with the u64 ring's layout (a cell
+    // passing 255 goes to the u64 ring, ysb_count.hip add16); fold_delta adds it to the u64
+    // ring before anything reads that.  delta_bound: events counted into it since the last
+    // fold; YSB_DELTA_FOLD_EVENTS (test hook) folds before a launch once it would pass that
+    u8* d_delta = nullptr;
     u64 delta_cells = 0;
     u64 delta_bound = 0;
-    u64 delta_limit = 1ull << 32;   // YSB_DELTA_FOLD_EVENTS lowers it (test hook: frequent folds)
+    u64 delta_limit = ~0ull;
+    // pending counts since the last exchange: the u64 ring holds some once a launch without
+    // record mode ran or a fold moved the delta there (pend_u64), or a record-mode path
+    // wrote it (*d_dirty, set on the device)
+    bool pend_u64 = true;
+    u32* d_dirty = nullptr;
     // group
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
-    bool rs_done = false;
+    // the range-limited exchange: per-slot maxima (all-reduced), the plan's slots, the packed
+    // send / receive buffers, and its accounting (HIP event pairs, collected on request)
+    unsigned long long* d_xmax = nullptr;
+    unsigned long long* h_xmax = nullptr;
+    u32* d_xslots = nullptr;
+    void* d_xsend = nullptr;
+    void* d_xrecv = nullptr;
+    u64 xsend_bytes = 0, xrecv_bytes = 0;
+    u64 x_count = 0, x_bytes = 0;
+    u32 x_last_slots = 0, x_last_width = 0;
+    double x_ms = 0;
+    std::vector<std::array<hipEvent_t, 2>> xev;
+    size_t xev_used = 0;
     // truth
     unsigned long long* d_truth = nullptr;
     unsigned long long* d_truth_out = nullptr;
@@ -143,6 +167,8 @@ extern "C" {
 
 static int agree_ring(ysb_ctx* c);
 static int allreduce_max(ysb_ctx* c, i64* h, int n);
+static int sync_streams(ysb_ctx* c);
+static int pull_side_list(ysb_ctx* c);
 
 int ysb_abi_version(void) { return YSB_ABI_VERSION; }
 
@@ -199,9 +225,20 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_rec);
     hipFree(c->d_rec_n);
     hipFree(c->d_delta);
+    hipFree(c->d_dirty);
+    hipFree(c->d_xmax);
+    hipHostFree(c->h_xmax);
+    hipFree(c->d_xslots);
+    hipFree(c->d_xsend);
+    hipFree(c->d_xrecv);
+    for (auto& p : c->xev) for (hipEvent_t e : p) hipEventDestroy(e);
     hipFree(c->d_part);
     hipFree(c->d_runs);
     if (c->ev_ring) hipEventDestroy(c->ev_ring);
+    hipHostFree(c->h_sample);
+    hipHostFree(c->h_used);
+    if (c->ev_used) hipEventDestroy(c->ev_used);
+    if (c->s_aux) hipStreamDestroy(c->s_aux);
     if (c->s_comp) hipStreamDestroy(c->s_comp);
     if (c->s_copy) hipStreamDestroy(c->s_copy);
     delete c;
@@ -264,7 +301,9 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
             return bad(YSB_ERR_HIP);
         }
     }
-    if (hipEventCreateWithFlags(&c->ev_ring, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&c->ev_ring, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_used, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(&c->h_used, 16) != hipSuccess) {
         fail(c, YSB_ERR_HIP, "event creation failed");
         return bad(YSB_ERR_HIP);
     }
@@ -277,7 +316,8 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
     // stats and the map's slot count share one allocation: ysb_sync reads both in one copy
     if (hipMalloc(&c->d_side, c->side_slots * sizeof(SideSlot)) != hipSuccess ||
         hipMalloc(&c->d_stats, (ST_COUNT_ + 1) * 8) != hipSuccess ||
-        hipMemset(c->d_stats, 0, (ST_COUNT_ + 1) * 8) != hipSuccess) {
+        hipMemset(c->d_stats, 0, (ST_COUNT_ + 1) * 8) != hipSuccess ||
+        hipMalloc(&c->d_dirty, 16) != hipSuccess || hipMemset(c->d_dirty, 0, 16) != hipSuccess) {
         fail(c, YSB_ERR_NOMEM, "device allocation failed");
         return bad(YSB_ERR_NOMEM);
     }
@@ -323,20 +363,60 @@ int ysb_close(ysb_ctx* c) {
 
 // ---- ad table -------------------------------------------------------------------------
 
+static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens, const uint32_t* campaign_idx,
+                    uint64_t n);
+
 int ysb_load_ad_map_packed(ysb_ctx* c, const char* keys, uint32_t key_len, const uint32_t* campaign_idx,
                            uint64_t n) {
+    return ysb_load_ad_map_packed_shard(c, keys, key_len, campaign_idx, n, 0, 1);
+}
+
+int ysb_load_ad_map_packed_shard(ysb_ctx* c, const char* keys, uint32_t key_len, const uint32_t* campaign_idx,
+                                 uint64_t n, uint32_t rank, uint32_t nranks) {
     if (!c) return YSB_ERR_ARG;
     if (n && (!keys || !campaign_idx)) return fail(c, YSB_ERR_ARG, "NULL ad map arrays");
     std::vector<const char*> ptr(n);
     std::vector<u32> len(n, key_len);
     for (u64 i = 0; i < n; ++i) ptr[i] = keys + i * key_len;
-    return ysb_load_ad_map(c, ptr.data(), len.data(), campaign_idx, n);
+    return ysb_load_ad_map_shard(c, ptr.data(), len.data(), campaign_idx, n, rank, nranks);
 }
 
 int ysb_load_ad_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens, const uint32_t* campaign_idx,
                     uint64_t n) {
+    return ysb_load_ad_map_shard(c, ad_ids, lens, campaign_idx, n, 0, 1);
+}
+
+// The entries of this rank's shard only (the host-side hash the router and the generator's
+// shard files use, ysb_ad_shard), then the tables; the context keeps its shard so that the
+// deferred-line kernel can tell a foreign key's miss from a real one.
+int ysb_load_ad_map_shard(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens, const uint32_t* campaign_idx,
+                          uint64_t n, uint32_t rank, uint32_t nranks) {
     if (!c) return YSB_ERR_ARG;
+    if (nranks == 0 || rank >= nranks) return fail(c, YSB_ERR_ARG, "bad shard %u / %u", rank, nranks);
     if (n && (!ad_ids || !campaign_idx)) return fail(c, YSB_ERR_ARG, "NULL ad map arrays");
+    int rc;
+    if (nranks == 1) {
+        rc = load_map(c, ad_ids, lens, campaign_idx, n);
+    } else {
+        std::vector<const char*> p;
+        std::vector<u32> l, cm;
+        for (u64 i = 0; i < n; ++i) {
+            const u32 len = lens ? lens[i] : 36u;
+            if (ad_ids[i] && ysb_ad_shard(ad_ids[i], len, nranks) != rank) continue;
+            p.push_back(ad_ids[i]);
+            l.push_back(len);
+            cm.push_back(campaign_idx[i]);
+        }
+        rc = load_map(c, p.data(), l.data(), cm.data(), p.size());
+    }
+    if (rc) return rc;
+    c->shard_rank = rank;
+    c->shard_n = nranks;
+    return YSB_OK;
+}
+
+static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens, const uint32_t* campaign_idx,
+                    uint64_t n) {
     u64 slots = 64;
     while (slots < 2 * n) slots <<= 1;   // load factor <= 0.5
     if (slots > (1ull << 31)) return fail(c, YSB_ERR_CAPACITY, "ad map too large (%llu)", (unsigned long long)n);
@@ -497,7 +577,12 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     p.ctable = c->d_ctable;
     p.ctable_mask = (u32)(c->ctable_slots - 1);
     p.cseed = c->cseed;
-    p.ctable_partial = c->ctable_partial ? 1u : 0u;
+    // a sharded table's misses go to the deferred-line kernel, which tells a foreign-shard
+    // key from a real miss (the scan kernels themselves carry no shard logic)
+    p.ctable_partial = (c->ctable_partial || c->shard_n > 1) ? 1u : 0u;
+    p.shard_rank = c->shard_rank;
+    p.shard_n = c->shard_n;
+    p.pend_dirty = c->d_dirty;
     // HBM-resident table: buckets, the second one read only after a miss in a full first
     p.probe_serial = c->ctable_buckets ? 1u : 0u;
     p.layout = (c->cfg.flags & YSB_F_FLAT_FIRST) ? 2u : (c->cfg.flags & YSB_F_COMPACT_FIRST) ? 1u : 0u;
@@ -582,6 +667,7 @@ static int fold_delta(ysb_ctx* c) {
     launch_fold(c->d_counts, c->d_delta, c->delta_cells, c->s_comp);
     HIPCHK(c, hipGetLastError());
     c->delta_bound = 0;
+    c->pend_u64 = true;   // pending counts now sit in the u64 ring
     return YSB_OK;
 }
 
@@ -629,21 +715,24 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     if ((rc = grow_u32(c, &c->d_rec_n, &c->rec_n_words, (u64)r.grid * r.bins))) return rc;
     if ((rc = grow_u32(c, &c->d_part, &c->part_words, part))) return rc;
     if ((rc = grow_u32(c, &c->d_runs, &c->runs_words, (u64)r.n_blocks * REC_QUARTERS * 2))) return rc;
-    if (c->delta_cells != cells) {   // the delta ring: the u64 ring's layout, zeroed
+    if (c->delta_cells != cells) {   // the delta ring: the u64 ring's layout, one byte a cell, zeroed
         if ((rc = fold_delta(c))) return rc;
         HIPCHK(c, hipStreamSynchronize(c->s_comp));
         hipFree(c->d_delta);
         c->d_delta = nullptr;
         c->delta_cells = 0;
-        HIPCHK(c, hipMalloc(&c->d_delta, cells * 4));
-        HIPCHK(c, hipMemset(c->d_delta, 0, cells * 4));
+        HIPCHK(c, hipMalloc(&c->d_delta, cells));
+        HIPCHK(c, hipMemset(c->d_delta, 0, cells));
         c->delta_cells = cells;
     }
-    // no delta cell may wrap: fold first if this launch's events could take the views
-    // added since the last fold to 2^32
+    // the delta saturates instead of wrapping, so it needs no fold between launches; the
+    // test hook YSB_DELTA_FOLD_EVENTS folds anyway once the events since the last fold
+    // would reach its bound
     if (c->delta_bound + n_events >= c->delta_limit && (rc = fold_delta(c))) return rc;
     c->delta_bound += n_events;
     r.delta = c->d_delta;
+    r.counts = c->d_counts;
+    r.dirty = c->d_dirty;
     r.rec = c->d_rec;
     r.rec_n = c->d_rec_n;
     r.part = c->d_part;
@@ -678,7 +767,18 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
         HIPCHK(c, hipMalloc(&c->d_defer_ctr, 16 + 4 * MAX_SEGS));
         HIPCHK(c, hipMemset(c->d_defer_ctr, 0, 16 + 4 * MAX_SEGS));
     }
+    // the out-of-ring map's fill level after an earlier launch (read without waiting): a
+    // quarter full empties it into the exact host list before this launch adds to it
+    if (c->used_pending && hipEventQuery(c->ev_used) == hipSuccess) {
+        c->used_pending = false;
+        if ((u64)*c->h_used * 4 > c->side_slots) {
+            int rc = sync_streams(c);
+            if (!rc) rc = pull_side_list(c);
+            if (rc) return rc;
+        }
+    }
     ScanParams p = make_params(c, segs, nseg);
+    p.used_out = c->used_pending ? nullptr : c->h_used;
     p.defer = c->d_defer;
     p.defer_count = c->d_defer_ctr;
     p.defer_done = c->d_defer_ctr + 1;
@@ -723,6 +823,12 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     }
     launch_scan(p, c->s_comp);
     HIPCHK(c, hipGetLastError());
+    if (!p.rec_on) c->pend_u64 = true;   // this launch counts into the u64 ring
+    // (launch_scan: the layout instantiations exist for JSON with the cache-resident table)
+    c->last_launch.layout = (p.tbl || p.rec_on || p.probe_serial) ? 0u : p.layout;
+    c->last_launch.record_mode = p.rec_on ? 1u : 0u;
+    c->last_launch.hbm_table = p.probe_serial ? 1u : 0u;
+    c->last_launch.tbl = p.tbl ? 1u : 0u;
     if (e1) HIPCHK(c, hipEventRecord(e1, c->s_comp));
     launch_defer(p, c->cus, c->s_comp);
     HIPCHK(c, hipGetLastError());
@@ -734,6 +840,10 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
         c->rec_launches++;
     }
     if (e2) HIPCHK(c, hipEventRecord(e2, c->s_comp));
+    if (p.used_out) {   // defer_kernel wrote the map's fill level into h_used
+        HIPCHK(c, hipEventRecord(c->ev_used, c->s_comp));
+        c->used_pending = true;
+    }
     c->batches += nin;   // each segment counts as the batch it is
     return YSB_OK;
 }
@@ -750,6 +860,64 @@ static int sniff_layout(const uint8_t* bytes, u64 nbytes, const u32* off, u64 n)
     if (len >= sizeof(gen) - 1 && std::memcmp(bytes + s, gen, sizeof(gen) - 1) == 0) return 0;
     if (len >= sizeof(cpt) - 1 && std::memcmp(bytes + s, cpt, sizeof(cpt) - 1) == 0) return 1;
     return 2;
+}
+
+// Whether batches pick the scan instantiation from their first line (the default): not
+// with an explicit hint or YSB_F_LAYOUT_FIXED, and only where the layout instantiations
+// exist (JSON, cache-resident join table).
+static bool layout_sampling(const ysb_ctx* c) {
+    const u32 f = c->cfg.flags;
+    return !(f & (YSB_F_LAYOUT_FIXED | YSB_F_COMPACT_FIRST | YSB_F_FLAT_FIRST | YSB_F_FORMAT_TBL)) &&
+           !c->ctable_buckets;
+}
+
+// Device batches: the first line of every segment, sampled by small device-to-host copies
+// on a stream of their own (the caller's contract: a device batch's bytes are complete
+// when it is submitted).  One layout for the launch: the segments' common one, else the
+// flat-object tier first (it takes every layout).
+static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
+    constexpr u32 SAMPLE = 64, STRIDE = 96;
+    if (!c->h_sample) {
+        HIPCHK(c, hipHostMalloc(&c->h_sample, (u64)MAX_SEGS * STRIDE));
+        HIPCHK(c, hipStreamCreateWithFlags(&c->s_aux, hipStreamNonBlocking));
+    }
+    u8* h = c->h_sample;
+    u32 n = 0;
+    for (u32 i = 0; i < nseg && n < (u32)MAX_SEGS; ++i) {
+        if (!segs[i].n_events) continue;
+        const u64 nb = std::min<u64>(segs[i].nbytes, SAMPLE);
+        std::memset(h + (u64)n * STRIDE, 0, STRIDE);
+        HIPCHK(c, hipMemcpyAsync(h + (u64)n * STRIDE, segs[i].d_line_off, segs[i].n_events > 1 ? 8 : 4,
+                                 hipMemcpyDeviceToHost, c->s_aux));
+        if (nb) HIPCHK(c, hipMemcpyAsync(h + (u64)n * STRIDE + 16, segs[i].d_bytes, nb, hipMemcpyDeviceToHost, c->s_aux));
+        ++n;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->s_aux));
+    int lay = -1;
+    n = 0;
+    for (u32 i = 0; i < nseg && n < (u32)MAX_SEGS; ++i) {
+        if (!segs[i].n_events) continue;
+        u8* s = h + (u64)n * STRIDE;
+        ++n;
+        u32 o[2];
+        std::memcpy(o, s, 8);
+        const u64 end = segs[i].n_events > 1 ? (u64)o[1] : segs[i].nbytes;
+        if (o[0] > end || end > segs[i].nbytes) return 0;   // bad offsets: the scan defers them anyway
+        u8 line[16] = {0};
+        const u64 len = std::min<u64>(end - o[0], 16);
+        if (o[0] + len <= SAMPLE) {
+            std::memcpy(line, s + 16 + o[0], len);
+        } else if (len) {   // the first line does not start in the sample: read its head
+            HIPCHK(c, hipMemcpyAsync(s + 16, segs[i].d_bytes + o[0], len, hipMemcpyDeviceToHost, c->s_aux));
+            HIPCHK(c, hipStreamSynchronize(c->s_aux));
+            std::memcpy(line, s + 16, len);
+        }
+        const u32 off0 = 0;
+        const int l = sniff_layout(line, len, &off0, 1);
+        if (lay < 0) lay = l;
+        else if (lay != l) lay = 2;
+    }
+    return lay < 0 ? 0 : lay;
 }
 
 static int ensure_slots(ysb_ctx* c) {
@@ -795,9 +963,9 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
     HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
     HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_h2d[slot], 0));
     const ysb_segment sg{c->d_bytes[slot], nbytes, c->d_off[slot], n};
-    // YSB_F_LAYOUT_AUTO: the scan instantiation named by the batch's first line, which
-    // the host holds in the pinned slot (counts are the same whichever runs)
-    if ((c->cfg.flags & YSB_F_LAYOUT_AUTO) && n) c->submit_layout = sniff_layout(c->h_bytes[slot], nbytes, c->h_off[slot], n);
+    // the scan instantiation named by the batch's first line, which the host holds in the
+    // pinned slot (counts are the same whichever runs)
+    if (layout_sampling(c) && n) c->submit_layout = sniff_layout(c->h_bytes[slot], nbytes, c->h_off[slot], n);
     rc = enqueue_scan(c, &sg, 1);
     c->submit_layout = -1;
     if (rc) return rc;
@@ -813,6 +981,18 @@ int ysb_wait(ysb_ctx* c, int slot) {
     return YSB_OK;
 }
 
+// Device batches: the layout sampled from their first lines (unless fixed), then the launch.
+static int enqueue_device(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
+    if (c->table_loaded && layout_sampling(c)) {
+        const int lay = sample_device_layout(c, segs, nseg);
+        if (lay < 0) return lay;
+        c->submit_layout = lay;
+    }
+    const int rc = enqueue_scan(c, segs, nseg);
+    c->submit_layout = -1;
+    return rc;
+}
+
 int ysb_submit_device(ysb_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const uint32_t* d_off, uint64_t n) {
     if (!c) return YSB_ERR_ARG;
     if (nbytes > (4ull << 30) - 64) return fail(c, YSB_ERR_CAPACITY, "device batch larger than 4 GiB (u32 offsets)");
@@ -820,7 +1000,7 @@ int ysb_submit_device(ysb_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const
     if (reinterpret_cast<uintptr_t>(d_bytes) & 15) return fail(c, YSB_ERR_ARG, "d_bytes must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
     const ysb_segment sg{d_bytes, nbytes, d_off, n};
-    return enqueue_scan(c, &sg, 1);
+    return enqueue_device(c, &sg, 1);
 }
 
 int ysb_submit_device_segments(ysb_ctx* c, const ysb_segment* segs, uint32_t n_segs) {
@@ -837,7 +1017,7 @@ int ysb_submit_device_segments(ysb_ctx* c, const ysb_segment* segs, uint32_t n_s
             return fail(c, YSB_ERR_ARG, "segment %u: d_bytes must be 16-byte aligned", i);
     }
     HIPCHK(c, hipSetDevice(c->device));
-    return enqueue_scan(c, segs, n_segs);
+    return enqueue_device(c, segs, n_segs);
 }
 
 static int sync_streams(ysb_ctx* c) {
@@ -866,9 +1046,16 @@ static int check_capacity(ysb_ctx* c) {
     if (v[ST_OVF_DROPPED])
         return fail(c, YSB_ERR_CAPACITY,
                     "%llu joined views outside the window ring were lost: the out-of-ring map and its "
-                    "fallback list (overflow_capacity %llu) filled within one launch; counts are not exact "
+                    "fallback list (overflow_capacity %llu) filled; counts are not exact "
                     "until ysb_reset (raise overflow_capacity or window_ring, or submit smaller batches)",
                     (unsigned long long)v[ST_OVF_DROPPED], (unsigned long long)c->cfg.overflow_capacity);
+    if ((c->cfg.flags & YSB_F_STRICT) && (v[ST_PARSE_ERR] || v[ST_TIME_ERR] || v[ST_FOREIGN]))
+        return fail(c, YSB_ERR_DATA,
+                    "strict mode: %llu lines JSONObject/getString would throw on, %llu event_times "
+                    "Long.parseLong rejects, %llu views of another rank's ad shard (routing does not match "
+                    "the sharded join table); sticky until ysb_reset",
+                    (unsigned long long)v[ST_PARSE_ERR], (unsigned long long)v[ST_TIME_ERR],
+                    (unsigned long long)v[ST_FOREIGN]);
     return YSB_OK;
 }
 
@@ -1066,6 +1253,7 @@ int ysb_stats_get(ysb_ctx* c, ysb_stats* s) {
     s->overflow_dropped = v[ST_OVF_DROPPED];
     s->batches = c->batches;
     s->deferred = v[ST_DEFERRED];
+    s->foreign_shard = v[ST_FOREIGN];
     return YSB_OK;
 }
 
@@ -1075,8 +1263,10 @@ int ysb_reset(ysb_ctx* c) {
     if (rc) return rc;
     const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
     HIPCHK(c, hipMemset(c->d_counts, 0, cells * 8));
-    if (c->d_delta) HIPCHK(c, hipMemset(c->d_delta, 0, c->delta_cells * 4));
+    if (c->d_delta) HIPCHK(c, hipMemset(c->d_delta, 0, c->delta_cells));
     c->delta_bound = 0;
+    HIPCHK(c, hipMemset(c->d_dirty, 0, 4));
+    c->pend_u64 = false;
     if (c->d_owned) HIPCHK(c, hipMemset(c->d_owned, 0, cells / c->nranks * 8));
     if (c->d_truth) HIPCHK(c, hipMemset(c->d_truth, 0, cells * 8));
     if (c->d_truth_out) HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
@@ -1126,6 +1316,12 @@ int ysb_path_time(ysb_ctx* c, double* total_ms, uint64_t* launches, uint64_t* re
     if (total_ms) *total_ms = c->path_ms_acc;
     if (launches) *launches = c->path_launches_acc;
     if (record_launches) *record_launches = c->rec_launches;
+    return YSB_OK;
+}
+
+int ysb_launch_info(ysb_ctx* c, ysb_launch_desc* out) {
+    if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
+    *out = c->last_launch;
     return YSB_OK;
 }
 
@@ -1242,12 +1438,53 @@ int ysb_group_init(ysb_ctx* c, int rank, int nranks, const uint8_t uid[YSB_UNIQU
     const u64 per = (u64)c->c_pad / nranks * c->cfg.window_ring;
     HIPCHK(c, hipMalloc(&c->d_owned, per * 8));
     HIPCHK(c, hipMemset(c->d_owned, 0, per * 8));
-    HIPCHK(c, hipMalloc(&c->d_rs_tmp, per * 8));
+    const u32 W = c->cfg.window_ring;
+    HIPCHK(c, hipMalloc(&c->d_xmax, (u64)W * 8));
+    HIPCHK(c, hipHostMalloc(&c->h_xmax, (u64)W * 8 + (u64)W * 4));   // maxima, then the plan's slots
+    HIPCHK(c, hipMalloc(&c->d_xslots, (u64)W * 4));
     // every rank's ring must start at the same bucket (the tables are summed cell by
     // cell): agreed here if any rank already knows its base, else at the first exchange
     return agree_ring(c);
 }
 
+static int grow_bytes(ysb_ctx* c, void** buf, u64* have, u64 bytes) {
+    if (*have >= bytes) return YSB_OK;
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    hipFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    const u64 b = std::max<u64>(bytes, 1ull << 16);
+    HIPCHK(c, hipMalloc(buf, b));
+    *have = b;
+    return YSB_OK;
+}
+
+int ysb_exchange_plan(const uint64_t* slot_max, uint32_t W, uint32_t nranks, uint32_t* slots, uint32_t* n_slots,
+                      uint32_t* width) {
+    if (!slot_max || !slots || !n_slots || !width || nranks == 0 || W == 0) return YSB_ERR_ARG;
+    u32 n = 0;
+    u64 mx = 0;
+    for (u32 s = 0; s < W; ++s)
+        if (slot_max[s]) {
+            slots[n++] = s;
+            mx = std::max<u64>(mx, slot_max[s]);
+        }
+    // the narrowest cell whose sum over the ranks cannot wrap: nranks * max < 2^(8 width)
+    // (RCCL has no 16-bit integer type)
+    const unsigned __int128 bound = (unsigned __int128)mx * nranks;
+    *width = bound <= 0xFFu ? 1u : bound <= 0xFFFFFFFFull ? 4u : 8u;
+    if (bound > ~0ull) return YSB_ERR_CAPACITY;
+    *n_slots = n;
+    return YSB_OK;
+}
+
+// The keyBy(0) exchange (AdvertisingTopologyNative.java:118-119), range-limited: only the
+// ring slots that hold a pending count on some rank travel, in the narrowest cell width
+// that cannot wrap, as the reference's keyed shuffle carries only the touched (campaign,
+// window) pairs.  Steps on the compute stream: per-slot maxima of the pending counts
+// (xplan) -> one W-element all-reduce(max) -> read back (the only host wait) -> plan
+// (ysb_exchange_plan: the same on every rank) -> pack the slots' cells [C_pad][R] and zero
+// them (xpack) -> ncclReduceScatter -> add the owner block into the owned table (xunpack).
 int ysb_group_reduce_scatter(ysb_ctx* c) {
     if (!c) return YSB_ERR_ARG;
     if (!c->comm) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
@@ -1256,14 +1493,116 @@ int ysb_group_reduce_scatter(ysb_ctx* c) {
         int rc = agree_ring(c);
         if (rc) return rc;
     }
-    int frc = fold_delta(c);
-    if (frc) return frc;
-    const u64 per = (u64)c->c_pad / c->nranks * c->cfg.window_ring;
-    ncclResult_t r = ncclReduceScatter(c->d_counts, c->d_rs_tmp, per, ncclUint64, ncclSum, c->comm, c->s_comp);
-    if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
-    launch_add_u64(c->d_owned, c->d_rs_tmp, per, c->s_comp);
-    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, (u64)c->c_pad * c->cfg.window_ring * 8, c->s_comp));
+    const u32 W = c->cfg.window_ring;
+    const u64 cells = (u64)c->c_pad * W;
+    const u8* delta = c->delta_bound ? c->d_delta : nullptr;   // (delta_bound 0: the delta ring is all zero)
+    if (c->xev_used == c->xev.size()) {
+        std::array<hipEvent_t, 2> ev{};
+        for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
+        c->xev.push_back(ev);
+    }
+    const auto ev = c->xev[c->xev_used++];
+    HIPCHK(c, hipEventRecord(ev[0], c->s_comp));
+    HIPCHK(c, hipMemsetAsync(c->d_xmax, 0, (u64)W * 8, c->s_comp));
+    launch_xplan(c->d_counts, delta, W, cells, c->pend_u64 ? 1 : 0, c->d_dirty, c->d_xmax, c->s_comp);
+    HIPCHK(c, hipGetLastError());
+    ncclResult_t r = ncclAllReduce(c->d_xmax, c->d_xmax, W, ncclUint64, ncclMax, c->comm, c->s_comp);
+    if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    HIPCHK(c, hipMemcpyAsync(c->h_xmax, c->d_xmax, (u64)W * 8, hipMemcpyDeviceToHost, c->s_comp));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    u32* slots = reinterpret_cast<u32*>(c->h_xmax + W);
+    u32 R = 0, width = 8;
+    if (ysb_exchange_plan(reinterpret_cast<const uint64_t*>(c->h_xmax), W, (u32)c->nranks, slots, &R, &width))
+        return fail(c, YSB_ERR_CAPACITY, "pending counts too large to sum over %d ranks", c->nranks);
+    const u32 rows = c->c_pad, per = c->c_pad / (u32)c->nranks;
+    if (R) {
+        int rc = grow_bytes(c, &c->d_xsend, &c->xsend_bytes, (u64)rows * R * width);
+        if (!rc) rc = grow_bytes(c, &c->d_xrecv, &c->xrecv_bytes, (u64)per * R * width);
+        if (rc) return rc;
+        HIPCHK(c, hipMemcpyAsync(c->d_xslots, slots, (u64)R * 4, hipMemcpyHostToDevice, c->s_comp));
+        launch_xpack(c->d_counts, delta ? c->d_delta : nullptr, W, rows, c->d_xslots, R, c->pend_u64 ? 1 : 0,
+                     c->d_dirty, c->d_xsend, width, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+        const ncclDataType_t ty = width == 1 ? ncclUint8 : width == 4 ? ncclUint32 : ncclUint64;
+        r = ncclReduceScatter(c->d_xsend, c->d_xrecv, (size_t)per * R, ty, ncclSum, c->comm, c->s_comp);
+        if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
+        launch_xunpack(c->d_owned, W, per, c->d_xslots, R, c->d_xrecv, width, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+    }
+    // every pending count sat in an exchanged slot: nothing is pending any more
+    HIPCHK(c, hipMemsetAsync(c->d_dirty, 0, 4, c->s_comp));
+    c->pend_u64 = false;
+    c->delta_bound = 0;
+    HIPCHK(c, hipEventRecord(ev[1], c->s_comp));
+    c->x_count++;
+    c->x_bytes += (u64)rows * R * width;
+    c->x_last_slots = R;
+    c->x_last_width = R ? width : 0;
     return YSB_OK;
+}
+
+int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
+    if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
+    int rc = sync_streams(c);
+    if (rc) return rc;
+    for (size_t i = 0; i < c->xev_used; ++i) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->xev[i][0], c->xev[i][1]));
+        c->x_ms += ms;
+    }
+    c->xev_used = 0;
+    out->exchanges = c->x_count;
+    out->bytes = c->x_bytes;
+    out->ms = c->x_ms;
+    out->last_buckets = c->x_last_slots;
+    out->last_width = c->x_last_width;
+    out->full_ring_bytes = (u64)c->c_pad * c->cfg.window_ring * 8;
+    if (reset) {
+        c->x_count = 0;
+        c->x_bytes = 0;
+        c->x_ms = 0;
+    }
+    return YSB_OK;
+}
+
+int ysb_group_checksum(ysb_ctx* c, int what, uint32_t nranks, uint64_t* out) {
+    if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
+    if (nranks == 0) return fail(c, YSB_ERR_ARG, "nranks must be >= 1");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = fold_delta(c);   // the checksums read the u64 ring
+    if (!rc) rc = sync_streams(c);
+    if (!rc) rc = read_ring(c);
+    if (rc) return rc;
+    if (!c->ring_known) return fail(c, YSB_ERR_STATE, "ring base not set yet");
+    const u32 W = c->cfg.window_ring, C = c->cfg.n_campaigns;
+    if (!c->d_cmp) HIPCHK(c, hipMalloc(&c->d_cmp, 32));
+    unsigned long long* acc = c->d_cmp;
+    auto sum = [&](const unsigned long long* t, u32 rows, u32 c_off, u32 lo, u32 hi, uint64_t* o) -> int {
+        HIPCHK(c, hipMemsetAsync(acc, 0, 8, c->s_comp));
+        launch_checksum(t, rows, W, c->ring_lo, c_off, lo, hi, acc, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(o, acc, 8, hipMemcpyDeviceToHost, c->s_comp));
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        return YSB_OK;
+    };
+    if (what == YSB_SUM_TRUTH_BLOCKS || what == YSB_SUM_PENDING_BLOCKS) {
+        const unsigned long long* t = what == YSB_SUM_TRUTH_BLOCKS ? c->d_truth : c->d_counts;
+        if (!t) return fail(c, YSB_ERR_STATE, "no truth accumulated");
+        for (u32 r = 0; r < nranks; ++r) {
+            u32 lo = 0, hi = 0;
+            ysb_group_block(C, (int)r, (int)nranks, &lo, &hi);
+            if ((rc = sum(t, c->c_pad, 0, lo, hi, &out[r]))) return rc;
+        }
+        return YSB_OK;
+    }
+    if (what == YSB_SUM_OWNED) {
+        if (!c->d_owned) { out[0] = 0; return YSB_OK; }
+        u32 lo = 0, hi = 0;
+        ysb_group_block(C, c->rank, c->nranks, &lo, &hi);
+        const u32 per = c->c_pad / (u32)c->nranks;   // row i of the owned table: campaign rank * per + i
+        return sum(c->d_owned, per, (u32)c->rank * per, lo, hi, &out[0]);
+    }
+    return fail(c, YSB_ERR_ARG, "unknown checksum %d", what);
 }
 
 int ysb_group_info(ysb_ctx* c, int* rank, int* nranks) {

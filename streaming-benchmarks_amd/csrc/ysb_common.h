@@ -508,8 +508,18 @@ YSB_HD i64 div_trunc(i64 t, const DivMagic& m) {
 // Stats slots in the device stats array.
 enum : u32 {
     ST_EVENTS = 0, ST_VIEWS, ST_JOINED, ST_MISSES, ST_PARSE_ERR, ST_TIME_ERR,
-    ST_OUT_OF_RING, ST_OVF_DROPPED, ST_DEFERRED, ST_COUNT_
+    ST_OUT_OF_RING, ST_OVF_DROPPED, ST_DEFERRED, ST_FOREIGN, ST_COUNT_
 };
+
+// ysb_ad_shard: the rank of nranks whose join-table shard holds a key (zero-padded words,
+// len <= MAX_KEY_BYTES); host and device (the deferred-line kernel's miss path) alike.
+YSB_HD u32 key_shard(u32 h, u32 nranks) { return (u32)(((mix64(h) >> 32) * (u64)nranks) >> 32); }
+
+// Weight of the (campaign, bucket) cell in the linear table checksums (ysb_group_checksum):
+// odd, so a single wrong count always changes the sum; sums of tables add like the tables.
+YSB_HD u64 cell_weight(u32 campaign, i64 bucket) {
+    return mix64(((u64)campaign << 40) ^ ((u64)bucket * 0x9E3779B97F4A7C15ULL)) | 1ull;
+}
 
 // Out-of-ring (campaign, bucket) cells: an open-addressing device hash map with one
 // 64-bit key per cell (bucket offset by 2^(63 - cbits) in the high bits, campaign in

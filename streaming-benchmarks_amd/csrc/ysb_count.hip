@@ -19,13 +19,14 @@
 //   count         per level-2 block (32768 / W campaigns, whose L2C x W cells are one
 //                 contiguous slab of the campaign-major ring): LDS u32 counters, then
 //                 every counted line of cells added ONCE with a plain load/add/store to
-//                 the u32 DELTA ring (the block's slab belongs to this workgroup alone;
+//                 the u8 DELTA ring (the block's slab belongs to this workgroup alone;
 //                 consecutive lanes take consecutive cells, so the loads and stores
-//                 coalesce) -- half the bytes of the u64 ring's read-modify-write;
-//   fold          before anything reads the u64 ring (drain, ring advance, exchange,
-//                 truth compare) and before the views added since the last fold could
-//                 reach 2^32 (so no delta cell can wrap), delta is added to the ring and
-//                 cleared (ysb_capi.cpp fold_delta).
+//                 coalesce) -- an eighth of the bytes of the u64 ring's read-modify-write;
+//                 a cell whose sum would pass 255 adds it to the u64 ring with one atomic
+//                 and restarts at 0 (saturation, never a wrap);
+//   fold          before anything reads the u64 ring (drain, ring advance, truth compare,
+//                 checksums) delta is added to the ring and cleared (ysb_capi.cpp
+//                 fold_delta); the exchange reads the delta ring itself (ysb_table.hip).
 //
 // Exact: the same additions, reordered (integer sums commute).
 #include "ysb_kernels.h"
@@ -165,6 +166,32 @@ __global__ __launch_bounds__(REC_TPB) void rec_partition_kernel(const RecParams 
         if (cur[k] > fl[k]) write_line(k, cur[k] - fl[k]);
 }
 
+// 16 cells of the u8 delta ring (one 16-B vector) plus their LDS counts.  A cell whose sum
+// passes 255 adds the whole sum to its u64 ring cell (one atomic; rare: ~0.3 views per cell
+// per launch on configs[2]) and restarts at 0, so the delta never wraps.
+__device__ __forceinline__ uint4 add16(uint4 d, const u32* cnt16, unsigned long long* ring16, u32* dirty) {
+    const u32 dw[4] = {d.x, d.y, d.z, d.w};
+    u32 o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint4 c = reinterpret_cast<const uint4*>(cnt16)[k];
+        const u32 cc[4] = {c.x, c.y, c.z, c.w};
+        u32 w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u32 s = ((dw[k] >> (8 * j)) & 0xFFu) + cc[j];
+            if (s > 255u) {
+                atomicAdd(&ring16[4 * k + j], (unsigned long long)s);
+                *dirty = 1u;
+            } else {
+                w |= s << (8 * j);
+            }
+        }
+        o[k] = w;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // One count workgroup: level-2 block j (campaigns [j*L2C, (j+1)*L2C), the slab of
 // L2C x W ring cells).  The block's QUARTERS runs flattened, 8 records per lane in flight
 // -> LDS u32 counters; then the slab is read, added to and written back whole (16-B
@@ -195,14 +222,16 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
     __syncthreads();
     const u32 total = roff[REC_QUARTERS];
     const u32 base_cell = c0 << R.w_log2;
-    // the slab of the delta ring: [base_cell, base_cell + cells) u32, as 16-B quads; 8
-    // consecutive threads cover one 128-B line; quads <= REC_TPB * SU, so each thread
-    // holds at most SU of them.  No cell wraps: the host folds the delta ring into the
-    // u64 ring before 2^32 views can have been added to it.
+    // the slab of the u8 delta ring: [base_cell, base_cell + cells) bytes, as 16-cell
+    // vectors (16 B); 8 consecutive threads cover one 128-B line; vectors <= REC_TPB * SU,
+    // so each thread holds at most SU of them.  A cell whose sum would pass 255 adds it to
+    // the u64 ring instead (add16), so no cell ever wraps and nothing needs folding between
+    // launches: per launch the slab costs a quarter of a u32 delta ring's bytes.
     uint4* dr = reinterpret_cast<uint4*>(R.delta + base_cell);
-    const u32 quads = cells / 4;   // a multiple of 4 (cells: of 16); lines of 8 quads
-    constexpr int SU = REC_BLOCK_CELLS / 4 / REC_TPB;
-    static_assert(SU * REC_TPB * 4 == REC_BLOCK_CELLS, "one slab quad set per thread");
+    const u32 quads = cells / 16;  // 16-cell vectors (cells: a multiple of 16); lines of 8
+    constexpr int SU = REC_BLOCK_CELLS / 16 / REC_TPB;
+    static_assert(SU * REC_TPB * 16 == REC_BLOCK_CELLS, "one slab vector set per thread");
+    unsigned long long* ring = R.counts + base_cell;
     // Dense block (at least one record per 16 cells: nearly every line is counted): the
     // whole slab is read up front, its round trip under the record loads and LDS atomics,
     // and written back whole.  Sparse block: after the counts, only the lines holding a
@@ -237,20 +266,22 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
             const u32 p = u * REC_TPB + tid;
-            if (p < quads) {
-                const uint4 c = reinterpret_cast<const uint4*>(cnt)[p];
-                dr[p] = make_uint4(r[u].x + c.x, r[u].y + c.y, r[u].z + c.z, r[u].w + c.w);
-            }
+            if (p < quads) dr[p] = add16(r[u], cnt + 16 * p, ring + 16 * (u64)p, R.dirty);
         }
         return;
     }
-    uint4 c[SU];
     bool live[SU];
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
         const u32 p = u * REC_TPB + tid;
-        c[u] = p < quads ? reinterpret_cast<const uint4*>(cnt)[p] : make_uint4(0u, 0u, 0u, 0u);
-        u32 any = c[u].x | c[u].y | c[u].z | c[u].w;
+        u32 any = 0;
+        if (p < quads) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint4 c = reinterpret_cast<const uint4*>(cnt)[4 * p + j];
+                any |= c.x | c.y | c.z | c.w;
+            }
+        }
         any |= __shfl_xor(any, 1, 64);
         any |= __shfl_xor(any, 2, 64);
         any |= __shfl_xor(any, 4, 64);
@@ -264,23 +295,25 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
         const u32 p = u * REC_TPB + tid;
-        if (live[u]) dr[p] = make_uint4(r[u].x + c[u].x, r[u].y + c[u].y, r[u].z + c[u].z, r[u].w + c[u].w);
+        if (live[u]) dr[p] = add16(r[u], cnt + 16 * p, ring + 16 * (u64)p, R.dirty);
     }
 }
 
-// counts[i] += delta[i], delta[i] = 0 for every cell (4 per thread; all-zero quads skipped)
-__global__ __launch_bounds__(256) void fold_kernel(unsigned long long* counts, u32* delta, u64 quads) {
-    for (u64 q = (u64)blockIdx.x * 256 + threadIdx.x; q < quads; q += (u64)gridDim.x * 256) {
+// counts[i] += delta[i], delta[i] = 0 for every cell (16 per thread; all-zero vectors skipped)
+__global__ __launch_bounds__(256) void fold_kernel(unsigned long long* counts, u8* delta, u64 vecs) {
+    for (u64 q = (u64)blockIdx.x * 256 + threadIdx.x; q < vecs; q += (u64)gridDim.x * 256) {
         const uint4 d = reinterpret_cast<const uint4*>(delta)[q];
         if ((d.x | d.y | d.z | d.w) == 0u) continue;
-        ulonglong2* c2 = reinterpret_cast<ulonglong2*>(counts + 4 * q);
-        ulonglong2 a = c2[0], b = c2[1];
-        a.x += d.x;
-        a.y += d.y;
-        b.x += d.z;
-        b.y += d.w;
-        c2[0] = a;
-        c2[1] = b;
+        const u32 dw[4] = {d.x, d.y, d.z, d.w};
+        ulonglong2* c2 = reinterpret_cast<ulonglong2*>(counts + 16 * q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (((dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) == 0u) continue;
+            ulonglong2 a = c2[j];
+            a.x += (dw[j >> 1] >> (16 * (j & 1))) & 0xFFu;
+            a.y += (dw[j >> 1] >> (16 * (j & 1) + 8)) & 0xFFu;
+            c2[j] = a;
+        }
         reinterpret_cast<uint4*>(delta)[q] = make_uint4(0u, 0u, 0u, 0u);
     }
 }
@@ -289,11 +322,11 @@ void launch_rec_partition(const RecParams& r, hipStream_t s) {
     hipLaunchKernelGGL(rec_partition_kernel, dim3(r.bins * REC_QUARTERS), dim3(REC_TPB), 0, s, r);
 }
 
-void launch_fold(unsigned long long* counts, u32* delta, u64 cells, hipStream_t s) {
-    const u64 quads = cells / 4;   // cells: c_pad * W, W a power of two >= 16
-    if (!quads) return;
-    const u64 blocks = std::min<u64>((quads + 255) / 256, 65536);
-    hipLaunchKernelGGL(fold_kernel, dim3((u32)blocks), dim3(256), 0, s, counts, delta, quads);
+void launch_fold(unsigned long long* counts, u8* delta, u64 cells, hipStream_t s) {
+    const u64 vecs = cells / 16;   // cells: c_pad * W, W a power of two >= 16
+    if (!vecs) return;
+    const u64 blocks = std::min<u64>((vecs + 255) / 256, 65536);
+    hipLaunchKernelGGL(fold_kernel, dim3((u32)blocks), dim3(256), 0, s, counts, delta, vecs);
 }
 
 void launch_rec_count(const RecParams& r, hipStream_t s) {

@@ -57,8 +57,11 @@ long skip_value(const u8* s, long p, long e) {
 
 }  // namespace
 
-// Raw bytes of the top-level "ad_id" string value of one line (escapes are not decoded:
-// routing only balances load, every rank holds the whole ad map).  Generator lines
+// Raw bytes of the top-level "ad_id" string value of one line.  Escapes are not decoded,
+// so an ad_id written with escapes may be routed to another shard than the one holding its
+// decoded key: with the whole ad map on every rank (ysb_load_ad_map) that only moves load;
+// with a sharded table (ysb_load_ad_map_shard) such a view misses and is counted as
+// foreign_shard -- an error under YSB_F_STRICT, never a silent loss.  Generator lines
 // (data/src/setup/core.clj:90-96) have it at byte 113; other layouts take a small
 // key scan.  Returns false when the line has no string ad_id.
 static bool find_ad_id(const u8* s, long n, long* vs, long* ve) {

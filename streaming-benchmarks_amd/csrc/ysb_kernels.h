@@ -138,6 +138,17 @@ struct ScanParams {
     u32* rec;                   // [grid][rec_bins][rec_cap]
     u32* rec_n;                 // [grid][rec_bins] records written
     u32 layout;                 // JSON layout tried first: 0 generator, 1 YSB_F_COMPACT_FIRST, 2 YSB_F_FLAT_FIRST
+    // the join table's shard (ysb_load_ad_map_shard): a miss of a key whose shard is not
+    // shard_rank counts as ST_FOREIGN (shard_n 1: unsharded).  Sharded contexts defer the
+    // scan's misses (ctable_partial) so that only the deferred-line kernel classifies them.
+    u32 shard_rank;
+    u32 shard_n;
+    // record mode: set when a view went to the u64 ring instead of a record (the exchange
+    // then reads that ring too; ysb_capi.cpp exchange)
+    u32* pend_dirty;
+    // pinned host word (or null): defer_kernel stores the out-of-ring map's fill level there
+    // (the host checks it at the next submit without waiting)
+    u32* used_out;
 };
 
 // Record-mode pipeline after the scan (ysb_count.hip).  Level-2 bins ("blocks") are
@@ -163,11 +174,32 @@ struct RecParams {
     u64 area;                   // u32 words of one (bin, quarter) output area
     u32* part;                  // partitioned records: [bins * QUARTERS][area], runs 32-record aligned
     u32* runs;                  // [n_blocks][QUARTERS] {offset, count} into part
-    u32* delta;                 // the u32 delta ring [c_pad][W], folded into the u64 ring before it is read
+    u8* delta;                  // the u8 delta ring [c_pad][W] (saturating: a cell that would pass
+                                // 255 adds its whole value to the u64 ring instead and restarts at 0)
+    unsigned long long* counts; // the u64 ring
+    u32* dirty;                 // set when the count kernel added to the u64 ring
 };
 void launch_rec_partition(const RecParams& r, hipStream_t s);
 void launch_rec_count(const RecParams& r, hipStream_t s);
-void launch_fold(unsigned long long* counts, u32* delta, u64 cells, hipStream_t s);
+// counts[i] += delta[i], delta[i] = 0 (cells: a multiple of 16)
+void launch_fold(unsigned long long* counts, u8* delta, u64 cells, hipStream_t s);
+
+// Range-limited exchange (ysb_group_reduce_scatter).  A rank's pending counts are its u64
+// ring (read when force_u64 or *dirty) plus, in record mode, its u8 delta ring.
+// xplan: slot_max[s] = max over campaigns of the pending count in ring slot s (atomicMax:
+// zero slot_max first).  xpack: the pending cells of slots[0..R) as a dense [rows][R] array
+// of `width`-byte cells (1, 4 or 8), the sources zeroed.  xunpack: owned[c][slots[k]] +=
+// in[c][k] for the owner block's rows.
+void launch_xplan(const unsigned long long* counts, const u8* delta, u32 W, u64 cells, int force_u64,
+                  const u32* dirty, unsigned long long* slot_max, hipStream_t s);
+void launch_xpack(unsigned long long* counts, u8* delta, u32 W, u32 rows, const u32* slots, u32 R, int force_u64,
+                  const u32* dirty, void* out, u32 width, hipStream_t s);
+void launch_xunpack(unsigned long long* owned, u32 W, u32 rows, const u32* slots, u32 R, const void* in, u32 width,
+                    hipStream_t s);
+// Linear checksum of a campaign-major [rows][W] u64 table (row i = campaign c_off + i) over
+// the campaigns [c_lo, c_hi): *out += SUM count * cell_weight(campaign, bucket) (mod 2^64).
+void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_lo, u32 c_off, u32 c_lo, u32 c_hi,
+                     unsigned long long* out, hipStream_t s);
 
 constexpr int N_STAMPS = 8;     // phases timed by the YSB_STAMPS diagnostic build
 

@@ -794,7 +794,16 @@ __device__ __forceinline__ bool tbl_stage2(const LdsSrc& src, int s, int e, cons
 
 // One line end to end: returns 0 not counted, 1 counted (campaign/bucket set).
 // Per-thread tallies go to st[].
-struct Tally { u32 ev, view, join, miss, perr, terr, oor; };
+struct Tally { u32 ev, view, join, miss, perr, terr, oor, frn; };
+
+// A view whose ad_id missed the table: dropped (RedisJoinBolt, :465-467) and counted as a
+// join miss -- or, when this context holds one shard of the table (P.shard_n > 1) and the
+// key belongs to another, as a foreign-shard view (mis-routed input).
+__device__ __forceinline__ void count_miss(const ScanParams& P, const u32 (&kw)[KEY_WORDS], u32 klen, bool keyed,
+                                           Tally& t) {
+    if (keyed && P.shard_n > 1u && key_shard(key_hash_dev(kw, klen), P.shard_n) != P.shard_rank) t.frn++;
+    else t.miss++;
+}
 
 // A parsed event's filter, join and bucket (the bolts after DeserializeBolt).
 template <class S>
@@ -805,8 +814,9 @@ __device__ __forceinline__ bool finish_line(const S& src, const Span& ad, const 
     u32 kw[KEY_WORDS];
     u32 klen = 0;
     int c = -1;
-    if (span_key(src, ad, kw, klen)) c = probe(P.table, P.table_mask, kw, klen);   // RedisJoinBolt
-    if (c < 0) { t.miss++; return false; }
+    const bool keyed = span_key(src, ad, kw, klen);
+    if (keyed) c = probe(P.table, P.table_mask, kw, klen);   // RedisJoinBolt
+    if (c < 0) { count_miss(P, kw, klen, keyed, t); return false; }
     t.join++;
     i64 tv;
     if (!span_long(src, tm, tv)) { t.terr++; return false; }   // CampaignProcessorCommon :58
@@ -1223,12 +1233,13 @@ __device__ __forceinline__ u32 wave_sum(u32 v) {
 }
 
 __device__ __forceinline__ void flush_tally(const ScanParams& P, const Tally& tl, int lane) {
-    const u32 sums[7] = {wave_sum(tl.ev), wave_sum(tl.view), wave_sum(tl.join), wave_sum(tl.miss),
-                         wave_sum(tl.perr), wave_sum(tl.terr), wave_sum(tl.oor)};
+    const u32 sums[8] = {wave_sum(tl.ev), wave_sum(tl.view), wave_sum(tl.join), wave_sum(tl.miss),
+                         wave_sum(tl.perr), wave_sum(tl.terr), wave_sum(tl.oor), wave_sum(tl.frn)};
     if (lane == 0) {
-        const u32 slots[7] = {ST_EVENTS, ST_VIEWS, ST_JOINED, ST_MISSES, ST_PARSE_ERR, ST_TIME_ERR, ST_OUT_OF_RING};
+        const u32 slots[8] = {ST_EVENTS, ST_VIEWS, ST_JOINED, ST_MISSES, ST_PARSE_ERR, ST_TIME_ERR, ST_OUT_OF_RING,
+                              ST_FOREIGN};
 #pragma unroll
-        for (int k = 0; k < 7; ++k)
+        for (int k = 0; k < 8; ++k)
             if (sums[k]) atomicAdd(&P.stats[slots[k]], (unsigned long long)sums[k]);
     }
 }
@@ -1288,6 +1299,7 @@ __device__ __forceinline__ void rec_fallback(const ScanParams& P, u32 cell, i64 
     const i64 slot = (i64)(cell & (P.ring_w - 1));
     const i64 b = ring_lo + ((slot - ring_lo) & (i64)(P.ring_w - 1));
     global_add(P, ring_lo, ring_set, c, b, 1u, tl);
+    *P.pend_dirty = 1u;   // the u64 ring holds pending counts now (the exchange reads it)
 }
 
 // Record mode: writes n (<= 32) staged records of bin b, ring positions [fl, fl + n), to
@@ -1349,7 +1361,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
     // bucket that fell ahead of the window, INT64_MIN = none
     if (!REC && tid < 2) misc64[tid] = INT64_MIN;
 
-    Tally tl{0, 0, 0, 0, 0, 0, 0};
+    Tally tl{0, 0, 0, 0, 0, 0, 0, 0};
     // Prefetch depth: tile t + PF_DEPTH is issued once tile t sits in LDS.  Depth 2 keeps
     // two tiles in flight per wave (two register buffers, the loop unrolled by two).
     constexpr int PF_DEPTH = YSB_PREFETCH_DEPTH;
@@ -1767,8 +1779,9 @@ __device__ __forceinline__ bool process_tbl_line(const S& src, int s, int e, con
     u32 kw[KEY_WORDS];
     u32 klen = 0;
     int c = -1;
-    if (span_key(src, ad, kw, klen)) c = probe(P.table, P.table_mask, kw, klen);   // RedisJoinBolt
-    if (c < 0) { t.miss++; return false; }
+    const bool keyed = span_key(src, ad, kw, klen);
+    if (keyed) c = probe(P.table, P.table_mask, kw, klen);   // RedisJoinBolt
+    if (c < 0) { count_miss(P, kw, klen, keyed, t); return false; }
     t.join++;
     i64 tv;
     if (!parse_digits(src, p[4] + 1, p[5], tv)) { t.terr++; return false; }   // Long.parseLong
@@ -1800,12 +1813,13 @@ __global__ __launch_bounds__(DEFER_TPB) void defer_kernel(const ScanParams P0) {
     __shared__ u32 stage[DEFER_TPB * DEFER_REGION_DW];
     ScanParams P = P0;   // batch fields: the segment of the line being parsed
     const int tid = threadIdx.x, lane = tid & 63;
+    if (blockIdx.x == 0 && tid == 0 && P.used_out) *P.used_out = *P.side_used;   // the scan's fill level, for the host
     const u32 total = *P.defer_count;
     if (total == 0u) return;   // nothing deferred (generator data): every workgroup leaves at once
     const u32 cnt = min(total, P.defer_cap);
     const i64 ring_lo = P.ring[0];
     const bool ring_set = P.ring[1] != 0;
-    Tally tl{0, 0, 0, 0, 0, 0, 0};
+    Tally tl{0, 0, 0, 0, 0, 0, 0, 0};
     u32* region = stage + tid * DEFER_REGION_DW;
     for (u32 i = blockIdx.x * DEFER_TPB + tid; i < cnt; i += gridDim.x * DEFER_TPB) {
         u64 li = P.defer[i];   // index among all segments' lines
@@ -1868,7 +1882,10 @@ __global__ __launch_bounds__(DEFER_TPB) void defer_kernel(const ScanParams P0) {
             ok = P.tbl ? process_tbl_line(gsrc, 0, len, P, tl, campaign, bucket)
                        : process_line(gsrc, 0, len, P, tl, campaign, bucket);
         }
-        if (ok) global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+        if (ok) {
+            global_add(P, ring_lo, ring_set, campaign, bucket, 1u, tl);
+            *P.pend_dirty = 1u;   // the u64 ring holds pending counts now (the exchange reads it)
+        }
     }
     flush_tally(P, tl, lane);
     __syncthreads();
@@ -1893,7 +1910,7 @@ __global__ __launch_bounds__(AUX_TPB) void ring_autobase_kernel(ScanParams P, i6
         const u64 ls = P.off[tid];
         const u64 le = ((u64)tid + 1 < P.n) ? (u64)P.off[tid + 1] : P.nbytes;
         if (ls <= le && le <= P.nbytes && le - ls < 0x7FFFFFFFull) {
-            Tally tl{0, 0, 0, 0, 0, 0, 0};
+            Tally tl{0, 0, 0, 0, 0, 0, 0, 0};
             u32 c;
             i64 bk;
             const GlbSrc gsrc{P.bytes + ls, le - ls};
@@ -1930,7 +1947,7 @@ __global__ __launch_bounds__(AUX_TPB) void tbl_ring_autobase_kernel(ScanParams P
         const u64 ls = P.off[tid];
         const u64 le = ((u64)tid + 1 < P.n) ? (u64)P.off[tid + 1] : P.nbytes;
         if (ls <= le && le <= P.nbytes && le - ls < 0x7FFFFFFFull) {
-            Tally tl{0, 0, 0, 0, 0, 0, 0};
+            Tally tl{0, 0, 0, 0, 0, 0, 0, 0};
             u32 c;
             i64 bk;
             const GlbSrc gsrc{P.bytes + ls, le - ls};

@@ -105,4 +105,142 @@ void launch_side_compact(const SideSlot* t, u64 slots, u32 cbits, bool count_onl
                        count_only ? 1 : 0, out, out_n, cap);
 }
 
+// ---- the range-limited exchange (keyBy(0), AdvertisingTopologyNative.java:118-119) -------
+// A rank's pending counts since its last exchange are its u64 ring plus (record mode) its
+// u8 delta ring.  The u64 ring is read only when a launch without record mode ran
+// (force_u64) or a record-mode path wrote it (*dirty): configs[2]'s exchange then reads a
+// 1-byte delta per cell instead of an 8-byte one.
+
+constexpr u32 XPLAN_LDS_W = 4096;   // ring slots whose maxima a plan workgroup keeps in LDS
+
+__device__ __forceinline__ bool read_u64(int force_u64, const u32* dirty) { return force_u64 || (dirty && *dirty); }
+
+// slot_max[s] = max pending count of ring slot s over this rank's campaigns; 16 cells
+// (one campaign's consecutive slots) per thread.
+__global__ __launch_bounds__(AUX_TPB) void xplan_kernel(const unsigned long long* counts, const u8* delta, u32 W,
+                                                        u64 vecs, int force_u64, const u32* dirty,
+                                                        unsigned long long* slot_max) {
+    __shared__ unsigned long long lmax[XPLAN_LDS_W];
+    const bool in_lds = W <= XPLAN_LDS_W;
+    if (in_lds)
+        for (u32 s = threadIdx.x; s < W; s += AUX_TPB) lmax[s] = 0;
+    __syncthreads();
+    const bool r64 = read_u64(force_u64, dirty);
+    for (u64 q = (u64)blockIdx.x * AUX_TPB + threadIdx.x; q < vecs; q += (u64)gridDim.x * AUX_TPB) {
+        const u64 i0 = 16 * q;
+        const u32 s0 = (u32)(i0 & (u64)(W - 1));
+        u32 dw[4] = {0u, 0u, 0u, 0u};
+        if (delta) {
+            const uint4 d = reinterpret_cast<const uint4*>(delta)[q];
+            dw[0] = d.x; dw[1] = d.y; dw[2] = d.z; dw[3] = d.w;
+        }
+        if (!r64 && (dw[0] | dw[1] | dw[2] | dw[3]) == 0u) continue;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            unsigned long long v = (dw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            if (r64) v += counts[i0 + j];
+            if (!v) continue;
+            if (in_lds) atomicMax(&lmax[s0 + j], v);
+            else atomicMax(&slot_max[s0 + j], v);
+        }
+    }
+    if (!in_lds) return;
+    __syncthreads();
+    for (u32 s = threadIdx.x; s < W; s += AUX_TPB)
+        if (lmax[s]) atomicMax(&slot_max[s], lmax[s]);
+}
+
+// out[c][k] = pending(c, slots[k]) as `width`-byte cells; the sources zeroed.  One thread
+// per output cell: consecutive threads take consecutive slots of a campaign.
+__global__ __launch_bounds__(AUX_TPB) void xpack_kernel(unsigned long long* counts, u8* delta, u32 W, u32 rows,
+                                                        const u32* slots, u32 R, int force_u64, const u32* dirty,
+                                                        void* out, u32 width) {
+    const bool r64 = read_u64(force_u64, dirty);
+    const u64 n = (u64)rows * R;
+    for (u64 i = (u64)blockIdx.x * AUX_TPB + threadIdx.x; i < n; i += (u64)gridDim.x * AUX_TPB) {
+        const u32 c = (u32)(i / R), k = (u32)(i % R);
+        const u64 cell = (u64)c * W + slots[k];
+        unsigned long long v = 0;
+        if (delta) {
+            v = delta[cell];
+            if (v) delta[cell] = 0;
+        }
+        if (r64) {
+            const unsigned long long x = counts[cell];
+            if (x) {
+                v += x;
+                counts[cell] = 0;
+            }
+        }
+        if (width == 1) static_cast<u8*>(out)[i] = (u8)v;
+        else if (width == 4) static_cast<u32*>(out)[i] = (u32)v;
+        else static_cast<unsigned long long*>(out)[i] = v;
+    }
+}
+
+__global__ __launch_bounds__(AUX_TPB) void xunpack_kernel(unsigned long long* owned, u32 W, u32 rows,
+                                                          const u32* slots, u32 R, const void* in, u32 width) {
+    const u64 n = (u64)rows * R;
+    for (u64 i = (u64)blockIdx.x * AUX_TPB + threadIdx.x; i < n; i += (u64)gridDim.x * AUX_TPB) {
+        const unsigned long long v = width == 1   ? (unsigned long long)static_cast<const u8*>(in)[i]
+                                     : width == 4 ? (unsigned long long)static_cast<const u32*>(in)[i]
+                                                  : static_cast<const unsigned long long*>(in)[i];
+        if (v) owned[(u64)(i / R) * W + slots[i % R]] += v;
+    }
+}
+
+// *out += SUM over rows whose campaign is in [c_lo, c_hi) of count * cell_weight (mod 2^64)
+__global__ __launch_bounds__(AUX_TPB) void checksum_kernel(const unsigned long long* table, u32 rows, u32 W,
+                                                           i64 ring_lo, u32 c_off, u32 c_lo, u32 c_hi,
+                                                           unsigned long long* out) {
+    unsigned long long acc = 0;
+    const u64 cells = (u64)rows * W;
+    for (u64 i = (u64)blockIdx.x * AUX_TPB + threadIdx.x; i < cells; i += (u64)gridDim.x * AUX_TPB) {
+        const unsigned long long v = table[i];
+        if (!v) continue;
+        const u32 c = c_off + (u32)(i / W);
+        if (c < c_lo || c >= c_hi) continue;
+        const i64 slot = (i64)(i & (u64)(W - 1));
+        const i64 b = ring_lo + ((slot - ring_lo) & (i64)(W - 1));
+        acc += v * cell_weight(c, b);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
+static u64 grid_for(u64 items, u64 cap = 8192) { return std::max<u64>(1, std::min<u64>((items + AUX_TPB - 1) / AUX_TPB, cap)); }
+
+void launch_xplan(const unsigned long long* counts, const u8* delta, u32 W, u64 cells, int force_u64,
+                  const u32* dirty, unsigned long long* slot_max, hipStream_t s) {
+    const u64 vecs = cells / 16;
+    if (!vecs) return;
+    hipLaunchKernelGGL(xplan_kernel, dim3((unsigned)grid_for(vecs, 2048)), dim3(AUX_TPB), 0, s, counts, delta, W, vecs,
+                       force_u64, dirty, slot_max);
+}
+
+void launch_xpack(unsigned long long* counts, u8* delta, u32 W, u32 rows, const u32* slots, u32 R, int force_u64,
+                  const u32* dirty, void* out, u32 width, hipStream_t s) {
+    const u64 n = (u64)rows * R;
+    if (!n) return;
+    hipLaunchKernelGGL(xpack_kernel, dim3((unsigned)grid_for(n)), dim3(AUX_TPB), 0, s, counts, delta, W, rows, slots, R,
+                       force_u64, dirty, out, width);
+}
+
+void launch_xunpack(unsigned long long* owned, u32 W, u32 rows, const u32* slots, u32 R, const void* in, u32 width,
+                    hipStream_t s) {
+    const u64 n = (u64)rows * R;
+    if (!n) return;
+    hipLaunchKernelGGL(xunpack_kernel, dim3((unsigned)grid_for(n)), dim3(AUX_TPB), 0, s, owned, W, rows, slots, R, in,
+                       width);
+}
+
+void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_lo, u32 c_off, u32 c_lo, u32 c_hi,
+                     unsigned long long* out, hipStream_t s) {
+    const u64 cells = (u64)rows * W;
+    if (!cells) return;
+    hipLaunchKernelGGL(checksum_kernel, dim3((unsigned)grid_for(cells, 4096)), dim3(AUX_TPB), 0, s, table, rows, W,
+                       ring_lo, c_off, c_lo, c_hi, out);
+}
+
 }  // namespace ysb

@@ -27,7 +27,12 @@ YSB_F_RECORD_COUNT = 0x20
 YSB_F_NO_RECORD_COUNT = 0x40
 YSB_F_COMPACT_FIRST = 0x80
 YSB_F_FLAT_FIRST = 0x100
-YSB_F_LAYOUT_AUTO = 0x200
+YSB_F_LAYOUT_AUTO = 0x200   # the default since ABI 2 (accepted, ignored)
+YSB_F_STRICT = 0x400
+YSB_F_LAYOUT_FIXED = 0x800
+YSB_SUM_TRUTH_BLOCKS = 0
+YSB_SUM_PENDING_BLOCKS = 1
+YSB_SUM_OWNED = 2
 INT64_MIN = -(1 << 63)
 UNIQUE_ID_BYTES = 128
 
@@ -41,12 +46,22 @@ class YsbConfig(C.Structure):
 
 class YsbStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("events", "views", "joined", "join_misses", "parse_errors",
-                                          "time_errors", "out_of_ring", "overflow_dropped", "batches", "deferred")]
+                                          "time_errors", "out_of_ring", "overflow_dropped", "batches", "deferred",
+                                          "foreign_shard")]
 
 
 class YsbCount(C.Structure):
     _fields_ = [("campaign", C.c_uint32), ("reserved", C.c_uint32), ("window_ms", C.c_int64),
                 ("count", C.c_uint64)]
+
+
+class YsbExchangeInfo(C.Structure):
+    _fields_ = [("exchanges", C.c_uint64), ("bytes", C.c_uint64), ("ms", C.c_double), ("last_buckets", C.c_uint32),
+                ("last_width", C.c_uint32), ("full_ring_bytes", C.c_uint64)]
+
+
+class YsbLaunchDesc(C.Structure):
+    _fields_ = [("layout", C.c_uint32), ("record_mode", C.c_uint32), ("hbm_table", C.c_uint32), ("tbl", C.c_uint32)]
 
 
 class YsbSegment(C.Structure):
@@ -79,6 +94,8 @@ SIGNATURES = {
     "ysb_last_error": (C.c_char_p, [_P]),
     "ysb_load_ad_map": (_I, [_P, C.POINTER(C.c_char_p), C.POINTER(_U32), C.POINTER(_U32), _U64]),
     "ysb_load_ad_map_packed": (_I, [_P, C.c_void_p, _U32, C.c_void_p, _U64]),
+    "ysb_load_ad_map_shard": (_I, [_P, C.POINTER(C.c_char_p), C.POINTER(_U32), C.POINTER(_U32), _U64, _U32, _U32]),
+    "ysb_load_ad_map_packed_shard": (_I, [_P, C.c_void_p, _U32, C.c_void_p, _U64, _U32, _U32]),
     "ysb_slot_buffers": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_P)]),
     "ysb_submit": (_I, [_P, _I, _PU8, _U64, _PU32, _U64]),
     "ysb_wait": (_I, [_P, _I]),
@@ -93,6 +110,7 @@ SIGNATURES = {
     "ysb_kernel_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64)]),
     "ysb_path_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_stream": (_P, [_P]),
+    "ysb_launch_info": (_I, [_P, C.POINTER(YsbLaunchDesc)]),
     "ysb_device_alloc": (_I, [_P, _U64, C.POINTER(_P)]),
     "ysb_device_free": (_I, [_P, _P]),
     "ysb_memcpy_h2d": (_I, [_P, _P, _P, _U64]),
@@ -100,6 +118,9 @@ SIGNATURES = {
     "ysb_group_unique_id": (_I, [C.c_char_p]),
     "ysb_group_init": (_I, [_P, _I, _I, C.c_char_p]),
     "ysb_group_reduce_scatter": (_I, [_P]),
+    "ysb_group_exchange_info": (_I, [_P, C.POINTER(YsbExchangeInfo), _I]),
+    "ysb_exchange_plan": (_I, [C.c_void_p, _U32, _U32, C.c_void_p, C.POINTER(_U32), C.POINTER(_U32)]),
+    "ysb_group_checksum": (_I, [_P, _I, _U32, C.c_void_p]),
     "ysb_group_owned": (_I, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "ysb_group_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I)]),
     "ysb_ad_shard": (_U32, [C.c_char_p, _U32, _U32]),

@@ -13,7 +13,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import INT64_MIN, YsbConfig, YsbCount, YsbSegment, YsbStats, check, lib
+from ._lib import INT64_MIN, YsbConfig, YsbCount, YsbExchangeInfo, YsbLaunchDesc, YsbSegment, YsbStats, check, lib
 
 
 def _ptr(a):
@@ -25,7 +25,7 @@ class YsbContext:
                  max_batch_events=1 << 20, max_batch_bytes=256 << 20, ring_base_bucket=None,
                  overflow_capacity=1 << 20, timing=False, require_ip=False, lds_count=True,
                  sparse_fast_join=False, input_format="json", record_count=None, compact_first=False,
-                 flat_first=False, layout_auto=False):
+                 flat_first=False, layout_auto=True, strict=False):
         L = lib()
         cfg = YsbConfig()
         L.ysb_config_default(C.byref(cfg))
@@ -42,7 +42,8 @@ class YsbContext:
                  | (_lib.YSB_F_FORMAT_TBL if input_format == "tbl" else 0)
                  | (_lib.YSB_F_COMPACT_FIRST if compact_first else 0)
                  | (_lib.YSB_F_FLAT_FIRST if flat_first else 0)
-                 | (_lib.YSB_F_LAYOUT_AUTO if layout_auto else 0)
+                 | (0 if layout_auto else _lib.YSB_F_LAYOUT_FIXED)
+                 | (_lib.YSB_F_STRICT if strict else 0)
                  | (0 if record_count is None else
                     _lib.YSB_F_RECORD_COUNT if record_count else _lib.YSB_F_NO_RECORD_COUNT))
         if input_format not in ("json", "tbl"):
@@ -79,31 +80,28 @@ class YsbContext:
         """ad_ids: sequence of str/bytes; campaign_idx: matching campaign indices.
 
         shard = (rank, nranks): load only the ads of this rank's ad_id-hash shard
-        (ysb_ad_shard) -- the join table sharded 1/N per GPU for
-        input that is pre-sharded by the same hash (bench.py's ranks, ysb_gen_dump_shards);
-        an event of another shard's ad is then a join miss, as the reference drops it."""
+        (ysb_load_ad_map_shard) -- the join table sharded 1/N per GPU
+        for input that is pre-sharded by the same hash (bench.py's ranks,
+        ysb_gen_dump_shards).  The library keeps the shard: a view of another shard's ad
+        counts as stats()["foreign_shard"] (an error with strict=True), not as a join miss."""
         keys = [a.encode() if isinstance(a, str) else bytes(a) for a in ad_ids]
-        if shard is not None:
-            from .generator import ad_shard
-            rank, nranks = shard
-            if not 0 <= rank < nranks:
-                raise ValueError("shard rank out of range")
-            pick = [i for i, k in enumerate(keys) if ad_shard(k, nranks) == rank]
-            campaign_idx = [campaign_idx[i] for i in pick]
-            keys = [keys[i] for i in pick]
+        rank, nranks = shard if shard is not None else (0, 1)
+        if not 0 <= rank < nranks:
+            raise ValueError("shard rank out of range")
         n = len(keys)
         arr = (C.c_char_p * max(n, 1))(*keys)
         lens = (C.c_uint32 * max(n, 1))(*[len(k) for k in keys])
         camp = (C.c_uint32 * max(n, 1))(*[int(c) for c in campaign_idx])
-        self._c(lib().ysb_load_ad_map(self._h, arr, lens, camp, n))
+        self._c(lib().ysb_load_ad_map_shard(self._h, arr, lens, camp, n, rank, nranks))
 
-    def load_ad_map_packed(self, keys, campaign_idx, key_len=36):
-        """keys: uint8 array of n * key_len bytes; campaign_idx: n uint32."""
+    def load_ad_map_packed(self, keys, campaign_idx, key_len=36, shard=None):
+        """keys: uint8 array of n * key_len bytes; campaign_idx: n uint32; shard as load_ad_map."""
         k = np.ascontiguousarray(keys, dtype=np.uint8)
         cidx = np.ascontiguousarray(campaign_idx, dtype=np.uint32)
         if k.size != cidx.size * key_len:
             raise ValueError("keys must hold n * key_len bytes")
-        self._c(lib().ysb_load_ad_map_packed(self._h, _ptr(k), key_len, _ptr(cidx), cidx.size))
+        rank, nranks = shard if shard is not None else (0, 1)
+        self._c(lib().ysb_load_ad_map_packed_shard(self._h, _ptr(k), key_len, _ptr(cidx), cidx.size, rank, nranks))
 
     # -- batches -----------------------------------------------------------------------
     def slot_buffers(self, slot):
@@ -178,6 +176,13 @@ class YsbContext:
         self._c(lib().ysb_path_time(self._h, C.byref(t), C.byref(k), C.byref(r)))
         return t.value, k.value, r.value
 
+    def launch_info(self):
+        """The scan instantiation of the last launch: layout (0 generator, 1 compact, 2 flat),
+        record_mode, hbm_table, tbl."""
+        d = YsbLaunchDesc()
+        self._c(lib().ysb_launch_info(self._h, C.byref(d)))
+        return {n: getattr(d, n) for n, _ in YsbLaunchDesc._fields_}
+
     def stream(self):
         return lib().ysb_stream(self._h)
 
@@ -210,6 +215,22 @@ class YsbContext:
 
     def group_reduce_scatter(self):
         self._c(lib().ysb_group_reduce_scatter(self._h))
+
+    def exchange_info(self, reset=False):
+        """Exchange accounting (ysb_group_exchange_info): exchanges, bytes, ms, last_buckets,
+        last_width, full_ring_bytes."""
+        x = YsbExchangeInfo()
+        self._c(lib().ysb_group_exchange_info(self._h, C.byref(x), int(reset)))
+        return {n: getattr(x, n) for n, _ in YsbExchangeInfo._fields_}
+
+    def checksum(self, what, nranks=1):
+        """Linear table checksums (ysb_group_checksum): what = 'truth' / 'pending' (one per
+        owner block of nranks) or 'owned' (this rank's owned table)."""
+        code = {"truth": _lib.YSB_SUM_TRUTH_BLOCKS, "pending": _lib.YSB_SUM_PENDING_BLOCKS,
+                "owned": _lib.YSB_SUM_OWNED}[what]
+        out = np.zeros(max(nranks, 1), dtype=np.uint64)
+        self._c(lib().ysb_group_checksum(self._h, code, nranks, _ptr(out)))
+        return [int(v) for v in (out[:1] if what == "owned" else out[:nranks])]
 
     def group_info(self):
         """(rank, nranks) as RCCL's communicator reports them (ncclCommUserRank / ncclCommCount)."""

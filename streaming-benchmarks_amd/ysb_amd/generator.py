@@ -118,3 +118,33 @@ def shard_ads(ad_ids, nranks):
     for i, a in enumerate(ad_ids):
         out[ad_shard(a, nranks)].append(i)
     return out
+
+
+def shard_packed(keys, nranks: int, key_len: int = 36):
+    """ysb_ad_shard of n keys of key_len bytes packed back to back (a uint8 array), vectorised:
+    the library's key_hash (zero-padded little-endian words) and key_shard restated in numpy
+    for 10M-ad maps, where one ctypes call per key would take minutes.  Equal to ad_shard
+    key by key (tests/test_generator.py)."""
+    k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, key_len)
+    n = k.shape[0]
+    if nranks <= 1:
+        return np.zeros(n, dtype=np.uint32)
+    nw = (key_len + 3) // 4
+    pad = np.zeros((n, 4 * nw), dtype=np.uint8)
+    pad[:, :key_len] = k
+    w = pad.view("<u4")
+    with np.errstate(over="ignore"):
+        h = np.full(n, (0x811C9DC5 ^ ((key_len * 0x9E3779B1) & 0xFFFFFFFF)) & 0xFFFFFFFF, dtype=np.uint32)
+        for j in range(nw):
+            h = (h ^ w[:, j]) * np.uint32(0x01000193)
+            h ^= h >> np.uint32(15)
+        h ^= h >> np.uint32(16)
+        h *= np.uint32(0x85EBCA6B)
+        h ^= h >> np.uint32(13)
+        h *= np.uint32(0xC2B2AE35)
+        h ^= h >> np.uint32(16)
+        z = h.astype(np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return (((z >> np.uint64(32)) * np.uint64(nranks)) >> np.uint64(32)).astype(np.uint32)

@@ -62,6 +62,20 @@ def table_rows(table, ring_lo, c_off=0):
     return {(int(c) + c_off, int(b)): int(t[c, s]) for c, s, b in zip(cs, ss, buckets)}
 
 
+def exchange_plan(slot_max, nranks: int):
+    """(slots, width) every rank derives from the all-reduced per-bucket maxima of its
+    pending counts (ysb_exchange_plan, the library's own host function): the ring slots
+    holding a count on some rank, ascending, and the cell width in bytes (1, 4 or 8) whose
+    sum over nranks cannot wrap."""
+    m = np.ascontiguousarray(slot_max, dtype=np.uint64)
+    W = m.size
+    slots = np.zeros(max(W, 1), dtype=np.uint32)
+    n, w = C.c_uint32(), C.c_uint32()
+    check(lib().ysb_exchange_plan(C.c_void_p(m.ctypes.data), W, nranks, C.c_void_p(slots.ctypes.data),
+                                  C.byref(n), C.byref(w)))
+    return slots[:n.value].copy(), w.value
+
+
 def ring_agreement(bases):
     """The common ring base the ranks agree on (ysb_group_init / the first exchange): the
     smallest base any rank holds (None: no rank has one yet)."""

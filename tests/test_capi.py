@@ -51,10 +51,12 @@ STRUCT_PROBE = r"""
 #include "ysb_hip.h"
 #define P(T, F) printf(#T "." #F " %zu\n", offsetof(T, F));
 int main(void) {
-  printf("ysb_config %zu\nysb_stats %zu\nysb_count %zu\nysb_gen_params %zu\n", sizeof(ysb_config),
-         sizeof(ysb_stats), sizeof(ysb_count), sizeof(ysb_gen_params));
+  printf("ysb_config %zu\nysb_stats %zu\nysb_count %zu\nysb_gen_params %zu\nysb_exchange_info %zu\n",
+         sizeof(ysb_config), sizeof(ysb_stats), sizeof(ysb_count), sizeof(ysb_gen_params), sizeof(ysb_exchange_info));
   P(ysb_config, flags) P(ysb_config, overflow_capacity) P(ysb_count, window_ms) P(ysb_count, count)
   P(ysb_gen_params, ad_subset) P(ysb_gen_params, n_ad_subset) P(ysb_stats, batches) P(ysb_stats, deferred)
+  P(ysb_stats, foreign_shard) P(ysb_exchange_info, ms) P(ysb_exchange_info, last_width)
+  P(ysb_exchange_info, full_ring_bytes)
   return 0;
 }
 """
@@ -76,11 +78,15 @@ def test_struct_layouts_match_ctypes(tmp_path):
     assert int(got["ysb_gen_params.ad_subset"]) == _lib.YsbGenParams.ad_subset.offset
     assert int(got["ysb_stats.batches"]) == _lib.YsbStats.batches.offset
     assert int(got["ysb_stats.deferred"]) == _lib.YsbStats.deferred.offset
+    assert int(got["ysb_stats.foreign_shard"]) == _lib.YsbStats.foreign_shard.offset
+    assert int(got["ysb_exchange_info"]) == C.sizeof(_lib.YsbExchangeInfo)
+    for f in ("ms", "last_width", "full_ring_bytes"):
+        assert int(got["ysb_exchange_info." + f]) == getattr(_lib.YsbExchangeInfo, f).offset
 
 
 def test_abi_version_and_defaults():
     L = _lib.lib()
-    assert L.ysb_abi_version() == 1
+    assert L.ysb_abi_version() == 2
     cfg = _lib.YsbConfig()
     L.ysb_config_default(C.byref(cfg))
     assert cfg.time_divisor_ms == 10000          # CampaignProcessorCommon.java:28
@@ -136,3 +142,30 @@ def test_config_flags_match_the_header():
         assert getattr(_lib, name) == v, name
     vals = list(flags.values())
     assert all(v & (v - 1) == 0 for v in vals) and len(set(vals)) == len(vals)
+
+
+def test_exchange_plan_width_and_slots():
+    """ysb_exchange_plan: the touched slots ascending, and the narrowest cell width whose sum
+    over the ranks cannot wrap (RCCL has no 16-bit integer type: 1, 4 or 8 bytes)."""
+    import numpy as np
+    from ysb_amd import YsbError, exchange_plan
+    m = np.zeros(64, dtype=np.uint64)
+    slots, w = exchange_plan(m, 8)
+    assert slots.size == 0 and w == 1
+    m[[3, 9, 63]] = [1, 31, 2]
+    slots, w = exchange_plan(m, 8)
+    assert slots.tolist() == [3, 9, 63] and w == 1          # 8 * 31 = 248 <= 255
+    assert exchange_plan(m, 9)[1] == 4                      # 9 * 31 = 279
+    m[9] = (1 << 32) // 8 - 1
+    assert exchange_plan(m, 8)[1] == 4
+    m[9] = 1 << 32
+    assert exchange_plan(m, 8)[1] == 8
+    m[9] = (1 << 63)
+    with pytest.raises(YsbError):
+        exchange_plan(m, 8)
+
+
+def test_load_shard_arguments_checked_without_gpu():
+    """The sharded loader rejects a bad shard before touching a device."""
+    L = _lib.lib()
+    assert L.ysb_load_ad_map_shard(None, None, None, None, 0, 0, 1) == -1

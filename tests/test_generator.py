@@ -174,3 +174,17 @@ def test_variant_lines_decode_to_the_same_events(variant):
         assert json.loads(x) == json.loads(y)
     if variant & 8:
         assert not lb[0].startswith(b'{"user_id"')
+
+
+def test_shard_packed_equals_ad_shard():
+    """The vectorised shard of packed 36-byte ids (bench.py's 10M-ad shards) equals the
+    library's ysb_ad_shard key by key, also for keys of other lengths."""
+    import numpy as np
+    from ysb_amd import ad_shard, shard_packed
+    g = GenParams(seed=3, n_campaigns=500, ads_per_campaign=4)
+    _, ab = g.ids_packed()
+    _, aids = g.ids()
+    for n in (1, 2, 3, 8):
+        assert shard_packed(ab, n).tolist() == [ad_shard(a, n) for a in aids]
+    odd = np.frombuffer(b"".join(b"ad-%05d-x" % i for i in range(300)), dtype=np.uint8)   # 10-byte keys
+    assert shard_packed(odd, 5, key_len=10).tolist() == [ad_shard(b"ad-%05d-x" % i, 5) for i in range(300)]

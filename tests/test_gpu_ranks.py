@@ -108,26 +108,124 @@ def test_one_rank_group_runs_bench_exchange_check():
         assert ctx.ring_range() == (lo + 1, w)
 
 
-def test_sharded_join_table_misses_other_shards_ads():
-    """A rank's sharded table joins exactly its own shard's ads: another rank's events are
-    join misses (dropped, as RedisJoinBolt drops an unknown ad), its own all join."""
+def test_sharded_join_table_classifies_foreign_shard_views():
+    """A rank's sharded table (ysb_load_ad_map_shard) joins exactly its own shard's ads.
+    Another rank's events are views of a foreign shard: counted as foreign_shard, not as
+    join misses (mis-routed input), and with strict=True ysb_sync fails with YSB_ERR_DATA.
+    An ad of the rank's own shard that the map lacks stays a join miss, as RedisJoinBolt
+    drops an unknown ad (AdvertisingTopologyNative.java:465-467)."""
+    from ysb_amd import YsbError, ad_shard
     world = 4
     n = 200_000
     g0, aids, camp = rank_params(world, 0)
     g1, _, _ = rank_params(world, 1)
+    for strict in (False, True):
+        with YsbContext(device=0, n_campaigns=100, window_ring=1024, ring_base_bucket=g0.c.t0_ms // 10000 - 128,
+                        max_batch_bytes=16 << 20, max_batch_events=1 << 16, strict=strict) as ctx:
+            ctx.load_ad_map(aids, camp, shard=(0, world))
+            cap = n * g0.max_line_bytes()
+            d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
+            nb = ctx.gen_events_device(g1, 0, n, d_b, cap, d_o)   # rank 1's events
+            ctx.submit_device_segments([(d_b, nb, d_o, n)])
+            if strict:
+                with pytest.raises(YsbError) as e:
+                    ctx.sync()
+                assert e.value.code == -8 and "another rank" in str(e.value)
+            else:
+                ctx.sync()
+            st = ctx.stats()
+            assert st["joined"] == 0 and st["join_misses"] == 0
+            assert st["foreign_shard"] == st["views"] > 0
+            ctx.reset()
+            nb = ctx.gen_events_device(g0, 0, n, d_b, cap, d_o)   # its own
+            ctx.submit_device_segments([(d_b, nb, d_o, n)])
+            ctx.sync()
+            st = ctx.stats()
+            assert st["join_misses"] == 0 and st["foreign_shard"] == 0 and st["joined"] == st["views"] > 0
+    # a map without some of shard 0's own ads: their views are real join misses
+    mine = [i for i, a in enumerate(aids) if ad_shard(a, world) == 0]
+    drop = set(mine[:5])
+    keep = [i for i in range(len(aids)) if i not in drop]
     with YsbContext(device=0, n_campaigns=100, window_ring=1024, ring_base_bucket=g0.c.t0_ms // 10000 - 128,
-                    max_batch_bytes=16 << 20, max_batch_events=1 << 16) as ctx:
-        ctx.load_ad_map(aids, camp, shard=(0, world))
-        cap = n * g0.max_line_bytes()
+                    max_batch_bytes=16 << 20, max_batch_events=1 << 16, strict=True) as ctx:
+        ctx.load_ad_map([aids[i] for i in keep], [camp[i] for i in keep], shard=(0, world))
+        raw, offs = g0.events_host(0, 60_000)
+        ctx.submit(raw, offs)
+        ctx.sync()   # real misses are not an error in strict mode (the reference drops them)
+        st = ctx.stats()
+    from oracle import oracle
+    rows, ost = oracle.run(oracle.AdMap([aids[i] for i in keep], [camp[i] for i in keep]), raw, offs)
+    assert st["foreign_shard"] == 0 and st["join_misses"] == ost["join_misses"] > 0
+    assert st["joined"] == ost["joined"]
+
+
+def _config3_rank(n_campaigns=200_000):
+    g = GenParams(seed=42, n_campaigns=n_campaigns, ads_per_campaign=10, events_per_sec=100_000)
+    _, ab = g.ids_packed()
+    return g, ab
+
+
+def test_one_rank_group_range_exchange_config3_sized():
+    """The range-limited exchange on a real (one-rank) RCCL group at configs[2]-like size
+    (200k campaigns x 10 ads, W = 128, record mode with the u8 delta ring): only the buckets
+    holding counts travel, as 1-byte cells while nranks x max <= 255; the owned table then
+    equals the generator truth (rows and linear checksums), nothing stays pending, and the
+    exchange's accounting reports what moved."""
+    from ysb_amd import table_rows
+    g, ab = _config3_rank()
+    n = 4_000_000
+    with YsbContext(device=0, n_campaigns=200_000, window_ring=128, max_batch_bytes=1 << 20,
+                    max_batch_events=1 << 12, record_count=True) as ctx:
+        ctx.load_ad_map_packed(ab, g.ad_campaign_index_array())
+        ctx.group_init(0, 1, YsbContext.group_unique_id())
+        cap = n * g.max_line_bytes()
         d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
-        nb = ctx.gen_events_device(g1, 0, n, d_b, cap, d_o)   # rank 1's events
-        ctx.submit_device_segments([(d_b, nb, d_o, n)])
-        ctx.sync()
+        nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+        for k in range(3):   # three steps: count, exchange (the ring agreed at the first)
+            ctx.submit_device_segments([(d_b, nb, d_o, n)])
+            ctx.group_reduce_scatter()
+            x = ctx.exchange_info()
+            assert x["exchanges"] == k + 1
+            assert x["last_width"] == 1, x            # ~0.2 views per cell per step
+            assert 0 < x["last_buckets"] <= 128
+        per_step = 200_000 * x["last_buckets"]
+        assert x["bytes"] == 3 * per_step and x["ms"] > 0
+        assert x["full_ring_bytes"] == 200_000 * 128 * 8
+        _, _, nrec = ctx.path_time()
+        assert nrec == 3                               # every launch in record mode
+        for _ in range(3):
+            ctx.truth_accumulate(g, 0, n)
+        truth, lo = ctx.truth_read()
+        expected = table_rows(truth, lo)
+        got = ctx.drain_buckets()
+        assert got == expected
+        assert ctx.checksum("owned")[0] == ctx.checksum("truth")[0]
+        assert ctx.checksum("pending") == [0]
         st = ctx.stats()
-        assert st["joined"] == 0 and st["join_misses"] == st["views"] > 0
-        ctx.reset()
-        nb = ctx.gen_events_device(g0, 0, n, d_b, cap, d_o)   # its own
-        ctx.submit_device_segments([(d_b, nb, d_o, n)])
-        ctx.sync()
-        st = ctx.stats()
-        assert st["join_misses"] == 0 and st["joined"] == st["views"] > 0
+        assert st["overflow_dropped"] == 0 and st["out_of_ring"] == 0
+
+
+def test_one_rank_group_ring_advance_to_lower_base_moves_to_side_list():
+    """After ysb_group_init, ring_advance is a collective; moving the ring to a LOWER base
+    runs the branch agree_ring takes on a later-starting rank (move_ring): the buckets the
+    new range no longer holds go to the exact side list, and the drain (owned table +
+    pending ring + side list) still equals the oracle."""
+    from oracle import oracle
+    g, aids, camp = rank_params(1, 0, rate=1000)
+    raw, offs = g.events_host(0, 300_000)   # 300 s of event time: ~30 buckets
+    rows, _ = oracle.run(oracle.AdMap(aids, camp), raw, offs)
+    with YsbContext(device=0, n_campaigns=100, window_ring=32, max_batch_bytes=256 << 20,
+                    max_batch_events=1 << 20) as ctx:
+        ctx.load_ad_map(aids, camp)
+        ctx.group_init(0, 1, YsbContext.group_unique_id())
+        ctx.submit(raw, offs)
+        ctx.group_reduce_scatter()
+        lo, w = ctx.ring_range()
+        ctx.ring_advance(lo - 10)                 # buckets [lo + 22, lo + 32) leave the ring
+        assert ctx.ring_range() == (lo - 10, w)
+        got = ctx.drain_buckets()
+        assert got == rows
+        ctx.submit(raw, offs)                     # counts after the move: ring + side again
+        ctx.group_reduce_scatter()
+        got = ctx.drain_buckets()
+        assert got == {k: 2 * v for k, v in rows.items()}

@@ -134,11 +134,10 @@ def test_bucket_table_sparse_and_misses(huge_map, record):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("fold_events", [None, "50000"])
 def test_record_delta_ring_folds(big_map, monkeypatch, fold_events):
-    """Record mode counts into a u32 delta ring folded into the u64 ring before anything
-    reads it and before 2^32 events could have been counted into it.  Eight launches
-    back to back with a stats read and a drain-with-clear in between -- with the default
-    bound (folds only at the drains) and with a bound of 50k events (a fold before every
-    launch) -- equal the oracle."""
+    """Record mode counts into a saturating u8 delta ring folded into the u64 ring before
+    anything reads it.  Eight launches back to back with a stats read and a drain-with-clear
+    in between -- with no bound (folds only at the drains) and with the test hook's bound of
+    50k events (a fold before every launch) -- equal the oracle."""
     if fold_events:
         monkeypatch.setenv("YSB_DELTA_FOLD_EVENTS", fold_events)
     g, aids, raw, offs = big_map
@@ -175,3 +174,26 @@ def test_record_delta_ring_folds(big_map, monkeypatch, fold_events):
         assert ctx.path_time()[2] == 8
     exp, _ = oracle.run(oracle.AdMap(aids, camp), raw, offs)
     assert got == exp
+
+
+@pytest.mark.timeout(300)
+def test_record_delta_saturates_into_u64_ring(big_map):
+    """Hot cells: every view in 50 campaigns (~125 views per cell per launch), six launches
+    back to back without a read in between -- the u8 delta cells pass 255 within two or three
+    launches and hand their sums to the u64 ring (ysb_count.hip add16).  Exact vs six times
+    the oracle."""
+    g, aids, raw, offs = big_map
+    camp = [i % 50 for i in range(len(aids))]
+    exp, _ = oracle.run(oracle.AdMap(aids, camp), raw, offs)
+    with YsbContext(n_campaigns=200_000, window_ring=16, record_count=True,
+                    max_batch_bytes=raw.size + 64, max_batch_events=offs.size + 1) as ctx:
+        ctx.load_ad_map(aids, camp)
+        d_b, d_o = ctx.device_alloc(raw.size + 64), ctx.device_alloc(4 * offs.size + 64)
+        ctx.h2d(d_b, raw)
+        ctx.h2d(d_o, offs)
+        for _ in range(6):
+            ctx.submit_device(d_b, raw.size, d_o, offs.size)
+        rows = ctx.drain_buckets()
+        assert ctx.path_time()[2] == 6
+    assert max(exp.values()) > 255 // 6 * 2
+    assert rows == {k: 6 * v for k, v in exp.items()}

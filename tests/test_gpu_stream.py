@@ -192,7 +192,9 @@ def test_side_map_spills_to_host_between_launches():
 def test_sharded_streaming_n_contexts_exact(n):
     """configs[4] rehearsal on one GPU: n contexts (one per would-be GPU), each with its
     own pinned double-buffered slots fed by its ad_id shard's event stream (skew and late
-    events), one global watermark; the deltas equal the batch path's counts exactly."""
+    events), one global watermark; the deltas equal the CPU oracle's counts over every
+    event the producers made (oracle/ysb_oracle.c: an independent restatement, not the
+    HIP batch path)."""
     from ysb_amd import shard_ads
     from ysb_amd.stream import ShardedStreamingOperator
     base = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=100_000)
@@ -224,15 +226,14 @@ def test_sharded_streaming_n_contexts_exact(n):
             op.fill_with(r, producer(r))
         op.tick()
     op.close()
+    from oracle import oracle
+    am = oracle.AdMap(aids, base.ad_campaign_index())
     ref = {}
     for r in range(n):
         raw, offs = gens[r].events_host(0, produced[r])
-        with YsbContext(n_campaigns=100, window_ring=64, max_batch_bytes=raw.size + 64,
-                        max_batch_events=offs.size + 1) as c2:
-            c2.load_ad_map(aids, base.ad_campaign_index())
-            c2.submit(raw, offs)
-            for k, v in c2.drain_buckets().items():
-                ref[k] = ref.get(k, 0) + v
+        rows, _ = oracle.run(am, raw, offs)
+        for k, v in rows.items():
+            ref[k] = ref.get(k, 0) + v
     for c in ctxs:
         c.close()
     assert op.totals == ref

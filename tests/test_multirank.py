@@ -187,3 +187,47 @@ def test_streaming_ranks_share_one_watermark(world, tmp_path):
     assert len(set(tuple(r["closed"]) for r in res)) == 1 and len(res[0]["closed"]) >= 2
     assert len(set(r["watermark"] for r in res)) == 1
     assert len(set(r["flushes"] for r in res)) == 1
+
+
+def _range_ranks(world, tmp_path, *extra):
+    port = free_port()
+    procs, outs = [], []
+    for r in range(world):
+        out = tmp_path / ("x%d.json" % r)
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "exchange_worker.py"), str(out)] +
+                                      list(extra), env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+        outs.append(out)
+    logs = [p.communicate(timeout=300)[0].decode(errors="replace") for p in procs]
+    for p, lg in zip(procs, logs):
+        assert p.returncode == 0, lg[-3000:]
+    return [json.load(open(o)) for o in outs]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_range_limited_exchange_250k_campaigns(world, tmp_path):
+    """ysb_group_reduce_scatter's protocol (per-bucket maxima -> all-reduce(max) ->
+    ysb_exchange_plan -> pack only the touched buckets in the narrowest width ->
+    reduce-scatter -> unpack), gloo standing in for RCCL, at configs[2]-like size (250k
+    campaigns, 500k ads sharded by ad_id hash), two exchanges: the owners' rows equal the
+    truth summed over ranks, nothing stays pending, and each exchange moved 1-byte cells of
+    the touched buckets only -- a small fraction of the whole u64 ring."""
+    res = _range_ranks(world, tmp_path)
+    mism, outside, cells = res[0]["exchange"]
+    assert mism == 0 and outside == 0 and cells > 0
+    for rr in res[0]["ranks_rounds"]:
+        for rnd in rr:
+            assert rnd["pending_left"] == 0 and rnd["width"] == 1
+            assert 0 < rnd["buckets"] < 64 and rnd["bytes"] * 16 < res[0]["full_ring_bytes"]
+    # every rank made the same plan (the all-reduced maxima)
+    assert len({json.dumps([(r["buckets"], r["width"]) for r in rr]) for rr in res[0]["ranks_rounds"]}) == 1
+
+
+def test_range_limited_exchange_wide_cells(tmp_path):
+    """Heavy cells (every view in 7 campaigns, hundreds per cell): the plan widens the cells
+    to 4 bytes so the sum over the ranks cannot wrap; still exact."""
+    res = _range_ranks(2, tmp_path, "20000", "2")
+    mism, outside, cells = res[0]["exchange"]
+    assert mism == 0 and outside == 0 and cells > 0
+    assert {rnd["width"] for rr in res[0]["ranks_rounds"] for rnd in rr} == {4}

@@ -423,28 +423,29 @@ def stream_sharded(args):
             log("stream_sharded: %.0f s, %d events, %d flushes" % (last_log - wall0 / 1000.0, sum(produced),
                                                                     op.flushes))
     op.close()
-    ref = {}
+    # the reference counts: the generator truth of every event each producer made, straight
+    # from the RNG (ysb_truth_accumulate: no bytes, no parsing -- independent of the path
+    # under test), in a ring wide enough for the late events (<= 60 s, core.clj:166-174)
+    from ysb_amd import table_rows
+    ref, outside = {}, 0
     for r in range(n):
-        with YsbContext(n_campaigns=100, window_ring=64) as c2:
-            c2.load_ad_map(aids, base.ad_campaign_index())
-            seg = 10_000_000
-            cap = seg * gens[r].max_line_bytes()
-            d_b, d_o = c2.device_alloc(cap), c2.device_alloc(4 * seg + 64)
-            for f in range(0, produced[r], seg):
-                m = min(seg, produced[r] - f)
-                nb = c2.gen_events_device(gens[r], f, m, d_b, cap, d_o)
-                c2.submit_device(d_b, nb, d_o, m)
-                c2.sync()
-            for k, v in c2.drain_buckets().items():
+        with YsbContext(n_campaigns=100, window_ring=64, ring_base_bucket=t0_ms // 10000 - 8) as c2:
+            c2.truth_accumulate(gens[r], 0, produced[r])
+            truth, lo = c2.truth_read()
+            _, ttotal, _ = c2.truth_compare()
+            outside += ttotal - int(truth.sum())
+            for k, v in table_rows(truth, lo).items():
                 ref[k] = ref.get(k, 0) + v
     for c in ctxs:
         c.close()
+    lat = op.latency_summary()
     return {"config": "configs[4] with %d shards (%d GPU(s) visible): real-time producers, %d events/s in all, "
-                      "skew +-50 ms, late p=1e-5 (core.clj:166-174); %d ms ticks, one global watermark"
-                      % (n, ndev.value, rate, args.batch_ms),
+                      "skew +-50 ms, late p=1e-5 (core.clj:166-174); %d ms ticks, one global watermark; %d s"
+                      % (n, ndev.value, rate, args.batch_ms, args.seconds),
             "shards": n, "devices": ndev.value, "events": op.events, "batches": op.batches, "flushes": op.flushes,
-            "window_close_latency": op.latency_summary(), "open_at_end": op.open_at_end,
-            "exact_vs_batch_path": op.totals == ref, "rows": len(ref)}
+            "window_close_latency": lat, "open_at_end": op.open_at_end,
+            "exact_vs_generator_truth": op.totals == ref and outside == 0, "rows": len(ref),
+            "truth_outside_ring": outside}
 
 
 def main():
