@@ -482,19 +482,13 @@ static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         while (cslots < 2 * keys36.size()) cslots <<= 1;
     }
     const u32 unit = buckets ? CB_WORDS : CSLOT_WORDS;
-    std::vector<u32> kw, cv;   // bucket layout: the keys packed (uuid_pack), their campaigns
-    u64 n_packed = 0;
+    std::vector<u32> kw, cv;   // bucket layout: the keys as words, their campaigns
     if (buckets) {
-        kw.resize(keys36.size() * CB_KEYW);
+        kw.resize(keys36.size() * CKEY_WORDS);
         cv.resize(keys36.size());
         for (size_t i = 0; i < keys36.size(); ++i) {
-            // a 36-byte key that is not a canonical UUID string stays out of the packed
-            // table: its lookups miss there and take the general table (exact)
-            if (!uuid_pack(keys36[i].first.data(), &kw[n_packed * CB_KEYW])) {
-                partial = true;
-                continue;
-            }
-            cv[n_packed++] = keys36[i].second;
+            std::memcpy(&kw[i * CKEY_WORDS], keys36[i].first.data(), 36);
+            cv[i] = keys36[i].second;
         }
     }
     std::vector<u32> ct;
@@ -515,7 +509,7 @@ static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         const u32 cm = (u32)(cslots - 1);
         bool ok = true;
         if (buckets) {
-            const u64 homeless = cuckoo_build_buckets(kw.data(), cv.data(), n_packed, cs, cslots, seed, partial,
+            const u64 homeless = cuckoo_build_buckets(kw.data(), cv.data(), keys36.size(), cs, cslots, seed, partial,
                                                       ct.data());
             ok = homeless == 0;
             if (ok || partial) break;

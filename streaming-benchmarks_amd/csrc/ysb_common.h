@@ -330,52 +330,14 @@ YSB_HD u32 key_hash(const u32* w, u32 len) {
 #define YSB_CSLOT_WORDS 16
 #endif
 enum : u32 { CSLOT_WORDS = YSB_CSLOT_WORDS, CKEY_WORDS = 9, CSLOT_CAMP = 9, CSLOT_Q = YSB_CSLOT_WORDS / 4 };
-// HBM-resident tables (beyond the L2s: configs[2]'s 10M ads) use BUCKETS instead: 64 B =
-// 3 entries of [4 key words, campaign] at a 5-word stride (+ 1 spare word), the key being
-// the 36-byte ad_id packed into 128 bits (uuid_pack: java.util.UUID.toString()'s canonical
-// lower-case 8-4-4-4-12 form, the only form core.clj:31-32 writes; any other 36-byte key
-// stays out of this table and its lookups take the general table).  A key goes to its
-// first bucket while that has a free entry, to its second only when the first is full
-// (cuckoo eviction keeps a full bucket full), so a lookup reads ONE 64-B line -- half the
-// HBM bytes of the earlier 128-B buckets of raw 36-byte keys -- and the second bucket only
-// when the key is not in a FULL first one (~0.1 % of keys at 2 buckets per key).
-enum : u32 { CB_KEYW = 4, CB_WORDS = 16, CB_ENTRIES = 3, CB_STRIDE = 5, CB_Q = CB_WORDS / 4 };
-
-// 4 hex digits of a 36-byte UUID word as nibbles (one per byte; bytes outside `hexmask`
-// give 0); bad |= nonzero unless every byte of the mask is [0-9a-f] (re-encoding the
-// nibble must give the byte back: upper-case hex, 'g'.. and the rest all fail).
-YSB_HD u32 hex_nibbles(u32 w, u32 hexmask, u32& bad) {
-    const u32 n = (w & 0x0F0F0F0Fu) + ((w >> 6) & 0x01010101u) * 9u;   // per byte <= 24: no carries
-    const u32 ge10 = ((n + 0x06060606u) >> 4) & 0x01010101u;           // n >= 10
-    const u32 enc = n + 0x30303030u + ge10 * 0x27u;                     // '0' + n, or 'a' + n - 10
-    bad |= ((enc ^ w) | (n & 0xF0F0F0F0u)) & hexmask;
-    return n & hexmask & 0x0F0F0F0Fu;
-}
-// 4 nibble bytes b0..b3 -> b0 | b1 << 4 | b2 << 8 | b3 << 12
-YSB_HD u32 nib16(u32 n) {
-    const u32 t = (n | (n >> 4)) & 0x00FF00FFu;
-    return (t | (t >> 8)) & 0xFFFFu;
-}
-// The 36 bytes w[0..8] (little-endian words) -> 128 bits k[0..3], injective on canonical
-// UUID strings; false (k undefined) for any other 36 bytes.  Dashes sit in bytes 8, 13,
-// 18, 23: byte 0 of w2, 1 of w3, 2 of w4, 3 of w5.
-YSB_HD bool uuid_pack(const u32* w, u32* k) {
-    u32 bad = 0;
-    const u32 f0 = nib16(hex_nibbles(w[0], 0xFFFFFFFFu, bad)), f1 = nib16(hex_nibbles(w[1], 0xFFFFFFFFu, bad));
-    const u32 f2 = nib16(hex_nibbles(w[2], 0xFFFFFF00u, bad)), f3 = nib16(hex_nibbles(w[3], 0xFFFF00FFu, bad));
-    const u32 f4 = nib16(hex_nibbles(w[4], 0xFF00FFFFu, bad)), f5 = nib16(hex_nibbles(w[5], 0x00FFFFFFu, bad));
-    const u32 f6 = nib16(hex_nibbles(w[6], 0xFFFFFFFFu, bad)), f7 = nib16(hex_nibbles(w[7], 0xFFFFFFFFu, bad));
-    const u32 f8 = nib16(hex_nibbles(w[8], 0xFFFFFFFFu, bad));
-    bad |= ((w[2] & 0xFFu) ^ 0x2Du) | ((w[3] & 0xFF00u) ^ 0x2D00u) | ((w[4] & 0xFF0000u) ^ 0x2D0000u) |
-           ((w[5] & 0xFF000000u) ^ 0x2D000000u);
-    const u32 g2 = f2 >> 4, g3 = (f3 & 0xFu) | ((f3 >> 8) << 4), g4 = (f4 & 0xFFu) | ((f4 >> 12) << 8),
-              g5 = f5 & 0xFFFu;   // 12 bits each
-    k[0] = f0 | (f1 << 16);
-    k[1] = f6 | (f7 << 16);
-    k[2] = f8 | (g2 << 16) | ((g3 & 0xFu) << 28);
-    k[3] = (g3 >> 4) | (g4 << 8) | (g5 << 20);
-    return bad == 0u;
-}
+// HBM-resident tables (beyond the L2s: configs[2]'s 10M ads) use BUCKETS instead: 128 B =
+// 3 entries of [9 key words, campaign] at a 10-word stride (+ 2 spare words).  A key goes
+// to its first bucket while that has a free entry, to its second only when the first is
+// full (cuckoo eviction keeps a full bucket full), so a lookup reads one 128-B line and
+// reads the second bucket only when the key is not in a FULL first bucket -- at 2 buckets
+// per key ~0.1 % of keys instead of the ~8 % a one-key slot table leaves in its second
+// slot, each of which cost the whole wave a dependent HBM round trip.
+enum : u32 { CB_WORDS = 32, CB_ENTRIES = 3, CB_STRIDE = 10, CB_Q = CB_WORDS / 4 };
 
 struct CuckooSeed {
     u32 s[CKEY_WORDS];   // additive salts of the XOR fold
@@ -404,24 +366,8 @@ YSB_HD void cuckoo_slots36(const u32* w, const CuckooSeed& cs, u32 mask, u32* a,
     *b = bb == *a ? ((bb + 1) & mask) : bb;
 }
 
-// The two buckets of a packed UUID key (the same fold as cuckoo_slots36, over 4 words).
-YSB_HD void cuckoo_slots_k4(const u32* w, const CuckooSeed& cs, u32 mask, u32* a, u32* b) {
-    const u32 R[CB_KEYW] = {1, 11, 21, 31};
-    u32 x = 0, y = 0;
-#pragma unroll
-    for (u32 k = 0; k < CB_KEYW; ++k) {
-        x ^= rotl32(w[k] + cs.s[k], R[k]);
-        y += w[k] ^ cs.t[k];
-    }
-    const u32 ha = fmix32(x ^ cs.fa);
-    const u32 hb = fmix32(y ^ cs.fb ^ rotl32(x, 16));
-    *a = ha & mask;
-    const u32 bb = hb & mask;
-    *b = bb == *a ? ((bb + 1) & mask) : bb;
-}
-
 #if !defined(__HIP_DEVICE_COMPILE__)
-// Host build of the bucket-layout table (ysb_load_ad_map): key i (CB_KEYW packed words) with campaign
+// Host build of the bucket-layout table (ysb_load_ad_map): key i (9 words) with campaign
 // camp[i] into nb buckets (ct: nb * CB_WORDS words, cleared here).  A key goes to its
 // first bucket while that has a free entry, else to its second; with both full it takes a
 // random entry of the bucket it is headed for (which so stays full) and the evicted key
@@ -432,15 +378,15 @@ static inline u64 cuckoo_build_buckets(const u32* keys, const u32* camp, u64 n, 
                                        u64 seed, bool keep_going, u32* ct) {
     for (u64 i = 0; i < nb * CB_WORDS; ++i) ct[i] = 0;
     for (u64 b = 0; b < nb; ++b)
-        for (u32 e = 0; e < CB_ENTRIES; ++e) ct[b * CB_WORDS + e * CB_STRIDE + CB_KEYW] = EMPTY_SLOT;
+        for (u32 e = 0; e < CB_ENTRIES; ++e) ct[b * CB_WORDS + e * CB_STRIDE + CKEY_WORDS] = EMPTY_SLOT;
     const u32 mask = (u32)(nb - 1);
     u64 rng = seed, homeless = 0;
     for (u64 i = 0; i < n; ++i) {
-        u32 k[CB_KEYW];
-        for (u32 j = 0; j < CB_KEYW; ++j) k[j] = keys[i * CB_KEYW + j];
+        u32 k[CKEY_WORDS];
+        for (u32 j = 0; j < CKEY_WORDS; ++j) k[j] = keys[i * CKEY_WORDS + j];
         u32 c = camp[i];
         u32 a, b;
-        cuckoo_slots_k4(k, cs, mask, &a, &b);
+        cuckoo_slots36(k, cs, mask, &a, &b);
         u32 pos = a;
         bool placed = false;
         for (int kicks = 0; kicks <= 500 && !placed; ++kicks) {
@@ -448,24 +394,24 @@ static inline u64 cuckoo_build_buckets(const u32* keys, const u32* camp, u64 n, 
             for (int ci = 0; ci < (kicks == 0 ? 2 : 1) && !placed; ++ci) {
                 u32* bk = &ct[(u64)cands[ci] * CB_WORDS];
                 for (u32 e = 0; e < CB_ENTRIES && !placed; ++e)
-                    if (bk[e * CB_STRIDE + CB_KEYW] == EMPTY_SLOT) {
-                        for (u32 j = 0; j < CB_KEYW; ++j) bk[e * CB_STRIDE + j] = k[j];
-                        bk[e * CB_STRIDE + CB_KEYW] = c;
+                    if (bk[e * CB_STRIDE + CKEY_WORDS] == EMPTY_SLOT) {
+                        for (u32 j = 0; j < CKEY_WORDS; ++j) bk[e * CB_STRIDE + j] = k[j];
+                        bk[e * CB_STRIDE + CKEY_WORDS] = c;
                         placed = true;
                     }
             }
             if (placed) break;
             rng = mix64(rng + 1);
             u32* en = &ct[(u64)pos * CB_WORDS + (u32)(rng % CB_ENTRIES) * CB_STRIDE];
-            for (u32 j = 0; j < CB_KEYW; ++j) {
+            for (u32 j = 0; j < CKEY_WORDS; ++j) {
                 const u32 t = en[j];
                 en[j] = k[j];
                 k[j] = t;
             }
-            const u32 oc = en[CB_KEYW];
-            en[CB_KEYW] = c;
+            const u32 oc = en[CKEY_WORDS];
+            en[CKEY_WORDS] = c;
             c = oc;
-            cuckoo_slots_k4(k, cs, mask, &a, &b);
+            cuckoo_slots36(k, cs, mask, &a, &b);
             pos = (pos == a) ? b : a;   // the evicted key's other bucket
         }
         if (!placed) {
@@ -480,15 +426,15 @@ static inline u64 cuckoo_build_buckets(const u32* keys, const u32* camp, u64 n, 
 // bucket after a miss in a full first one): the campaign, or EMPTY_SLOT.
 static inline u32 cuckoo_lookup_buckets(const u32* ct, u64 nb, const CuckooSeed& cs, const u32* k) {
     u32 a, b;
-    cuckoo_slots_k4(k, cs, (u32)(nb - 1), &a, &b);
+    cuckoo_slots36(k, cs, (u32)(nb - 1), &a, &b);
     for (int round = 0; round < 2; ++round) {
         const u32* bk = &ct[(u64)(round ? b : a) * CB_WORDS];
         bool full = true;
         for (u32 e = 0; e < CB_ENTRIES; ++e) {
-            const u32 c = bk[e * CB_STRIDE + CB_KEYW];
+            const u32 c = bk[e * CB_STRIDE + CKEY_WORDS];
             if (c == EMPTY_SLOT) { full = false; continue; }
             bool eq = true;
-            for (u32 j = 0; j < CB_KEYW; ++j) eq &= bk[e * CB_STRIDE + j] == k[j];
+            for (u32 j = 0; j < CKEY_WORDS; ++j) eq &= bk[e * CB_STRIDE + j] == k[j];
             if (eq) return c;
         }
         if (!full) return EMPTY_SLOT;

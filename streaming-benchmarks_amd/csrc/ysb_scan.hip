@@ -1156,7 +1156,7 @@ constexpr int AUX_NT = YSB_AUX_NT;
 #define YSB_SETPRIO 1
 #endif
 
-// The campaign of packed key k in a 64-B bucket (EMPTY_SLOT: not there); full = all three
+// The campaign of key k in a 128-B bucket (EMPTY_SLOT: not there); full = all three
 // entries taken (only then may the key sit in its second bucket)
 __device__ __forceinline__ u32 bucket_find(const uint4 (&q)[CB_Q], const u32* k, bool& full) {
     u32 w[CB_WORDS];
@@ -1173,8 +1173,8 @@ __device__ __forceinline__ u32 bucket_find(const uint4 (&q)[CB_Q], const u32* k,
     for (int e = 0; e < (int)CB_ENTRIES; ++e) {
         u32 d = 0;
 #pragma unroll
-        for (int j = 0; j < (int)CB_KEYW; ++j) d |= w[e * CB_STRIDE + j] ^ k[j];
-        const u32 c = w[e * CB_STRIDE + CB_KEYW];
+        for (int j = 0; j < (int)CKEY_WORDS; ++j) d |= w[e * CB_STRIDE + j] ^ k[j];
+        const u32 c = w[e * CB_STRIDE + CKEY_WORDS];
         if (c == EMPTY_SLOT) full = false;
         else if (d == 0u) found = c;
     }
@@ -1514,8 +1514,6 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
 #pragma unroll
         for (int j = 0; j < (int)CB_Q; ++j) q[j] = a0;
         u32 ib_s = 0;
-        u32 k4[CB_KEYW] = {0u, 0u, 0u, 0u};   // SERIAL: the ad_id packed (uuid_pack)
-        bool packed = false;
 #ifdef YSB_DIAG_NO_PROBE
         if (pend) {   // diagnostic build: the first slot / entry "holds" the key, campaign from its bytes
             a0 = make_uint4(ca.kw[0], ca.kw[1], ca.kw[2], ca.kw[3]);
@@ -1530,18 +1528,12 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         if (pend) {
 #endif
             u32 ia, ib;
+            cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
             if constexpr (SERIAL) {
-                // one 64-B bucket line per probe; an ad_id that is not a canonical UUID string
-                // is in no bucket (its key, if the map has it, only in the general table)
-                packed = uuid_pack(ca.kw, k4);
-                if (packed) {
-                    cuckoo_slots_k4(k4, P.cseed, P.ctable_mask, &ia, &ib);
 #pragma unroll
-                    for (int j = 0; j < (int)CB_Q; ++j) q[j] = ct4[CB_Q * (u64)ia + j];
-                    ib_s = ib;
-                }
+                for (int j = 0; j < (int)CB_Q; ++j) q[j] = ct4[CB_Q * (u64)ia + j];
+                ib_s = ib;
             } else {
-                cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
                 a0 = ct4[CSLOT_Q * (u64)ia]; a1 = ct4[CSLOT_Q * (u64)ia + 1]; a2 = ct4[CSLOT_Q * (u64)ia + 2];
                 b0 = ct4[CSLOT_Q * (u64)ib]; b1 = ct4[CSLOT_Q * (u64)ib + 1]; b2 = ct4[CSLOT_Q * (u64)ib + 2];
             }
@@ -1568,13 +1560,13 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             const u32* k = ca.kw;
             u32 ci;
             if constexpr (SERIAL) {
-                bool full = false;
-                ci = packed ? bucket_find(q, k4, full) : EMPTY_SLOT;
+                bool full;
+                ci = bucket_find(q, k, full);
 #ifndef YSB_DIAG_NO_PROBE2
                 if (ci == EMPTY_SLOT && full) {   // the second bucket
 #pragma unroll
                     for (int j = 0; j < (int)CB_Q; ++j) q[j] = ct4[CB_Q * (u64)ib_s + j];
-                    ci = bucket_find(q, k4, full);
+                    ci = bucket_find(q, k, full);
                 }
 #endif
             } else {

@@ -197,37 +197,3 @@ def test_record_delta_saturates_into_u64_ring(big_map):
         assert ctx.path_time()[2] == 6
     assert max(exp.values()) > 255 // 6 * 2
     assert rows == {k: 6 * v for k, v in exp.items()}
-
-
-@pytest.mark.timeout(300)
-def test_bucket_table_non_canonical_uuid_keys(huge_map):
-    """The HBM-resident table packs canonical (lower-case) UUID keys into 128 bits
-    (uuid_pack); other 36-byte keys -- here every 7th ad id upper-cased, in the map and in
-    the events -- stay out of it and join through the general table.  Lower- and upper-case
-    spellings are different keys (HashMap<String,String> semantics): an event keeps its own
-    spelling's campaign.  Counts equal the oracle's."""
-    g, aids, raw, offs = huge_map
-    camp = g.ad_campaign_index()
-    up = {a: a.upper() for i, a in enumerate(aids) if i % 7 == 0}
-    idx = {a: i for i, a in enumerate(aids)}
-    lower = list(up)[:1000]                                              # + some lower-case spellings too
-    a2 = [up.get(a, a) for a in aids] + lower
-    c2 = list(camp) + [(camp[idx[a]] + 1) % 600_000 for a in lower]
-    data = bytearray(raw.tobytes())
-    for i in range(offs.size):
-        s = int(offs[i]) + 113
-        k = data[s:s + 36].decode()
-        if k in up and i % 3:                        # two thirds of those events spelled upper-case
-            data[s:s + 36] = up[k].encode()
-    raw2 = np.frombuffer(bytes(data), dtype=np.uint8)
-    exp, est = oracle.run(oracle.AdMap(a2, c2), raw2, offs)
-    with YsbContext(n_campaigns=600_000, window_ring=16, record_count=True,
-                    max_batch_bytes=raw2.size + 64, max_batch_events=offs.size + 1) as ctx:
-        ctx.load_ad_map(a2, c2)
-        ctx.submit(raw2, offs)
-        rows = ctx.drain_buckets()
-        st = ctx.stats()
-        assert ctx.launch_info()["hbm_table"] == 1
-    assert st["deferred"] > 0 and rows == exp
-    for k, v in est.items():
-        assert st[k] == v, k
