@@ -24,6 +24,13 @@ namespace ysb {
 int scan_lds_bytes();
 }
 
+// A key order read off a batch's first line (layout 3, learn_layout).
+struct LearnDesc {
+    u32 order[8];
+    u32 n;
+    u32 cp;
+};
+
 struct ysb_ctx {
     int device = 0;
     ysb_config cfg{};
@@ -37,6 +44,7 @@ struct ysb_ctx {
     u64 ctable_slots = 0;      // slots, or buckets when ctable_buckets
     bool ctable_buckets = false; // HBM-resident table: 3-entry 128-B buckets (CB_*), serial probes
     int submit_layout = -1;      // the layout a submit read off its batch's first line (-1: the flags')
+    LearnDesc submit_learn{};    // ... and, layout 3, the key order
     ysb_launch_desc last_launch{};   // the instantiation of the last launch
     u8* h_sample = nullptr;      // pinned: device batches' first-line samples
     u32* h_used = nullptr;       // pinned: the out-of-ring map's fill level after a launch ...
@@ -587,6 +595,12 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     p.probe_serial = c->ctable_buckets ? 1u : 0u;
     p.layout = (c->cfg.flags & YSB_F_FLAT_FIRST) ? 2u : (c->cfg.flags & YSB_F_COMPACT_FIRST) ? 1u : 0u;
     if (c->submit_layout >= 0) p.layout = (u32)c->submit_layout;
+    if (p.layout == 3) {
+        p.learn_code = 0;
+        for (u32 i = 0; i < c->submit_learn.n; ++i) p.learn_code |= c->submit_learn.order[i] << (3 * i);
+        p.learn_n = c->submit_learn.n;
+        p.learn_cp = c->submit_learn.cp;
+    }
     p.n_campaigns = c->cfg.n_campaigns;
     p.counts = c->d_counts;
     p.ring_w = c->cfg.window_ring;
@@ -848,18 +862,64 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     return YSB_OK;
 }
 
-// The JSON layout of a batch's first line: 0 the generator's ({"user_id": "...), 1 compact
-// ({"user_id":"...), 2 anything else (the flat-object tier first).
-static int sniff_layout(const uint8_t* bytes, u64 nbytes, const u32* off, u64 n) {
+// The JSON layout of a batch's first line l[0, len): 0 the generator's (core.clj:90-96), 1
+// the generator's keys in its order as compact JSON, 3 another key order or subset of
+// DeserializeBolt's keys with one consistent spacing (", " / ": " or "," / ":") and plain
+// string values (36 bytes for the three ids) -- d then holds the order for the scan's
+// learned-order instantiation -- and 2 anything else (the flat-object tier first).  Only a
+// choice of instantiation: every instantiation counts every line exactly.
+static int learn_layout(const u8* l, u64 len, u32 require_mask, LearnDesc* d) {
+    static const char* keys[7] = {"user_id", "page_id", "ad_id", "ad_type", "event_type", "event_time", "ip_address"};
+    if (len < 2 || l[0] != '{' || l[1] != '"') return 2;
+    auto plain_end = [&](u64 q) {   // the closing quote of a plain string from q (len: none)
+        while (q < len && l[q] != '"' && l[q] != '\\' && l[q] >= 0x20) ++q;
+        return (q < len && l[q] == '"') ? q : len;
+    };
+    u64 p = 2;
+    int cp = -1;
+    u32 seen = 0, n = 0, order[8] = {0};
+    for (;;) {
+        u64 q = plain_end(p);
+        if (q >= len) return 2;
+        int id = -1;
+        for (int i = 0; i < 7; ++i)
+            if (std::strlen(keys[i]) == q - p && std::memcmp(l + p, keys[i], q - p) == 0) id = i;
+        if (id < 0 || ((seen >> id) & 1u) || n >= 7) return 2;
+        seen |= 1u << id;
+        order[n++] = (u32)id;
+        p = q + 1;
+        int c1;
+        if (p + 2 < len && l[p] == ':' && l[p + 1] == ' ' && l[p + 2] == '"') { c1 = 0; p += 3; }
+        else if (p + 1 < len && l[p] == ':' && l[p + 1] == '"') { c1 = 1; p += 2; }
+        else return 2;
+        if (cp < 0) cp = c1;
+        else if (cp != c1) return 2;
+        q = plain_end(p);
+        if (q >= len || (id <= 2 && q - p != 36)) return 2;
+        p = q + 1;
+        if (p < len && l[p] == '}') break;
+        if (cp == 0 && p + 2 < len && l[p] == ',' && l[p + 1] == ' ' && l[p + 2] == '"') p += 3;
+        else if (cp == 1 && p + 1 < len && l[p] == ',' && l[p + 1] == '"') p += 2;
+        else return 2;
+    }
+    // key index i is bit i of the required-key mask (ysb_scan.hip K_*)
+    if ((seen & require_mask) != require_mask || !((seen >> 2) & 1u) || !((seen >> 4) & 1u) || !((seen >> 5) & 1u))
+        return 2;
+    bool gen_order = n == 7;
+    for (u32 i = 0; i < n; ++i) gen_order &= order[i] == i;
+    if (gen_order) return cp ? 1 : 0;
+    d->n = n;
+    d->cp = (u32)cp;
+    for (u32 i = 0; i < 8; ++i) d->order[i] = order[i];
+    return 3;
+}
+
+// The layout of a host batch from its first line (held in the pinned slot).
+static int sniff_layout(const ysb_ctx* c, const uint8_t* bytes, u64 nbytes, const u32* off, u64 n, LearnDesc* d) {
     const u64 s = off[0];
     const u64 e = n > 1 ? (u64)off[1] : nbytes;
     if (s >= e || e > nbytes) return 0;
-    static const char gen[] = "{\"user_id\": \"";
-    static const char cpt[] = "{\"user_id\":\"";
-    const u64 len = e - s;
-    if (len >= sizeof(gen) - 1 && std::memcmp(bytes + s, gen, sizeof(gen) - 1) == 0) return 0;
-    if (len >= sizeof(cpt) - 1 && std::memcmp(bytes + s, cpt, sizeof(cpt) - 1) == 0) return 1;
-    return 2;
+    return learn_layout(bytes + s, e - s, (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu, d);
 }
 
 // Whether batches pick the scan instantiation from their first line (the default): not
@@ -875,8 +935,8 @@ static bool layout_sampling(const ysb_ctx* c) {
 // on a stream of their own (the caller's contract: a device batch's bytes are complete
 // when it is submitted).  One layout for the launch: the segments' common one, else the
 // flat-object tier first (it takes every layout).
-static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
-    constexpr u32 SAMPLE = 64, STRIDE = 96;
+static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, LearnDesc* d) {
+    constexpr u32 SAMPLE = 288, STRIDE = 16 + SAMPLE;   // a line of the scan's tile capacity
     if (!c->h_sample) {
         HIPCHK(c, hipHostMalloc(&c->h_sample, (u64)MAX_SEGS * STRIDE));
         HIPCHK(c, hipStreamCreateWithFlags(&c->s_aux, hipStreamNonBlocking));
@@ -886,13 +946,14 @@ static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     for (u32 i = 0; i < nseg && n < (u32)MAX_SEGS; ++i) {
         if (!segs[i].n_events) continue;
         const u64 nb = std::min<u64>(segs[i].nbytes, SAMPLE);
-        std::memset(h + (u64)n * STRIDE, 0, STRIDE);
+        std::memset(h + (u64)n * STRIDE, 0, 16);
         HIPCHK(c, hipMemcpyAsync(h + (u64)n * STRIDE, segs[i].d_line_off, segs[i].n_events > 1 ? 8 : 4,
                                  hipMemcpyDeviceToHost, c->s_aux));
         if (nb) HIPCHK(c, hipMemcpyAsync(h + (u64)n * STRIDE + 16, segs[i].d_bytes, nb, hipMemcpyDeviceToHost, c->s_aux));
         ++n;
     }
     HIPCHK(c, hipStreamSynchronize(c->s_aux));
+    const u32 req = (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu;
     int lay = -1;
     n = 0;
     for (u32 i = 0; i < nseg && n < (u32)MAX_SEGS; ++i) {
@@ -903,19 +964,21 @@ static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
         std::memcpy(o, s, 8);
         const u64 end = segs[i].n_events > 1 ? (u64)o[1] : segs[i].nbytes;
         if (o[0] > end || end > segs[i].nbytes) return 0;   // bad offsets: the scan defers them anyway
-        u8 line[16] = {0};
-        const u64 len = std::min<u64>(end - o[0], 16);
-        if (o[0] + len <= SAMPLE) {
-            std::memcpy(line, s + 16 + o[0], len);
-        } else if (len) {   // the first line does not start in the sample: read its head
+        const u64 len = std::min<u64>(end - o[0], SAMPLE);
+        const u8* line = s + 16 + o[0];
+        if (o[0] + len > SAMPLE && len) {   // the first line does not lie in the sample: read it
             HIPCHK(c, hipMemcpyAsync(s + 16, segs[i].d_bytes + o[0], len, hipMemcpyDeviceToHost, c->s_aux));
             HIPCHK(c, hipStreamSynchronize(c->s_aux));
-            std::memcpy(line, s + 16, len);
+            line = s + 16;
         }
-        const u32 off0 = 0;
-        const int l = sniff_layout(line, len, &off0, 1);
-        if (lay < 0) lay = l;
-        else if (lay != l) lay = 2;
+        LearnDesc di{};
+        const int l = learn_layout(line, len, req, &di);
+        if (lay < 0) {
+            lay = l;
+            *d = di;
+        } else if (lay != l || (l == 3 && std::memcmp(&di, d, sizeof di) != 0)) {
+            lay = 2;
+        }
     }
     return lay < 0 ? 0 : lay;
 }
@@ -965,7 +1028,8 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
     const ysb_segment sg{c->d_bytes[slot], nbytes, c->d_off[slot], n};
     // the scan instantiation named by the batch's first line, which the host holds in the
     // pinned slot (counts are the same whichever runs)
-    if (layout_sampling(c) && n) c->submit_layout = sniff_layout(c->h_bytes[slot], nbytes, c->h_off[slot], n);
+    if (layout_sampling(c) && n)
+        c->submit_layout = sniff_layout(c, c->h_bytes[slot], nbytes, c->h_off[slot], n, &c->submit_learn);
     rc = enqueue_scan(c, &sg, 1);
     c->submit_layout = -1;
     if (rc) return rc;
@@ -984,7 +1048,7 @@ int ysb_wait(ysb_ctx* c, int slot) {
 // Device batches: the layout sampled from their first lines (unless fixed), then the launch.
 static int enqueue_device(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     if (c->table_loaded && layout_sampling(c)) {
-        const int lay = sample_device_layout(c, segs, nseg);
+        const int lay = sample_device_layout(c, segs, nseg, &c->submit_learn);
         if (lay < 0) return lay;
         c->submit_layout = lay;
     }

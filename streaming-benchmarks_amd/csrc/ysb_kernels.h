@@ -149,6 +149,13 @@ struct ScanParams {
     // pinned host word (or null): defer_kernel stores the out-of-ring map's fill level there
     // (the host checks it at the next submit without waiting)
     u32* used_out;
+    // layout 3 (a learned key order): the batch's key order as key indices (0 user_id,
+    // 1 page_id, 2 ad_id, 3 ad_type, 4 event_type, 5 event_time, 6 ip_address), 3 bits per
+    // key (key k in bits 3k..3k+2: no array, so no indexed private memory), read off its
+    // first line by the host (ysb_capi.cpp learn_layout); learn_cp: compact separators
+    u32 learn_code;
+    u32 learn_n;
+    u32 learn_cp;
 };
 
 // Record-mode pipeline after the scan (ysb_count.hip).  Level-2 bins ("blocks") are

@@ -1018,6 +1018,134 @@ __device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 requ
     return true;
 }
 
+// ---- layout 3: a learned key order --------------------------------------------------------
+// Another producer's serializer writes every line with the same key order and the same
+// spacing (", " / ": " or compact "," / ":").  The host reads that order off the batch's
+// first line (ysb_capi.cpp learn_layout) and the scan then checks each line against it
+// the way the vocabulary path checks the generator's: per pair, the key text with its
+// separator and the value's opening quote compared in place as words (one aligned read
+// span, one shift), a 36-byte id value and the separator after it in one span, any other
+// value's closing quote found 16 bytes per step -- no key naming, no whitespace skips, the
+// key order a uniform (scalar) branch.  Every byte up to the closing '}' is compared or
+// shown to be a plain string byte, so an accepted line parses as org.json parses it
+// (JSONObject(JSONTokener) on this subset: nextClean, nextString, putOnce, ',' / '}');
+// any other line goes on to the flat tier, then the general parser.
+
+// key index -> its text (ScanParams.learn_order)
+__host__ __device__ constexpr const char* learn_key(int i) {
+    return i == 0 ? "user_id" : i == 1 ? "page_id" : i == 2 ? "ad_id" : i == 3 ? "ad_type" : i == 4 ? "event_type"
+         : i == 5 ? "event_time" : "ip_address";
+}
+constexpr int cstr_len(const char* s) { return *s ? 1 + cstr_len(s + 1) : 0; }
+// the key text, its closing quote, the separator and the value's opening quote
+template <int KI, bool CP>
+struct KeyLit {
+    static constexpr int KL = cstr_len(learn_key(KI));
+    static constexpr int LEN = KL + (CP ? 3 : 4);
+    static constexpr WordTpl<4> tpl() {
+        char buf[20] = {};
+        const char* k = learn_key(KI);
+        int n = 0;
+        for (; k[n]; ++n) buf[n] = k[n];
+        buf[n++] = '"';
+        buf[n++] = ':';
+        if (!CP) buf[n++] = ' ';
+        buf[n++] = '"';
+        return make_words<4>(buf, 0, n);
+    }
+};
+
+// 36 value bytes (w[0..8]) are plain string bytes: no quote, backslash or byte < 0x20.
+// Fast test: every byte in [0x2D, 0x7F) and not a backslash (UUID text always is); else
+// the exact flags.
+__device__ __forceinline__ bool plain36(const u32 (&w)[10]) {
+    u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        lo &= w[k] + 0x53535353u;   // bit 7 set per byte iff byte >= 0x2D (bytes < 0x80: no carries)
+        hi |= w[k];
+        bs |= zero_bytes(w[k] ^ 0x5C5C5C5Cu);
+    }
+    if (((lo & 0x80808080u) == 0x80808080u) & ((hi & 0x80808080u) == 0u) & (bs == 0u)) return true;
+    u32 f = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f |= ft_flags(w[k]);
+    return f == 0u;
+}
+
+// One pair of a learned order: the key literal at p, its value, the separator after it
+// (", " + the next key's quote, or the closing quote + '}' when `last`).  p moves to the
+// next key's text, or (last) to the '}'.  KI 0..2: 36-byte id values.
+template <int KI, bool CP>
+__device__ __forceinline__ bool learned_pair(const LdsSrc& src, int& p, int e, bool last, u32 (&kw)[9], int& vs,
+                                             int& ve) {
+    using K = KeyLit<KI, CP>;
+    constexpr WordTpl<4> T = K::tpl();
+    constexpr u32 SEP = CP ? w4('"', ',', '"', 0) : w4('"', ',', ' ', '"');
+    constexpr u32 SEPM = CP ? 0x00FFFFFFu : 0xFFFFFFFFu;
+    constexpr int SEPL = CP ? 3 : 4;
+    u32 kwd[4];
+    load_span(src, p, kwd);
+    bool ok = words_diff(kwd, T) == 0u;
+    const int v = p + K::LEN;
+    vs = v;
+    if constexpr (KI <= 2) {
+        u32 w[10];
+        load_span(src, v, w);
+        ok &= plain36(w);
+        ok &= last ? (w[9] & 0xFFFFu) == w4('"', '}', 0, 0) : (w[9] & SEPM) == SEP;
+        ve = v + 36;
+        if constexpr (KI == 2) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) kw[k] = w[k];
+        }
+    } else {
+        ve = ft_string_end(src, v, e);
+        ok &= ve >= v;
+        const u32 x = src.load4(ok ? ve : v);
+        ok &= last ? (x & 0xFFFFu) == w4('"', '}', 0, 0) : (x & SEPM) == SEP;
+    }
+    p = last ? ve + 1 : ve + SEPL;
+    return ok;
+}
+
+template <bool CP>
+__device__ __forceinline__ bool learned_parse(const LdsSrc& src, int s, int e, const ScanParams& P, CanonA& a,
+                                              CanonB& b) {
+    bool ok = (src.load4(s) & 0xFFFFu) == w4('{', '"', 0, 0);
+    int p = s + 2;
+    int ets = s, ete = s, tms = s, tme = s;
+    u32 kw[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) kw[k] = 0u;
+    const int n = (int)P.learn_n;
+#pragma unroll 1
+    for (int k = 0; k < n; ++k) {
+        const bool last = k + 1 == n;
+        int vs = 0, ve = 0;
+        bool pk;
+        switch ((P.learn_code >> (3 * k)) & 7u) {   // uniform: a scalar branch
+        case 0: pk = learned_pair<0, CP>(src, p, e, last, kw, vs, ve); break;
+        case 1: pk = learned_pair<1, CP>(src, p, e, last, kw, vs, ve); break;
+        case 2: pk = learned_pair<2, CP>(src, p, e, last, kw, vs, ve); break;
+        case 3: pk = learned_pair<3, CP>(src, p, e, last, kw, vs, ve); break;
+        case 4: pk = learned_pair<4, CP>(src, p, e, last, kw, vs, ve); ets = vs; ete = ve; break;
+        case 5: pk = learned_pair<5, CP>(src, p, e, last, kw, vs, ve); tms = vs; tme = ve; break;
+        default: pk = learned_pair<6, CP>(src, p, e, last, kw, vs, ve); break;
+        }
+        ok &= pk;
+        if (!ok) p = s + 2;   // a failed lane keeps reading inside its line (result ignored)
+    }
+    ok &= p < e;              // the '}' (every compared byte lies before it)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a.kw[k] = kw[k];
+    a.t0 = tms - s;
+    b.tlen = tme - tms;
+    load_span(src, tms, b.td);
+    b.view = ete - ets == 4 && src.load4(ets) == VIEW_W;
+    return ok;
+}
+
 // The deferred-line kernel's use: true = decided here (ok = counted); false = nothing
 // counted, parse it in full.
 __device__ __forceinline__ bool flat_line(const LdsSrc3& src, int s, int e, const ScanParams& P, Tally& t,
@@ -1446,6 +1574,11 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             le = (int)(my_end - cur.s0 + cur.delta);
             if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
             else if constexpr (LAY == 2) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb);
+            else if constexpr (LAY == 3) {
+                ok1 = P.learn_cp ? learned_parse<true>(lsrc, ls, le, P, ca, cb) : learned_parse<false>(lsrc, ls, le, P, ca, cb);
+                // a line off the learned order: the flat tier (any order or spacing)
+                if (__builtin_expect(!ok1, 0)) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb);
+            }
             else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1<LAY == 1>(lsrc, ls, le, ca);
             else ok1 = canon_stage1<false>(lsrc, ls, le, ca);
         }
@@ -1454,12 +1587,12 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         bool ok2 = false;
         if (li < cur.count) {
             if constexpr (TBL) ok2 = ok1 && tbl_stage2(lsrc, ls, le, ca, cb);
-            else if constexpr (LAY == 2) ok2 = ok1;
+            else if constexpr (LAY == 2 || LAY == 3) ok2 = ok1;
             else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2<LAY == 1>(lsrc, ls, le, ca, cb);
             else ok2 = ok1 && canon_stage2<false>(lsrc, ls, le, ca, cb);
         }
 #if YSB_CANON_TIERS
-        if constexpr (!TBL && YSB_VOCAB != 0 && LAY != 2) {
+        if constexpr (!TBL && YSB_VOCAB != 0 && LAY < 2) {
             // second and third tiers for the lanes the vocabulary path rejected (a branch
             // no lane takes on the generator's own lines): any values in the generator's
             // layout, then the same keys as compact JSON
@@ -1989,6 +2122,7 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
         else if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false, false>), g, b, Geom<false>::LDS, s, p);
         else if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<false, false, false, 1>), g, b, Geom<false>::LDS, s, p);
         else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<false, false, false, 2>), g, b, Geom<false>::LDS, s, p);
+        else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<false, false, false, 3>), g, b, Geom<false>::LDS, s, p);
         else hipLaunchKernelGGL((scan_kernel<false, false, false>), g, b, Geom<false>::LDS, s, p);
     }
 }

@@ -13,12 +13,22 @@ from ysb_amd import GEN_COMPACT, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER, 
 
 pytestmark = pytest.mark.gpu
 
+
+def hint_kw(hint):
+    """None: the default (each batch's first line picks the instantiation); "fixed": no
+    sampling (the generator's layout first); else an explicit layout hint."""
+    if hint is None:
+        return {}
+    if hint == "fixed":
+        return {"layout_auto": False}
+    return {hint: True}
+
 VARIANTS = [GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_RANDOM_IP | GEN_MORE_AD_TYPES, GEN_COMPACT,
             GEN_COMPACT | GEN_RANDOM_IP, GEN_COMPACT | GEN_RANDOM_IP | GEN_MORE_AD_TYPES,
             GEN_REORDER, GEN_REORDER | GEN_COMPACT | GEN_RANDOM_IP]
 
 
-@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "layout_auto"])
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "fixed"])
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_tier_lines_exact_and_not_deferred(variant, hint):
     g = GenParams(seed=23, n_campaigns=50, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
@@ -27,7 +37,7 @@ def test_tier_lines_exact_and_not_deferred(variant, hint):
     raw, offs = g.events_host(0, 150_000)
     exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), raw, offs)
     with YsbContext(n_campaigns=50, window_ring=256, max_batch_bytes=raw.size + 64,
-                    max_batch_events=offs.size + 1, **({hint: True} if hint else {})) as ctx:
+                    max_batch_events=offs.size + 1, **hint_kw(hint)) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         ctx.submit(raw, offs)
         got = ctx.drain_buckets()
@@ -47,7 +57,7 @@ def test_tier_device_generator_truth(variant, hint):
     _, aids = g.ids()
     n = 4_000_000
     hraw, _ = g.events_host(0, 20_000)
-    with YsbContext(n_campaigns=100, window_ring=1024, **({hint: True} if hint else {})) as ctx:
+    with YsbContext(n_campaigns=100, window_ring=1024, **hint_kw(hint)) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         cap = n * g.max_line_bytes()
         d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
@@ -62,7 +72,7 @@ def test_tier_device_generator_truth(variant, hint):
     assert st["deferred"] == 0 and st["parse_errors"] == 0 and st["join_misses"] == 0
 
 
-@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "layout_auto"])
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "fixed"])
 def test_tier_mixed_with_off_template_lines(hint):
     """Tier lines, vocabulary lines and general-path lines (whitespace, escapes, other key
     orders) interleaved in one batch: still exactly the oracle."""
@@ -83,7 +93,7 @@ def test_tier_mixed_with_off_template_lines(hint):
     offs = np.zeros(len(lines), dtype=np.uint32)
     offs[1:] = np.cumsum([len(x) + 1 for x in lines[:-1]])
     exp, est = oracle.run(oracle.AdMap(aids, g0.ad_campaign_index()), data, offs)
-    with YsbContext(n_campaigns=20, window_ring=64, **({hint: True} if hint else {})) as ctx:
+    with YsbContext(n_campaigns=20, window_ring=64, **hint_kw(hint)) as ctx:
         ctx.load_ad_map(aids, g0.ad_campaign_index())
         ctx.submit(data, offs)
         got = ctx.drain_buckets()
@@ -94,7 +104,7 @@ def test_tier_mixed_with_off_template_lines(hint):
     assert 0 < st["deferred"] <= 1000
 
 
-@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "layout_auto"])
+@pytest.mark.parametrize("hint", [None, "compact_first", "flat_first", "fixed"])
 def test_canonical_tier_other_event_types_and_times(hint):
     """Lines in the generator's layout whose event_type is none of the three or whose
     event_time is not 13 digits (the vocabulary path names both from closed sets) go to
@@ -121,7 +131,7 @@ def test_canonical_tier_other_event_types_and_times(hint):
     offs2[1:] = np.cumsum([len(x) + 1 for x in out[:-1]])
     exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), data, offs2)
     with YsbContext(n_campaigns=40, window_ring=256, max_batch_bytes=len(data) + 64,
-                    max_batch_events=len(out) + 1, **({hint: True} if hint else {})) as ctx:
+                    max_batch_events=len(out) + 1, **hint_kw(hint)) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         ctx.submit(data, offs2)
         got = ctx.drain_buckets()
@@ -159,3 +169,120 @@ def test_layout_auto_host_batches_exact(variant):
     assert got == exp_rows
     for k, v in exp_st.items():
         assert st[k] == v, k
+
+
+def _batch(lines):
+    data = b"\n".join(lines) + b"\n"
+    offs = np.zeros(len(lines), dtype=np.uint32)
+    offs[1:] = np.cumsum([len(x) + 1 for x in lines[:-1]])
+    return data, offs
+
+
+@pytest.mark.parametrize("variant", [GEN_REORDER, GEN_REORDER | GEN_COMPACT,
+                                     GEN_REORDER | GEN_RANDOM_IP | GEN_MORE_AD_TYPES])
+@pytest.mark.parametrize("device", [False, True])
+def test_learned_key_order_layout(variant, device):
+    """Another key order (the generator's GEN_REORDER lines, also compact and with other
+    values): the batch's first line names the order (ysb_capi.cpp learn_layout) and the
+    scan runs the learned-order instantiation (layout 3) -- host batches from the pinned
+    slot, device batches from a sampled first line -- exact vs the oracle, nothing
+    deferred."""
+    g = GenParams(seed=29, n_campaigns=60, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
+                  variant=variant)
+    _, aids = g.ids()
+    raw, offs = g.events_host(0, 120_000)
+    exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), raw, offs)
+    with YsbContext(n_campaigns=60, window_ring=256, max_batch_bytes=raw.size + 64,
+                    max_batch_events=offs.size + 1) as ctx:
+        ctx.load_ad_map(aids, g.ad_campaign_index())
+        if device:
+            d_b, d_o = ctx.device_alloc(raw.size + 64), ctx.device_alloc(4 * offs.size + 64)
+            ctx.h2d(d_b, raw)
+            ctx.h2d(d_o, offs)
+            ctx.submit_device(d_b, raw.size, d_o, offs.size)
+        else:
+            ctx.submit(raw, offs)
+        assert ctx.launch_info()["layout"] == 3
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+    assert got == exp
+    for k, v in est.items():
+        assert st[k] == v, k
+    assert st["deferred"] == 0
+
+
+@pytest.mark.parametrize("require_ip", [False, True])
+def test_learned_order_with_off_order_lines(require_ip):
+    """A batch whose first line is in a learned order, then lines that break it in every way
+    the learned check must reject -- another order, other spacing, a missing or an extra
+    key, a repeated key, an id value of another length, an escape, a nested value, a
+    single-quoted value, text after '}' -- interleaved with lines in the order.  The learned
+    instantiation hands each off to the flat tier / the general parser: exactly the
+    oracle's counts (with and without YSB_F_REQUIRE_IP)."""
+    g = GenParams(seed=37, n_campaigns=20, ads_per_campaign=5, events_per_sec=100, variant=GEN_REORDER)
+    g0 = GenParams(seed=37, n_campaigns=20, ads_per_campaign=5, events_per_sec=100)
+    _, aids = g.ids()
+    a, _ = g.events_host(0, 4000)
+    b, _ = g0.events_host(0, 4000)
+    la, lb = bytes(a).split(b"\n")[:-1], bytes(b).split(b"\n")[:-1]
+    breaks = [
+        lambda ln: ln.replace(b'", "', b'","', 1),                                  # other spacing
+        lambda ln: ln.replace(b', "ip_address": "1.2.3.4"', b''),                   # a key missing
+        lambda ln: ln[:-1] + b', "extra": "x"}',                                    # an extra key
+        lambda ln: ln[:-1] + b', "ad_type": "x"}',                                  # a repeated key
+        lambda ln: ln.replace(b'"user_id": "', b'"user_id": "z', 1),                # a 37-byte id
+        lambda ln: ln.replace(b'"event_type": "view"', b'"event_type": "vi\\u0065w"'),   # an escape
+        lambda ln: ln.replace(b'"ip_address": "1.2.3.4"', b'"ip_address": {"a": "1"}'),  # nested
+        lambda ln: ln.replace(b'"ad_type": "', b"'ad_type': '", 1).replace(b'", "event_time"', b"', \"event_time\"", 1),
+        lambda ln: ln + b' trailing',                                               # text after '}'
+        lambda ln: ln.replace(b'{"ad_type"', b'{ "ad_type"', 1),                    # space after '{'
+    ]
+    lines = [la[0]]
+    for i in range(1, 4000):
+        if i % 5 == 0:
+            lines.append(breaks[(i // 5) % len(breaks)](la[i]))
+        elif i % 5 == 1:
+            lines.append(lb[i])                                                     # generator order
+        else:
+            lines.append(la[i])
+    data, offs = _batch(lines)
+    am = oracle.AdMap(aids, g.ad_campaign_index())
+    exp, est = oracle.run(am, data, offs, require_ip=require_ip) if require_ip else oracle.run(am, data, offs)
+    with YsbContext(n_campaigns=20, window_ring=64, max_batch_bytes=len(data) + 64, max_batch_events=len(lines) + 1,
+                    require_ip=require_ip) as ctx:
+        ctx.load_ad_map(aids, g.ad_campaign_index())
+        ctx.submit(data, offs)
+        assert ctx.launch_info()["layout"] == 3
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+    assert got == exp
+    for k, v in est.items():
+        assert st[k] == v, k
+    assert st["parse_errors"] > 0 and st["deferred"] > 0
+
+
+def test_learned_order_subset_of_keys():
+    """Lines with only DeserializeBolt's six keys (no ip_address) in another order: a learned
+    order of six keys (layout 3); with YSB_F_REQUIRE_IP the same first line cannot name an
+    order (ip_address is required) and the flat tier takes the batch (layout 2) -- where
+    every line is a parse error, as the Storm deserializer's getString("ip_address") throws."""
+    g = GenParams(seed=43, n_campaigns=20, ads_per_campaign=5, events_per_sec=100, variant=GEN_REORDER)
+    _, aids = g.ids()
+    a, _ = g.events_host(0, 3000)
+    lines = [ln.replace(b', "ip_address": "1.2.3.4"', b'') for ln in bytes(a).split(b"\n")[:-1]]
+    assert all(b"ip_address" not in ln for ln in lines)
+    data, offs = _batch(lines)
+    am = oracle.AdMap(aids, g.ad_campaign_index())
+    for req in (False, True):
+        exp, est = oracle.run(am, data, offs, require_ip=req) if req else oracle.run(am, data, offs)
+        with YsbContext(n_campaigns=20, window_ring=64, max_batch_bytes=len(data) + 64,
+                        max_batch_events=len(lines) + 1, require_ip=req) as ctx:
+            ctx.load_ad_map(aids, g.ad_campaign_index())
+            ctx.submit(data, offs)
+            assert ctx.launch_info()["layout"] == (2 if req else 3)
+            got = ctx.drain_buckets()
+            st = ctx.stats()
+        assert got == exp
+        for k, v in est.items():
+            assert st[k] == v, k
+        assert (st["parse_errors"] == len(lines)) == req

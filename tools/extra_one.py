@@ -1,0 +1,35 @@
+"""Runs one of bench.py's extra legs by itself (profiling passes, A/B runs):
+    python tools/extra_one.py config3|tbl|stream|reorder|reorder_fixed|compact [bench.py options]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def layout(args, variant, **kw):
+    from ysb_amd import GenParams, YsbContext
+    g = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, variant=variant)
+    _, aids = g.ids()
+    with YsbContext(device=0, n_campaigns=100, window_ring=1024, timing=True, max_batch_bytes=16 << 20,
+                    max_batch_events=1 << 16, **kw) as ctx:
+        ctx.load_ad_map(aids, g.ad_campaign_index())
+        segs = bench.gen_segments(ctx, g, args.events, 14_285_715)
+        r = bench.timed_extra("layout variant %d %s" % (variant, kw), ctx, g, segs, args.extra_steps, args.warmup, None)
+        r["kernel"] = "ysb::scan_kernel<false, false, false, %d>" % ctx.launch_info()["layout"]
+        bench.free_segments(ctx, segs)
+    return r
+
+
+if __name__ == "__main__":
+    leg = sys.argv[1]
+    args = bench.parse_args(sys.argv[2:])
+    from ysb_amd import GEN_COMPACT, GEN_REORDER
+    fn = {"config3": lambda: bench.extra_config3(args, 0), "tbl": lambda: bench.extra_tbl(args, 0),
+          "stream": lambda: bench.extra_stream(args),
+          "reorder": lambda: layout(args, GEN_REORDER),
+          "reorder_fixed": lambda: layout(args, GEN_REORDER, layout_auto=False),
+          "compact": lambda: layout(args, GEN_COMPACT)}[leg]
+    print(json.dumps(fn()), flush=True)
