@@ -283,6 +283,15 @@ typedef struct ysb_launch_desc {
     uint32_t tbl;
 } ysb_launch_desc;
 int         ysb_launch_info(ysb_ctx* ctx, ysb_launch_desc* out);
+/* The layout sampling's decision for one line (host function; what every submit applies
+ * to its batch's first line): 0 the generator's layout (core.clj:90-96), 1 its keys in its
+ * order as compact JSON, 3 another order or subset of DeserializeBolt's keys with one
+ * consistent spacing -- order[0..*n) then receives the key indices (0 user_id, 1 page_id,
+ * 2 ad_id, 3 ad_type, 4 event_type, 5 event_time, 6 ip_address) and *compact the spacing
+ * -- or 2 anything else (the flat-object tier first).  require_ip: YSB_F_REQUIRE_IP's
+ * rule (ip_address must be among the keys). */
+int         ysb_layout_of_line(const uint8_t* line, uint64_t len, int require_ip, uint32_t order[8],
+                               uint32_t* n, uint32_t* compact);
 /* The compute stream (hipStream_t) for callers that want to order work with it. */
 void*       ysb_stream(ysb_ctx* ctx);
 

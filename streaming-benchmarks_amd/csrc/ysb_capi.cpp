@@ -1383,6 +1383,17 @@ int ysb_path_time(ysb_ctx* c, double* total_ms, uint64_t* launches, uint64_t* re
     return YSB_OK;
 }
 
+int ysb_layout_of_line(const uint8_t* line, uint64_t len, int require_ip, uint32_t order[8], uint32_t* n,
+                       uint32_t* compact) {
+    if (!line && len) return YSB_ERR_ARG;
+    LearnDesc d{};
+    const int l = learn_layout(line, len, require_ip ? 0x7Fu : 0x3Fu, &d);
+    if (order) for (int i = 0; i < 8; ++i) order[i] = d.order[i];
+    if (n) *n = l == 3 ? d.n : 0;
+    if (compact) *compact = l == 3 ? d.cp : (l == 1 ? 1u : 0u);
+    return l;
+}
+
 int ysb_launch_info(ysb_ctx* c, ysb_launch_desc* out) {
     if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
     *out = c->last_launch;

@@ -111,6 +111,7 @@ SIGNATURES = {
     "ysb_path_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_stream": (_P, [_P]),
     "ysb_launch_info": (_I, [_P, C.POINTER(YsbLaunchDesc)]),
+    "ysb_layout_of_line": (_I, [C.c_char_p, _U64, _I, C.c_void_p, C.POINTER(_U32), C.POINTER(_U32)]),
     "ysb_device_alloc": (_I, [_P, _U64, C.POINTER(_P)]),
     "ysb_device_free": (_I, [_P, _P]),
     "ysb_memcpy_h2d": (_I, [_P, _P, _P, _U64]),

@@ -148,3 +148,20 @@ def shard_packed(keys, nranks: int, key_len: int = 36):
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z ^= z >> np.uint64(31)
     return (((z >> np.uint64(32)) * np.uint64(nranks)) >> np.uint64(32)).astype(np.uint32)
+
+
+KEY_ORDER_NAMES = ("user_id", "page_id", "ad_id", "ad_type", "event_type", "event_time", "ip_address")
+
+
+def layout_of_line(line: bytes, require_ip: bool = False):
+    """The layout sampling's decision for one line (ysb_layout_of_line): (layout, key order
+    as names or None, compact).  0 the generator's, 1 compact generator order, 2 the
+    flat-object tier first, 3 a learned key order."""
+    order = np.zeros(8, dtype=np.uint32)
+    n, cp = C.c_uint32(), C.c_uint32()
+    lay = lib().ysb_layout_of_line(bytes(line), len(line), int(require_ip), C.c_void_p(order.ctypes.data),
+                                   C.byref(n), C.byref(cp))
+    if lay < 0:
+        raise ValueError("bad arguments")
+    names = [KEY_ORDER_NAMES[i] for i in order[:n.value]] if lay == 3 else None
+    return lay, names, bool(cp.value)

@@ -188,3 +188,33 @@ def test_shard_packed_equals_ad_shard():
         assert shard_packed(ab, n).tolist() == [ad_shard(a, n) for a in aids]
     odd = np.frombuffer(b"".join(b"ad-%05d-x" % i for i in range(300)), dtype=np.uint8)   # 10-byte keys
     assert shard_packed(odd, 5, key_len=10).tolist() == [ad_shard(b"ad-%05d-x" % i, 5) for i in range(300)]
+
+
+def test_layout_sampling_decisions():
+    """The layout every submit reads off its batch's first line (ysb_layout_of_line, host
+    code): the generator's own lines -> 0, compact -> 1, another key order -> 3 with that
+    order, and everything the learned-order check cannot express -> 2."""
+    from ysb_amd import GEN_COMPACT, GEN_RANDOM_IP, GEN_REORDER, layout_of_line
+    first = lambda v: bytes(GenParams(seed=1, variant=v).events_host(0, 1)[0])   # noqa: E731
+    assert layout_of_line(first(0)) == (0, None, False)
+    assert layout_of_line(first(GEN_RANDOM_IP)) == (0, None, False)
+    assert layout_of_line(first(GEN_COMPACT)) == (1, None, True)
+    lay, order, cp = layout_of_line(first(GEN_REORDER))
+    assert lay == 3 and not cp
+    assert order == ["ad_type", "event_time", "ad_id", "ip_address", "user_id", "event_type", "page_id"]
+    lay, order, cp = layout_of_line(first(GEN_REORDER | GEN_COMPACT))
+    assert lay == 3 and cp and len(order) == 7
+    g = first(0)
+    no_ip = g.replace(b', "ip_address": "1.2.3.4"', b'')
+    assert layout_of_line(no_ip)[0] == 3 and layout_of_line(no_ip)[1][-1] == "event_time"
+    assert layout_of_line(no_ip, require_ip=True)[0] == 2          # ip_address required, absent
+    for bad in (g.replace(b'{"', b'{ "', 1),                         # space after '{'
+                g.replace(b'", "page_id"', b'","page_id"'),          # mixed spacing
+                g.replace(b'"ad_type"', b'"ad_kind"'),               # another key
+                g[:-2] + b', "ad_type": "x"}\n',                     # a repeated key
+                g.replace(b'"user_id": "', b'"user_id": "z'),        # a 37-byte id
+                g.replace(b'"view"', b'"v\\u0069ew"').replace(b'"click"', b'"cl\\u0069ck"')
+                 .replace(b'"purchase"', b'"purch\\u0061se"'),       # an escape
+                g.replace(b'"1.2.3.4"', b'1234'),                    # a non-string value
+                b"", b"not json"):
+        assert layout_of_line(bad)[0] == 2, bad
