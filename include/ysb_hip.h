@@ -314,6 +314,19 @@ int         ysb_group_unique_id(uint8_t uid[YSB_UNIQUE_ID_BYTES]);
  * After ysb_group_init, ysb_ring_advance is collective too (same new_lo on every rank). */
 int         ysb_group_init(ysb_ctx* ctx, int rank, int nranks,
                            const uint8_t uid[YSB_UNIQUE_ID_BYTES]);
+/* The same group over the caller's own collectives instead of RCCL (a job whose ranks
+ * already share a transport; the test rehearsal of N ranks on one GPU, where RCCL refuses
+ * two ranks per device).  Both callbacks run on the calling thread, on host memory, and
+ * must be collective over the nranks ranks; nonzero = failure:
+ *   allreduce_max_u64: buf[0..n) <- elementwise max over the ranks, in place;
+ *   reduce_scatter_sum: recv[0..count) <- sum over the ranks of their send blocks
+ *     [rank * count, (rank + 1) * count), cells of `width` bytes (1, 4 or 8), unsigned. */
+typedef struct ysb_collectives {
+    int (*allreduce_max_u64)(void* user, uint64_t* buf, uint64_t n);
+    int (*reduce_scatter_sum)(void* user, const void* send, void* recv, uint64_t count, uint32_t width);
+    void* user;
+} ysb_collectives;
+int         ysb_group_init_host(ysb_ctx* ctx, int rank, int nranks, const ysb_collectives* ops);
 /* Collective: sums the ranks' pending counts (everything counted since the previous call)
  * into the owner ranks' tables and zeroes them.  Range-limited, like the reference's keyed
  * shuffle, which carries only the touched (campaign, window) pairs: per ring bucket the

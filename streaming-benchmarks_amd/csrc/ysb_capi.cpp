@@ -116,8 +116,10 @@ struct ysb_ctx {
     // wrote it (*d_dirty, set on the device)
     bool pend_u64 = true;
     u32* d_dirty = nullptr;
-    // group
+    // group: an RCCL communicator, or the caller's host collectives (ysb_group_init_host)
     ncclComm_t comm = nullptr;
+    bool host_coll = false;
+    ysb_collectives hops{};
     int rank = 0, nranks = 1;
     // the range-limited exchange: per-slot maxima (all-reduced), the plan's slots, the packed
     // send / receive buffers, and its accounting (HIP event pairs, collected on request)
@@ -177,6 +179,7 @@ static int agree_ring(ysb_ctx* c);
 static int allreduce_max(ysb_ctx* c, i64* h, int n);
 static int sync_streams(ysb_ctx* c);
 static int pull_side_list(ysb_ctx* c);
+static bool grouped(const ysb_ctx* c);
 
 int ysb_abi_version(void) { return YSB_ABI_VERSION; }
 
@@ -1289,7 +1292,7 @@ int ysb_ring_advance(ysb_ctx* c, int64_t new_lo) {
     int rc = sync_streams(c);
     if (rc) return rc;
     if ((rc = read_ring(c))) return rc;
-    if (c->comm) {
+    if (grouped(c)) {
         // collective after ysb_group_init: every rank's ring moves together (all ranks call
         // it with the same new_lo; a disagreement fails on every rank alike)
         if (!c->ring_agreed && (rc = agree_ring(c))) return rc;
@@ -1431,18 +1434,60 @@ int ysb_memcpy_d2h(ysb_ctx* c, void* h, const void* d, uint64_t bytes) {
 
 // ---- multi-GPU ---------------------------------------------------------------------------------
 
-// h[0..n) <- elementwise max over the ranks (one small RCCL all-reduce, synchronous).
+static bool grouped(const ysb_ctx* c) { return c->comm != nullptr || c->host_coll; }
+
+// d[0..n) <- elementwise max over the ranks, in place: one RCCL all-reduce on the compute
+// stream, or (host collectives) the buffer through host memory and the caller's all-reduce.
+static int coll_max_u64(ysb_ctx* c, unsigned long long* d, u64 n) {
+    if (c->comm) {
+        ncclResult_t r = ncclAllReduce(d, d, n, ncclUint64, ncclMax, c->comm, c->s_comp);
+        if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+        return YSB_OK;
+    }
+    std::vector<uint64_t> h(n);
+    HIPCHK(c, hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, c->s_comp));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    if (c->hops.allreduce_max_u64(c->hops.user, h.data(), n))
+        return fail(c, YSB_ERR_RCCL, "host all-reduce(max) failed");
+    HIPCHK(c, hipMemcpyAsync(d, h.data(), n * 8, hipMemcpyHostToDevice, c->s_comp));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    return YSB_OK;
+}
+
+// recv[0..count) <- sum over the ranks of their send blocks [rank * count, (rank + 1) * count),
+// cells of `width` bytes (1, 4 or 8, unsigned).
+static int coll_reduce_scatter(ysb_ctx* c, const void* d_send, void* d_recv, u64 count, u32 width) {
+    if (c->comm) {
+        const ncclDataType_t ty = width == 1 ? ncclUint8 : width == 4 ? ncclUint32 : ncclUint64;
+        ncclResult_t r = ncclReduceScatter(d_send, d_recv, (size_t)count, ty, ncclSum, c->comm, c->s_comp);
+        if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
+        return YSB_OK;
+    }
+    const u64 nb = count * width;
+    std::vector<u8> hs(nb * (u64)c->nranks), hr(nb);
+    HIPCHK(c, hipMemcpyAsync(hs.data(), d_send, hs.size(), hipMemcpyDeviceToHost, c->s_comp));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    if (c->hops.reduce_scatter_sum(c->hops.user, hs.data(), hr.data(), count, width))
+        return fail(c, YSB_ERR_RCCL, "host reduce-scatter failed");
+    HIPCHK(c, hipMemcpyAsync(d_recv, hr.data(), nb, hipMemcpyHostToDevice, c->s_comp));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    return YSB_OK;
+}
+
+// h[0..n) <- elementwise max over the ranks (signed: mapped to unsigned by the sign bit).
 static int allreduce_max(ysb_ctx* c, i64* h, int n) {
-    i64* d = nullptr;
-    HIPCHK(c, hipMalloc(&d, sizeof(i64) * n));
-    hipError_t e = hipMemcpy(d, h, sizeof(i64) * n, hipMemcpyHostToDevice);
-    ncclResult_t r = ncclSuccess;
-    if (e == hipSuccess) r = ncclAllReduce(d, d, n, ncclInt64, ncclMax, c->comm, c->s_comp);
-    if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(h, d, sizeof(i64) * n, hipMemcpyDeviceToHost, c->s_comp);
-    if (e == hipSuccess && r == ncclSuccess) e = hipStreamSynchronize(c->s_comp);
+    unsigned long long* d = nullptr;
+    HIPCHK(c, hipMalloc(&d, 8 * (u64)n));
+    std::vector<u64> u(n);
+    for (int i = 0; i < n; ++i) u[i] = (u64)h[i] ^ (1ull << 63);
+    hipError_t e = hipMemcpy(d, u.data(), 8 * (u64)n, hipMemcpyHostToDevice);
+    int rc = e == hipSuccess ? coll_max_u64(c, d, (u64)n) : YSB_OK;
+    if (e == hipSuccess && !rc) e = hipMemcpyAsync(u.data(), d, 8 * (u64)n, hipMemcpyDeviceToHost, c->s_comp);
+    if (e == hipSuccess && !rc) e = hipStreamSynchronize(c->s_comp);
     hipFree(d);
-    if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    if (rc) return rc;
     if (e != hipSuccess) return fail(c, YSB_ERR_HIP, "%s", hipGetErrorString(e));
+    for (int i = 0; i < n; ++i) h[i] = (i64)(u[i] ^ (1ull << 63));
     return YSB_OK;
 }
 
@@ -1473,15 +1518,31 @@ int ysb_group_unique_id(uint8_t uid[YSB_UNIQUE_ID_BYTES]) {
     return YSB_OK;
 }
 
+static int group_setup(ysb_ctx* c, int rank, int nranks);
+
 int ysb_group_init(ysb_ctx* c, int rank, int nranks, const uint8_t uid[YSB_UNIQUE_ID_BYTES]) {
     if (!c || !uid) return YSB_ERR_ARG;
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(c, YSB_ERR_ARG, "bad rank %d / %d", rank, nranks);
-    if (c->comm) return fail(c, YSB_ERR_STATE, "group already initialised");
+    if (grouped(c)) return fail(c, YSB_ERR_STATE, "group already initialised");
     HIPCHK(c, hipSetDevice(c->device));
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof id);
     ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
     if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    return group_setup(c, rank, nranks);
+}
+
+int ysb_group_init_host(ysb_ctx* c, int rank, int nranks, const ysb_collectives* ops) {
+    if (!c || !ops || !ops->allreduce_max_u64 || !ops->reduce_scatter_sum) return YSB_ERR_ARG;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(c, YSB_ERR_ARG, "bad rank %d / %d", rank, nranks);
+    if (grouped(c)) return fail(c, YSB_ERR_STATE, "group already initialised");
+    HIPCHK(c, hipSetDevice(c->device));
+    c->hops = *ops;
+    c->host_coll = true;
+    return group_setup(c, rank, nranks);
+}
+
+static int group_setup(ysb_ctx* c, int rank, int nranks) {
     c->rank = rank;
     c->nranks = nranks;
     // pad campaigns to a multiple of nranks; keep the current counts
@@ -1562,7 +1623,7 @@ int ysb_exchange_plan(const uint64_t* slot_max, uint32_t W, uint32_t nranks, uin
 // them (xpack) -> ncclReduceScatter -> add the owner block into the owned table (xunpack).
 int ysb_group_reduce_scatter(ysb_ctx* c) {
     if (!c) return YSB_ERR_ARG;
-    if (!c->comm) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
+    if (!grouped(c)) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->ring_agreed) {
         int rc = agree_ring(c);
@@ -1581,8 +1642,8 @@ int ysb_group_reduce_scatter(ysb_ctx* c) {
     HIPCHK(c, hipMemsetAsync(c->d_xmax, 0, (u64)W * 8, c->s_comp));
     launch_xplan(c->d_counts, delta, W, cells, c->pend_u64 ? 1 : 0, c->d_dirty, c->d_xmax, c->s_comp);
     HIPCHK(c, hipGetLastError());
-    ncclResult_t r = ncclAllReduce(c->d_xmax, c->d_xmax, W, ncclUint64, ncclMax, c->comm, c->s_comp);
-    if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    int crc = coll_max_u64(c, c->d_xmax, W);
+    if (crc) return crc;
     HIPCHK(c, hipMemcpyAsync(c->h_xmax, c->d_xmax, (u64)W * 8, hipMemcpyDeviceToHost, c->s_comp));
     HIPCHK(c, hipStreamSynchronize(c->s_comp));
     u32* slots = reinterpret_cast<u32*>(c->h_xmax + W);
@@ -1598,9 +1659,7 @@ int ysb_group_reduce_scatter(ysb_ctx* c) {
         launch_xpack(c->d_counts, delta ? c->d_delta : nullptr, W, rows, c->d_xslots, R, c->pend_u64 ? 1 : 0,
                      c->d_dirty, c->d_xsend, width, c->s_comp);
         HIPCHK(c, hipGetLastError());
-        const ncclDataType_t ty = width == 1 ? ncclUint8 : width == 4 ? ncclUint32 : ncclUint64;
-        r = ncclReduceScatter(c->d_xsend, c->d_xrecv, (size_t)per * R, ty, ncclSum, c->comm, c->s_comp);
-        if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
+        if ((rc = coll_reduce_scatter(c, c->d_xsend, c->d_xrecv, (u64)per * R, width))) return rc;
         launch_xunpack(c->d_owned, W, per, c->d_xslots, R, c->d_xrecv, width, c->s_comp);
         HIPCHK(c, hipGetLastError());
     }
@@ -1682,7 +1741,12 @@ int ysb_group_checksum(ysb_ctx* c, int what, uint32_t nranks, uint64_t* out) {
 
 int ysb_group_info(ysb_ctx* c, int* rank, int* nranks) {
     if (!c) return YSB_ERR_ARG;
-    if (!c->comm) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
+    if (!grouped(c)) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
+    if (c->host_coll) {   // the caller's collectives: the ranks it declared
+        if (rank) *rank = c->rank;
+        if (nranks) *nranks = c->nranks;
+        return YSB_OK;
+    }
     int n = 0, r = 0;
     ncclResult_t e = ncclCommCount(c->comm, &n);
     if (e == ncclSuccess) e = ncclCommUserRank(c->comm, &r);

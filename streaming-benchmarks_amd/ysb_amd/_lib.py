@@ -64,6 +64,15 @@ class YsbLaunchDesc(C.Structure):
     _fields_ = [("layout", C.c_uint32), ("record_mode", C.c_uint32), ("hbm_table", C.c_uint32), ("tbl", C.c_uint32)]
 
 
+ALLREDUCE_MAX_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint64)
+REDUCE_SCATTER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32)
+
+
+class YsbCollectives(C.Structure):
+    _fields_ = [("allreduce_max_u64", ALLREDUCE_MAX_FN), ("reduce_scatter_sum", REDUCE_SCATTER_FN),
+                ("user", C.c_void_p)]
+
+
 class YsbSegment(C.Structure):
     _fields_ = [("d_bytes", C.c_void_p), ("nbytes", C.c_uint64), ("d_line_off", C.c_void_p),
                 ("n_events", C.c_uint64)]
@@ -119,6 +128,7 @@ SIGNATURES = {
     "ysb_group_unique_id": (_I, [C.c_char_p]),
     "ysb_group_init": (_I, [_P, _I, _I, C.c_char_p]),
     "ysb_group_reduce_scatter": (_I, [_P]),
+    "ysb_group_init_host": (_I, [_P, _I, _I, C.POINTER(YsbCollectives)]),
     "ysb_group_exchange_info": (_I, [_P, C.POINTER(YsbExchangeInfo), _I]),
     "ysb_exchange_plan": (_I, [C.c_void_p, _U32, _U32, C.c_void_p, C.POINTER(_U32), C.POINTER(_U32)]),
     "ysb_group_checksum": (_I, [_P, _I, _U32, C.c_void_p]),

@@ -213,6 +213,36 @@ class YsbContext:
     def group_init(self, rank, nranks, uid: bytes):
         self._c(lib().ysb_group_init(self._h, rank, nranks, C.create_string_buffer(uid, _lib.UNIQUE_ID_BYTES)))
 
+    def group_init_host(self, rank, nranks, dist):
+        """ysb_group_init_host over torch.distributed (e.g. gloo) as the transport: the
+        library's exchange with the process group's collectives on host memory (N ranks on
+        one GPU, where RCCL refuses two ranks per device)."""
+        import torch
+
+        def amax(_user, buf, n):
+            try:
+                a = np.ctypeslib.as_array(buf, shape=(n,))
+                t = torch.from_numpy((a ^ np.uint64(1 << 63)).view(np.int64).copy())
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                a[:] = t.numpy().view(np.uint64) ^ np.uint64(1 << 63)
+                return 0
+            except Exception:   # noqa: BLE001 (a failing callback fails the call)
+                return 1
+
+        def rsum(_user, send, recv, count, width):
+            try:
+                cell = {1: np.uint8, 4: np.int32, 8: np.int64}[width]
+                nb = count * width
+                s_ = np.frombuffer((C.c_char * (nb * nranks)).from_address(send), dtype=cell).copy()
+                out = torch.zeros(count, dtype={1: torch.uint8, 4: torch.int32, 8: torch.int64}[width])
+                dist.reduce_scatter_tensor(out, torch.from_numpy(s_))
+                C.memmove(recv, out.numpy().ctypes.data, nb)
+                return 0
+            except Exception:   # noqa: BLE001
+                return 1
+        self._coll = _lib.YsbCollectives(_lib.ALLREDUCE_MAX_FN(amax), _lib.REDUCE_SCATTER_FN(rsum), None)
+        self._c(lib().ysb_group_init_host(self._h, rank, nranks, C.byref(self._coll)))
+
     def group_reduce_scatter(self):
         self._c(lib().ysb_group_reduce_scatter(self._h))
 
