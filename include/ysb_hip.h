@@ -338,6 +338,16 @@ int         ysb_group_init_host(ysb_ctx* ctx, int rank, int nranks, const ysb_co
  * fold): configs[2]'s 1M campaigns x 100 live buckets move 100 MB per rank and exchange
  * instead of the whole 1 GB u64 ring. */
 int         ysb_group_reduce_scatter(ysb_ctx* ctx);
+/* Collective, the streaming form of ysb_group_reduce_scatter: no wait for the device.  This
+ * call's per-bucket maxima are only enqueued (all-reduced and read back asynchronously);
+ * the buckets and width that travel are the PREVIOUS call's plan, read back while the
+ * step's scan ran.  Counts in buckets outside that plan, or larger than its width sums over
+ * the ranks, stay pending for a later exchange (nothing is lost or double counted; the
+ * owners' tables lag by at most one call).  The first call after ysb_group_init, ysb_reset
+ * or ysb_ring_advance is a complete ysb_group_reduce_scatter; a complete call settles
+ * everything (do one before reading the owned tables).  Every rank must use the same
+ * sequence of the two calls. */
+int         ysb_group_exchange_pipelined(ysb_ctx* ctx);
 /* Exchange accounting: exchanges run, reduce-scatter input bytes this rank contributed,
  * device time of the exchanges (HIP events on the compute stream around plan, all-reduce,
  * read-back, pack, reduce-scatter and unpack), the last exchange's bucket count and cell

@@ -123,8 +123,14 @@ struct ysb_ctx {
     int rank = 0, nranks = 1;
     // the range-limited exchange: per-slot maxima (all-reduced), the plan's slots, the packed
     // send / receive buffers, and its accounting (HIP event pairs, collected on request)
-    unsigned long long* d_xmax = nullptr;
-    unsigned long long* h_xmax = nullptr;
+    // Two plan buffers (device maxima; pinned host maxima + slots): a pipelined exchange
+    // packs with the previous call's plan (buffer xb, ready at xplan_ev[xb]) while its own
+    // plan is reduced into the other one.
+    unsigned long long* d_xmax = nullptr;   // [2][W]
+    unsigned long long* h_xmax = nullptr;   // [2][W] maxima, then [2][W] u32 slots
+    hipEvent_t xplan_ev[2] = {nullptr, nullptr};
+    int xb = 0;
+    bool x_have_plan = false;
     u32* d_xslots = nullptr;
     void* d_xsend = nullptr;
     void* d_xrecv = nullptr;
@@ -239,6 +245,8 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_dirty);
     hipFree(c->d_xmax);
     hipHostFree(c->h_xmax);
+    for (hipEvent_t e : c->xplan_ev)
+        if (e) hipEventDestroy(e);
     hipFree(c->d_xslots);
     hipFree(c->d_xsend);
     hipFree(c->d_xrecv);
@@ -1299,6 +1307,7 @@ int ysb_ring_advance(ysb_ctx* c, int64_t new_lo) {
         i64 h[2] = {new_lo, -new_lo};
         if ((rc = allreduce_max(c, h, 2))) return rc;
         if (h[0] != -h[1]) return fail(c, YSB_ERR_ARG, "ysb_ring_advance: ranks asked for different ring bases");
+        c->x_have_plan = false;   // the plan's slots held other buckets
     }
     if (new_lo <= INT64_MIN / 2 || new_lo >= INT64_MAX / 2) return fail(c, YSB_ERR_ARG, "ring base out of range");
     return move_ring(c, new_lo);
@@ -1334,6 +1343,7 @@ int ysb_reset(ysb_ctx* c) {
     c->delta_bound = 0;
     HIPCHK(c, hipMemset(c->d_dirty, 0, 4));
     c->pend_u64 = false;
+    c->x_have_plan = false;
     if (c->d_owned) HIPCHK(c, hipMemset(c->d_owned, 0, cells / c->nranks * 8));
     if (c->d_truth) HIPCHK(c, hipMemset(c->d_truth, 0, cells * 8));
     if (c->d_truth_out) HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
@@ -1575,9 +1585,11 @@ static int group_setup(ysb_ctx* c, int rank, int nranks) {
     HIPCHK(c, hipMalloc(&c->d_owned, per * 8));
     HIPCHK(c, hipMemset(c->d_owned, 0, per * 8));
     const u32 W = c->cfg.window_ring;
-    HIPCHK(c, hipMalloc(&c->d_xmax, (u64)W * 8));
-    HIPCHK(c, hipHostMalloc(&c->h_xmax, (u64)W * 8 + (u64)W * 4));   // maxima, then the plan's slots
+    HIPCHK(c, hipMalloc(&c->d_xmax, 2 * (u64)W * 8));
+    HIPCHK(c, hipHostMalloc(&c->h_xmax, 2 * ((u64)W * 8 + (u64)W * 4)));   // maxima, then the plans' slots
     HIPCHK(c, hipMalloc(&c->d_xslots, (u64)W * 4));
+    for (hipEvent_t& e : c->xplan_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->x_have_plan = false;
     // every rank's ring must start at the same bucket (the tables are summed cell by
     // cell): agreed here if any rank already knows its base, else at the first exchange
     return agree_ring(c);
@@ -1618,17 +1630,25 @@ int ysb_exchange_plan(const uint64_t* slot_max, uint32_t W, uint32_t nranks, uin
 // ring slots that hold a pending count on some rank travel, in the narrowest cell width
 // that cannot wrap, as the reference's keyed shuffle carries only the touched (campaign,
 // window) pairs.  Steps on the compute stream: per-slot maxima of the pending counts
-// (xplan) -> one W-element all-reduce(max) -> read back (the only host wait) -> plan
-// (ysb_exchange_plan: the same on every rank) -> pack the slots' cells [C_pad][R] and zero
-// them (xpack) -> ncclReduceScatter -> add the owner block into the owned table (xunpack).
-int ysb_group_reduce_scatter(ysb_ctx* c) {
-    if (!c) return YSB_ERR_ARG;
+// (xplan) -> one W-element all-reduce(max) -> read back -> plan (ysb_exchange_plan: the
+// same on every rank) -> pack the slots' cells [C_pad][R] and zero them (xpack) ->
+// ncclReduceScatter -> add the owner block into the owned table (xunpack).
+//
+// Complete (pipelined false): the plan is this call's, read back with a host wait; every
+// pending count travels.  Pipelined: this call's plan is only enqueued (reduced into the
+// other buffer, read back by an async copy) and the pack uses the previous call's plan,
+// whose read-back finished while the step's scan ran -- no host wait, so the next launch
+// queues behind the exchange without a gap.  Counts in slots outside that plan, or above
+// what its width sums over the ranks (cap), stay pending for a later exchange; the first
+// call after group init / reset / ring advance is complete.
+static int exchange(ysb_ctx* c, bool pipelined) {
     if (!grouped(c)) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->ring_agreed) {
         int rc = agree_ring(c);
         if (rc) return rc;
     }
+    if (!c->x_have_plan) pipelined = false;
     const u32 W = c->cfg.window_ring;
     const u64 cells = (u64)c->c_pad * W;
     const u8* delta = c->delta_bound ? c->d_delta : nullptr;   // (delta_bound 0: the delta ring is all zero)
@@ -1639,34 +1659,49 @@ int ysb_group_reduce_scatter(ysb_ctx* c) {
     }
     const auto ev = c->xev[c->xev_used++];
     HIPCHK(c, hipEventRecord(ev[0], c->s_comp));
-    HIPCHK(c, hipMemsetAsync(c->d_xmax, 0, (u64)W * 8, c->s_comp));
-    launch_xplan(c->d_counts, delta, W, cells, c->pend_u64 ? 1 : 0, c->d_dirty, c->d_xmax, c->s_comp);
+    // this call's plan into buffer nb
+    const int nb = c->xb ^ 1;
+    unsigned long long* dmax = c->d_xmax + (u64)nb * W;
+    unsigned long long* hmax = c->h_xmax + (u64)nb * W;
+    HIPCHK(c, hipMemsetAsync(dmax, 0, (u64)W * 8, c->s_comp));
+    launch_xplan(c->d_counts, delta, W, cells, c->pend_u64 ? 1 : 0, c->d_dirty, dmax, c->s_comp);
     HIPCHK(c, hipGetLastError());
-    int crc = coll_max_u64(c, c->d_xmax, W);
+    int crc = coll_max_u64(c, dmax, W);
     if (crc) return crc;
-    HIPCHK(c, hipMemcpyAsync(c->h_xmax, c->d_xmax, (u64)W * 8, hipMemcpyDeviceToHost, c->s_comp));
-    HIPCHK(c, hipStreamSynchronize(c->s_comp));
-    u32* slots = reinterpret_cast<u32*>(c->h_xmax + W);
+    HIPCHK(c, hipMemcpyAsync(hmax, dmax, (u64)W * 8, hipMemcpyDeviceToHost, c->s_comp));
+    HIPCHK(c, hipEventRecord(c->xplan_ev[nb], c->s_comp));
+    // the plan the pack uses: this one (complete) or the previous call's (pipelined)
+    const int pb = pipelined ? c->xb : nb;
+    HIPCHK(c, hipEventSynchronize(c->xplan_ev[pb]));
+    c->xb = nb;
+    c->x_have_plan = true;
+    u32* slots = reinterpret_cast<u32*>(c->h_xmax + 2 * (u64)W) + (u64)pb * W;
     u32 R = 0, width = 8;
-    if (ysb_exchange_plan(reinterpret_cast<const uint64_t*>(c->h_xmax), W, (u32)c->nranks, slots, &R, &width))
+    if (ysb_exchange_plan(reinterpret_cast<const uint64_t*>(c->h_xmax + (u64)pb * W), W, (u32)c->nranks, slots, &R,
+                          &width))
         return fail(c, YSB_ERR_CAPACITY, "pending counts too large to sum over %d ranks", c->nranks);
+    const unsigned long long cap = width == 8 ? ~0ull / (u64)c->nranks : ((1ull << (8 * width)) - 1) / (u64)c->nranks;
     const u32 rows = c->c_pad, per = c->c_pad / (u32)c->nranks;
     if (R) {
         int rc = grow_bytes(c, &c->d_xsend, &c->xsend_bytes, (u64)rows * R * width);
         if (!rc) rc = grow_bytes(c, &c->d_xrecv, &c->xrecv_bytes, (u64)per * R * width);
         if (rc) return rc;
+        // (the slots' pinned area is rewritten two calls later, after xplan_ev of the call
+        // in between: this copy has run by then)
         HIPCHK(c, hipMemcpyAsync(c->d_xslots, slots, (u64)R * 4, hipMemcpyHostToDevice, c->s_comp));
         launch_xpack(c->d_counts, delta ? c->d_delta : nullptr, W, rows, c->d_xslots, R, c->pend_u64 ? 1 : 0,
-                     c->d_dirty, c->d_xsend, width, c->s_comp);
+                     c->d_dirty, c->d_xsend, width, pipelined ? cap : ~0ull, c->s_comp);
         HIPCHK(c, hipGetLastError());
         if ((rc = coll_reduce_scatter(c, c->d_xsend, c->d_xrecv, (u64)per * R, width))) return rc;
         launch_xunpack(c->d_owned, W, per, c->d_xslots, R, c->d_xrecv, width, c->s_comp);
         HIPCHK(c, hipGetLastError());
     }
-    // every pending count sat in an exchanged slot: nothing is pending any more
-    HIPCHK(c, hipMemsetAsync(c->d_dirty, 0, 4, c->s_comp));
-    c->pend_u64 = false;
-    c->delta_bound = 0;
+    if (!pipelined) {
+        // every pending count sat in an exchanged slot: nothing is pending any more
+        HIPCHK(c, hipMemsetAsync(c->d_dirty, 0, 4, c->s_comp));
+        c->pend_u64 = false;
+        c->delta_bound = 0;
+    }
     HIPCHK(c, hipEventRecord(ev[1], c->s_comp));
     c->x_count++;
     c->x_bytes += (u64)rows * R * width;
@@ -1674,6 +1709,10 @@ int ysb_group_reduce_scatter(ysb_ctx* c) {
     c->x_last_width = R ? width : 0;
     return YSB_OK;
 }
+
+int ysb_group_reduce_scatter(ysb_ctx* c) { return c ? exchange(c, false) : YSB_ERR_ARG; }
+
+int ysb_group_exchange_pipelined(ysb_ctx* c) { return c ? exchange(c, true) : YSB_ERR_ARG; }
 
 int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
     if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;

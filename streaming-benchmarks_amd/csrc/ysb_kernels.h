@@ -200,7 +200,7 @@ void launch_fold(unsigned long long* counts, u8* delta, u64 cells, hipStream_t s
 void launch_xplan(const unsigned long long* counts, const u8* delta, u32 W, u64 cells, int force_u64,
                   const u32* dirty, unsigned long long* slot_max, hipStream_t s);
 void launch_xpack(unsigned long long* counts, u8* delta, u32 W, u32 rows, const u32* slots, u32 R, int force_u64,
-                  const u32* dirty, void* out, u32 width, hipStream_t s);
+                  const u32* dirty, void* out, u32 width, unsigned long long cap, hipStream_t s);
 void launch_xunpack(unsigned long long* owned, u32 W, u32 rows, const u32* slots, u32 R, const void* in, u32 width,
                     hipStream_t s);
 // Linear checksum of a campaign-major [rows][W] u64 table (row i = campaign c_off + i) over

@@ -150,27 +150,26 @@ __global__ __launch_bounds__(AUX_TPB) void xplan_kernel(const unsigned long long
         if (lmax[s]) atomicMax(&slot_max[s], lmax[s]);
 }
 
-// out[c][k] = pending(c, slots[k]) as `width`-byte cells; the sources zeroed.  One thread
-// per output cell: consecutive threads take consecutive slots of a campaign.
+// out[c][k] = pending(c, slots[k]) as `width`-byte cells, the sources zeroed -- except a
+// cell above `cap` (a pipelined exchange whose plan is one call old: the cell grew past what
+// the width can sum over the ranks), which stays pending for a later exchange and sends 0.
+// One thread per output cell: consecutive threads take consecutive slots of a campaign.
 __global__ __launch_bounds__(AUX_TPB) void xpack_kernel(unsigned long long* counts, u8* delta, u32 W, u32 rows,
                                                         const u32* slots, u32 R, int force_u64, const u32* dirty,
-                                                        void* out, u32 width) {
+                                                        void* out, u32 width, unsigned long long cap) {
     const bool r64 = read_u64(force_u64, dirty);
     const u64 n = (u64)rows * R;
     for (u64 i = (u64)blockIdx.x * AUX_TPB + threadIdx.x; i < n; i += (u64)gridDim.x * AUX_TPB) {
         const u32 c = (u32)(i / R), k = (u32)(i % R);
         const u64 cell = (u64)c * W + slots[k];
-        unsigned long long v = 0;
-        if (delta) {
-            v = delta[cell];
-            if (v) delta[cell] = 0;
-        }
-        if (r64) {
-            const unsigned long long x = counts[cell];
-            if (x) {
-                v += x;
-                counts[cell] = 0;
-            }
+        const unsigned long long d = delta ? delta[cell] : 0ull;
+        const unsigned long long x = r64 ? counts[cell] : 0ull;
+        unsigned long long v = d + x;
+        if (v > cap) {
+            v = 0;
+        } else {
+            if (d) delta[cell] = 0;
+            if (x) counts[cell] = 0;
         }
         if (width == 1) static_cast<u8*>(out)[i] = (u8)v;
         else if (width == 4) static_cast<u32*>(out)[i] = (u32)v;
@@ -220,11 +219,11 @@ void launch_xplan(const unsigned long long* counts, const u8* delta, u32 W, u64 
 }
 
 void launch_xpack(unsigned long long* counts, u8* delta, u32 W, u32 rows, const u32* slots, u32 R, int force_u64,
-                  const u32* dirty, void* out, u32 width, hipStream_t s) {
+                  const u32* dirty, void* out, u32 width, unsigned long long cap, hipStream_t s) {
     const u64 n = (u64)rows * R;
     if (!n) return;
     hipLaunchKernelGGL(xpack_kernel, dim3((unsigned)grid_for(n)), dim3(AUX_TPB), 0, s, counts, delta, W, rows, slots, R,
-                       force_u64, dirty, out, width);
+                       force_u64, dirty, out, width, cap);
 }
 
 void launch_xunpack(unsigned long long* owned, u32 W, u32 rows, const u32* slots, u32 R, const void* in, u32 width,

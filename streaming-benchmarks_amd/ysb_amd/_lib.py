@@ -128,6 +128,7 @@ SIGNATURES = {
     "ysb_group_unique_id": (_I, [C.c_char_p]),
     "ysb_group_init": (_I, [_P, _I, _I, C.c_char_p]),
     "ysb_group_reduce_scatter": (_I, [_P]),
+    "ysb_group_exchange_pipelined": (_I, [_P]),
     "ysb_group_init_host": (_I, [_P, _I, _I, C.POINTER(YsbCollectives)]),
     "ysb_group_exchange_info": (_I, [_P, C.POINTER(YsbExchangeInfo), _I]),
     "ysb_exchange_plan": (_I, [C.c_void_p, _U32, _U32, C.c_void_p, C.POINTER(_U32), C.POINTER(_U32)]),

@@ -244,7 +244,13 @@ class YsbContext:
         self._c(lib().ysb_group_init_host(self._h, rank, nranks, C.byref(self._coll)))
 
     def group_reduce_scatter(self):
+        """The complete exchange: every pending count reaches its owner."""
         self._c(lib().ysb_group_reduce_scatter(self._h))
+
+    def group_exchange_pipelined(self):
+        """The streaming exchange (ysb_group_exchange_pipelined): no host wait, packs with the
+        previous call's plan; what it leaves pending travels with a later exchange."""
+        self._c(lib().ysb_group_exchange_pipelined(self._h))
 
     def exchange_info(self, reset=False):
         """Exchange accounting (ysb_group_exchange_info): exchanges, bytes, ms, last_buckets,

@@ -71,6 +71,56 @@ def config3(rank, world, res):
         res["per_rank"] = per
 
 
+def pipelined(rank, world, res):
+    """ysb_group_exchange_pipelined: a step whose counts outgrow the previous plan's width
+    (held back by the cap) and fill buckets outside it (held back by the plan), then steps
+    that catch up, then a complete exchange.  After every exchange: owned + pending = truth,
+    summed over the ranks, per owner block."""
+    C = 1000
+    base = GenParams(seed=7, n_campaigns=C, ads_per_campaign=10, events_per_sec=100_000)
+    _, ab = base.ids_packed()
+    subset = np.nonzero(shard_packed(ab, world) == rank)[0].astype(np.uint32)
+    g = GenParams(seed=7, event_stream=1 + rank, n_campaigns=C, ads_per_campaign=10, events_per_sec=100_000,
+                  ad_subset=subset)
+    W = 128
+    n = 2_000_000
+    # step ranges: 1 s of events (small cells: a 1-byte plan), the next 19 s (cells past
+    # the 1-byte cap, a second bucket), nothing new (catch up), the complete exchange
+    ranges = [(0, 100_000), (100_000, n), None, None]
+    kinds = ["pipelined", "pipelined", "pipelined", "complete"]
+    res["log"] = []
+    with YsbContext(device=0, n_campaigns=C, window_ring=W, ring_base_bucket=g.c.t0_ms // 10000 - W // 8,
+                    max_batch_bytes=1 << 20, max_batch_events=1 << 12, record_count=True, strict=True) as ctx:
+        ctx.load_ad_map_packed(ab, base.ad_campaign_index_array(), shard=(rank, world))
+        ctx.group_init_host(rank, world, dist)
+        segs = {}
+        for rg in ranges:
+            if rg is not None:
+                f, t = rg
+                cap = (t - f) * g.max_line_bytes()
+                d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * (t - f) + 64)
+                segs[rg] = (d_b, ctx.gen_events_device(g, f, t - f, d_b, cap, d_o), d_o, t - f)
+        ctx.group_reduce_scatter()   # the first exchange is complete anyway: agree the ring
+        for rg, kind in zip(ranges, kinds):
+            if rg is not None:
+                ctx.submit_device_segments([segs[rg]])
+                ctx.truth_accumulate(g, rg[0], rg[1] - rg[0])
+            (ctx.group_exchange_pipelined if kind == "pipelined" else ctx.group_reduce_scatter)()
+            x = ctx.exchange_info(reset=True)
+            tsum = ctx.checksum("truth", world)
+            own = ctx.checksum("owned")[0]
+            pend = ctx.checksum("pending", world)
+            per = [None] * world
+            dist.all_gather_object(per, {"tsum": tsum, "own": own, "pend": pend})
+            bad = sum((sum(p["tsum"][r] for p in per) & M64) != ((per[r]["own"] + sum(p["pend"][r] for p in per)) & M64)
+                      for r in range(world))
+            res["log"].append({"kind": kind, "bad_blocks": bad, "pending_nonzero": any(any(p["pend"]) for p in per),
+                               "width": x["last_width"], "buckets": x["last_buckets"]})
+        # (the local ring is empty now: everything went to the owners)
+        _, truth, ring = ctx.truth_compare()
+        res["views"] = {"truth": truth, "ring": ring, "owned": sum(ctx.drain_buckets().values())}
+
+
 def config2(rank, world, res):
     """bench.py's own N > 1 config-2 workload (100 campaigns, LDS window counters, the u64
     ring), run through bench.exchange_check -- owners' rows against the truth summed over
@@ -110,7 +160,7 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = {"rank": rank}
-    {"config3": config3, "config2": config2}[scenario](rank, world, res)
+    {"config3": config3, "config2": config2, "pipelined": pipelined}[scenario](rank, world, res)
     dist.barrier()
     dist.destroy_process_group()
     with open(out_path, "w") as f:

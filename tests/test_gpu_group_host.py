@@ -70,3 +70,17 @@ def test_n_ranks_bench_exchange_check_config2(tmp_path):
     assert ex["ring_bases_equal"] and ex["rccl_ranks"] == [2]
     for r in res:
         assert r["steps"]["exchanges"] == 2 and r["steps"]["width"] == 4   # config-2 cells: thousands of views
+
+
+@pytest.mark.timeout(300)
+def test_n_ranks_pipelined_exchange_holds_back_then_settles(tmp_path):
+    res = run("pipelined", 2, tmp_path)
+    for r in res:
+        log = r["log"]
+        assert [e["bad_blocks"] for e in log] == [0, 0, 0, 0]     # owned + pending = truth after every call
+        assert log[0]["buckets"] == 0 and log[0]["pending_nonzero"]   # packs the agreeing call's empty plan
+        assert log[1]["pending_nonzero"]        # outgrew step 0's 1-byte plan / new buckets: held back
+        assert log[2]["width"] == 4 and log[2]["buckets"] >= 2 and not log[2]["pending_nonzero"]   # caught up
+        assert log[3]["buckets"] == 0 and not log[3]["pending_nonzero"]
+        assert r["views"]["ring"] == 0
+    assert sum(r["views"]["owned"] for r in res) == sum(r["views"]["truth"] for r in res) > 0
