@@ -703,6 +703,9 @@ __device__ __forceinline__ bool vocab_stage2(const LdsSrc& src, int s, int e, co
 // other row is deferred to process_tbl_line.  Same two-batch shape as the JSON path.
 // ---------------------------------------------------------------------------
 constexpr int TBL_WORDS = 40;                          // bytes 0..159 of the line
+#ifndef YSB_TBL_READ64
+#define YSB_TBL_READ64 0     // round 3 A/B: 1 (ds_read2_b64) -2 %, 2 (ds_read_b64) -1 %
+#endif
 #ifndef YSB_TBL_ZCMP
 #define YSB_TBL_ZCMP 1
 #endif
@@ -719,11 +722,30 @@ __device__ __forceinline__ u32 bar_nib(u32 w) {
 __device__ __forceinline__ bool tbl_stage1(const LdsSrc& src, int s, int e, CanonA& c) {
     const int L = e - s;
     if (L < TBL_MIN_LEN || L > TBL_MAX_LEN) return false;
-    const int a = s >> 2;
     const u32 sb = (u32)(s & 3);
     u32 P[TBL_WORDS + 1];
+#if YSB_TBL_READ64
+    // 8-byte reads (ds_read_b64: half the instructions of dword reads, banks (a/4) mod 64)
+    // from the row start rounded down to 8 bytes, then one dword select per word
+    const int a8 = s >> 3;
+    const u32 odd = 0u - (u32)((s >> 2) & 1);   // all ones: the row starts in the pair's upper dword
+    u32 R[TBL_WORDS + 2];
+#pragma unroll
+    for (int k = 0; k < TBL_WORDS / 2 + 1; ++k) {
+        const uint2 v = reinterpret_cast<const uint2*>(src.d)[a8 + k];
+#if YSB_TBL_READ64 == 2
+        asm volatile("" ::: "memory");   // keep ds_read_b64 (paired into ds_read2_b64: 8 cycles, banks mod 32)
+#endif
+        R[2 * k] = v.x;
+        R[2 * k + 1] = v.y;
+    }
+#pragma unroll
+    for (int k = 0; k <= TBL_WORDS; ++k) P[k] = (R[k] & ~odd) | (R[k + 1] & odd);   // v_bfi, not an indexed select
+#else
+    const int a = s >> 2;
 #pragma unroll
     for (int k = 0; k <= TBL_WORDS; ++k) P[k] = src.d[a + k];
+#endif
     u32 W[TBL_WORDS];
     u32 B[5] = {0u, 0u, 0u, 0u, 0u};   // bit i = line byte i may be '|'
 #if YSB_TBL_ZCMP
@@ -757,6 +779,49 @@ __device__ __forceinline__ bool tbl_stage1(const LdsSrc& src, int s, int e, Cano
     // the first three '|' exactly at 36, 73, 110 (each the lowest flag of its word: true)
     const bool fixed = B[0] == 0u && B[1] == (1u << 4) && B[2] == (1u << 9) && (B[3] & 0x7FFFu) == (1u << 14);
 #endif
+    const u64 hi = ((u64)B[4] << 32) | (B[3] & ~0x7FFFu);   // bytes 96..159, above 110
+    const int p3 = hi ? 96 + (int)__builtin_ctzll(hi) : (1 << 20);
+    const u64 hi2 = hi & (hi - 1);
+    const int p4 = hi2 ? 96 + (int)__builtin_ctzll(hi2) : (1 << 20);
+    c.e3 = p3;
+    c.e4 = p4;
+    c.e5 = (int)B[3];
+    c.e6 = (int)B[4];
+    c.t0 = p4 + 1;
+    return fixed && p4 + 2 <= L;
+}
+
+// Phase A of a .tbl tile: the 16 '|' flags of a 16-byte chunk (bit i = byte i may be '|',
+// the SWAR flags of bar_nib: a flag above a true '|' in its dword may be false).
+__device__ __forceinline__ u32 bar_chunk(const uint4& v) {
+    return bar_nib(v.x) | (bar_nib(v.y) << 4) | (bar_nib(v.z) << 8) | (bar_nib(v.w) << 12);
+}
+
+// tbl_stage1 from the tile's '|' bitmap (Geom::BITMAP): the row's flags for bytes 0..159
+// are 5 dwords of the bitmap shifted by the row's start (6 LDS reads instead of the row's
+// 41), the ad_id's 36 bytes 10 more.  The flags are those of tile dwords, not row dwords,
+// so a false flag may sit on any byte right above a true '|': the fixed-position checks
+// only reject on an extra flag, and p3 / p4 are verified to be '|' in tbl_stage2, as there.
+__device__ __forceinline__ bool tbl_stage1_bm(const LdsSrc& src, const u32* bm, int s, int e, CanonA& c) {
+    const int L = e - s;
+    if (L < TBL_MIN_LEN || L > TBL_MAX_LEN) return false;
+    const int wb = s >> 5;
+    const u32 sh = (u32)(s & 31);
+    u32 M[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) M[k] = bm[wb + k];
+    u32 B[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) B[k] = __builtin_amdgcn_alignbit(M[k + 1], M[k], sh);   // row bytes 32k..32k+31
+    const int ka = (s + 74) >> 2;
+    const u32 kb = (u32)((s + 74) & 3);
+    u32 Q[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) Q[k] = src.d[ka + k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(Q[k + 1], Q[k], kb);   // bytes 74..109
+    // the first three '|' exactly at 36, 73, 110, nothing else flagged below 110
+    const bool fixed = B[0] == 0u && B[1] == (1u << 4) && B[2] == (1u << 9) && (B[3] & 0x7FFFu) == (1u << 14);
     const u64 hi = ((u64)B[4] << 32) | (B[3] & ~0x7FFFu);   // bytes 96..159, above 110
     const int p3 = hi ? 96 + (int)__builtin_ctzll(hi) : (1 << 20);
     const u64 hi2 = hi & (hi - 1);
@@ -1464,6 +1529,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
     u32* lcnt = reinterpret_cast<u32*>(smem + G::OFF_LCNT);
     i64* misc64 = reinterpret_cast<i64*>(smem + G::OFF_MISC);   // [0] lbase, [1] lset, [2..5] scratch
     u32* tb = reinterpret_cast<u32*>(smem + G::OFF_TB);
+    u32* bm32w = reinterpret_cast<u32*>(smem + G::OFF_BM);   // .tbl '|' bitmap (G::BITMAP)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1536,6 +1602,14 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 if (j * SCAN_TPB + SCAN_TPB <= G::CHUNKS || k < (u32)G::CHUNKS) {
                     reinterpret_cast<uint4*>(tile32)[k] = pre[j];
                 }
+                if constexpr (G::BITMAP && YSB_TBL_BITMAP != 3) {
+                    // chunk k's 16 flags -> bitmap halfword k: the odd lane's flags join the
+                    // even lane's (DPP swap within pairs), one dword store per pair
+                    const u32 f = bar_chunk(pre[j]);
+                    const u32 fo = (u32)__builtin_amdgcn_mov_dpp((int)f, 0xB1, 0xF, 0xF, false);   // quad_perm(1,0,3,2)
+                    if (!(tid & 1) && (j * SCAN_TPB + SCAN_TPB <= G::CHUNKS || k < (u32)G::CHUNKS))
+                        bm32w[k >> 1] = f | (fo << 16);
+                }
             }
         }
         // The previous tile asked to move the LDS window: flush it (its counts are all
@@ -1572,7 +1646,8 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             elig = true;
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
-            if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
+            if constexpr (G::BITMAP && YSB_TBL_BITMAP == 1) ok1 = tbl_stage1_bm(lsrc, bm32w, ls, le, ca);
+            else if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
             else if constexpr (LAY == 2) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb);
             else if constexpr (LAY == 3) {
                 ok1 = P.learn_cp ? learned_parse<true>(lsrc, ls, le, P, ca, cb) : learned_parse<false>(lsrc, ls, le, P, ca, cb);
