@@ -24,6 +24,12 @@ namespace ysb {
 int scan_lds_bytes();
 }
 
+// HBM-resident join table (bucket layout): buckets per key, x4 (8: 2 per key, a 4 GiB
+// table at 10M ads; fewer buckets -> a smaller table, more keys in their second bucket)
+#ifndef YSB_BUCKETS_X4
+#define YSB_BUCKETS_X4 8
+#endif
+
 // A key order read off a batch's first line (layout 3, learn_layout).
 struct LearnDesc {
     u32 order[8];
@@ -497,8 +503,9 @@ static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
     // tables far beyond the L2s (32 MiB) go to HBM per probe: bucket layout
     const bool buckets = cslots * CSLOT_WORDS * 4 > (64ull << 20);
     if (buckets) {
+        // buckets >= YSB_BUCKETS_X4 / 4 per key (3 entries each)
         cslots = 64;
-        while (cslots < 2 * keys36.size()) cslots <<= 1;
+        while (cslots * 4 < (u64)YSB_BUCKETS_X4 * keys36.size()) cslots <<= 1;
     }
     const u32 unit = buckets ? CB_WORDS : CSLOT_WORDS;
     std::vector<u32> kw, cv;   // bucket layout: the keys as words, their campaigns

@@ -54,7 +54,9 @@ constexpr int REC_RING = 64;          // staged records per bin (two 128-B lines
 template <bool TBL, bool REC = false>
 struct Geom {
     static constexpr int WG_PER_CU = TBL ? YSB_TBL_WG_PER_CU : SCAN_WG_PER_CU;
-    static constexpr int CAP = TILE_LINES * (TBL ? YSB_TBL_LINE_BYTES : YSB_TILE_LINE_BYTES);
+    // (.tbl record mode: 8 B less per row, so its record staging lines fit 12 workgroups per
+    // CU in whole LDS granules; the generator's rows average 140 B, at most 151)
+    static constexpr int CAP = TILE_LINES * (TBL ? YSB_TBL_LINE_BYTES - (REC ? 8 : 0) : YSB_TILE_LINE_BYTES);
     static constexpr int CHUNKS = CAP / 16;
     static constexpr int CPT = (CHUNKS + SCAN_TPB - 1) / SCAN_TPB;   // 16-byte chunks per thread
     static constexpr int OFF_TILE = 0;

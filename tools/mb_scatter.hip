@@ -14,7 +14,9 @@
 //   mode 6: 48-B random reads of a 4 GiB table, consumed in the same tile (probe)
 //   mode 7: like 6, consumed one tile later (pipelined probe)
 //   mode 10: 128-B bucket reads (one 128-B line per probe); 11: 48-B probes plus, for 1 in
-//   13 lanes, a dependent second probe (serial cuckoo); 12: 64-B probes
+//   13 lanes, a dependent second probe (serial cuckoo); 12: 64-B probes; 13 (argument 13): 128-B
+//   bucket probes vs table size, 64 MiB .. 4 GiB (does a table that fits the 256 MiB Infinity
+//   Cache stay resident beside the nontemporal stream?)
 //
 //   hipcc --offload-arch=gfx950 -O3 -o mb_scatter tools/mb_scatter.hip && ./mb_scatter
 #include <hip/hip_runtime.h>
@@ -104,6 +106,14 @@ __global__ __launch_bounds__(64) void k(const unsigned char* __restrict__ buf, u
                 acc += a2.x ^ b2.y ^ c2.z;
             }
         }
+        if (MODE == 13 && act) {   // a 128-B bucket of a table of probe_mask buckets (any count)
+            const uint4* p = probe_tab + 8 * (((h >> 32) * probe_mask) >> 32);   // multiply-shift range reduction
+            uint4 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = p[q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc += v[q].x ^ v[q].w;
+        }
         if (MODE == 12 && act) {   // 64-B probe: 4 x 16 B of one 64-B slot
             const uint4* p = probe_tab + 4 * (h & probe_mask);
             const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
@@ -176,6 +186,23 @@ int main(int argc, char** argv) {
                            "128-B bucket probes (8 loads)", "48-B probes + 1/13 dependent 2nd",
                            "64-B probes (4 loads)"};
     int only = argc > 1 ? atoi(argv[1]) : -1;
+    if (only == 13) {   // 128-B bucket probes beside the stream vs table size (Infinity Cache residency)
+        for (u64 mib : {64ull, 128ull, 192ull, 224ull, 256ull, 320ull, 512ull, 1024ull, 4096ull}) {
+            const u64 nb = mib << 13;   // 128-B buckets
+            float best = 1e9;
+            for (int rep = 0; rep < 6; ++rep) {
+                hipEventRecord(a);
+                hipLaunchKernelGGL(k<13>, dim3(grid), dim3(64), 0, 0, buf, tpw, table, (u32*)table, cells - 1, rec, rec_cap, sink, probe, nb);
+                hipEventRecord(b);
+                hipEventSynchronize(b);
+                float ms;
+                hipEventElapsedTime(&ms, a, b);
+                if (rep > 0 && ms < best) best = ms;
+            }
+            printf("128-B bucket probes into %llu MiB beside the stream: %.3f ms\n", mib, best);
+        }
+        only = 0;   // and the stream alone
+    }
     if (only == 6) {   // probe cost vs table size
         for (u64 sz : {1ull << 26, 1ull << 24, 1ull << 22, 1ull << 21, 1ull << 20}) {
             float best = 1e9;
