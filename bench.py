@@ -303,16 +303,14 @@ def timed_extra(name, ctx, g, segs, steps, warmup, kernel):
     alg = nbytes + 4 * events
     avg = kms / max(launches, 1)
     path = pms / max(launches, 1)
-    step_ms = el / steps * 1e3
-    ach = alg / (step_ms * 1e-3) / 1e9
+    ach = alg / (path * 1e-3) / 1e9
     return {"workload": name, "events": events, "bytes_per_event": round(nbytes / events, 3),
-            "events_per_s": round(events * steps / el, 1), "ms_per_step": round(step_ms, 4),
+            "events_per_s": round(events * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
             "kernel": kernel, "avg_launch_ms": round(avg, 4),
             "avg_path_ms": round(path, 4), "record_mode": nrec > 0,
             "alg_GBs": round(ach, 1), "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
-            "note": "alg_GBs / hbm_frac over the whole step (ms_per_step: scan, general path and, in record "
-                    "mode, the partition + count kernels, which run beside the next launch's scan); "
-                    "avg_path_ms: one launch's device sequence from its scan's start to its count's end",
+            "note": "alg_GBs / hbm_frac over the launch's whole device sequence (scan, general path and, "
+                    "in record mode, the partition + count kernels: avg_path_ms)",
             "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
                       "join_misses": st["join_misses"], "parse_errors": st["parse_errors"],
                       "deferred": st["deferred"], "out_of_ring": st["out_of_ring"],

@@ -99,27 +99,16 @@ struct ysb_ctx {
     size_t tev_used = 0;
     double path_ms_acc = 0;                // ysb_path_time's share, collected by ysb_kernel_time
     u64 path_launches_acc = 0;
-    // record mode (ysb_count.hip).  Two sets of the record buffers: with rec_overlap the
-    // partition + count kernels of launch k run on s_rec while the scan of launch k + 1 (the
-    // other set) runs on s_comp; a launch into a set first waits for that set's last count
-    // (ev_rec_done[set]), and anything else that reads the rings joins s_rec first (join_rec)
-    u32* d_rec[2] = {nullptr, nullptr};
-    u64 rec_words[2] = {0, 0};
-    u32* d_rec_n[2] = {nullptr, nullptr};
-    u64 rec_n_words[2] = {0, 0};
-    u32* d_part[2] = {nullptr, nullptr};
-    u64 part_words[2] = {0, 0};
-    u32* d_runs[2] = {nullptr, nullptr};
-    u64 runs_words[2] = {0, 0};
+    // record mode (ysb_count.hip)
+    u32* d_rec = nullptr;
+    u64 rec_words = 0;
+    u32* d_rec_n = nullptr;
+    u64 rec_n_words = 0;
+    u32* d_part = nullptr;
+    u64 part_words = 0;
+    u32* d_runs = nullptr;
+    u64 runs_words = 0;
     u64 rec_launches = 0;
-    bool rec_overlap = true;               // YSB_REC_OVERLAP=0: partition + count on s_comp
-    hipStream_t s_rec = nullptr;
-    int rec_prio = 0;                      // s_rec's priority (YSB_REC_PRIO: s_comp the greatest, s_rec the least)
-    hipEvent_t ev_scan_done[2] = {nullptr, nullptr}, ev_rec_done[2] = {nullptr, nullptr};
-    bool rec_busy[2] = {false, false};     // ev_rec_done[set] recorded and maybe not yet waited on
-    int rec_set = 0;                       // the set the next record-mode launch uses
-    int rec_last = -1;                     // the set of the last launch whose count ran on s_rec
-    bool rec_pending = false;              // s_comp has not yet joined that count
     // record mode counts into a saturating u8 delta ring with the u64 ring's layout (a cell
     // passing 255 goes to the u64 ring, ysb_count.hip add16); fold_delta adds it to the u64
     // ring before anything reads that.  delta_bound: events counted into it since the last
@@ -193,23 +182,6 @@ static int fail(ysb_ctx* c, int code, const char* fmt, ...) {
                         __LINE__);                                                                \
     } while (0)
 
-// s_comp waits for the last count kernel queued on s_rec (record mode with overlap):
-// called before anything on s_comp reads or writes the u64 / delta rings or d_dirty.
-static int join_rec(ysb_ctx* c) {
-    if (!c->rec_pending) return YSB_OK;
-    HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_rec_done[c->rec_last], 0));
-    c->rec_pending = false;
-    return YSB_OK;
-}
-
-// s_comp synchronised, the record-mode counts queued on s_rec included.
-#define COMP_SYNC(ctx)                                                                          \
-    do {                                                                                        \
-        const int jr_ = join_rec(ctx);                                                          \
-        if (jr_) return jr_;                                                                    \
-        HIPCHK(ctx, hipStreamSynchronize((ctx)->s_comp));                                       \
-    } while (0)
-
 static bool is_pow2(u64 x) { return x && !(x & (x - 1)); }
 static u32 log2u(u64 x) { u32 l = 0; while (((u64)1 << l) < x) ++l; return l; }
 
@@ -243,7 +215,6 @@ static void destroy(ysb_ctx* c) {
     hipSetDevice(c->device);
     if (c->s_comp) hipStreamSynchronize(c->s_comp);
     if (c->s_copy) hipStreamSynchronize(c->s_copy);
-    if (c->s_rec) hipStreamSynchronize(c->s_rec);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_table);
     hipFree(c->d_ctable);
@@ -274,15 +245,8 @@ static void destroy(ysb_ctx* c) {
         if (c->ev_kdone[s]) hipEventDestroy(c->ev_kdone[s]);
     }
     for (auto& p : c->tev) for (hipEvent_t e : p) hipEventDestroy(e);
-    for (int k = 0; k < 2; ++k) {
-        hipFree(c->d_rec[k]);
-        hipFree(c->d_rec_n[k]);
-        hipFree(c->d_part[k]);
-        hipFree(c->d_runs[k]);
-        if (c->ev_scan_done[k]) hipEventDestroy(c->ev_scan_done[k]);
-        if (c->ev_rec_done[k]) hipEventDestroy(c->ev_rec_done[k]);
-    }
-    if (c->s_rec) hipStreamDestroy(c->s_rec);
+    hipFree(c->d_rec);
+    hipFree(c->d_rec_n);
     hipFree(c->d_delta);
     hipFree(c->d_dirty);
     hipFree(c->d_xmax);
@@ -293,6 +257,8 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_xsend);
     hipFree(c->d_xrecv);
     for (auto& p : c->xev) for (hipEvent_t e : p) hipEventDestroy(e);
+    hipFree(c->d_part);
+    hipFree(c->d_runs);
     if (c->ev_ring) hipEventDestroy(c->ev_ring);
     hipHostFree(c->h_sample);
     hipHostFree(c->h_used);
@@ -348,13 +314,7 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
         if (v > 0 && v < c->delta_limit) c->delta_limit = v;
     }
     if (const char* e = getenv("YSB_DYN_CHUNK")) c->dyn_chunk = (u32)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("YSB_REC_OVERLAP")) c->rec_overlap = strtoul(e, nullptr, 10) != 0;
-    int prio_lo = 0, prio_hi = 0;
-    const bool rec_prio = getenv("YSB_REC_PRIO") && strtoul(getenv("YSB_REC_PRIO"), nullptr, 10) != 0;
-    if (rec_prio) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    c->rec_prio = prio_lo;
-    if ((rec_prio ? hipStreamCreateWithPriority(&c->s_comp, hipStreamNonBlocking, prio_hi)
-                  : hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking)) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking) != hipSuccess) {
         fail(c, YSB_ERR_HIP, "stream creation failed");
         return bad(YSB_ERR_HIP);
@@ -512,7 +472,7 @@ static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         }
     }
     HIPCHK(c, hipSetDevice(c->device));
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     if (slots != c->table_slots) {
         hipFree(c->d_table);
         c->d_table = nullptr;
@@ -724,8 +684,7 @@ static void poll_ring(ysb_ctx* c) {
 // Grows a device u32 buffer to at least `words` (contents not kept).
 static int grow_u32(ysb_ctx* c, u32** buf, u64* have, u64 words) {
     if (*have >= words) return YSB_OK;
-    COMP_SYNC(c);
-    if (c->s_rec) HIPCHK(c, hipStreamSynchronize(c->s_rec));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     hipFree(*buf);
     *buf = nullptr;
     *have = 0;
@@ -736,8 +695,6 @@ static int grow_u32(ysb_ctx* c, u32** buf, u64* have, u64 words) {
 
 // The delta ring into the u64 ring (queued on the compute stream), delta cleared.
 static int fold_delta(ysb_ctx* c) {
-    int jrc = join_rec(c);
-    if (jrc) return jrc;
     if (!c->d_delta || c->delta_bound == 0) return YSB_OK;
     launch_fold(c->d_counts, c->d_delta, c->delta_cells, c->s_comp);
     HIPCHK(c, hipGetLastError());
@@ -786,14 +743,13 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     r.cap = (u32)cap;
     r.area = area;
     int rc;
-    const int k = c->rec_set;
-    if ((rc = grow_u32(c, &c->d_rec[k], &c->rec_words[k], (u64)r.grid * r.bins * cap))) return rc;
-    if ((rc = grow_u32(c, &c->d_rec_n[k], &c->rec_n_words[k], (u64)r.grid * r.bins))) return rc;
-    if ((rc = grow_u32(c, &c->d_part[k], &c->part_words[k], part))) return rc;
-    if ((rc = grow_u32(c, &c->d_runs[k], &c->runs_words[k], (u64)r.n_blocks * REC_QUARTERS * 2))) return rc;
+    if ((rc = grow_u32(c, &c->d_rec, &c->rec_words, (u64)r.grid * r.bins * cap))) return rc;
+    if ((rc = grow_u32(c, &c->d_rec_n, &c->rec_n_words, (u64)r.grid * r.bins))) return rc;
+    if ((rc = grow_u32(c, &c->d_part, &c->part_words, part))) return rc;
+    if ((rc = grow_u32(c, &c->d_runs, &c->runs_words, (u64)r.n_blocks * REC_QUARTERS * 2))) return rc;
     if (c->delta_cells != cells) {   // the delta ring: the u64 ring's layout, one byte a cell, zeroed
         if ((rc = fold_delta(c))) return rc;
-        COMP_SYNC(c);
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
         hipFree(c->d_delta);
         c->d_delta = nullptr;
         c->delta_cells = 0;
@@ -809,16 +765,16 @@ static int plan_records(ysb_ctx* c, ScanParams& p, u64 n_events, RecParams& r) {
     r.delta = c->d_delta;
     r.counts = c->d_counts;
     r.dirty = c->d_dirty;
-    r.rec = c->d_rec[k];
-    r.rec_n = c->d_rec_n[k];
-    r.part = c->d_part[k];
-    r.runs = c->d_runs[k];
+    r.rec = c->d_rec;
+    r.rec_n = c->d_rec_n;
+    r.part = c->d_part;
+    r.runs = c->d_runs;
     p.rec_on = 1;
     p.rec_bins = r.bins;
     p.rec_shift = r.blk_shift + r.sub_log2;
     p.rec_cap = r.cap;
-    p.rec = c->d_rec[k];
-    p.rec_n = c->d_rec_n[k];
+    p.rec = c->d_rec;
+    p.rec_n = c->d_rec_n;
     return YSB_OK;
 }
 
@@ -832,7 +788,7 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     if (n == 0) { c->batches += nin; return YSB_OK; }
     if (n >= (1ull << 31)) return fail(c, YSB_ERR_CAPACITY, "at most 2^31-1 events per launch");
     if (n > c->defer_cap) {   // the deferred-line list can hold every line of a batch
-        COMP_SYNC(c);
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
         hipFree(c->d_defer);
         c->d_defer = nullptr;
         const u64 cap = std::max<u64>(n, 1u << 16);
@@ -884,21 +840,6 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     RecParams rp{};
     int rc = plan_records(c, p, n, rp);
     if (rc) return rc;
-    const bool overlap = p.rec_on && c->rec_overlap;
-    const int rset = c->rec_set;
-    if (overlap) {
-        if (!c->s_rec) {
-            HIPCHK(c, hipStreamCreateWithPriority(&c->s_rec, hipStreamNonBlocking, c->rec_prio));
-            for (int k = 0; k < 2; ++k) {
-                HIPCHK(c, hipEventCreateWithFlags(&c->ev_scan_done[k], hipEventDisableTiming));
-                HIPCHK(c, hipEventCreateWithFlags(&c->ev_rec_done[k], hipEventDisableTiming));
-            }
-        }
-        // this set's buffers are free once the count of the launch before last is done
-        if (c->rec_busy[rset]) HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_rec_done[rset], 0));
-    } else if (p.rec_on) {
-        if ((rc = join_rec(c))) return rc;   // the count kernels below run on s_comp again
-    }
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (c->cfg.flags & YSB_F_TIMING) {
         if (c->tev_used == c->tev.size()) {
@@ -923,27 +864,14 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     if (e1) HIPCHK(c, hipEventRecord(e1, c->s_comp));
     launch_defer(p, c->cus, c->s_comp);
     HIPCHK(c, hipGetLastError());
-    hipStream_t s_cnt = overlap ? c->s_rec : c->s_comp;
-    if (overlap) {
-        // partition + count of this launch on s_rec, beside the next launch's scan
-        HIPCHK(c, hipEventRecord(c->ev_scan_done[rset], c->s_comp));
-        HIPCHK(c, hipStreamWaitEvent(c->s_rec, c->ev_scan_done[rset], 0));
-    }
     if (p.rec_on) {
-        launch_rec_partition(rp, s_cnt);
+        launch_rec_partition(rp, c->s_comp);
         HIPCHK(c, hipGetLastError());
-        launch_rec_count(rp, s_cnt);
+        launch_rec_count(rp, c->s_comp);
         HIPCHK(c, hipGetLastError());
         c->rec_launches++;
     }
-    if (e2) HIPCHK(c, hipEventRecord(e2, s_cnt));
-    if (overlap) {
-        HIPCHK(c, hipEventRecord(c->ev_rec_done[rset], c->s_rec));
-        c->rec_busy[rset] = true;
-        c->rec_last = rset;
-        c->rec_pending = true;
-        c->rec_set = rset ^ 1;
-    }
+    if (e2) HIPCHK(c, hipEventRecord(e2, c->s_comp));
     if (p.used_out) {   // defer_kernel wrote the map's fill level into h_used
         HIPCHK(c, hipEventRecord(c->ev_used, c->s_comp));
         c->used_pending = true;
@@ -1177,10 +1105,7 @@ int ysb_submit_device_segments(ysb_ctx* c, const ysb_segment* segs, uint32_t n_s
 static int sync_streams(ysb_ctx* c) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->s_copy));
-    const int jrc = join_rec(c);
-    if (jrc) return jrc;
-    COMP_SYNC(c);
-    if (c->s_rec) HIPCHK(c, hipStreamSynchronize(c->s_rec));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     poll_ring(c);
     return YSB_OK;
 }
@@ -1252,7 +1177,7 @@ static int pull_side_list(ysb_ctx* c) {
         HIPCHK(c, hipMemsetAsync(c->d_rows_n, 0, 4, c->s_comp));
         launch_side_compact(c->d_side, c->side_slots, c->side_cbits, true, nullptr, c->d_rows_n, 0, c->s_comp);
         HIPCHK(c, hipMemcpyAsync(&k, c->d_rows_n, 4, hipMemcpyDeviceToHost, c->s_comp));
-        COMP_SYNC(c);
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
         if (k > c->rows_cap) {
             hipFree(c->d_rows);
             c->d_rows = nullptr;
@@ -1265,12 +1190,12 @@ static int pull_side_list(ysb_ctx* c) {
             HIPCHK(c, hipMemsetAsync(c->d_rows_n, 0, 4, c->s_comp));
             launch_side_compact(c->d_side, c->side_slots, c->side_cbits, false, c->d_rows, c->d_rows_n, k, c->s_comp);
             HIPCHK(c, hipMemcpyAsync(h.data(), c->d_rows, (u64)k * sizeof(TableRow), hipMemcpyDeviceToHost, c->s_comp));
-            COMP_SYNC(c);
+            HIPCHK(c, hipStreamSynchronize(c->s_comp));
             for (const TableRow& r : h) c->side[{r.campaign, r.bucket}] += r.count;
         }
         launch_side_clear(c->d_side, c->side_slots, c->s_comp);
         HIPCHK(c, hipMemsetAsync(c->d_side_used, 0, 4, c->s_comp));
-        COMP_SYNC(c);
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
     }
     return YSB_OK;
 }
@@ -1299,7 +1224,7 @@ static int ring_rows(ysb_ctx* c, i64 blo, i64 bhi, bool clear, std::map<std::pai
         HIPCHK(c, hipMemsetAsync(c->d_rows_n, 0, 4, c->s_comp));
         launch_compact(t.t, t.rows, W, a, nb, t.off, true, false, nullptr, c->d_rows_n, 0, c->s_comp);
         HIPCHK(c, hipMemcpyAsync(&n, c->d_rows_n, 4, hipMemcpyDeviceToHost, c->s_comp));
-        COMP_SYNC(c);
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
         if (!n) continue;
         if (n > c->rows_cap) {
             hipFree(c->d_rows);
@@ -1314,7 +1239,7 @@ static int ring_rows(ysb_ctx* c, i64 blo, i64 bhi, bool clear, std::map<std::pai
         launch_compact(t.t, t.rows, W, a, nb, t.off, false, clear, c->d_rows, c->d_rows_n, n, c->s_comp);
         HIPCHK(c, hipMemcpyAsync(&m, c->d_rows_n, 4, hipMemcpyDeviceToHost, c->s_comp));
         HIPCHK(c, hipMemcpyAsync(h.data(), c->d_rows, (u64)n * sizeof(TableRow), hipMemcpyDeviceToHost, c->s_comp));
-        COMP_SYNC(c);
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
         if (m != n) return fail(c, YSB_ERR_STATE, "table changed during drain (%u vs %u cells)", m, n);
         for (const TableRow& r : h) into[{r.campaign, r.bucket}] += r.count;
     }
@@ -1431,7 +1356,7 @@ int ysb_reset(ysb_ctx* c) {
     if (c->d_truth_out) HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
     HIPCHK(c, hipMemset(c->d_ovf_count, 0, 16));
     launch_side_clear(c->d_side, c->side_slots, c->s_comp);
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     HIPCHK(c, hipMemset(c->d_side_used, 0, 4));
     HIPCHK(c, hipMemset(c->d_stats, 0, ST_COUNT_ * 8));
     c->side.clear();
@@ -1538,11 +1463,11 @@ static int coll_max_u64(ysb_ctx* c, unsigned long long* d, u64 n) {
     }
     std::vector<uint64_t> h(n);
     HIPCHK(c, hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, c->s_comp));
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     if (c->hops.allreduce_max_u64(c->hops.user, h.data(), n))
         return fail(c, YSB_ERR_RCCL, "host all-reduce(max) failed");
     HIPCHK(c, hipMemcpyAsync(d, h.data(), n * 8, hipMemcpyHostToDevice, c->s_comp));
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     return YSB_OK;
 }
 
@@ -1558,11 +1483,11 @@ static int coll_reduce_scatter(ysb_ctx* c, const void* d_send, void* d_recv, u64
     const u64 nb = count * width;
     std::vector<u8> hs(nb * (u64)c->nranks), hr(nb);
     HIPCHK(c, hipMemcpyAsync(hs.data(), d_send, hs.size(), hipMemcpyDeviceToHost, c->s_comp));
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     if (c->hops.reduce_scatter_sum(c->hops.user, hs.data(), hr.data(), count, width))
         return fail(c, YSB_ERR_RCCL, "host reduce-scatter failed");
     HIPCHK(c, hipMemcpyAsync(d_recv, hr.data(), nb, hipMemcpyHostToDevice, c->s_comp));
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     return YSB_OK;
 }
 
@@ -1591,7 +1516,7 @@ static int allreduce_max(ysb_ctx* c, i64* h, int n) {
 // place); a rank without a base takes the common one.  Skewed per-rank streams
 // (core.clj:166-174) that auto-based differently therefore still exchange.
 static int agree_ring(ysb_ctx* c) {
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     int rc = read_ring(c);
     if (rc) return rc;
     i64 h[2] = {c->ring_known ? -c->ring_lo : INT64_MIN + 1, c->ring_known ? 1 : 0};
@@ -1642,7 +1567,7 @@ static int group_setup(ysb_ctx* c, int rank, int nranks) {
     if (cp != c->c_pad) {
         int frc = fold_delta(c);   // the delta ring has the old layout: fold it, drop it
         if (frc) return frc;
-        COMP_SYNC(c);
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
         hipFree(c->d_delta);
         c->d_delta = nullptr;
         c->delta_cells = 0;
@@ -1679,7 +1604,7 @@ static int group_setup(ysb_ctx* c, int rank, int nranks) {
 
 static int grow_bytes(ysb_ctx* c, void** buf, u64* have, u64 bytes) {
     if (*have >= bytes) return YSB_OK;
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     hipFree(*buf);
     *buf = nullptr;
     *have = 0;
@@ -1731,10 +1656,6 @@ static int exchange(ysb_ctx* c, bool pipelined) {
         if (rc) return rc;
     }
     if (!c->x_have_plan) pipelined = false;
-    {
-        const int jrc = join_rec(c);   // the plan / pack read the delta and u64 rings
-        if (jrc) return jrc;
-    }
     const u32 W = c->cfg.window_ring;
     const u64 cells = (u64)c->c_pad * W;
     const u8* delta = c->delta_bound ? c->d_delta : nullptr;   // (delta_bound 0: the delta ring is all zero)
@@ -1841,7 +1762,7 @@ int ysb_group_checksum(ysb_ctx* c, int what, uint32_t nranks, uint64_t* out) {
         launch_checksum(t, rows, W, c->ring_lo, c_off, lo, hi, acc, c->s_comp);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(o, acc, 8, hipMemcpyDeviceToHost, c->s_comp));
-        COMP_SYNC(c);
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
         return YSB_OK;
     };
     if (what == YSB_SUM_TRUTH_BLOCKS || what == YSB_SUM_PENDING_BLOCKS) {
@@ -1992,7 +1913,7 @@ int ysb_gen_events_device(ysb_ctx* c, const ysb_gen_params* p, uint64_t first, u
     if (!gen_ok(p) || !nbytes || (n && (!d_out || !d_off))) return fail(c, YSB_ERR_ARG, "bad generator arguments");
     if (n > 0x7FFFFFFFull) return fail(c, YSB_ERR_ARG, "at most 2^31-1 events per call");
     HIPCHK(c, hipSetDevice(c->device));
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     const u32* dsub = nullptr;
     int rc = upload_subset(c, p, &dsub);
     if (rc) return rc;
@@ -2019,7 +1940,7 @@ int ysb_truth_accumulate(ysb_ctx* c, const ysb_gen_params* p, uint64_t first, ui
         HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
         HIPCHK(c, hipMalloc(&c->d_cmp, 32));
     }
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     int rc = read_ring(c);
     if (rc) return rc;
     if (!c->ring_known) return fail(c, YSB_ERR_STATE, "ring base not set (submit a batch first or set ring_base_bucket)");
@@ -2041,7 +1962,7 @@ int ysb_truth_compare(ysb_ctx* c, uint64_t* mismatched, uint64_t* truth_total, u
     unsigned long long r[3], outside = 0;
     HIPCHK(c, hipMemcpyAsync(r, c->d_cmp, 24, hipMemcpyDeviceToHost, c->s_comp));
     HIPCHK(c, hipMemcpyAsync(&outside, c->d_truth_out, 8, hipMemcpyDeviceToHost, c->s_comp));
-    COMP_SYNC(c);
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
     if (mismatched) *mismatched = r[0];
     if (truth_total) *truth_total = r[1] + outside;
     if (ring_total) *ring_total = r[2];

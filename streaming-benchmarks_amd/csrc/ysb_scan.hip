@@ -709,9 +709,6 @@ constexpr int TBL_WORDS = 40;                          // bytes 0..159 of the li
 #ifndef YSB_TBL_ZCMP
 #define YSB_TBL_ZCMP 1
 #endif
-#ifndef YSB_TBL_TILEFLAGS
-#define YSB_TBL_TILEFLAGS 0  // round 3 A/B: flags on the tile's own dwords (no per-word realignment)
-#endif
 constexpr int TBL_MIN_LEN = 116, TBL_MAX_LEN = 4 * TBL_WORDS;
 
 // Per byte, bit 7 set if the byte may be '|' (SWAR has-zero of w ^ '|'); the lowest flag
@@ -749,43 +746,9 @@ __device__ __forceinline__ bool tbl_stage1(const LdsSrc& src, int s, int e, Cano
 #pragma unroll
     for (int k = 0; k <= TBL_WORDS; ++k) P[k] = src.d[a + k];
 #endif
-    u32 B[5] = {0u, 0u, 0u, 0u, 0u};   // bit i = line byte i may be '|'
-#if YSB_TBL_TILEFLAGS
-    // The flags of the tile's own dwords P[j] (line bytes 4j - sb .. 4j + 3 - sb): no word
-    // is realigned to the line; the only '|' a generator row has in bytes 0..95 (36, 73)
-    // sit at tile bytes 36 + sb / 73 + sb, so the expected pattern moves with sb, and the
-    // bitmap of bytes 96..159 is the tile's nibble flags funnel-shifted by sb.
-    const u32 sh8 = 8u * sb;
-    u32 dz = 0;
-#pragma unroll
-    for (int j = 0; j < 24; ++j) {
-        const u32 t = P[j] ^ 0x7C7C7C7Cu;
-        u32 z = ((t - 0x01010101u) & ~t) & 0x80808080u;
-        if (j == 0) z &= 0xFFFFFFFFu << sh8;                  // the bytes before the line
-        if (j == 9) z ^= 0x80u << sh8;                        // byte 36
-        if (j == 18) z ^= sb < 3u ? 0x8000u << sh8 : 0u;      // byte 73 ...
-        if (j == 19) z ^= sb == 3u ? 0x80u : 0u;              // ... or in the next dword
-        dz |= z;
-    }
-    u32 N[3] = {0u, 0u, 0u};   // flags of tile bytes 96..163 = line bytes 96 - sb .. 163 - sb
-#pragma unroll
-    for (int j = 24; j <= TBL_WORDS; ++j) N[(j - 24) >> 3] |= bar_nib(P[j]) << (4 * ((j - 24) & 7));
-    dz |= N[0] & ((1u << sb) - 1u);                           // line bytes 96 - sb .. 95
-    B[3] = __builtin_amdgcn_alignbit(N[1], N[0], sb);
-    B[4] = __builtin_amdgcn_alignbit(N[2], N[1], sb);
-    // ad_id = line bytes 74..109 = tile bytes 74 + sb ..: dword 18 + (sb + 2) / 4, byte (sb + 2) % 4
-    {
-        const bool up = sb >= 2u;
-        const u32 r = (sb + 2u) & 3u;
-        u32 Q[10];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) Q[k] = up ? P[19 + k] : P[18 + k];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) c.kw[k] = __builtin_amdgcn_alignbyte(Q[k + 1], Q[k], r);
-    }
-    const bool fixed = dz == 0u && (B[3] & 0x7FFFu) == (1u << 14);
-#elif YSB_TBL_ZCMP
     u32 W[TBL_WORDS];
+    u32 B[5] = {0u, 0u, 0u, 0u, 0u};   // bit i = line byte i may be '|'
+#if YSB_TBL_ZCMP
     // bytes 0..95: the '|' flags of each word compared with the only pattern a generator
     // row has there -- '|' at 36 and 73 (word 9 byte 0, word 18 byte 1), no other byte
     // flagged (a false flag above a true '|' only rejects the line); no bitmap is packed
@@ -806,7 +769,6 @@ __device__ __forceinline__ bool tbl_stage1(const LdsSrc& src, int s, int e, Cano
     // the first three '|' exactly at 36, 73, 110 (each the lowest flag of its word: true)
     const bool fixed = dz == 0u && (B[3] & 0x7FFFu) == (1u << 14);
 #else
-    u32 W[TBL_WORDS];
 #pragma unroll
     for (int j = 0; j < TBL_WORDS; ++j) {
         W[j] = __builtin_amdgcn_alignbyte(P[j + 1], P[j], sb);   // line bytes 4j..4j+3

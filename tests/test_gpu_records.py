@@ -132,18 +132,14 @@ def test_bucket_table_sparse_and_misses(huge_map, record):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("overlap", ["1", "0"])
 @pytest.mark.parametrize("fold_events", [None, "50000"])
-def test_record_delta_ring_folds(big_map, monkeypatch, fold_events, overlap):
+def test_record_delta_ring_folds(big_map, monkeypatch, fold_events):
     """Record mode counts into a saturating u8 delta ring folded into the u64 ring before
     anything reads it.  Eight launches back to back with a stats read and a drain-with-clear
     in between -- with no bound (folds only at the drains) and with the test hook's bound of
-    50k events (a fold before every launch) -- equal the oracle.  overlap "1" (the default):
-    each launch's partition + count run on their own stream beside the next launch's scan
-    (two record-buffer sets, alternating); "0": all on the compute stream."""
+    50k events (a fold before every launch) -- equal the oracle."""
     if fold_events:
         monkeypatch.setenv("YSB_DELTA_FOLD_EVENTS", fold_events)
-    monkeypatch.setenv("YSB_REC_OVERLAP", overlap)
     g, aids, raw, offs = big_map
     camp = g.ad_campaign_index()
     n = offs.size
