@@ -420,11 +420,18 @@ def extra_layouts(args, device, out):
 
 
 def extra_stream(args):
-    # configs[4]: real-time producers into double-buffered pinned slots of 2 contexts
-    # (2 shards; on a one-GPU box both on it), one global watermark, p50 / p99 close latency
+    # configs[4]: real-time producers into double-buffered pinned slots, one context per
+    # visible GPU (2..8 shards: configs[4]'s 8 GPUs on an 8-GPU node; on a one-GPU box two
+    # contexts share it), one global watermark, p50 / p99 close latency
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_extra
-    ns = argparse.Namespace(shards=2, rate=1_000_000, seconds=args.stream_seconds, batch_ms=20, ooo_ms=100)
+    try:
+        import torch
+        visible = torch.cuda.device_count()
+    except Exception:   # noqa: BLE001
+        visible = 1
+    ns = argparse.Namespace(shards=min(8, max(2, visible)), rate=1_000_000, seconds=args.stream_seconds,
+                            batch_ms=20, ooo_ms=100)
     r = bench_extra.stream_sharded(ns)
     log("extras: stream %s" % json.dumps(r["window_close_latency"]))
     return r
