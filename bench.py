@@ -393,7 +393,11 @@ def extra_layouts(args, device, out):
                                     "compact JSON without a hint (the layout read from each batch's first line)"),
                                    ("reordered_keys", GEN_REORDER, "flat",
                                     "the keys in another order (ad_type, event_time, ad_id, ip_address, user_id, "
-                                    "event_type, page_id), layout hint YSB_F_FLAT_FIRST: the flat-object tier first"),
+                                    "event_type, page_id), layout hint YSB_F_FLAT_FIRST (the first line names one key "
+                                    "order: the learned-order instantiation, off-order lines to the flat tier)"),
+                                   ("reordered_keys_flat_tier", GEN_REORDER, "flat_fixed",
+                                    "the keys in another order, YSB_F_FLAT_FIRST with YSB_F_LAYOUT_FIXED: the "
+                                    "flat-object tier (any key order or spacing) parses every line"),
                                    ("reordered_keys_no_hint", GEN_REORDER, False,
                                     "the keys in another order without a hint (the layout read from each batch's "
                                     "first line)"),
@@ -405,7 +409,7 @@ def extra_layouts(args, device, out):
             _, aids = g.ids()
             with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True,
                             max_batch_bytes=16 << 20, max_batch_events=1 << 16, compact_first=cf is True,
-                            flat_first=cf == "flat", layout_auto=cf != "fixed") as ctx:
+                            flat_first=cf in ("flat", "flat_fixed"), layout_auto=cf not in ("fixed", "flat_fixed")) as ctx:
                 ctx.load_ad_map(aids, g.ad_campaign_index())
                 # lines up to ~280 B: 7 batches keep each under the 4 GiB of u32 offsets
                 segs = gen_segments(ctx, g, 100_000_000, 14_285_715)

@@ -77,16 +77,23 @@ extern "C" {
                                    order or spacing (another producer's serializer); the
                                    scan parses every line with its flat-object tier first
                                    (generator-layout lines too, a little slower than their
-                                   own path).  Counts are identical; takes precedence over
-                                   YSB_F_COMPACT_FIRST.  Cache-resident join tables only. */
+                                   own path) -- unless a batch's first line names one key
+                                   order of DeserializeBolt's keys with one spacing: then
+                                   the learned-order instantiation, which sends lines off
+                                   that order to the same flat tier (without
+                                   YSB_F_LAYOUT_FIXED).  Counts are identical; takes
+                                   precedence over YSB_F_COMPACT_FIRST.  Cache-resident
+                                   join tables only. */
 #define YSB_F_LAYOUT_AUTO 0x200u /* (the default since ABI 2; the bit is accepted and
                                    ignored) layout read from the data: every submit picks
                                    the scan instantiation from the first line of each batch
                                    -- host batches from the pinned slot, device batches from
-                                   a <= 64-byte device-to-host sample per segment -- the
-                                   generator's layout, compact JSON, or the flat-object
-                                   tier first.  Counts are identical whichever runs.  The
-                                   explicit hints above take precedence.  Cache-resident
+                                   a <= 288-byte device-to-host sample per segment -- the
+                                   generator's layout, compact JSON, a learned key order
+                                   (the first line's order and spacing, checked in place
+                                   on every line), or the flat-object tier first.  Counts
+                                   are identical whichever runs.  The explicit hints above
+                                   take precedence.  Cache-resident
                                    join tables only (the HBM-table and record-mode
                                    instantiations keep the generator layout first). */
 #define YSB_F_LAYOUT_FIXED 0x800u /* no layout sampling: the generator's layout first (or

@@ -941,12 +941,20 @@ static int sniff_layout(const ysb_ctx* c, const uint8_t* bytes, u64 nbytes, cons
 }
 
 // Whether batches pick the scan instantiation from their first line (the default): not
-// with an explicit hint or YSB_F_LAYOUT_FIXED, and only where the layout instantiations
-// exist (JSON, cache-resident join table).
+// with YSB_F_COMPACT_FIRST or YSB_F_LAYOUT_FIXED, and only where the layout instantiations
+// exist (JSON, cache-resident join table).  Under YSB_F_FLAT_FIRST the sample only tells
+// whether the batch has one learnable key order (hinted_layout).
 static bool layout_sampling(const ysb_ctx* c) {
     const u32 f = c->cfg.flags;
-    return !(f & (YSB_F_LAYOUT_FIXED | YSB_F_COMPACT_FIRST | YSB_F_FLAT_FIRST | YSB_F_FORMAT_TBL)) &&
-           !c->ctable_buckets;
+    return !(f & (YSB_F_LAYOUT_FIXED | YSB_F_COMPACT_FIRST | YSB_F_FORMAT_TBL)) && !c->ctable_buckets;
+}
+
+// The sampled layout under the flags' hint: YSB_F_FLAT_FIRST keeps the flat-object tier
+// first unless the first line names a key order (3: the learned-order instantiation, whose
+// lines off that order go to the same flat tier).
+static int hinted_layout(const ysb_ctx* c, int sampled) {
+    if ((c->cfg.flags & YSB_F_FLAT_FIRST) && sampled >= 0 && sampled != 3) return 2;
+    return sampled;
 }
 
 // Device batches: the first line of every segment, sampled by small device-to-host copies
@@ -1047,7 +1055,8 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
     // the scan instantiation named by the batch's first line, which the host holds in the
     // pinned slot (counts are the same whichever runs)
     if (layout_sampling(c) && n)
-        c->submit_layout = sniff_layout(c, c->h_bytes[slot], nbytes, c->h_off[slot], n, &c->submit_learn);
+        c->submit_layout =
+            hinted_layout(c, sniff_layout(c, c->h_bytes[slot], nbytes, c->h_off[slot], n, &c->submit_learn));
     rc = enqueue_scan(c, &sg, 1);
     c->submit_layout = -1;
     if (rc) return rc;
@@ -1068,7 +1077,7 @@ static int enqueue_device(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     if (c->table_loaded && layout_sampling(c)) {
         const int lay = sample_device_layout(c, segs, nseg, &c->submit_learn);
         if (lay < 0) return lay;
-        c->submit_layout = lay;
+        c->submit_layout = hinted_layout(c, lay);
     }
     const int rc = enqueue_scan(c, segs, nseg);
     c->submit_layout = -1;

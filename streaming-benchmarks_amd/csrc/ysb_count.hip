@@ -34,6 +34,10 @@
 
 namespace ysb {
 
+#ifndef YSB_COUNT_BY_QUARTER
+#define YSB_COUNT_BY_QUARTER 1   // count kernel: 32 threads per partition slice (0: a search per record)
+#endif
+
 constexpr int REC_TPB = 1024;
 constexpr int REC_WAVES = REC_TPB / 64;
 constexpr int REC_UNROLL = 8;        // records in flight per lane (loads issued together)
@@ -245,6 +249,25 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
             r[u] = p < quads ? dr[p] : make_uint4(0u, 0u, 0u, 0u);
         }
     }
+#if YSB_COUNT_BY_QUARTER
+    // 32 threads per partition slice (REC_TPB = 32 x REC_QUARTERS): thread (q, k) reads
+    // records k, k + 32, ... of run q -- coalesced 128-B lines, no search for the run
+    static_assert(REC_TPB == 32 * REC_QUARTERS, "one 32-thread group per partition slice");
+    const u32 q = tid >> 5, k = tid & 31u;
+    const u32 nq = roff[q + 1] - roff[q];
+    const u32* src = R.part + rbeg[q];
+    for (u32 j0 = 0; j0 < nq; j0 += 32 * REC_UNROLL) {
+        u32 v[REC_UNROLL];
+#pragma unroll
+        for (int u = 0; u < REC_UNROLL; ++u) {
+            const u32 jj = j0 + u * 32 + k;
+            v[u] = jj < nq ? src[jj] : REC_NONE;
+        }
+#pragma unroll
+        for (int u = 0; u < REC_UNROLL; ++u)
+            if (v[u] != REC_NONE) atomicAdd(&cnt[v[u] - base_cell], 1u);
+    }
+#else
     for (u32 i0 = 0; i0 < total; i0 += REC_TPB * REC_UNROLL) {
         u32 v[REC_UNROLL];
 #pragma unroll
@@ -261,6 +284,7 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
         for (int u = 0; u < REC_UNROLL; ++u)
             if (v[u] != REC_NONE) atomicAdd(&cnt[v[u] - base_cell], 1u);
     }
+#endif
     __syncthreads();
     if (dense) {
 #pragma unroll

@@ -286,3 +286,36 @@ def test_learned_order_subset_of_keys():
         for k, v in est.items():
             assert st[k] == v, k
         assert (st["parse_errors"] == len(lines)) == req
+
+
+@pytest.mark.parametrize("variant,fixed,want", [(GEN_REORDER, False, 3), (0, False, 2), (GEN_COMPACT, False, 2),
+                                                 (GEN_REORDER, True, 2)])
+def test_flat_first_hint_takes_a_learned_order(variant, fixed, want):
+    """YSB_F_FLAT_FIRST keeps the flat-object tier first (layout 2) unless the batch's first
+    line names a key order (layout 3, whose off-order lines go to the same flat tier);
+    with YSB_F_LAYOUT_FIXED nothing is sampled.  Host and device batches, exact vs the oracle."""
+    g = GenParams(seed=29, n_campaigns=40, ads_per_campaign=10, events_per_sec=1000, with_skew=True, variant=variant)
+    _, aids = g.ids()
+    raw, offs = g.events_host(0, 60_000)
+    exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), raw, offs)
+    kw = {"flat_first": True}
+    if fixed:
+        kw["layout_auto"] = False
+    for device in (False, True):
+        with YsbContext(n_campaigns=40, window_ring=256, max_batch_bytes=raw.size + 64,
+                        max_batch_events=offs.size + 1, **kw) as ctx:
+            ctx.load_ad_map(aids, g.ad_campaign_index())
+            if device:
+                d_b, d_o = ctx.device_alloc(raw.size + 64), ctx.device_alloc(4 * offs.size + 64)
+                ctx.h2d(d_b, raw)
+                ctx.h2d(d_o, offs)
+                ctx.submit_device(d_b, raw.size, d_o, offs.size)
+            else:
+                ctx.submit(raw, offs)
+            got = ctx.drain_buckets()
+            st = ctx.stats()
+            assert ctx.launch_info()["layout"] == want
+        assert got == exp
+        for k, v in est.items():
+            assert st[k] == v, k
+        assert st["deferred"] == 0

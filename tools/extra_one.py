@@ -1,5 +1,5 @@
 """Runs one of bench.py's extra legs by itself (profiling passes, A/B runs):
-    python tools/extra_one.py config3|tbl|stream|reorder|reorder_fixed|compact [bench.py options]"""
+    python tools/extra_one.py config3|tbl|stream|reorder|reorder_fixed|reorder_flat|reorder_flat_fixed|compact [bench.py options]"""
 import json
 import os
 import sys
@@ -31,5 +31,7 @@ if __name__ == "__main__":
           "stream": lambda: bench.extra_stream(args),
           "reorder": lambda: layout(args, GEN_REORDER),
           "reorder_fixed": lambda: layout(args, GEN_REORDER, layout_auto=False),
+          "reorder_flat": lambda: layout(args, GEN_REORDER, flat_first=True),
+          "reorder_flat_fixed": lambda: layout(args, GEN_REORDER, flat_first=True, layout_auto=False),
           "compact": lambda: layout(args, GEN_COMPACT)}[leg]
     print(json.dumps(fn()), flush=True)
