@@ -38,7 +38,13 @@ namespace ysb {
 #define YSB_COUNT_BY_QUARTER 1   // count kernel: 32 threads per partition slice (0: a search per record)
 #endif
 
+#ifndef YSB_PART_RING
+#define YSB_PART_RING 32         // the partition's staged records per level-2 block (one 128-B line: 72 KiB of LDS, two workgroups per CU)
+#endif
+
 constexpr int REC_TPB = 1024;
+constexpr int PART_RING = YSB_PART_RING;
+static_assert(PART_RING == 32 || PART_RING == 64, "whole 128-B lines");
 constexpr int REC_WAVES = REC_TPB / 64;
 constexpr int REC_UNROLL = 8;        // records in flight per lane (loads issued together)
 constexpr u32 REC_NONE = 0xFFFFFFFFu;
@@ -50,8 +56,11 @@ constexpr u32 REC_NONE = 0xFFFFFFFFu;
 // workgroup's output area.  Sweep 2 stages every record in its block's 64-record LDS ring
 // (a record arriving when its ring is full goes straight to its final slot) and after
 // every round each block's full 128-B lines are written out by one thread.
-__global__ __launch_bounds__(REC_TPB) void rec_partition_kernel(const RecParams R) {
-    __shared__ __attribute__((aligned(16))) u32 stage[REC_SUB_MAX * REC_RING];
+// (a 32-record ring keeps the workgroup under 80 KiB of LDS: two per CU, so 8 waves per
+// SIMD, which the register budget must allow)
+__global__ __launch_bounds__(REC_TPB) __attribute__((amdgpu_waves_per_eu(PART_RING == 32 ? 8 : 4)))
+void rec_partition_kernel(const RecParams R) {
+    __shared__ __attribute__((aligned(16))) u32 stage[REC_SUB_MAX * PART_RING];
     __shared__ u32 hist[REC_SUB_MAX];
     __shared__ u32 boff[REC_SUB_MAX];
     __shared__ u32 cur[REC_SUB_MAX];
@@ -127,15 +136,15 @@ __global__ __launch_bounds__(REC_TPB) void rec_partition_kernel(const RecParams 
     auto write_line = [&](u32 k, u32 n) {
         const u32 f = fl[k];
         u32* dst = out + boff[k] + f;
-        const u32* src = stage + k * REC_RING;
+        const u32* src = stage + k * PART_RING;
         if (n == 32 && (f & 31u) == 0) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const u32 o = (f + 4 * j) & (REC_RING - 1);
+                const u32 o = (f + 4 * j) & (PART_RING - 1);
                 reinterpret_cast<uint4*>(dst)[j] = make_uint4(src[o], src[o + 1], src[o + 2], src[o + 3]);
             }
         } else {
-            for (u32 j = 0; j < n; ++j) dst[j] = src[(f + j) & (REC_RING - 1)];
+            for (u32 j = 0; j < n; ++j) dst[j] = src[(f + j) & (PART_RING - 1)];
         }
         fl[k] = f + n;
     };
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(REC_TPB) void rec_partition_kernel(const RecParams 
                 if (v[u] == REC_NONE) continue;
                 const u32 k = (v[u] >> sh) - first_blk;
                 const u32 pos = atomicAdd(&cur[k], 1u);
-                if (pos - fl[k] < (u32)REC_RING) stage[k * REC_RING + (pos & (REC_RING - 1))] = v[u];
+                if (pos - fl[k] < (u32)PART_RING) stage[k * PART_RING + (pos & (PART_RING - 1))] = v[u];
                 else out[boff[k] + pos] = v[u];   // its ring is full this round: straight to its slot
             }
         }
@@ -160,9 +169,9 @@ __global__ __launch_bounds__(REC_TPB) void rec_partition_kernel(const RecParams 
         for (u32 k = tid; k < S; k += REC_TPB) {
             const u32 f0 = fl[k], c = cur[k];
             // staged this round: positions [f0, f0 + 64); beyond that they went direct
-            const u32 lines = min(c - f0, (u32)REC_RING) / 32;
+            const u32 lines = min(c - f0, (u32)PART_RING) / 32;
             for (u32 l = 0; l < lines; ++l) write_line(k, 32);
-            if (c - f0 > (u32)REC_RING) fl[k] = c;   // direct positions are written already
+            if (c - f0 > (u32)PART_RING) fl[k] = c;   // direct positions are written already
         }
         __syncthreads();
     }
@@ -250,17 +259,18 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
         }
     }
 #if YSB_COUNT_BY_QUARTER
-    // 32 threads per partition slice (REC_TPB = 32 x REC_QUARTERS): thread (q, k) reads
-    // records k, k + 32, ... of run q -- coalesced 128-B lines, no search for the run
-    static_assert(REC_TPB == 32 * REC_QUARTERS, "one 32-thread group per partition slice");
-    const u32 q = tid >> 5, k = tid & 31u;
+    // TPS threads per partition slice (REC_TPB = TPS x REC_QUARTERS): thread (q, k) reads
+    // records k, k + TPS, ... of run q -- coalesced lines, no search for the run
+    constexpr u32 TPS = REC_TPB / REC_QUARTERS;
+    static_assert(TPS * REC_QUARTERS == REC_TPB && TPS >= 16, "one thread group per partition slice");
+    const u32 q = tid / TPS, k = tid % TPS;
     const u32 nq = roff[q + 1] - roff[q];
     const u32* src = R.part + rbeg[q];
-    for (u32 j0 = 0; j0 < nq; j0 += 32 * REC_UNROLL) {
+    for (u32 j0 = 0; j0 < nq; j0 += TPS * REC_UNROLL) {
         u32 v[REC_UNROLL];
 #pragma unroll
         for (int u = 0; u < REC_UNROLL; ++u) {
-            const u32 jj = j0 + u * 32 + k;
+            const u32 jj = j0 + u * TPS + k;
             v[u] = jj < nq ? src[jj] : REC_NONE;
         }
 #pragma unroll

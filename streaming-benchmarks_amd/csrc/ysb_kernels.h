@@ -179,7 +179,10 @@ struct ScanParams {
 // memory write of its own (the XCD L2s are write-through for stores), which made scattered
 // 4-B record stores as slow as the atomics they replace (tools/mb_scatter.hip).
 constexpr int REC_BLOCK_CELLS = 32768;  // u32 LDS counters per count workgroup (128 KiB)
-constexpr int REC_QUARTERS = 32;      // partition workgroups per level-1 bin (each a slice of the scan workgroups)
+#ifndef YSB_REC_QUARTERS
+#define YSB_REC_QUARTERS 64
+#endif
+constexpr int REC_QUARTERS = YSB_REC_QUARTERS;   // partition workgroups per level-1 bin (each a slice of the scan workgroups)
 constexpr int REC_SUB_MAX = 512;      // level-2 blocks per level-1 bin (the partition's staging rings)
 struct RecParams {
     const u32* rec;             // the scan's sub-buffers
