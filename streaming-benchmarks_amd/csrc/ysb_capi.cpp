@@ -442,6 +442,9 @@ int ysb_load_ad_map_shard(ysb_ctx* c, const char* const* ad_ids, const uint32_t*
 
 static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens, const uint32_t* campaign_idx,
                     uint64_t n) {
+    // the tables live on this context's GPU, whichever device the calling thread last set
+    // (one process may drive several contexts, e.g. one per GPU of a node)
+    HIPCHK(c, hipSetDevice(c->device));
     u64 slots = 64;
     while (slots < 2 * n) slots <<= 1;   // load factor <= 0.5
     if (slots > (1ull << 31)) return fail(c, YSB_ERR_CAPACITY, "ad map too large (%llu)", (unsigned long long)n);
@@ -1212,6 +1215,7 @@ static int pull_side_list(ysb_ctx* c) {
 // Non-zero ring cells of buckets [blo, bhi) (rank-local table + owned block), compacted
 // on the device (two passes: count, then rows), added to `into`; clear zeroes them.
 static int ring_rows(ysb_ctx* c, i64 blo, i64 bhi, bool clear, std::map<std::pair<u32, i64>, u64>& into) {
+    HIPCHK(c, hipSetDevice(c->device));
     int frc = fold_delta(c);
     if (frc) return frc;
     if (!c->ring_known) return YSB_OK;
