@@ -71,6 +71,8 @@ def parse_args(argv=None):
     ap.add_argument("--stream-seconds", type=int, default=125,
                     help="extras: seconds of real-time sharded streaming (configs[4]; 125 s closes >= 10 windows); "
                          "0 skips it")
+    ap.add_argument("--extras-timeout", type=int, default=300,
+                    help="N > 1: seconds the configs[2]-table leg may take before rank 0 prints the headline without it")
     ap.add_argument("--c3-events", type=int, default=100_000_000,
                     help="extras at N > 1: events per GPU of the configs[2]-table leg (1M campaigns / 10M ads)")
     ap.add_argument("--layout-fixed", action="store_true",
@@ -723,16 +725,7 @@ def main():
         s0 = segs[0]
         cpu = cpu_baseline(ctx, s0[2], s0[4], s0[3], s0[1], aids, camp, args.cpu_sample, args.cpu_seconds)
 
-    extra = None
-    if not args.no_extras:
-        free_segments(ctx, segs)
-        ctx.close()
-        if d.world == 1:
-            extra = extras(args, d.device)
-        else:
-            extra = {}
-            guarded(extra, "config3", lambda: config3_ranks(args, d))
-
+    out = None
     if d.rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "events/s", "n_gpus": d.world,
@@ -763,6 +756,30 @@ def main():
                                "bytes_per_step_per_gpu": xinfo["bytes"] // max(xinfo["exchanges"], 1),
                                "buckets": xinfo["last_buckets"], "cell_bytes": xinfo["last_width"],
                                "whole_ring_u64_bytes": xinfo["full_ring_bytes"]}
+    extra = None
+    if not args.no_extras:
+        free_segments(ctx, segs)
+        ctx.close()
+        if d.world == 1:
+            extra = extras(args, d.device)
+        else:
+            # a rank that stopped inside a collective of the leg would hold every rank (and
+            # the headline line) forever: after --extras-timeout seconds rank 0 prints the
+            # headline with the leg marked timed out and every rank exits
+            def give_up():
+                if d.rank == 0:
+                    out["extras"] = {"config3": {"error": "timed out after %d s" % args.extras_timeout}}
+                    print(json.dumps(out), flush=True)
+                os._exit(0)
+            import threading
+            dog = threading.Timer(args.extras_timeout, give_up)
+            dog.daemon = True
+            dog.start()
+            extra = {}
+            guarded(extra, "config3", lambda: config3_ranks(args, d))
+            dog.cancel()
+
+    if d.rank == 0:
         if extra is not None:
             out["extras"] = extra
         print(json.dumps(out), flush=True)
