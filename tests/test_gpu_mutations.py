@@ -131,3 +131,32 @@ def test_random_edits_tbl_rows_match_oracle(seed):
     for k in STAT_KEYS:
         assert st[k] == est[k], (k, st[k], est[k])
     assert got == exp
+
+
+@pytest.mark.timeout(300)
+def test_random_edits_hbm_table_record_mode_match_oracle():
+    """configs[2]'s path: an HBM-resident bucket join table (1.2M ads) and record-mode
+    counting (LDS-staged records -> partition -> per-block counts into the u8 delta ring),
+    400k lines, 20 % edited."""
+    rng = np.random.default_rng(9)
+    g = GenParams(seed=61, n_campaigns=600_000, ads_per_campaign=2, events_per_sec=1000, with_skew=True)
+    _, aids = g.ids()
+    camp = g.ad_campaign_index()
+    lines = lines_of(g, 400_000)
+    lines = [lines[0]] + mutate(lines[1:], rng, 0.20)
+    data = b"".join(lines)
+    offs = np.cumsum([0] + [len(x) for x in lines[:-1]]).astype(np.uint32)
+    exp, est = oracle.run(oracle.AdMap(aids, camp), data, offs, threads=8)
+    raw = np.frombuffer(data, dtype=np.uint8)
+    with YsbContext(n_campaigns=600_000, window_ring=128, record_count=True, timing=True,
+                    max_batch_bytes=raw.size + 64, max_batch_events=offs.size + 1) as ctx:
+        ctx.load_ad_map(aids, camp)
+        ctx.submit(raw, offs)
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+        ctx.kernel_time()
+        assert ctx.path_time()[2] == 1 and ctx.launch_info()["hbm_table"] == 1
+    assert est["parse_errors"] > 1000 and est["join_misses"] > 100
+    for k in STAT_KEYS:
+        assert st[k] == est[k], (k, st[k], est[k])
+    assert got == exp
