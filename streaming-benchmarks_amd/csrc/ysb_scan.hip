@@ -30,7 +30,8 @@ namespace ysb {
 // Key ids (bit masks) of the fields DeserializeBolt reads.
 enum : u32 {
     K_USER = 1u << 0, K_PAGE = 1u << 1, K_AD = 1u << 2, K_ADTYPE = 1u << 3,
-    K_ETYPE = 1u << 4, K_ETIME = 1u << 5, K_IP = 1u << 6
+    K_ETYPE = 1u << 4, K_ETIME = 1u << 5, K_IP = 1u << 6,
+    K_OTHER = 1u << 7   // flat_parse_fast: a key DeserializeBolt does not read
 };
 
 __host__ __device__ constexpr u32 w4(char a, char b, char c, char d) {
@@ -913,10 +914,12 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
 // counted nothing, and parse_line decides the line.
 // true: the line is a flat object of the subset above with every field of `require` (and
 // the three the topology reads); ad / et / tm = the values' spans
-// The flat-first instantiation's parser of the same subset (flat_parse below decides every
-// line identically): a key is one of DeserializeBolt's seven, so it is named by its first
-// four bytes and its remaining bytes and closing quote compared in place (any other key,
-// or one with an escape, fails the compare as it fails match_key_raw); the separators
+// The flat-first / learned-order instantiations' parser of the same subset plus ONE other
+// key with a plain string value (a producer's extra field: org.json puts it, DeserializeBolt
+// never reads it; a second one goes to parse_line, which sees a repeat as putOnce does): a
+// key of DeserializeBolt's seven is named by its first four bytes and its remaining bytes
+// and closing quote compared in place (a key with an escape fails the compare and the
+// plain-string scan alike, as it fails match_key_raw); the separators
 // `": "` / `":"` after a key and `", "` / `","` / `}` after a value are compared in place,
 // any other spacing takes the ft_clean scans; the id values are checked as 36-byte UUIDs
 // in one step.  Positions read past e are never accepted (each fast compare checks the
@@ -960,8 +963,18 @@ __device__ __forceinline__ bool flat_parse_fast(const S& src, int s, int e, u32 
                 id = (src.load4(kq + 5) == w4('d', 'd', 'r', 'e') && src.load4(kq + 7) == w4('r', 'e', 's', 's')) ? K_IP
                                                                                                                  : 0u;
             }
-            const int ke = kq + 1 + kl;                   // the key's closing quote
-            if (id == 0u || (seen & id) != 0u || ke >= e || src.b(ke) != '"') return false;
+            int ke = kq + 1 + kl;                         // the key's closing quote
+            if (id == 0u || ke >= e || src.b(ke) != '"') {
+                // another key (a producer's extra field): skipped when it is a plain string
+                // with a plain string value, at most one per line -- org.json puts it and
+                // DeserializeBolt never reads it; a second one could repeat it (putOnce
+                // throws), so that line, and any other value form, goes to parse_line
+                ke = ft_string_end(src, kq + 1, e);
+                if (ke < 0 || (seen & K_OTHER) != 0u) return false;
+                id = K_OTHER;
+            } else if ((seen & id) != 0u) {
+                return false;                             // a repeated key: putOnce throws
+            }
             seen |= id;
             // ':' and the value's opening quote
             int vq;
@@ -1317,6 +1330,9 @@ struct TileInfo {
 
 // Tile bounds come from the LDS copy tb[] (loaded once per workgroup), so no HBM
 // round trip sits between two tiles.
+#ifndef YSB_TILE_TRUNCATE
+#define YSB_TILE_TRUNCATE 1
+#endif
 template <int CAP>
 __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_begin, const u32* tb) {
     TileInfo ti;
@@ -1333,8 +1349,16 @@ __device__ __forceinline__ TileInfo tile_info(const ScanParams& P, u64 t, u64 t_
     ti.delta = s0 & 15u;   // P.bytes is 16-byte aligned
     const bool sane = (u64)s0 <= e && e <= P.nbytes;
     const u64 len = sane ? e - s0 + ti.delta : ~0ULL;
+#if YSB_TILE_TRUNCATE
+    // a tile of long lines is staged up to its capacity: the lines that end inside it are
+    // parsed, the rest deferred (the whole tile before)
+    ti.oversize = !sane;
+    if (sane && len > (u64)CAP) ti.e = s0 - ti.delta + (u32)CAP;
+    ti.len = ti.oversize ? 0u : (u32)(len < (u64)CAP ? len : (u64)CAP);
+#else
     ti.oversize = !sane || len > (u64)CAP;
     ti.len = ti.oversize ? 0u : (u32)len;
+#endif
     return ti;
 }
 

@@ -319,3 +319,72 @@ def test_flat_first_hint_takes_a_learned_order(variant, fixed, want):
         for k, v in est.items():
             assert st[k] == v, k
         assert st["deferred"] == 0
+
+
+# short fields: a tile holds 64 lines of 272 bytes on average (a longer tile is deferred
+# whole, still exact), generator lines are 249-265 bytes
+EXTRA_FIELDS = [b'"src": "w", ', b'"ad_idx":"7",', b'"event":"",', b'"user_id2":"",', b'"ip_a": "", ',
+                b'"k" : "v" , ']
+
+
+def _with_extra(line, rng, kind):
+    """One generator line with extra fields spliced in after '{' or after a pair."""
+    body = line[:-1]
+    cuts = [1] + [i + 3 for i in range(len(body) - 2) if body[i:i + 3] == b'", "']
+    def put(b, fld):
+        at = cuts[int(rng.integers(0, len(cuts)))]
+        return b[:at] + fld + b[at:]
+    if kind == "one":
+        body = put(body, EXTRA_FIELDS[int(rng.integers(0, len(EXTRA_FIELDS)))])
+    elif kind == "two":
+        body = put(body, b'"a1": "x", ')
+        body = body[:1] + b'"a2": "y", ' + body[1:]
+    elif kind == "dup":
+        body = body[:1] + b'"a1": "x", "a1": "y", ' + body[1:]
+    elif kind == "number":
+        body = body[:1] + b'"n": 12, ' + body[1:]
+    elif kind == "nested":
+        body = body[:1] + b'"o": {"p": "q"}, ' + body[1:]
+    elif kind == "escaped":
+        body = body[:1] + b'"a\\u0031": "x", ' + body[1:]
+    elif kind == "quote_in_value":
+        body = body[:1] + b'"a": "x\\"y", ' + body[1:]
+    return body + b"\n"
+
+
+@pytest.mark.parametrize("hint", [None, "flat_first"])
+@pytest.mark.parametrize("base_variant", [0, GEN_REORDER])
+def test_extra_fields_match_oracle(hint, base_variant):
+    """A producer's extra fields (org.json puts them, DeserializeBolt never reads them): one
+    plain-string extra pair per line is parsed by the flat tier (nothing deferred); two,
+    a repeat (putOnce throws: a parse error), other value forms and escapes go to the
+    general path -- all exactly as the oracle decides them."""
+    g = GenParams(seed=31, n_campaigns=40, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
+                  variant=base_variant)
+    _, aids = g.ids()
+    raw, offs = g.events_host(0, 40_000)
+    data = raw.tobytes()
+    ends = list(offs[1:]) + [len(data)]
+    base = [data[s:e] for s, e in zip(offs, ends)]
+    rng = np.random.default_rng(3)
+    for kinds in (["one"], ["one", "two", "dup", "number", "nested", "escaped", "quote_in_value"]):
+        lines = [_with_extra(ln, rng, kinds[int(rng.integers(0, len(kinds)))]) for ln in base]
+        if len(kinds) > 1:
+            lines[0] = base[0]   # the first line plain: its layout (generator / learned order) is sampled
+        buf = b"".join(lines)
+        o = np.cumsum([0] + [len(x) for x in lines[:-1]]).astype(np.uint32)
+        exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), buf, o)
+        with YsbContext(n_campaigns=40, window_ring=256, max_batch_bytes=len(buf) + 64,
+                        max_batch_events=o.size + 1, **hint_kw(hint)) as ctx:
+            ctx.load_ad_map(aids, g.ad_campaign_index())
+            ctx.submit(np.frombuffer(buf, dtype=np.uint8), o)
+            got = ctx.drain_buckets()
+            st = ctx.stats()
+            lay = ctx.launch_info()["layout"]
+        assert got == exp
+        for k, v in est.items():
+            assert st[k] == v, k
+        if kinds == ["one"]:
+            assert lay == 2 and st["deferred"] == 0    # the flat tier took every line
+        else:
+            assert est["parse_errors"] > 0 and st["deferred"] > 0

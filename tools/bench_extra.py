@@ -214,6 +214,8 @@ def general(args):
         data = data.replace(b'{"XXXX_id": ', b'{"page_id": ')
     elif args.shape == "spaced":     # '" : "': the flat tier too
         data = data.replace(b'": "', b'" : "')
+    elif args.shape == "extra":      # a producer's extra field first: the flat tier (one extra key allowed)
+        data = data.replace(b'{"user_id": ', b'{"source": "web", "user_id": ')
     elif args.shape == "escaped":    # a \u escape in every key: org.json's full machine
         data = data.replace(b'"ad_id"', b'"ad_\\u0069d"')
     offs2 = np.zeros(n, dtype=np.uint32)
@@ -464,7 +466,7 @@ def main():
     ap.add_argument("--c3-rate", type=int, default=100_000, help="config3: events per second of event time")
     ap.add_argument("--batch-ms", type=int, default=100)
     ap.add_argument("--ooo-ms", type=int, default=100)
-    ap.add_argument("--shape", default="reorder", choices=["generator", "compact", "reorder", "spaced", "escaped"],
+    ap.add_argument("--shape", default="reorder", choices=["generator", "compact", "reorder", "spaced", "extra", "escaped"],
                     help="general: how the generator's lines are re-laid")
     ap.add_argument("--shards", type=int, default=2, help="stream_sharded: contexts (one per GPU)")
     ap.add_argument("--hint", default="none", choices=["none", "compact", "flat", "auto"],
