@@ -47,8 +47,6 @@ struct ysb_ctx {
     u32* d_table = nullptr;
     u64 table_slots = 0;
     u32* d_ctable = nullptr;   // 36-byte-key cuckoo table
-    unsigned short* d_disp = nullptr;   // YSB_CHD: the cache-resident table's displacements
-    u32 disp_shift = 0;
     u64 ctable_slots = 0;      // slots, or buckets when ctable_buckets
     bool ctable_buckets = false; // HBM-resident table: 3-entry 128-B buckets (CB_*), serial probes
     int submit_layout = -1;      // the layout a submit read off its batch's first line (-1: the flags')
@@ -220,7 +218,6 @@ static void destroy(ysb_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_table);
     hipFree(c->d_ctable);
-    hipFree(c->d_disp);
     hipFree(c->d_counts);
     hipFree(c->d_owned);
     hipFree(c->d_rs_tmp);
@@ -514,9 +511,8 @@ static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         while (cslots * 4 < (u64)YSB_BUCKETS_X4 * keys36.size()) cslots <<= 1;
     }
     const u32 unit = buckets ? CB_WORDS : CSLOT_WORDS;
-    const bool chd = !buckets && YSB_CHD;
-    std::vector<u32> kw, cv;   // bucket layout / CHD: the keys as words, their campaigns
-    if (buckets || chd) {
+    std::vector<u32> kw, cv;   // bucket layout: the keys as words, their campaigns
+    if (buckets) {
         kw.resize(keys36.size() * CKEY_WORDS);
         cv.resize(keys36.size());
         for (size_t i = 0; i < keys36.size(); ++i) {
@@ -525,8 +521,6 @@ static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         }
     }
     std::vector<u32> ct;
-    std::vector<unsigned short> disp;
-    u32 dshift = 0;
     CuckooSeed cs{};
     u64 seed = 0x5EEDC0FFEEULL;
     for (int attempt = 0;; ++attempt) {
@@ -543,18 +537,6 @@ static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         ct.assign(cslots * unit, 0);
         const u32 cm = (u32)(cslots - 1);
         bool ok = true;
-        if (chd) {
-            // ~4 keys per displacement bucket (at least two buckets)
-            u32 rl = 1;
-            while ((1ull << rl) * 4 < keys36.size()) ++rl;
-            dshift = 32 - rl;
-            disp.assign(1ull << rl, 0);
-            const u64 left = chd_build(kw.data(), cv.data(), keys36.size(), cs, cm, dshift, partial, disp.data(),
-                                       ct.data());
-            ok = left == 0;
-            if (ok || partial) break;
-            continue;
-        }
         if (buckets) {
             const u64 homeless = cuckoo_build_buckets(kw.data(), cv.data(), keys36.size(), cs, cslots, seed, partial,
                                                       ct.data());
@@ -601,13 +583,6 @@ static int load_map(ysb_ctx* c, const char* const* ad_ids, const uint32_t* lens,
         c->ctable_slots = cslots;
     }
     HIPCHK(c, hipMemcpy(c->d_ctable, ct.data(), ct.size() * 4, hipMemcpyHostToDevice));
-    hipFree(c->d_disp);
-    c->d_disp = nullptr;
-    if (chd) {
-        HIPCHK(c, hipMalloc(&c->d_disp, disp.size() * 2));
-        HIPCHK(c, hipMemcpy(c->d_disp, disp.data(), disp.size() * 2, hipMemcpyHostToDevice));
-        c->disp_shift = dshift;
-    }
     c->cseed = cs;
     c->ctable_buckets = buckets;
     c->ctable_partial = partial;
@@ -631,8 +606,6 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     p.ctable = c->d_ctable;
     p.ctable_mask = (u32)(c->ctable_slots - 1);
     p.cseed = c->cseed;
-    p.disp = c->d_disp;
-    p.disp_shift = c->disp_shift;
     // a sharded table's misses go to the deferred-line kernel, which tells a foreign-shard
     // key from a real miss (the scan kernels themselves carry no shard logic)
     p.ctable_partial = (c->ctable_partial || c->shard_n > 1) ? 1u : 0u;

@@ -8,8 +8,6 @@
 //    Long.parseLong(t) / time_divisor (CampaignProcessorCommon.java:58).
 #pragma once
 #include <stdint.h>
-#include <algorithm>
-#include <vector>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -332,9 +330,6 @@ YSB_HD u32 key_hash(const u32* w, u32 len) {
 #define YSB_CSLOT_WORDS 16
 #endif
 enum : u32 { CSLOT_WORDS = YSB_CSLOT_WORDS, CKEY_WORDS = 9, CSLOT_CAMP = 9, CSLOT_Q = YSB_CSLOT_WORDS / 4 };
-#ifndef YSB_CHD
-#define YSB_CHD 1   // cache-resident tables as hash-and-displace (one slot per key); 0: two-choice cuckoo
-#endif
 // HBM-resident tables (beyond the L2s: configs[2]'s 10M ads) use BUCKETS instead: 128 B =
 // 3 entries of [9 key words, campaign] at a 10-word stride (+ 2 spare words).  A key goes
 // to its first bucket while that has a free entry, to its second only when the first is
@@ -355,22 +350,6 @@ YSB_HD u32 fmix32(u32 h) {
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
     return h;
 }
-
-// The cache-resident join table as hash-and-displace (CHD): bucket = ha >> shift picks a
-// 16-bit displacement d (a 2-byte read from a tiny, L1-resident array), the key's ONE slot
-// is (hb + d * (ha | 1)) & mask -- one 48-byte probe instead of two candidate slots.
-YSB_HD void chd_hash36(const u32* w, const CuckooSeed& cs, u32* ha, u32* hb) {
-    const u32 R[CKEY_WORDS] = {1, 6, 11, 16, 21, 26, 31, 4, 9};
-    u32 x = 0, y = 0;
-#pragma unroll
-    for (u32 k = 0; k < CKEY_WORDS; ++k) {
-        x ^= rotl32(w[k] + cs.s[k], R[k]);
-        y += w[k] ^ cs.t[k];
-    }
-    *ha = fmix32(x ^ cs.fa);
-    *hb = fmix32(y ^ cs.fb ^ rotl32(x, 16));
-}
-YSB_HD u32 chd_slot(u32 ha, u32 hb, u32 d, u32 mask) { return (hb + d * (ha | 1u)) & mask; }
 
 YSB_HD void cuckoo_slots36(const u32* w, const CuckooSeed& cs, u32 mask, u32* a, u32* b) {
     const u32 R[CKEY_WORDS] = {1, 6, 11, 16, 21, 26, 31, 4, 9};
@@ -441,64 +420,6 @@ static inline u64 cuckoo_build_buckets(const u32* keys, const u32* camp, u64 n, 
         }
     }
     return homeless;
-}
-
-// Host: the CHD build of a cache-resident table of m = mask + 1 slots (CSLOT_WORDS u32
-// each, key words then the campaign) and 2^(32 - shift) buckets: buckets in decreasing
-// size, each takes the first displacement d < 65536 that puts all its keys in distinct
-// free slots.  Returns the keys left out (a bucket no d fits); with keep_going false the
-// build stops at the first.
-static inline u64 chd_build(const u32* keys, const u32* camp, u64 n, const CuckooSeed& cs, u32 mask, u32 shift,
-                            bool keep_going, unsigned short* disp, u32* ct) {
-    const u64 m = (u64)mask + 1, r = 1ull << (32 - shift);
-    for (u64 i = 0; i < m * CSLOT_WORDS; ++i) ct[i] = 0;
-    for (u64 sl = 0; sl < m; ++sl) ct[sl * CSLOT_WORDS + CSLOT_CAMP] = EMPTY_SLOT;
-    for (u64 b = 0; b < r; ++b) disp[b] = 0;
-    std::vector<u32> ha(n), hb(n), cnt(r + 1, 0), order(n);
-    for (u64 i = 0; i < n; ++i) {
-        chd_hash36(keys + i * CKEY_WORDS, cs, &ha[i], &hb[i]);
-        ++cnt[(ha[i] >> shift) + 1];
-    }
-    for (u64 b = 0; b < r; ++b) cnt[b + 1] += cnt[b];
-    {
-        std::vector<u32> at(cnt.begin(), cnt.end() - 1);
-        for (u64 i = 0; i < n; ++i) order[at[ha[i] >> shift]++] = (u32)i;
-    }
-    std::vector<u32> bks(r);
-    for (u64 b = 0; b < r; ++b) bks[b] = (u32)b;
-    std::stable_sort(bks.begin(), bks.end(), [&](u32 x, u32 y) { return cnt[x + 1] - cnt[x] > cnt[y + 1] - cnt[y]; });
-    std::vector<unsigned char> used(m, 0);
-    std::vector<u32> sl;
-    u64 left = 0;
-    for (u32 b : bks) {
-        const u32 lo = cnt[b], hi = cnt[b + 1];
-        if (lo == hi) break;
-        bool ok = false;
-        for (u32 d = 0; d < 65536u && !ok; ++d) {
-            sl.clear();
-            ok = true;
-            for (u32 j = lo; j < hi && ok; ++j) {
-                const u32 s = chd_slot(ha[order[j]], hb[order[j]], d, mask);
-                if (used[s]) ok = false;
-                for (u32 t : sl) ok = ok && t != s;
-                sl.push_back(s);
-            }
-            if (ok) {
-                disp[b] = (unsigned short)d;
-                for (u32 j = lo; j < hi; ++j) {
-                    const u32 i = order[j], s = sl[j - lo];
-                    used[s] = 1;
-                    for (u32 w = 0; w < CKEY_WORDS; ++w) ct[(u64)s * CSLOT_WORDS + w] = keys[(u64)i * CKEY_WORDS + w];
-                    ct[(u64)s * CSLOT_WORDS + CSLOT_CAMP] = camp[i];
-                }
-            }
-        }
-        if (!ok) {
-            left += hi - lo;
-            if (!keep_going) return left;
-        }
-    }
-    return left;
 }
 
 // Host restatement of the scan's bucket probe (ysb_scan.hip bucket_find + the second

@@ -113,8 +113,6 @@ struct ScanParams {
     u32 probe_serial;           // 1: probe the second cuckoo slot only after a first-slot miss
     u32 tbl;                    // 1: the fork's .tbl rows (YSB_F_FORMAT_TBL) instead of JSON lines
     CuckooSeed cseed;
-    const unsigned short* disp; // YSB_CHD cache-resident table: per-bucket displacements (nullptr: cuckoo)
-    u32 disp_shift;             // bucket = ha >> disp_shift
     u32 n_campaigns;
     unsigned long long* counts; // [c_pad][W] u64, campaign-major
     u32 ring_w;                 // W (power of two)

@@ -1759,25 +1759,15 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
 #else
         if (pend) {
 #endif
+            u32 ia, ib;
+            cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
             if constexpr (SERIAL) {
-                u32 ia, ib;
-                cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
 #pragma unroll
                 for (int j = 0; j < (int)CB_Q; ++j) q[j] = ct4[CB_Q * (u64)ia + j];
                 ib_s = ib;
             } else {
-#if YSB_CHD
-                // the key's one slot: its bucket's displacement (a 2-byte read, L1-resident)
-                u32 ha, hb;
-                chd_hash36(ca.kw, P.cseed, &ha, &hb);
-                const u32 ia = chd_slot(ha, hb, (u32)P.disp[ha >> P.disp_shift], P.ctable_mask);
-                a0 = ct4[CSLOT_Q * (u64)ia]; a1 = ct4[CSLOT_Q * (u64)ia + 1]; a2 = ct4[CSLOT_Q * (u64)ia + 2];
-#else
-                u32 ia, ib;
-                cuckoo_slots36(ca.kw, P.cseed, P.ctable_mask, &ia, &ib);
                 a0 = ct4[CSLOT_Q * (u64)ia]; a1 = ct4[CSLOT_Q * (u64)ia + 1]; a2 = ct4[CSLOT_Q * (u64)ia + 2];
                 b0 = ct4[CSLOT_Q * (u64)ib]; b1 = ct4[CSLOT_Q * (u64)ib + 1]; b2 = ct4[CSLOT_Q * (u64)ib + 2];
-#endif
             }
         }
         if (ok2) {
@@ -1816,12 +1806,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                                (a1.y ^ k[5]) | (a1.z ^ k[6]) | (a1.w ^ k[7]) | (a2.x ^ k[8]);
                 const u32 db = (b0.x ^ k[0]) | (b0.y ^ k[1]) | (b0.z ^ k[2]) | (b0.w ^ k[3]) | (b1.x ^ k[4]) |
                                (b1.y ^ k[5]) | (b1.z ^ k[6]) | (b1.w ^ k[7]) | (b2.x ^ k[8]);
-#if YSB_CHD
-                (void)db;
-                ci = (da == 0u && a2.y != EMPTY_SLOT) ? a2.y : EMPTY_SLOT;
-#else
                 ci = (da == 0u && a2.y != EMPTY_SLOT) ? a2.y : (db == 0u ? b2.y : EMPTY_SLOT);
-#endif
             }
             if (ci == EMPTY_SLOT) {
                 if (P.ctable_partial) {   // the key may be one the cuckoo build left out
