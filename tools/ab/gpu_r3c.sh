@@ -1,16 +1,18 @@
-# config 3 after the packed 64-B buckets + u8 delta: tests, two timed runs, trace, PMC traffic
+#!/bin/bash
+# Round 3: cache-resident join table as hash-and-displace (one slot per key; default) vs the
+# two-choice cuckoo (YSB_CHD=0) -- parity / tier / mutation / topology tests, .tbl and
+# headline A/B pairs.
 set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r3c; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_records.py tests/test_gpu_ranks.py -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-tail -3 $O/tests.log
-for i in 1 2; do timeout -k 10 300 python -u tools/extra_one.py config3 > $O/c3_$i.json 2> $O/c3_$i.err || exit 1; done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 tools/extra_one.py config3 --extra-steps 5 --warmup 2 > $O/trace.json 2> $O/trace.err || exit 1
-timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 tools/extra_one.py config3 --extra-steps 2 --warmup 1 > $O/pmc_fetch.json 2>$O/pmc_fetch.err || exit 1
-timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 tools/extra_one.py config3 --extra-steps 2 --warmup 1 > $O/pmc_write.json 2>$O/pmc_write.err || exit 1
-for k in scan_kernel rec_partition rec_count; do echo "== $k"; python3 tools/pmc_summary.py $O $k | tail -4; done
-python3 -c "
-import json
-for i in (1,2):
-    d=json.load(open('$O/c3_%d.json'%i)); print(d['events_per_s']/1e9, d['hbm_frac'], d['avg_launch_ms'], d['avg_path_ms'], d['check'])
-"
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-r3c}; mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_tiers.py tests/test_gpu_mutations.py tests/test_gpu_topology.py tests/test_gpu_segments.py -x -q --timeout 300 --timeout-method thread > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+tail -1 $O/t.log
+for i in 1 2 3; do
+for v in base cuckoo; do
+  if [ "$v" = base ]; then unset YSB_LIB_VARIANT; else export YSB_LIB_VARIANT=$v; fi
+  timeout -k 10 200 python3 tools/extra_one.py tbl > $O/tbl_${v}_$i.json 2> $O/tbl_${v}_$i.err || { tail -20 $O/tbl_${v}_$i.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/tbl_${v}_$i.json')); print('tbl $v', round(d['events_per_s']/1e9,3), d['avg_launch_ms'], d['hbm_frac'], d['check']['truth_mismatched_cells'], d['check']['deferred'])"
+  timeout -k 10 200 python3 bench.py --no-cpu --no-check --no-extras > $O/h_${v}_$i.json 2> $O/h_${v}_$i.err || { tail -20 $O/h_${v}_$i.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/h_${v}_$i.json')); print('headline $v', round(d['value']/1e9,3), d['roofline']['avg_launch_ms'])"
+done
+done
