@@ -1,18 +1,16 @@
-# A/B: layout sampling of device batches (default) vs YSB_F_LAYOUT_FIXED on the headline,
-# then the extras (no stream) on the new tree.
+#!/bin/bash
+# Round 3: record staging positions by per-bin ballots (no LDS atomics) -- record / stream /
+# rank / mutation tests with it, then config-3 A/B pairs.
 set -o pipefail
-mkdir -p gpurun_out/r3b
-for i in 1 2; do
-  timeout -k 10 300 python -u bench.py --no-extras --no-cpu --no-check > gpurun_out/r3b/a$i.json 2> gpurun_out/r3b/a$i.err || exit 1
-  timeout -k 10 300 python -u bench.py --no-extras --no-cpu --no-check --layout-fixed > gpurun_out/r3b/b$i.json 2> gpurun_out/r3b/b$i.err || exit 1
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-r3b}; mkdir -p $O
+export YSB_LIB_VARIANT=ballot
+timeout -k 10 400 python -u -m pytest tests/test_gpu_records.py tests/test_gpu_stream.py tests/test_gpu_ranks.py tests/test_gpu_mutations.py -x -q --timeout 300 --timeout-method thread > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+echo "ballot $(tail -1 $O/t.log)"
+for i in 1 2 3; do
+for v in base ballot; do
+  if [ "$v" = base ]; then unset YSB_LIB_VARIANT; else export YSB_LIB_VARIANT=$v; fi
+  timeout -k 10 200 python3 tools/extra_one.py config3 > $O/c3_${v}_$i.json 2> $O/c3_${v}_$i.err || { tail -20 $O/c3_${v}_$i.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/c3_${v}_$i.json')); print('c3 $v', round(d['events_per_s']/1e9,3), d['avg_launch_ms'], d['avg_path_ms'], d['hbm_frac'], d['check']['truth_mismatched_cells'])"
 done
-timeout -k 10 900 python -u bench.py --no-cpu --stream-seconds 0 > gpurun_out/r3b/full.json 2> gpurun_out/r3b/full.err || exit 1
-python - <<'PY'
-import json
-for n in ("a1","b1","a2","b2"):
-    d=json.load(open("gpurun_out/r3b/%s.json"%n)); print(n, d["value"]/1e9, d["roofline"]["avg_launch_ms"], d["roofline"]["kernel"])
-d=json.load(open("gpurun_out/r3b/full.json"))
-print("headline", d["value"]/1e9, d["check"])
-for k,v in d["extras"].items():
-    print(k, v.get("events_per_s",0)/1e9, v.get("hbm_frac"), v.get("kernel"), v.get("check",{}).get("truth_mismatched_cells"), v.get("error"))
-PY
+done
