@@ -47,6 +47,16 @@ def test_token_kind(tok, kind):
     (b'{"user_id"="u","page_id":"p","ad_id":"a","ad_type":"t","event_type":"view","event_time":"1"}', False),
     (b'{"user_id":"u","page_id":"p","ad_id":"a","ad_type":"t","event_type":"view"}', False),
     (b"", False), (b"[]", False), (b"{}", False), (b"{", False), (b"{\"a\": [", False),
+    # a producer's extra fields (the GPU flat tier takes exactly one plain-string extra pair)
+    (b'{"src": "w", "user_id":"u","page_id":"p","ad_id":"a","ad_type":"t","event_type":"view","event_time":"1"}', True),
+    (b'{"user_id":"u","page_id":"p","ad_idx":"7","ad_id":"a","ad_type":"t","event_type":"view","event_time":"1"}', True),
+    (b'{"a1":"x","a2":"y","user_id":"u","page_id":"p","ad_id":"a","ad_type":"t","event_type":"view","event_time":"1"}',
+     True),
+    (b'{"a1":"x","a1":"y","user_id":"u","page_id":"p","ad_id":"a","ad_type":"t","event_type":"view","event_time":"1"}',
+     False),                                                                                   # putOnce: duplicate
+    (b'{"":"x","user_id":"u","page_id":"p","ad_id":"a","ad_type":"t","event_type":"view","event_time":"1"}', True),
+    (b'{"user_id":"u","user_id":"v","page_id":"p","ad_id":"a","ad_type":"t","event_type":"view","event_time":"1"}',
+     False),
 ])
 def test_line_known_answers(line, ok):
     def parses(ln):
