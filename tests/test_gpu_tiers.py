@@ -388,3 +388,38 @@ def test_extra_fields_match_oracle(hint, base_variant):
             assert lay == 2 and st["deferred"] == 0    # the flat tier took every line
         else:
             assert est["parse_errors"] > 0 and st["deferred"] > 0
+
+
+@pytest.mark.parametrize("hint", [None, "flat_first"])
+def test_extra_field_edge_lines_match_oracle(hint):
+    """Edge forms around the flat tier's one extra field: an empty key, a key named like
+    one of DeserializeBolt's with more bytes, an extra pair after a repeated known key,
+    the extra pair last (before '}'), compact and spaced separators -- each line in a
+    batch of its own kind, exact vs the oracle."""
+    g = GenParams(seed=37, n_campaigns=20, ads_per_campaign=5, events_per_sec=1000)
+    _, aids = g.ids()
+    raw, offs = g.events_host(0, 2000)
+    data = raw.tobytes()
+    ends = list(offs[1:]) + [len(data)]
+    base = [data[s:e] for s, e in zip(offs, ends)]
+    edits = [lambda ln: ln.replace(b'{"user_id"', b'{"": "x", "user_id"', 1),
+             lambda ln: ln.replace(b'{"user_id"', b'{"event_timex": "1", "user_id"', 1),
+             lambda ln: ln.replace(b'{"user_id"', b'{"ad_i": "1", "user_id"', 1),
+             lambda ln: ln[:-2] + b', "zz": "last"}\n',
+             lambda ln: ln[:-2] + b',"zz":"last"}\n',
+             lambda ln: ln.replace(b'{"user_id"', b'{"x": "1", "user_id": "u", "user_id"', 1),
+             lambda ln: ln.replace(b'{"user_id"', b'{ "x" :"1" ;"user_id"', 1)]
+    for ed in edits:
+        lines = [ed(ln) for ln in base]
+        buf = b"".join(lines)
+        o = np.cumsum([0] + [len(x) for x in lines[:-1]]).astype(np.uint32)
+        exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), buf, o)
+        with YsbContext(n_campaigns=20, window_ring=64, max_batch_bytes=len(buf) + 64,
+                        max_batch_events=o.size + 1, **hint_kw(hint)) as ctx:
+            ctx.load_ad_map(aids, g.ad_campaign_index())
+            ctx.submit(np.frombuffer(buf, dtype=np.uint8), o)
+            got = ctx.drain_buckets()
+            st = ctx.stats()
+        assert got == exp, lines[0]
+        for k, v in est.items():
+            assert st[k] == v, (k, lines[0])
