@@ -71,6 +71,11 @@ def parse_args(argv=None):
     ap.add_argument("--stream-seconds", type=int, default=125,
                     help="extras: seconds of real-time sharded streaming (configs[4]; 125 s closes >= 10 windows); "
                          "0 skips it")
+    ap.add_argument("--dropin-events", type=int, default=100_000_000,
+                    help="extras: events through the host-staged (pinned slots, H2D) path")
+    ap.add_argument("--runner-file-events", type=int, default=20_000_000,
+                    help="extras: events in the native runner's replay file")
+    ap.add_argument("--runner-repeat", type=int, default=5, help="extras: times the runner reads its replay file")
     ap.add_argument("--extras-timeout", type=int, default=300,
                     help="N > 1: seconds the configs[2]-table leg may take before rank 0 prints the headline without it")
     ap.add_argument("--c3-events", type=int, default=100_000_000,
@@ -336,12 +341,51 @@ def extras(args, device):
     headline (one launch per step), and configs[4]'s sharded streaming.  Each leg is
     guarded: a failure is recorded as {"error": ...} under its key."""
     out = {}
+    guarded(out, "host_staged", lambda: extra_host_staged(args, device))
+    guarded(out, "native_runner", lambda: extra_native_runner(args, device, out.get("host_staged")))
     guarded(out, "config3", lambda: extra_config3(args, device))
     guarded(out, "tbl", lambda: extra_tbl(args, device))
     extra_layouts(args, device, out)
     if args.stream_seconds > 0:
         guarded(out, "stream_sharded", lambda: extra_stream(args))
     return out
+
+
+def extra_host_staged(args, device):
+    """The drop-in's host-staged path (AdvertisingTopologyNative.java:111-119): configs[1]'s
+    events through the pinned double-buffered slots, H2D + scan, with host line offsets
+    (ysb_submit) and as raw lines split on the GPU (ysb_submit_raw) -- tools/bench_dropin.py."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_dropin
+    r = {"offsets": bench_dropin.host_staged(device, args.dropin_events, raw=False),
+         "raw": bench_dropin.host_staged(device, args.dropin_events, raw=True)}
+    log("extras: host_staged %.3f / raw %.3f G events/s" % (r["offsets"]["events_per_s"] / 1e9,
+                                                           r["raw"]["events_per_s"] / 1e9))
+    return r
+
+
+def extra_native_runner(args, device, staged):
+    """bin/ysb_topology (the native drop-in for `flink run ... --confPath`) over a replay file
+    in the page cache, read --runner-repeat times: raw lines with the split on the GPU (the
+    default) and host-split offsets, against the generator truth; vs_host_staged = its stream
+    rate / the host-staged raw path's (the H2D-bound rate)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_dropin
+    import tempfile
+    path = tempfile.mkdtemp(prefix="ysb_replay_", dir=os.environ.get("TMPDIR") or "/tmp")
+    try:
+        r = {"gpu_split": bench_dropin.native_runner(device, args.runner_file_events, args.runner_repeat,
+                                                    workdir=path),
+             "host_split": bench_dropin.native_runner(device, args.runner_file_events, args.runner_repeat,
+                                                     host_split=True, workdir=path)}
+    finally:
+        import shutil
+        shutil.rmtree(path, ignore_errors=True)
+    if staged and "raw" in staged:
+        r["vs_host_staged"] = round(r["gpu_split"]["stream_events_per_s"] / staged["raw"]["events_per_s"], 4)
+    log("extras: native_runner %.3f G events/s (host split %.3f)" % (r["gpu_split"]["stream_events_per_s"] / 1e9,
+                                                                     r["host_split"]["stream_events_per_s"] / 1e9))
+    return r
 
 
 def extra_config3(args, device):

@@ -30,8 +30,10 @@ extern "C" {
  *    range-limited exchange (ysb_group_exchange_info / ysb_exchange_plan),
  *    ysb_group_checksum, layout selection on by default (YSB_F_LAYOUT_FIXED turns it off),
  *    ysb_sync's sticky YSB_ERR_CAPACITY, the collective ysb_ring_advance after
- *    ysb_group_init, ysb_gen_params.variant */
-#define YSB_ABI_VERSION 2
+ *    ysb_group_init, ysb_gen_params.variant
+ * 3: raw batches with the line split on the GPU (ysb_submit_raw, ysb_split_lines_device),
+ *    ysb_slot_capacity, ysb_copy_time; device batches' layout sampled in stream order */
+#define YSB_ABI_VERSION 3
 
 /* status codes */
 #define YSB_OK            0
@@ -218,7 +220,33 @@ int         ysb_slot_buffers(ysb_ctx* ctx, int slot, uint8_t** bytes, uint32_t**
 int         ysb_submit(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes,
                        const uint32_t* line_off, uint64_t n_events);
 int         ysb_wait(ysb_ctx* ctx, int slot);
-/* Device-resident batch (HBM pointers, e.g. from ysb_device_alloc). Asynchronous. */
+/* The capacity the context was opened with (ysb_config.max_batch_bytes / max_batch_events):
+ * the size of each slot's pinned buffers from ysb_slot_buffers, for a caller (e.g. a JNI
+ * NewDirectByteBuffer over them) that must not write past them. */
+int         ysb_slot_capacity(ysb_ctx* ctx, uint64_t* max_bytes, uint64_t* max_events);
+/* A raw batch: whole lines as bytes, no offsets.  The line starts are found on the GPU
+ * (ysb_split.hip) where BufferedReader.readLine ends a line -- '\n', "\r\n" or a lone '\r';
+ * a last line without a terminator is a line, a terminator that ends the batch starts none --
+ * so the caller (FileBasedDataSource.run, AdvertisingTopologyNative.java:144-165) only reads
+ * the file into the pinned slot (max_batch_bytes; max_batch_events does not apply).
+ * Asynchronous and double-buffered like ysb_submit: H2D on the copy stream, the split on a
+ * stream of its own; the batch's scan is launched once its line count is back, at the next
+ * call on the context (the next submit, ysb_sync, ...), so a caller that fills the other slot
+ * in between keeps the copy engine busy; ysb_wait(ctx, slot) before the slot's pinned buffer
+ * is rewritten.  An error of that deferred launch is returned by the call that performs it. */
+int         ysb_submit_raw(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes);
+/* The same split of a device-resident batch (16-byte aligned, < 4 GiB): d_off[0..*n) <- its
+ * line starts (YSB_ERR_CAPACITY, *n = the lines, if more than cap).  Synchronous. */
+int         ysb_split_lines_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, uint32_t* d_off,
+                                   uint64_t cap, uint64_t* n);
+/* Device-resident batch (HBM pointers, e.g. from ysb_device_alloc). Asynchronous.  The batch
+ * must be complete when submitted, or its producer ordered before the compute stream
+ * (hipStreamWaitEvent(ysb_stream(ctx), ...), or produced on that stream).  Unless
+ * YSB_F_LAYOUT_FIXED, the first line of every segment is copied into pinned memory by a small
+ * kernel on the compute stream (so after that producer) to pick the scan's instantiation: the
+ * launch's own sample when the compute stream is idle at the submit (the host waits for that
+ * copy, microseconds), else the previous launch's (no wait for the device: one launch late --
+ * counts never depend on the choice). */
 int         ysb_submit_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes,
                               const uint32_t* d_line_off, uint64_t n_events);
 /* Several device-resident batches in ONE kernel launch.  Each segment is a batch as
@@ -275,6 +303,9 @@ int         ysb_ring_advance(ysb_ctx* ctx, int64_t new_lo);
 /* With YSB_F_TIMING: total device time of the scan kernel launches (HIP events on
  * the compute stream) and the number of launches since the last call (resets). */
 int         ysb_kernel_time(ysb_ctx* ctx, double* total_ms, uint64_t* launches);
+/* With YSB_F_TIMING: device time of the host-to-device copies of ysb_submit / ysb_submit_raw
+ * (HIP events on the copy stream), their number and bytes since the last call (resets). */
+int         ysb_copy_time(ysb_ctx* ctx, double* total_ms, uint64_t* copies, uint64_t* bytes);
 /* The same launches' whole device sequence -- scan, general-path and (record mode)
  * partition + count kernels -- as measured by the last ysb_kernel_time call (which
  * collects both), and the launches so far that used record mode. */

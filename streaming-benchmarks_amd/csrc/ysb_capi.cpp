@@ -52,11 +52,34 @@ struct ysb_ctx {
     int submit_layout = -1;      // the layout a submit read off its batch's first line (-1: the flags')
     LearnDesc submit_learn{};    // ... and, layout 3, the key order
     ysb_launch_desc last_launch{};   // the instantiation of the last launch
-    u8* h_sample = nullptr;      // pinned: device batches' first-line samples
+    // device batches' first-line samples: written by sample_kernel on the compute stream (so
+    // after whatever produced the batch there) into pinned memory, two buffers alternating
+    // by launch; ev_sample[k] marks buffer k complete, sample_nseg[k] its segments (0: none)
+    u8* h_sample = nullptr;
+    hipEvent_t ev_sample[2] = {nullptr, nullptr};
+    u32 sample_nseg[2] = {0, 0};
+    int sample_cur = 0;
     u32* h_used = nullptr;       // pinned: the out-of-ring map's fill level after a launch ...
     hipEvent_t ev_used = nullptr; // ... readable once this has completed
     bool used_pending = false;
-    hipStream_t s_aux = nullptr; // the samples' copies
+    // raw batches (ysb_submit_raw): the line starts are found on the GPU (ysb_split.hip) on
+    // s_split after the slot's H2D, into d_roff[slot]; the scan is launched once the line
+    // count is back (launch_pending_raw, at the next call), so the next H2D queues first
+    hipStream_t s_split = nullptr;
+    u32* d_roff[2] = {nullptr, nullptr};        // max_batch_bytes + 1 starts per slot
+    u32* d_split_chunk = nullptr;               // per-chunk counts, then bases
+    u64 split_chunk_words = 0;
+    unsigned long long* d_rawn = nullptr;       // [2] lines of the slot's raw batch
+    unsigned long long* h_rawn = nullptr;       // pinned mirror
+    hipEvent_t ev_raw[2] = {nullptr, nullptr};  // split done and its count read back
+    int raw_pend = -1;                          // the slot whose raw batch awaits its launch
+    u64 raw_nbytes[2] = {0, 0};
+    int raw_layout[2] = {-1, -1};               // its first line's layout (sampled on the host)
+    LearnDesc raw_learn[2]{};
+    // H2D timing (YSB_F_TIMING): {start, end} of each slot copy since the last ysb_copy_time
+    std::vector<std::array<hipEvent_t, 2>> cev;
+    size_t cev_used = 0;
+    u64 copy_bytes = 0;
     CuckooSeed cseed{};
     bool ctable_partial = false;
     bool table_loaded = false;
@@ -192,6 +215,7 @@ static int allreduce_max(ysb_ctx* c, i64* h, int n);
 static int sync_streams(ysb_ctx* c);
 static int pull_side_list(ysb_ctx* c);
 static bool grouped(const ysb_ctx* c);
+static int launch_pending_raw(ysb_ctx* c);
 
 int ysb_abi_version(void) { return YSB_ABI_VERSION; }
 
@@ -215,6 +239,7 @@ static void destroy(ysb_ctx* c) {
     hipSetDevice(c->device);
     if (c->s_comp) hipStreamSynchronize(c->s_comp);
     if (c->s_copy) hipStreamSynchronize(c->s_copy);
+    if (c->s_split) hipStreamSynchronize(c->s_split);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_table);
     hipFree(c->d_ctable);
@@ -261,9 +286,19 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_runs);
     if (c->ev_ring) hipEventDestroy(c->ev_ring);
     hipHostFree(c->h_sample);
+    for (hipEvent_t e : c->ev_sample)
+        if (e) hipEventDestroy(e);
     hipHostFree(c->h_used);
     if (c->ev_used) hipEventDestroy(c->ev_used);
-    if (c->s_aux) hipStreamDestroy(c->s_aux);
+    for (int s = 0; s < 2; ++s) {
+        hipFree(c->d_roff[s]);
+        if (c->ev_raw[s]) hipEventDestroy(c->ev_raw[s]);
+    }
+    hipFree(c->d_split_chunk);
+    hipFree(c->d_rawn);
+    hipHostFree(c->h_rawn);
+    for (auto& p : c->cev) for (hipEvent_t e : p) hipEventDestroy(e);
+    if (c->s_split) hipStreamDestroy(c->s_split);
     if (c->s_comp) hipStreamDestroy(c->s_comp);
     if (c->s_copy) hipStreamDestroy(c->s_copy);
     delete c;
@@ -419,7 +454,8 @@ int ysb_load_ad_map_shard(ysb_ctx* c, const char* const* ad_ids, const uint32_t*
     if (!c) return YSB_ERR_ARG;
     if (nranks == 0 || rank >= nranks) return fail(c, YSB_ERR_ARG, "bad shard %u / %u", rank, nranks);
     if (n && (!ad_ids || !campaign_idx)) return fail(c, YSB_ERR_ARG, "NULL ad map arrays");
-    int rc;
+    int rc = launch_pending_raw(c);   // a batch submitted before the new map joins against the old one
+    if (rc) return rc;
     if (nranks == 1) {
         rc = load_map(c, ad_ids, lens, campaign_idx, n);
     } else {
@@ -960,48 +996,50 @@ static int hinted_layout(const ysb_ctx* c, int sampled) {
     return sampled;
 }
 
-// Device batches: the first line of every segment, sampled by small device-to-host copies
-// on a stream of their own (the caller's contract: a device batch's bytes are complete
-// when it is submitted).  One layout for the launch: the segments' common one, else the
-// flat-object tier first (it takes every layout).
+// Device batches: the first line of every segment, copied by sample_kernel on the compute
+// stream -- in stream order, so after whatever produced the batch there (the caller's
+// contract: a device batch is complete when submitted, or its producer is ordered before
+// ysb_stream(ctx)) -- into one of two pinned buffers.  Which sample decides: this launch's
+// own when the compute stream was idle at the submit (the copy finishes in microseconds) or
+// no earlier sample exists; otherwise the previous launch's, read without waiting for the
+// device (one launch late: a producer writes one layout, and counts do not depend on the
+// choice).  One layout for the launch: the segments' common one, else the flat-object tier
+// first (it takes every layout).
 static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, LearnDesc* d) {
-    constexpr u32 SAMPLE = 288, STRIDE = 16 + SAMPLE;   // a line of the scan's tile capacity
+    const u64 buf = (u64)MAX_SEGS * SAMPLE_STRIDE;
     if (!c->h_sample) {
-        HIPCHK(c, hipHostMalloc(&c->h_sample, (u64)MAX_SEGS * STRIDE));
-        HIPCHK(c, hipStreamCreateWithFlags(&c->s_aux, hipStreamNonBlocking));
+        HIPCHK(c, hipHostMalloc(&c->h_sample, 2 * buf));
+        for (hipEvent_t& e : c->ev_sample) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    u8* h = c->h_sample;
+    const bool idle = hipStreamQuery(c->s_comp) == hipSuccess;
+    const int k = c->sample_cur;
+    c->sample_cur ^= 1;
+    SampleSegs ss{};
     u32 n = 0;
     for (u32 i = 0; i < nseg && n < (u32)MAX_SEGS; ++i) {
         if (!segs[i].n_events) continue;
-        const u64 nb = std::min<u64>(segs[i].nbytes, SAMPLE);
-        std::memset(h + (u64)n * STRIDE, 0, 16);
-        HIPCHK(c, hipMemcpyAsync(h + (u64)n * STRIDE, segs[i].d_line_off, segs[i].n_events > 1 ? 8 : 4,
-                                 hipMemcpyDeviceToHost, c->s_aux));
-        if (nb) HIPCHK(c, hipMemcpyAsync(h + (u64)n * STRIDE + 16, segs[i].d_bytes, nb, hipMemcpyDeviceToHost, c->s_aux));
+        ss.bytes[n] = segs[i].d_bytes;
+        ss.off[n] = segs[i].d_line_off;
+        ss.nbytes[n] = segs[i].nbytes;
+        ss.n[n] = segs[i].n_events;
         ++n;
     }
-    HIPCHK(c, hipStreamSynchronize(c->s_aux));
+    launch_sample(ss, n, c->h_sample + (u64)k * buf, c->s_comp);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev_sample[k], c->s_comp));
+    c->sample_nseg[k] = n;
+    const int use = (!idle && c->sample_nseg[k ^ 1]) ? k ^ 1 : k;
+    HIPCHK(c, hipEventSynchronize(c->ev_sample[use]));
+    const u8* h = c->h_sample + (u64)use * buf;
     const u32 req = (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu;
     int lay = -1;
-    n = 0;
-    for (u32 i = 0; i < nseg && n < (u32)MAX_SEGS; ++i) {
-        if (!segs[i].n_events) continue;
-        u8* s = h + (u64)n * STRIDE;
-        ++n;
-        u32 o[2];
-        std::memcpy(o, s, 8);
-        const u64 end = segs[i].n_events > 1 ? (u64)o[1] : segs[i].nbytes;
-        if (o[0] > end || end > segs[i].nbytes) return 0;   // bad offsets: the scan defers them anyway
-        const u64 len = std::min<u64>(end - o[0], SAMPLE);
-        const u8* line = s + 16 + o[0];
-        if (o[0] + len > SAMPLE && len) {   // the first line does not lie in the sample: read it
-            HIPCHK(c, hipMemcpyAsync(s + 16, segs[i].d_bytes + o[0], len, hipMemcpyDeviceToHost, c->s_aux));
-            HIPCHK(c, hipStreamSynchronize(c->s_aux));
-            line = s + 16;
-        }
+    for (u32 i = 0; i < c->sample_nseg[use]; ++i) {
+        const u8* s = h + (u64)i * SAMPLE_STRIDE;
+        u32 hd[3];
+        std::memcpy(hd, s, 12);
+        if (!hd[2]) return 0;   // bad offsets: the scan defers them anyway
         LearnDesc di{};
-        const int l = learn_layout(line, len, req, &di);
+        const int l = learn_layout(s + 16, hd[1], req, &di);
         if (lay < 0) {
             lay = l;
             *d = di;
@@ -1010,6 +1048,20 @@ static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, L
         }
     }
     return lay < 0 ? 0 : lay;
+}
+
+// With YSB_F_TIMING: an event pair around a slot's H2D copy (ysb_copy_time), else none.
+static int copy_events(ysb_ctx* c, hipEvent_t** out, u64 bytes) {
+    *out = nullptr;
+    if (!(c->cfg.flags & YSB_F_TIMING)) return YSB_OK;
+    if (c->cev_used == c->cev.size()) {
+        std::array<hipEvent_t, 2> ev{};
+        for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
+        c->cev.push_back(ev);
+    }
+    *out = c->cev[c->cev_used++].data();
+    c->copy_bytes += bytes;
+    return YSB_OK;
 }
 
 static int ensure_slots(ysb_ctx* c) {
@@ -1041,7 +1093,8 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
         return fail(c, YSB_ERR_CAPACITY, "batch (%llu B, %llu events) exceeds max_batch_bytes/max_batch_events",
                     (unsigned long long)nbytes, (unsigned long long)n);
     if ((nbytes && !bytes) || (n && !line_off)) return fail(c, YSB_ERR_ARG, "NULL batch buffers");
-    int rc = ensure_slots(c);
+    int rc = launch_pending_raw(c);   // batches launch in submission order
+    if (!rc) rc = ensure_slots(c);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     // the slot's previous H2D must be done before its pinned buffers are rewritten
@@ -1050,8 +1103,12 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
     if (line_off != c->h_off[slot] && n) std::memcpy(c->h_off[slot], line_off, n * 4);
     // ... and the slot's previous kernel must be done before its device buffers are
     HIPCHK(c, hipStreamWaitEvent(c->s_copy, c->ev_kdone[slot], 0));
+    hipEvent_t* ce = nullptr;
+    if ((rc = copy_events(c, &ce, nbytes + n * 4))) return rc;
+    if (ce) HIPCHK(c, hipEventRecord(ce[0], c->s_copy));
     if (nbytes) HIPCHK(c, hipMemcpyAsync(c->d_bytes[slot], c->h_bytes[slot], nbytes, hipMemcpyHostToDevice, c->s_copy));
     if (n) HIPCHK(c, hipMemcpyAsync(c->d_off[slot], c->h_off[slot], n * 4, hipMemcpyHostToDevice, c->s_copy));
+    if (ce) HIPCHK(c, hipEventRecord(ce[1], c->s_copy));
     HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
     HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_h2d[slot], 0));
     const ysb_segment sg{c->d_bytes[slot], nbytes, c->d_off[slot], n};
@@ -1075,8 +1132,160 @@ int ysb_wait(ysb_ctx* c, int slot) {
     return YSB_OK;
 }
 
+// ---- raw batches (ysb_submit_raw): the line split on the GPU ----------------------------------
+
+static int ensure_raw(ysb_ctx* c) {
+    if (c->h_rawn) return YSB_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    for (int s = 0; s < 2; ++s) {   // (a failed earlier attempt may have left some of these)
+        hipFree(c->d_roff[s]);
+        c->d_roff[s] = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_roff[s], (c->cfg.max_batch_bytes + 1) * 4));   // n <= nbytes lines
+        if (!c->ev_raw[s]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_raw[s], hipEventDisableTiming));
+    }
+    if (!c->s_split) HIPCHK(c, hipStreamCreateWithFlags(&c->s_split, hipStreamNonBlocking));
+    const u64 words = split_chunks(c->cfg.max_batch_bytes) + 1;
+    if (c->split_chunk_words < words) {
+        hipFree(c->d_split_chunk);
+        c->d_split_chunk = nullptr;
+        c->split_chunk_words = 0;
+        HIPCHK(c, hipMalloc(&c->d_split_chunk, words * 4));
+        c->split_chunk_words = words;
+    }
+    HIPCHK(c, hipHostMalloc(&c->h_rawn, 16));
+    return YSB_OK;
+}
+
+// The raw batch waiting for its launch (if any): its line count is back from the device
+// (ev_raw), so its scan is enqueued now -- the order of submission is kept.
+static int launch_pending_raw(ysb_ctx* c) {
+    if (c->raw_pend < 0) return YSB_OK;
+    const int slot = c->raw_pend;
+    c->raw_pend = -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipEventSynchronize(c->ev_raw[slot]));
+    HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_raw[slot], 0));
+    const ysb_segment sg{c->d_bytes[slot], c->raw_nbytes[slot], c->d_roff[slot], c->h_rawn[slot]};
+    c->submit_layout = c->raw_layout[slot];
+    c->submit_learn = c->raw_learn[slot];
+    const int rc = enqueue_scan(c, &sg, 1);
+    c->submit_layout = -1;
+    // the slot's device buffers are free again once this launch has run
+    HIPCHK(c, hipEventRecord(c->ev_kdone[slot], c->s_comp));
+    return rc;
+}
+
+// The layout of a raw batch from its first line (host bytes: up to the first terminator).
+static int sniff_raw(const ysb_ctx* c, const u8* b, u64 nbytes, LearnDesc* d) {
+    const u64 lim = std::min<u64>(nbytes, 4096);
+    u64 e = 0;
+    while (e < lim && b[e] != '\n' && b[e] != '\r') ++e;
+    return learn_layout(b, std::min<u64>(e + 1, nbytes), (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu, d);
+}
+
+int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) {
+    if (!c) return YSB_ERR_ARG;
+    if (slot < 0 || slot > 1) return fail(c, YSB_ERR_ARG, "slot must be 0 or 1");
+    if (nbytes > c->cfg.max_batch_bytes)
+        return fail(c, YSB_ERR_CAPACITY, "raw batch of %llu B exceeds max_batch_bytes", (unsigned long long)nbytes);
+    if (nbytes && !bytes) return fail(c, YSB_ERR_ARG, "NULL batch buffer");
+    if (!c->table_loaded) return fail(c, YSB_ERR_STATE, "ysb_load_ad_map has not been called");
+    // the slot's own earlier batch launches first (its device buffers are about to be reused)
+    int rc = c->raw_pend == slot ? launch_pending_raw(c) : YSB_OK;
+    if (!rc) rc = ensure_slots(c);
+    if (!rc) rc = ensure_raw(c);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    // the slot's previous H2D must be done before its pinned buffer is rewritten
+    HIPCHK(c, hipEventSynchronize(c->ev_h2d[slot]));
+    if (bytes != c->h_bytes[slot] && nbytes) std::memcpy(c->h_bytes[slot], bytes, nbytes);
+    c->raw_layout[slot] = -1;
+    if (layout_sampling(c) && nbytes)
+        c->raw_layout[slot] = hinted_layout(c, sniff_raw(c, c->h_bytes[slot], nbytes, &c->raw_learn[slot]));
+    // H2D once the slot's previous kernel has run; the split on a stream of its own, so the
+    // next slot's copy queues right behind this one
+    HIPCHK(c, hipStreamWaitEvent(c->s_copy, c->ev_kdone[slot], 0));
+    hipEvent_t* ce = nullptr;
+    if ((rc = copy_events(c, &ce, nbytes))) return rc;
+    if (ce) HIPCHK(c, hipEventRecord(ce[0], c->s_copy));
+    if (nbytes) HIPCHK(c, hipMemcpyAsync(c->d_bytes[slot], c->h_bytes[slot], nbytes, hipMemcpyHostToDevice, c->s_copy));
+    if (ce) HIPCHK(c, hipEventRecord(ce[1], c->s_copy));
+    HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
+    HIPCHK(c, hipStreamWaitEvent(c->s_split, c->ev_h2d[slot], 0));
+    if (nbytes) {
+        // the line count goes straight to pinned memory (read at the launch)
+        HIPCHK(c, launch_split_lines(c->d_bytes[slot], nbytes, c->d_split_chunk, c->d_roff[slot],
+                                     c->cfg.max_batch_bytes + 1, c->h_rawn + slot, c->s_split));
+    } else {
+        c->h_rawn[slot] = 0;
+    }
+    HIPCHK(c, hipEventRecord(c->ev_raw[slot], c->s_split));
+    c->raw_nbytes[slot] = nbytes;
+    // the other slot's batch, submitted before this one, launches now; this one at the next call
+    rc = launch_pending_raw(c);
+    c->raw_pend = slot;
+    return rc;
+}
+
+int ysb_split_lines_device(ysb_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint32_t* d_off, uint64_t cap,
+                           uint64_t* n) {
+    if (!c || !n) return c ? fail(c, YSB_ERR_ARG, "n is NULL") : YSB_ERR_ARG;
+    if (nbytes > (4ull << 30) - 64) return fail(c, YSB_ERR_CAPACITY, "batch larger than 4 GiB (u32 offsets)");
+    if ((nbytes && !d_bytes) || (cap && !d_off)) return fail(c, YSB_ERR_ARG, "NULL buffers");
+    if (reinterpret_cast<uintptr_t>(d_bytes) & 15) return fail(c, YSB_ERR_ARG, "d_bytes must be 16-byte aligned");
+    int rc = launch_pending_raw(c);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    const u64 words = split_chunks(nbytes) + 1;
+    if (c->split_chunk_words < words) {
+        if (c->s_split) HIPCHK(c, hipStreamSynchronize(c->s_split));
+        HIPCHK(c, hipStreamSynchronize(c->s_comp));
+        hipFree(c->d_split_chunk);
+        c->d_split_chunk = nullptr;
+        c->split_chunk_words = 0;
+        HIPCHK(c, hipMalloc(&c->d_split_chunk, words * 4));
+        c->split_chunk_words = words;
+    }
+    if (!c->d_cmp) HIPCHK(c, hipMalloc(&c->d_cmp, 32));
+    unsigned long long* d_n = c->d_cmp + 3;
+    HIPCHK(c, launch_split_lines(d_bytes, nbytes, c->d_split_chunk, d_off, cap, d_n, c->s_comp));
+    unsigned long long got = 0;
+    HIPCHK(c, hipMemcpyAsync(&got, d_n, 8, hipMemcpyDeviceToHost, c->s_comp));
+    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    *n = got;
+    if (got > cap) return fail(c, YSB_ERR_CAPACITY, "%llu lines, cap %llu", (unsigned long long)got, (unsigned long long)cap);
+    return YSB_OK;
+}
+
+int ysb_slot_capacity(ysb_ctx* c, uint64_t* max_bytes, uint64_t* max_events) {
+    if (!c) return YSB_ERR_ARG;
+    if (max_bytes) *max_bytes = c->cfg.max_batch_bytes;
+    if (max_events) *max_events = c->cfg.max_batch_events;
+    return YSB_OK;
+}
+
+int ysb_copy_time(ysb_ctx* c, double* total_ms, uint64_t* copies, uint64_t* bytes) {
+    if (!c) return YSB_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->s_copy));
+    double t = 0;
+    for (size_t i = 0; i < c->cev_used; ++i) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->cev[i][0], c->cev[i][1]));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (copies) *copies = c->cev_used;
+    if (bytes) *bytes = c->copy_bytes;
+    c->cev_used = 0;
+    c->copy_bytes = 0;
+    return YSB_OK;
+}
+
 // Device batches: the layout sampled from their first lines (unless fixed), then the launch.
 static int enqueue_device(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
+    int prc = launch_pending_raw(c);   // batches launch in submission order
+    if (prc) return prc;
     if (c->table_loaded && layout_sampling(c)) {
         const int lay = sample_device_layout(c, segs, nseg, &c->submit_learn);
         if (lay < 0) return lay;
@@ -1115,6 +1324,8 @@ int ysb_submit_device_segments(ysb_ctx* c, const ysb_segment* segs, uint32_t n_s
 }
 
 static int sync_streams(ysb_ctx* c) {
+    int rc = launch_pending_raw(c);
+    if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->s_copy));
     HIPCHK(c, hipStreamSynchronize(c->s_comp));
@@ -1429,11 +1640,17 @@ int ysb_layout_of_line(const uint8_t* line, uint64_t len, int require_ip, uint32
 
 int ysb_launch_info(ysb_ctx* c, ysb_launch_desc* out) {
     if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
+    int rc = launch_pending_raw(c);
+    if (rc) return rc;
     *out = c->last_launch;
     return YSB_OK;
 }
 
-void* ysb_stream(ysb_ctx* c) { return c ? (void*)c->s_comp : nullptr; }
+void* ysb_stream(ysb_ctx* c) {
+    if (!c) return nullptr;
+    launch_pending_raw(c);   // work the caller orders after it follows every submitted batch
+    return (void*)c->s_comp;
+}
 
 // ---- device memory ----------------------------------------------------------------------------
 
@@ -1573,6 +1790,8 @@ int ysb_group_init_host(ysb_ctx* c, int rank, int nranks, const ysb_collectives*
 }
 
 static int group_setup(ysb_ctx* c, int rank, int nranks) {
+    int prc = launch_pending_raw(c);
+    if (prc) return prc;
     c->rank = rank;
     c->nranks = nranks;
     // pad campaigns to a multiple of nranks; keep the current counts
@@ -1663,6 +1882,8 @@ int ysb_exchange_plan(const uint64_t* slot_max, uint32_t W, uint32_t nranks, uin
 // call after group init / reset / ring advance is complete.
 static int exchange(ysb_ctx* c, bool pipelined) {
     if (!grouped(c)) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
+    int prc = launch_pending_raw(c);
+    if (prc) return prc;
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->ring_agreed) {
         int rc = agree_ring(c);
@@ -1762,7 +1983,8 @@ int ysb_group_checksum(ysb_ctx* c, int what, uint32_t nranks, uint64_t* out) {
     if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
     if (nranks == 0) return fail(c, YSB_ERR_ARG, "nranks must be >= 1");
     HIPCHK(c, hipSetDevice(c->device));
-    int rc = fold_delta(c);   // the checksums read the u64 ring
+    int rc = launch_pending_raw(c);
+    if (!rc) rc = fold_delta(c);   // the checksums read the u64 ring
     if (!rc) rc = sync_streams(c);
     if (!rc) rc = read_ring(c);
     if (rc) return rc;
@@ -1944,6 +2166,8 @@ int ysb_truth_accumulate(ysb_ctx* c, const ysb_gen_params* p, uint64_t first, ui
     if (!c) return YSB_ERR_ARG;
     if (!gen_ok(p)) return fail(c, YSB_ERR_ARG, "bad generator parameters");
     if (p->n_campaigns > c->cfg.n_campaigns) return fail(c, YSB_ERR_ARG, "generator has more campaigns than the context");
+    int prc = launch_pending_raw(c);
+    if (prc) return prc;
     HIPCHK(c, hipSetDevice(c->device));
     const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
     if (!c->d_truth) {
@@ -1951,7 +2175,7 @@ int ysb_truth_accumulate(ysb_ctx* c, const ysb_gen_params* p, uint64_t first, ui
         HIPCHK(c, hipMemset(c->d_truth, 0, cells * 8));
         HIPCHK(c, hipMalloc(&c->d_truth_out, 8));
         HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
-        HIPCHK(c, hipMalloc(&c->d_cmp, 32));
+        if (!c->d_cmp) HIPCHK(c, hipMalloc(&c->d_cmp, 32));
     }
     HIPCHK(c, hipStreamSynchronize(c->s_comp));
     int rc = read_ring(c);
@@ -1968,7 +2192,8 @@ int ysb_truth_compare(ysb_ctx* c, uint64_t* mismatched, uint64_t* truth_total, u
     if (!c) return YSB_ERR_ARG;
     if (!c->d_truth) return fail(c, YSB_ERR_STATE, "no truth accumulated");
     HIPCHK(c, hipSetDevice(c->device));
-    int frc = fold_delta(c);
+    int frc = launch_pending_raw(c);
+    if (!frc) frc = fold_delta(c);
     if (frc) return frc;
     HIPCHK(c, hipMemsetAsync(c->d_cmp, 0, 32, c->s_comp));
     launch_compare(c->d_truth, c->d_counts, (u64)c->c_pad * c->cfg.window_ring, c->d_cmp, c->s_comp);

@@ -226,6 +226,25 @@ void launch_xunpack(unsigned long long* owned, u32 W, u32 rows, const u32* slots
 void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_lo, u32 c_off, u32 c_lo, u32 c_hi,
                      unsigned long long* out, hipStream_t s);
 
+// BufferedReader.readLine's line split of raw bytes (ysb_split.hip): off[0..min(n, cap)) <-
+// the line starts of b[0, nbytes) (b 16-byte aligned, nbytes < 4 GiB), *d_n <- n.  chunk:
+// split_chunks(nbytes) u32 of scratch.  Asynchronous on s.
+u64 split_chunks(u64 nbytes);
+hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64 cap, unsigned long long* d_n,
+                              hipStream_t s);
+// Layout sampling of device launches: each segment's first line, copied on the device (in
+// stream order after the batch's producer) into pinned host memory, SAMPLE_STRIDE bytes per
+// segment: u32 {line start, sampled length, valid, 0}, then <= SAMPLE_BYTES line bytes.
+constexpr u32 SAMPLE_BYTES = 288;   // a line of the scan's tile capacity
+constexpr u32 SAMPLE_STRIDE = 16 + SAMPLE_BYTES;
+struct SampleSegs {
+    const u8* bytes[MAX_SEGS];
+    const u32* off[MAX_SEGS];
+    u64 nbytes[MAX_SEGS];
+    u64 n[MAX_SEGS];   // >= 1
+};
+void launch_sample(const SampleSegs& s, u32 nseg, u8* out, hipStream_t st);
+
 constexpr int N_STAMPS = 8;     // phases timed by the YSB_STAMPS diagnostic build
 
 void launch_scan(const ScanParams& p, hipStream_t s);

@@ -1,0 +1,167 @@
+// ysb_split.hip -- FileBasedDataSource's line split on the GPU (ysb_submit_raw,
+// ysb_split_lines_device).
+//
+// The reference reads the replay file with BufferedReader.readLine and hands each line to
+// the chain (flink-benchmarks/.../AdvertisingTopologyNative.java:144-165).  A raw batch is
+// whole lines as bytes: the host only reads the file into the pinned slot, and the u32 line
+// starts the scan kernel needs are found here, at HBM speed, instead of by a host pass over
+// every byte (the native runner's bound until round 4: 54 M events/s).
+//
+// readLine's terminators: '\n', "\r\n" and a lone '\r'.  Line i starts at position 0 or right
+// after a terminator; a terminator that ends the batch starts no line, and a last line
+// without a terminator is a line.  So the starts are {0} and every s in [1, nbytes) with
+//     b[s-1] == '\n'  ||  (b[s-1] == '\r' && b[s] != '\n').
+//
+// Three kernels, all on the byte stream in 64 KiB chunks (one 256-thread workgroup each,
+// every thread one 16-byte vector per step, so each load instruction of a wave covers 1 KiB):
+// count (starts per chunk), prefix (chunk bases, one workgroup), write (each chunk's starts in
+// order: a block-wide exclusive scan of the per-vector counts per step).  Algorithmic bytes:
+// the batch read twice plus 4 B per line written -- for a 256 MiB slot ~0.1 ms, against the
+// ~5 ms its PCIe copy takes.
+#include <hipcub/hipcub.hpp>
+#include "ysb_kernels.h"
+
+namespace ysb {
+
+constexpr int SPLIT_TPB = 256;
+constexpr int SPLIT_STEPS = 16;                                   // 16-byte vectors per thread and chunk
+constexpr u64 SPLIT_CHUNK = (u64)SPLIT_TPB * 16 * SPLIT_STEPS;    // 64 KiB
+constexpr int SPLIT_PREFIX_TPB = 1024;
+
+u64 split_chunks(u64 nbytes) { return (nbytes + SPLIT_CHUNK - 1) / SPLIT_CHUNK; }
+
+// high bit of every zero byte of x (exact, no carries between bytes)
+__device__ __forceinline__ u32 zero_bytes(u32 x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu); }
+
+// the four zero-byte flags of zero_bytes() as bits 0..3
+__device__ __forceinline__ u32 flag4(u32 z) {
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+// Byte by byte (a vector holding a '\r', or the batch's last partial vector): bit j set when
+// s = p + j + 1 starts a line.
+__device__ __noinline__ u32 start_mask_bytes(const u8* b, u64 nbytes, u64 p) {
+    u32 m = 0;
+    for (u32 j = 0; j < 16; ++j) {
+        const u64 q = p + j;
+        if (q + 1 >= nbytes) break;   // a start must lie inside the batch (and b[q + 1] exists)
+        const u8 c = b[q];
+        if (c == '\n' || (c == '\r' && b[q + 1] != '\n')) m |= 1u << j;
+    }
+    return m;
+}
+
+// Line starts s = p + j + 1 (bit j) of the 16-byte vector at p (16-byte aligned, p < nbytes).
+__device__ __forceinline__ u32 start_mask16(const u8* b, u64 nbytes, u64 p) {
+    if (p + 17 > nbytes) return start_mask_bytes(b, nbytes, p);   // the last vector: bounds per byte
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(b + p));
+    const u32 w[4] = {v.x, v.y, v.z, v.w};
+    u32 m = 0, cr = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        m |= flag4(zero_bytes(w[k] ^ 0x0A0A0A0Au)) << (4 * k);
+        cr |= zero_bytes(w[k] ^ 0x0D0D0D0Du);
+    }
+    if (cr) return start_mask_bytes(b, nbytes, p);   // a '\r': its next byte decides (never on generator data)
+    return m;
+}
+
+__global__ __launch_bounds__(SPLIT_TPB) void split_count_kernel(const u8* b, u64 nbytes, u32* chunk_cnt) {
+    typedef hipcub::BlockReduce<u32, SPLIT_TPB> Reduce;
+    __shared__ typename Reduce::TempStorage tmp;
+    const u64 base = (u64)blockIdx.x * SPLIT_CHUNK;
+    u32 cnt = 0;
+#pragma unroll 4
+    for (int it = 0; it < SPLIT_STEPS; ++it) {
+        const u64 p = base + ((u64)it * SPLIT_TPB + threadIdx.x) * 16;
+        if (p < nbytes) cnt += __popc(start_mask16(b, nbytes, p));
+    }
+    const u32 total = Reduce(tmp).Sum(cnt);
+    if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = total;
+}
+
+// chunk_cnt[0..nchunks) -> exclusive bases in place; *n = lines of the batch (0 when empty)
+__global__ __launch_bounds__(SPLIT_PREFIX_TPB) void split_prefix_kernel(u32* chunk, u64 nchunks, u64 nbytes,
+                                                                        unsigned long long* n) {
+    typedef hipcub::BlockScan<unsigned long long, SPLIT_PREFIX_TPB> Scan;
+    __shared__ typename Scan::TempStorage tmp;
+    const u64 per = (nchunks + SPLIT_PREFIX_TPB - 1) / SPLIT_PREFIX_TPB;
+    const u64 a = (u64)threadIdx.x * per, e = a + per < nchunks ? a + per : nchunks;
+    unsigned long long s = 0;
+    for (u64 i = a; i < e; ++i) s += chunk[i];
+    unsigned long long pre = 0, total = 0;
+    Scan(tmp).ExclusiveSum(s, pre, total);
+    for (u64 i = a; i < e; ++i) {
+        const u32 c = chunk[i];
+        chunk[i] = (u32)pre;   // < nbytes < 2^32
+        pre += c;
+    }
+    if (threadIdx.x == 0) *n = nbytes ? 1ull + total : 0ull;
+}
+
+__global__ __launch_bounds__(SPLIT_TPB) void split_write_kernel(const u8* b, u64 nbytes, const u32* chunk_base,
+                                                                u32* off, u64 cap) {
+    typedef hipcub::BlockScan<u32, SPLIT_TPB> Scan;
+    __shared__ typename Scan::TempStorage tmp;
+    const u64 base = (u64)blockIdx.x * SPLIT_CHUNK;
+    u64 run = (u64)chunk_base[blockIdx.x] + 1;   // off index of the chunk's first start (off[0] = 0)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && cap) off[0] = 0;
+    for (int it = 0; it < SPLIT_STEPS; ++it) {
+        const u64 p = base + ((u64)it * SPLIT_TPB + threadIdx.x) * 16;
+        u32 m = p < nbytes ? start_mask16(b, nbytes, p) : 0u;
+        u32 pre = 0, agg = 0;
+        Scan(tmp).ExclusiveSum((u32)__popc(m), pre, agg);
+        u64 o = run + pre;
+        while (m) {
+            const u32 j = __builtin_ctz(m);
+            if (o < cap) off[o] = (u32)(p + j + 1);
+            ++o;
+            m &= m - 1;
+        }
+        run += agg;
+        __syncthreads();   // the scan's storage is reused by the next step
+    }
+}
+
+// The first line of every segment of a device launch, for the host's layout sampling
+// (ysb_capi.cpp sample_device_layout): block i writes out[i * SAMPLE_STRIDE] = {line start,
+// sampled length, valid} and then the line's first <= SAMPLE_BYTES bytes.  It runs on the
+// compute stream, so it reads the batch after whatever produced it there; out is pinned host
+// memory (no copy of its own).
+__global__ __launch_bounds__(64) void sample_kernel(SampleSegs s, u8* out) {
+    __shared__ u32 hdr[2];
+    const u32 i = blockIdx.x;
+    u8* o = out + (u64)i * SAMPLE_STRIDE;
+    if (threadIdx.x == 0) {
+        const u32 o0 = s.off[i][0];
+        const u64 end = s.n[i] > 1 ? (u64)s.off[i][1] : s.nbytes[i];
+        const bool valid = o0 <= end && end <= s.nbytes[i];
+        const u32 len = valid ? (u32)(end - o0 < SAMPLE_BYTES ? end - o0 : SAMPLE_BYTES) : 0u;
+        hdr[0] = o0;
+        hdr[1] = len;
+        u32* h = reinterpret_cast<u32*>(o);
+        h[0] = o0;
+        h[1] = len;
+        h[2] = valid ? 1u : 0u;
+        h[3] = 0;
+    }
+    __syncthreads();
+    for (u32 j = threadIdx.x; j < hdr[1]; j += 64) o[16 + j] = s.bytes[i][(u64)hdr[0] + j];
+}
+
+void launch_sample(const SampleSegs& s, u32 nseg, u8* out, hipStream_t st) {
+    if (nseg) hipLaunchKernelGGL(sample_kernel, dim3(nseg), dim3(64), 0, st, s, out);
+}
+
+hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64 cap, unsigned long long* d_n,
+                              hipStream_t s) {
+    if (nbytes == 0) return hipMemsetAsync(d_n, 0, 8, s);
+    const u64 nch = split_chunks(nbytes);
+    hipLaunchKernelGGL(split_count_kernel, dim3((unsigned)nch), dim3(SPLIT_TPB), 0, s, b, nbytes, chunk);
+    hipLaunchKernelGGL(split_prefix_kernel, dim3(1), dim3(SPLIT_PREFIX_TPB), 0, s, chunk, nch, nbytes, d_n);
+    hipLaunchKernelGGL(split_write_kernel, dim3((unsigned)nch), dim3(SPLIT_TPB), 0, s, b, nbytes, chunk, off, cap);
+    return hipGetLastError();
+}
+
+}  // namespace ysb

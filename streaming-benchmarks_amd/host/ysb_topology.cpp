@@ -9,6 +9,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cerrno>
 #include <chrono>
 #include <cstring>
@@ -233,40 +236,95 @@ AdCampaignMap AdCampaignMap::fromFile(const std::string& path) {
 
 // ---- FileBasedDataSource -----------------------------------------------------------------------
 
+class WorkerPool {
+public:
+    explicit WorkerPool(unsigned n) {
+        for (unsigned t = 1; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& x : th_) x.join();
+    }
+    unsigned size() const { return (unsigned)th_.size() + 1; }
+    // f(t) for t in [0, n), n <= size(); t = 0 on the calling thread
+    void run(unsigned n, const std::function<void(unsigned)>& f) {
+        if (n <= 1) { f(0u); return; }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &f;
+            active_ = n;
+            left_ = n - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0u);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* job_ = nullptr;
+    unsigned active_ = 0, left_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+    void loop(unsigned t) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)>* f;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (t >= active_) continue;
+                f = job_;
+            }
+            (*f)(t);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+};
+
 FileBasedDataSource::FileBasedDataSource(const std::string& path, unsigned threads) {
     fd_ = ::open(path.c_str(), O_RDONLY);
     if (fd_ < 0) throw std::runtime_error("java.io.FileNotFoundException: " + path);
     threads_ = threads ? threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    pool_.reset(new WorkerPool(threads_));
 }
 
 FileBasedDataSource::~FileBasedDataSource() {
+    pool_.reset();
     if (fd_ >= 0) ::close(fd_);
 }
 
-// Runs f(t) for t in [0, n) on n threads (inline when n == 1).
-template <class F>
-static void parallel(unsigned n, F f) {
-    if (n <= 1) { f(0u); return; }
-    std::vector<std::thread> th;
-    for (unsigned t = 1; t < n; ++t) th.emplace_back(f, t);
-    f(0u);
-    for (auto& x : th) x.join();
+void FileBasedDataSource::rewind() {
+    pos_ = 0;
+    eof_ = false;
+    carry_.clear();
 }
 
-uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, uint64_t maxLines, uint64_t* nbytes) {
-    *nbytes = 0;
-    if (!maxLines || !cap) return 0;
+// The carried partial line, then parallel preads of disjoint pieces (>= 4 MiB each) straight
+// into the buffer: the bytes buf holds.
+uint64_t FileBasedDataSource::readBlock(uint8_t* buf, uint64_t cap) {
     if (carry_.size() > cap) throw std::runtime_error("a line is longer than the batch buffer");
     uint64_t have = carry_.size();
     std::memcpy(buf, carry_.data(), have);
     carry_.clear();
     if (!eof_ && have < cap) {
-        // parallel preads of disjoint pieces (>= 4 MiB each) straight into the buffer
         const uint64_t want = cap - have;
         const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads_, want >> 22));
         std::vector<uint64_t> got(T, 0);
         std::vector<int> err(T, 0);
-        parallel(T, [&](unsigned t) {
+        pool_->run(T, [&](unsigned t) {
             const uint64_t a = want * t / T, b = want * (t + 1) / T;
             uint64_t p = a;
             while (p < b) {
@@ -286,30 +344,53 @@ uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, ui
         pos_ += read;
         have += read;
     }
-    if (have == 0) return 0;
-    // BufferedReader.readLine's terminators: "\n", "\r\n" and a lone "\r" (:153-159).  A
-    // line keeps its terminator bytes in the batch (the parsers ignore them).
-    const bool any_cr = std::memchr(buf, '\r', have) != nullptr;   // generator files: none
-    // complete lines: up to the last terminator (at end of file, everything); a '\r' that
-    // ends the buffer may still be followed by '\n', so it waits for the next read
-    uint64_t end = have;
-    if (!eof_) {
-        end = 0;
-        for (uint64_t q = have; q > 0; --q) {
-            const uint8_t c = buf[q - 1];
-            if (c == '\n' || (c == '\r' && q < have)) { end = q; break; }
-            if (!any_cr) {   // only '\n' can end a line: jump to it
-                const void* nl = memrchr(buf, '\n', q);
-                end = nl ? (uint64_t)((const uint8_t*)nl - buf) + 1 : 0;
-                break;
-            }
+    return have;
+}
+
+// BufferedReader.readLine's terminators: "\n", "\r\n" and a lone "\r" (:153-159).  The end
+// of the complete lines among buf[0, have): up to the last terminator (at end of file,
+// everything); a '\r' that ends the buffer may still be followed by '\n', so it waits.
+uint64_t FileBasedDataSource::completeEnd(const uint8_t* buf, uint64_t have, bool anyCr) const {
+    if (eof_) return have;
+    uint64_t end = 0;
+    for (uint64_t q = have; q > 0; --q) {
+        const uint8_t c = buf[q - 1];
+        if (c == '\n' || (c == '\r' && q < have)) { end = q; break; }
+        if (!anyCr) {   // only '\n' can end a line: jump to it
+            const void* nl = memrchr(buf, '\n', q);
+            end = nl ? (uint64_t)((const uint8_t*)nl - buf) + 1 : 0;
+            break;
         }
-        if (end == 0) throw std::runtime_error("a line is longer than the batch buffer");
     }
+    if (end == 0) throw std::runtime_error("a line is longer than the batch buffer");
+    return end;
+}
+
+uint64_t FileBasedDataSource::fillRaw(uint8_t* buf, uint64_t cap) {
+    if (!cap) return 0;
+    const uint64_t have = readBlock(buf, cap);
+    if (have == 0) return 0;
+    // only the tail decides where the complete lines end: a '\r' there needs the slow walk
+    const uint64_t tail = std::min<uint64_t>(have, 1u << 16);
+    const bool anyCr = std::memchr(buf + have - tail, '\r', tail) != nullptr;
+    const uint64_t end = completeEnd(buf, have, anyCr);
+    carry_.assign(buf + end, buf + have);
+    bytes_ += end;
+    return end;
+}
+
+uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, uint64_t maxLines, uint64_t* nbytes) {
+    *nbytes = 0;
+    if (!maxLines || !cap) return 0;
+    const uint64_t have = readBlock(buf, cap);
+    if (have == 0) return 0;
+    // A line keeps its terminator bytes in the batch (the parsers ignore them).
+    const bool any_cr = std::memchr(buf, '\r', have) != nullptr;   // generator files: none
+    const uint64_t end = completeEnd(buf, have, any_cr);
     // line starts: 0 and every byte after a terminator below `end`, in parallel pieces
     const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads_, end >> 22));
     std::vector<std::vector<uint32_t>> starts(T);
-    parallel(T, [&](unsigned t) {
+    pool_->run(T, [&](unsigned t) {
         const uint64_t a = end * t / T, b = end * (t + 1) / T;
         auto& v = starts[t];
         v.reserve((b - a) / 200 + 16);
@@ -340,6 +421,7 @@ uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, ui
     carry_.assign(buf + p_end, buf + have);
     *nbytes = p_end;
     lines_ += n;
+    bytes_ += p_end;
     return n;
 }
 
@@ -391,6 +473,13 @@ void GpuAdCampaignOperator::flatMap(const char* line, uint64_t len) {
     if (!nl) bytes_[cur_][fillBytes_++] = '\n';
 }
 
+uint64_t GpuAdCampaignOperator::fillFromRaw(FileBasedDataSource& src) {
+    const uint64_t nb = src.fillRaw(bytes_[cur_] + fillBytes_, o_.batchBytes - fillBytes_);
+    fillBytes_ += nb;
+    rawBytes_ += nb;
+    return nb;
+}
+
 uint64_t GpuAdCampaignOperator::fillFrom(FileBasedDataSource& src) {
     uint64_t nb = 0;
     const uint64_t n = src.fill(bytes_[cur_] + fillBytes_, o_.batchBytes - fillBytes_, off_[cur_] + fillEvents_,
@@ -402,8 +491,13 @@ uint64_t GpuAdCampaignOperator::fillFrom(FileBasedDataSource& src) {
 }
 
 void GpuAdCampaignOperator::submit() {
-    if (!fillEvents_) return;
-    check(ysb_submit(ctx_, cur_, bytes_[cur_], fillBytes_, off_[cur_], fillEvents_), "ysb_submit");
+    if (rawBytes_) {   // raw lines (fillFromRaw): the GPU finds the line starts
+        check(ysb_submit_raw(ctx_, cur_, bytes_[cur_], fillBytes_), "ysb_submit_raw");
+        rawBytes_ = 0;
+    } else {
+        if (!fillEvents_) return;
+        check(ysb_submit(ctx_, cur_, bytes_[cur_], fillBytes_, off_[cur_], fillEvents_), "ysb_submit");
+    }
     submitted_ += fillEvents_;
     fillBytes_ = fillEvents_ = 0;
     cur_ ^= 1;

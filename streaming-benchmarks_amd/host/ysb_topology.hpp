@@ -76,10 +76,14 @@ private:
 };
 
 // ---- event source ----------------------------------------------------------------------------
+// Threads that stay up for the source's lifetime: run(n, f) calls f(t) for t in [0, n) on
+// n threads (the caller's is t = 0) and returns when all are done.
+class WorkerPool;
+
 // The events file as complete lines ('\n'-terminated; the last line may lack it), read
-// in large blocks straight into a caller buffer with line offsets; a partial line at the
-// end of a block is carried into the next one.  Empty lines are records, as readLine
-// returns them.
+// in large blocks straight into a caller buffer, by parallel preads of a persistent pool;
+// a partial line at the end of a block is carried into the next one.  Empty lines are
+// records, as readLine returns them.
 class FileBasedDataSource {
 public:
     // threads: readers/splitters per block (0 = min(16, hardware threads)).
@@ -90,15 +94,24 @@ public:
     // Fills buf (cap bytes) with whole lines and off (maxLines) with their offsets;
     // returns the number of lines (0 = end of file).  Throws if one line exceeds cap.
     uint64_t fill(uint8_t* buf, uint64_t cap, uint32_t* off, uint64_t maxLines, uint64_t* nbytes);
+    // The same without the line split: buf receives whole lines, the return value is their
+    // bytes (0 = end of file); the GPU finds the line starts (ysb_submit_raw).
+    uint64_t fillRaw(uint8_t* buf, uint64_t cap);
+    // Back to the file's start (a replay source read again).
+    void rewind();
     uint64_t linesRead() const { return lines_; }
+    uint64_t bytesRead() const { return bytes_; }
 
 private:
     int fd_ = -1;
     uint64_t pos_ = 0;                  // file offset of the next read
     unsigned threads_ = 1;
+    std::unique_ptr<WorkerPool> pool_;
     std::vector<uint8_t> carry_;
     bool eof_ = false;
-    uint64_t lines_ = 0;
+    uint64_t lines_ = 0, bytes_ = 0;
+    uint64_t readBlock(uint8_t* buf, uint64_t cap);   // carry + file bytes into buf: bytes held
+    uint64_t completeEnd(const uint8_t* buf, uint64_t have, bool anyCr) const;
 };
 
 // One (campaign, window) delta: what writeWindow HINCRBYs into seen_count.
@@ -119,6 +132,7 @@ public:
         uint64_t batchEvents = 1ull << 20;
         bool tbl = false;                   // MockWindowedFlatMap's .tbl rows (:197-226)
         bool requireIp = false;             // Storm/Spark's 7-field deserializer
+        bool gpuSplit = true;               // fillFromRaw + ysb_submit_raw: line starts found on the GPU
     };
     GpuAdCampaignOperator(const AdCampaignMap& map, const Options& o);
     ~GpuAdCampaignOperator();
@@ -128,6 +142,7 @@ public:
     void open();                                           // RichFlatMapFunction.open
     void flatMap(const char* line, uint64_t len);          // one record
     uint64_t fillFrom(FileBasedDataSource& src);           // a slot's worth of records, zero-copy
+    uint64_t fillFromRaw(FileBasedDataSource& src);        // the same as raw lines (bytes returned)
     void submit();                                         // hand the open slot to the GPU
     std::vector<WindowDelta> flushWindows();               // CampaignProcessorCommon.flushWindows (:91-98)
     void close();                                          // RichFlatMapFunction.close
@@ -141,7 +156,7 @@ private:
     uint8_t* bytes_[2] = {nullptr, nullptr};
     uint32_t* off_[2] = {nullptr, nullptr};
     int cur_ = 0;
-    uint64_t fillBytes_ = 0, fillEvents_ = 0, submitted_ = 0;
+    uint64_t fillBytes_ = 0, fillEvents_ = 0, submitted_ = 0, rawBytes_ = 0;
     void check(int rc, const char* what);
 };
 

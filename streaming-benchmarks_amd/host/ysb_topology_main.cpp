@@ -7,12 +7,15 @@
 //   ysb_topology --confPath PATH [--device N] [--sink none|csv:FILE|redis[:HOST[:PORT]]]
 //                [--format json|tbl] [--flush-ms MS] [--batch-mb MB | --batch-bytes B] [--batch-events N]
 //                [--window-ring W] [--require-ip] [--dry-run] [--print-config]
-//                [--replay-rows CSV]
+//                [--replay-rows CSV] [--host-split] [--repeat K] [--io-threads T]
 //
 // --dry-run reads the config, the map and the events file (FileBasedDataSource) without a
 // GPU and reports what it found; --replay-rows writes the (campaign_id,window_ms,count)
-// rows of a CSV through the sink without a GPU (the Redis writer on its own).  The last
-// stdout line is a JSON summary.
+// rows of a CSV through the sink without a GPU (the Redis writer on its own).  The events
+// file is read as raw lines and the GPU finds the line starts (ysb_submit_raw); --host-split
+// splits the lines on the host instead (ysb_submit with offsets).  --repeat K reads the file
+// K times (a replay source; the counts are K times the file's).  The last stdout line is a
+// JSON summary.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -32,14 +35,17 @@ struct Args {
     long long flush_ms = 1000;                  // CampaignProcessorCommon's flusher period (:45)
     long long batch_bytes = 256ll << 20, batch_events = 1 << 20;
     unsigned window_ring = 1024;
-    bool require_ip = false, dry = false, print_config = false;
+    bool require_ip = false, dry = false, print_config = false, host_split = false;
+    long long repeat = 1;
+    unsigned io_threads = 0;
 };
 
 void usage() {
     std::fprintf(stderr,
                  "usage: ysb_topology --confPath PATH [--device N] [--sink none|csv:FILE|redis[:HOST[:PORT]]]\n"
                  "       [--format json|tbl] [--flush-ms MS] [--batch-mb MB | --batch-bytes B] [--batch-events N]\n"
-                 "       [--window-ring W] [--require-ip] [--dry-run] [--print-config] [--replay-rows CSV]\n");
+                 "       [--window-ring W] [--require-ip] [--dry-run] [--print-config] [--replay-rows CSV]\n"
+                 "       [--host-split] [--repeat K] [--io-threads T]\n");
 }
 
 Args parse(int argc, char** argv) {
@@ -63,6 +69,9 @@ Args parse(int argc, char** argv) {
         else if (k == "--dry-run") a.dry = true;
         else if (k == "--print-config") a.print_config = true;
         else if (k == "--replay-rows") a.replay = val();
+        else if (k == "--host-split") a.host_split = true;
+        else if (k == "--repeat") a.repeat = std::max(1ll, std::atoll(val().c_str()));
+        else if (k == "--io-threads") a.io_threads = (unsigned)std::atoll(val().c_str());
         else { usage(); std::exit(2); }
     }
     if (a.conf.empty()) {   // ParameterTool.getRequired("confPath")
@@ -117,8 +126,9 @@ int run(const Args& a) {
     o.batchEvents = (uint64_t)a.batch_events;
     o.tbl = tbl;
     o.requireIp = a.require_ip;
+    o.gpuSplit = !a.host_split;
 
-    FileBasedDataSource src(events);
+    FileBasedDataSource src(events, a.io_threads);
     const double t0 = now_s();
     if (a.dry) {   // host half only: map + source, no device
         std::vector<uint8_t> buf(o.batchBytes);
@@ -175,6 +185,7 @@ int run(const Args& a) {
 
     GpuAdCampaignOperator op(map, o);
     op.open();
+    const double t_open = now_s();   // the stream itself: from the first read to close
     uint64_t rows = 0, flushes = 0;
     auto flush = [&]() {
         const std::vector<WindowDelta> d = op.flushWindows();
@@ -184,14 +195,19 @@ int run(const Args& a) {
         if (!csv_path.empty()) csv.add(d);
     };
     double last_flush = now_s();
-    while (op.fillFrom(src) > 0) {
-        op.submit();
-        if (a.flush_ms > 0 && (now_s() - last_flush) * 1000.0 >= (double)a.flush_ms) {
-            flush();
-            last_flush = now_s();
+    for (long long rep = 0; rep < a.repeat; ++rep) {
+        if (rep) src.rewind();
+        while ((o.gpuSplit ? op.fillFromRaw(src) : op.fillFrom(src)) > 0) {
+            op.submit();
+            if (a.flush_ms > 0 && (now_s() - last_flush) * 1000.0 >= (double)a.flush_ms) {
+                flush();
+                last_flush = now_s();
+            }
         }
+        op.submit();   // a last partial slot
     }
     op.close();
+    const double el_stream = now_s() - t_open;
     flush();
     const double el = now_s() - t0;
     if (!csv_path.empty()) csv.write(csv_path);
@@ -199,12 +215,17 @@ int run(const Args& a) {
     std::printf("{\"mode\": \"gpu\", \"events\": %llu, \"views\": %llu, \"joined\": %llu, \"join_misses\": %llu, "
                 "\"parse_errors\": %llu, \"time_errors\": %llu, \"out_of_ring\": %llu, \"overflow_dropped\": %llu, "
                 "\"batches\": %llu, \"rows_written\": %llu, \"flushes\": %llu, \"seconds\": %.3f, "
-                "\"events_per_s\": %.1f, \"format\": \"%s\", \"sink\": %s}\n",
+                "\"events_per_s\": %.1f, \"stream_seconds\": %.3f, \"stream_events_per_s\": %.1f, "
+                "\"bytes\": %llu, \"stream_GBs\": %.2f, \"line_split\": \"%s\", \"repeat\": %lld, "
+                "\"format\": \"%s\", \"sink\": %s}\n",
                 (unsigned long long)s.events, (unsigned long long)s.views, (unsigned long long)s.joined,
                 (unsigned long long)s.join_misses, (unsigned long long)s.parse_errors,
                 (unsigned long long)s.time_errors, (unsigned long long)s.out_of_ring,
                 (unsigned long long)s.overflow_dropped, (unsigned long long)s.batches, (unsigned long long)rows,
-                (unsigned long long)flushes, el, el > 0 ? (double)s.events / el : 0.0, tbl ? "tbl" : "json",
+                (unsigned long long)flushes, el, el > 0 ? (double)s.events / el : 0.0, el_stream,
+                el_stream > 0 ? (double)s.events / el_stream : 0.0, (unsigned long long)src.bytesRead(),
+                el_stream > 0 ? (double)src.bytesRead() / el_stream / 1e9 : 0.0, o.gpuSplit ? "gpu" : "host",
+                a.repeat, tbl ? "tbl" : "json",
                 json_str(a.sink).c_str());
     return s.overflow_dropped ? 3 : 0;
 }

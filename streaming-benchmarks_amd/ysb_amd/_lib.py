@@ -108,6 +108,10 @@ SIGNATURES = {
     "ysb_slot_buffers": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_P)]),
     "ysb_submit": (_I, [_P, _I, _PU8, _U64, _PU32, _U64]),
     "ysb_wait": (_I, [_P, _I]),
+    "ysb_slot_capacity": (_I, [_P, C.POINTER(_U64), C.POINTER(_U64)]),
+    "ysb_submit_raw": (_I, [_P, _I, _PU8, _U64]),
+    "ysb_split_lines_device": (_I, [_P, _PU8, _U64, _PU32, _U64, C.POINTER(_U64)]),
+    "ysb_copy_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_submit_device": (_I, [_P, _PU8, _U64, _PU32, _U64]),
     "ysb_submit_device_segments": (_I, [_P, C.c_void_p, _U32]),
     "ysb_sync": (_I, [_P]),

@@ -118,6 +118,31 @@ class YsbContext:
     def wait(self, slot):
         self._c(lib().ysb_wait(self._h, slot))
 
+    def slot_capacity(self):
+        """(max_bytes, max_events) of each pinned slot (ysb_slot_capacity)."""
+        b, e = C.c_uint64(), C.c_uint64()
+        self._c(lib().ysb_slot_capacity(self._h, C.byref(b), C.byref(e)))
+        return b.value, e.value
+
+    def submit_raw(self, data, slot=0):
+        """Raw batch (ysb_submit_raw): whole lines as bytes, the line starts found on the GPU
+        (readLine's terminators); the scan launches at the next call on the context."""
+        buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
+        self._c(lib().ysb_submit_raw(self._h, slot, _ptr(buf), buf.size))
+
+    def split_lines_device(self, d_bytes, nbytes, d_off, cap):
+        """ysb_split_lines_device: the line starts of a device batch into d_off; returns n."""
+        n = C.c_uint64()
+        self._c(lib().ysb_split_lines_device(self._h, C.c_void_p(d_bytes), nbytes, C.c_void_p(d_off), cap,
+                                             C.byref(n)))
+        return n.value
+
+    def copy_time(self):
+        """(total ms, copies, bytes) of the slot H2D copies since the last call (timing=True)."""
+        t, k, b = C.c_double(), C.c_uint64(), C.c_uint64()
+        self._c(lib().ysb_copy_time(self._h, C.byref(t), C.byref(k), C.byref(b)))
+        return t.value, k.value, b.value
+
     def submit_device(self, d_bytes, nbytes, d_off, n):
         self._c(lib().ysb_submit_device(self._h, C.c_void_p(d_bytes), nbytes, C.c_void_p(d_off), n))
 

@@ -1,0 +1,224 @@
+"""GPU: raw batches (ABI 3) -- the line split on the GPU (ysb_split_lines_device,
+ysb_submit_raw; FileBasedDataSource.run's BufferedReader.readLine,
+AdvertisingTopologyNative.java:144-165) against readLine's split restated in
+oracle/dostats.split_lines, and the chain's counts through raw submits equal to the golden
+fixtures and the C oracle; plus the device batches' layout sample taken in stream order
+after a producer on another stream."""
+import numpy as np
+import pytest
+
+import golden_data as gd
+from oracle import dostats, oracle
+from ysb_amd import GEN_COMPACT, GEN_REORDER, GenParams, YsbContext
+from test_gpu_parity import check_against, make_ctx
+
+pytestmark = pytest.mark.gpu
+
+CHUNK = 65536   # ysb_split.hip SPLIT_CHUNK
+
+
+def gpu_split(ctx, data):
+    """Line starts of `data` by ysb_split_lines_device."""
+    d_b = ctx.device_alloc(len(data) + 64)
+    cap = len(data) + 1
+    d_o = ctx.device_alloc(4 * cap + 64)
+    try:
+        if data:
+            ctx.h2d(d_b, np.frombuffer(data, dtype=np.uint8))
+        n = ctx.split_lines_device(d_b, len(data), d_o, cap)
+        out = ctx.d2h(np.empty(n, dtype=np.uint32), d_o) if n else np.empty(0, dtype=np.uint32)
+        return out.tolist()
+    finally:
+        ctx.device_free(d_b)
+        ctx.device_free(d_o)
+
+
+def random_text(rng, n, p_term):
+    """n bytes of printable text with '\\n', '\\r' and "\\r\\n" terminators at rate p_term."""
+    b = rng.integers(0x20, 0x7F, size=n, dtype=np.uint8)
+    t = rng.random(n) < p_term
+    b[t] = rng.choice(np.frombuffer(b"\n\r\n\r", dtype=np.uint8), size=int(t.sum()))
+    return b.tobytes()
+
+
+SMALL = [b"", b"\n", b"a", b"a\n", b"\r", b"\r\n", b"\n\r", b"a\rb", b"a\r\nb\r", b"\n\n\r\r\n", b"\r\r\r",
+         b"x" * 15 + b"\r" + b"\n" + b"y", b"x" * 16 + b"\r\n", b"x" * 31 + b"\n", b"{}\r\n{}\n{}"]
+
+
+def test_split_small_cases_match_readline():
+    with YsbContext() as ctx:
+        for data in SMALL:
+            assert gpu_split(ctx, data) == dostats.split_lines(data)[1], data
+
+
+@pytest.mark.parametrize("seed,n,p", [(1, 1000, 0.05), (2, 3 * CHUNK + 17, 0.004), (3, 2 * CHUNK, 0.3),
+                                      (4, 5 * CHUNK + 1, 0.0), (5, 700_001, 0.01)])
+def test_split_random_text_matches_readline(seed, n, p):
+    rng = np.random.default_rng(seed)
+    data = random_text(rng, n, p)
+    with YsbContext() as ctx:
+        assert gpu_split(ctx, data) == dostats.split_lines(data)[1]
+
+
+def test_split_terminators_on_vector_and_chunk_edges():
+    """'\\r' / "\\r\\n" / '\\n' on either side of every 16-byte vector and 64-KiB chunk edge
+    (the '\\r' test reads the next vector's first byte)."""
+    data = bytearray(b"z" * (3 * CHUNK + 64))
+    for edge in (16, 32, 48, CHUNK, 2 * CHUNK, 3 * CHUNK):
+        data[edge - 1:edge + 1] = b"\r\n"
+    for edge in (64, CHUNK + 16):
+        data[edge - 1] = ord("\r")
+    for edge in (80, 2 * CHUNK + 16):
+        data[edge] = ord("\r")
+    data[CHUNK + 33] = ord("\n")
+    data[-1] = ord("\r")   # a terminator that ends the batch starts no line
+    data = bytes(data)
+    with YsbContext() as ctx:
+        assert gpu_split(ctx, data) == dostats.split_lines(data)[1]
+
+
+def test_split_capacity_is_reported():
+    with YsbContext() as ctx:
+        data = b"a\nb\nc\nd\n"
+        d_b, d_o = ctx.device_alloc(64), ctx.device_alloc(64)
+        ctx.h2d(d_b, np.frombuffer(data, dtype=np.uint8))
+        from ysb_amd import YsbError
+        with pytest.raises(YsbError):
+            ctx.split_lines_device(d_b, len(data), d_o, 2)
+        assert ctx.split_lines_device(d_b, len(data), d_o, 4) == 4
+        ctx.device_free(d_b)
+        ctx.device_free(d_o)
+
+
+def test_split_generator_batch_equals_generator_offsets():
+    g = GenParams(seed=11, events_per_sec=100_000)
+    n = 1_000_000
+    with YsbContext() as ctx:
+        cap = n * g.max_line_bytes()
+        d_b, d_o, d_s = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64), ctx.device_alloc(4 * n + 64)
+        nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+        assert ctx.split_lines_device(d_b, nb, d_s, n) == n
+        want = ctx.d2h(np.empty(n, dtype=np.uint32), d_o)
+        got = ctx.d2h(np.empty(n, dtype=np.uint32), d_s)
+        assert np.array_equal(want, got)
+        for d in (d_b, d_o, d_s):
+            ctx.device_free(d)
+
+
+@pytest.mark.parametrize("stem,require_ip", gd.FIXTURES)
+def test_raw_submit_fixture(stem, require_ip):
+    raw, _ = gd.events(stem)
+    with make_ctx(require_ip=require_ip) as ctx:
+        ctx.submit_raw(raw, slot=0)
+        check_against(ctx, *gd.expected(stem, require_ip))
+
+
+@pytest.mark.parametrize("stem", sorted(gd.TBL_FILES))
+def test_raw_submit_tbl_fixture(stem):
+    raw, _ = gd.tbl_events(stem)
+    with make_ctx(input_format="tbl") as ctx:
+        ctx.submit_raw(raw, slot=1)
+        check_against(ctx, *gd.expected(stem))
+
+
+def test_raw_batches_alternate_slots_and_mix_with_other_submits():
+    """The gen_s7 fixture cut at line boundaries into raw batches over both slots, with an
+    offsets batch (ysb_submit) and a device batch in between: the batches launch in order and
+    the counts equal the fixture's."""
+    raw, offs = gd.events("gen_s7")
+    cuts = [0, 1, 2, 300, 301, 900, 1200, len(offs)]
+    ends = list(offs) + [len(raw)]
+    with make_ctx(max_batch_bytes=1 << 20) as ctx:
+        for k in range(len(cuts) - 1):
+            a, b = ends[cuts[k]], ends[cuts[k + 1]]
+            piece = raw[a:b]
+            if k == 3:   # offsets batch
+                ctx.submit(piece, [o - a for o in offs[cuts[k]:cuts[k + 1]]], slot=k & 1)
+            elif k == 5:   # device batch
+                d_b = ctx.device_alloc(len(piece) + 64)
+                d_o = ctx.device_alloc(4 * (cuts[k + 1] - cuts[k]) + 64)
+                ctx.h2d(d_b, np.frombuffer(piece, dtype=np.uint8))
+                ctx.h2d(d_o, np.asarray([o - a for o in offs[cuts[k]:cuts[k + 1]]], dtype=np.uint32))
+                ctx.submit_device(d_b, len(piece), d_o, cuts[k + 1] - cuts[k])
+                ctx.sync()
+                ctx.device_free(d_b)
+                ctx.device_free(d_o)
+            else:
+                ctx.submit_raw(piece, slot=k & 1)
+        ctx.submit_raw(b"", slot=0)   # an empty raw batch: no lines
+        check_against(ctx, *gd.expected("gen_s7"))
+        assert ctx.stats()["events"] == len(offs)
+
+
+def test_raw_crlf_and_lone_cr_lines_match_oracle():
+    """Generator lines re-terminated with "\\r\\n" and lone '\\r' (readLine takes both), some
+    blank lines (parse errors), through raw batches of 20k lines: counts and counters equal
+    the C oracle on the same records."""
+    g = GenParams(seed=5, events_per_sec=1000)
+    _, aids = g.ids()
+    camp = g.ad_campaign_index()
+    raw, offs = g.events_host(0, 60_000)
+    lines = [raw[a:b] for a, b in zip(offs, list(offs[1:]) + [len(raw)])]
+    rng = np.random.default_rng(9)
+    out = []
+    for i, ln in enumerate(lines):
+        body = bytes(ln[:-1])
+        r = rng.random()
+        out.append(body + (b"\r\n" if r < 0.3 else b"\r" if r < 0.5 else b"\n"))
+        if i % 997 == 0:
+            out.append(b"\n")
+    data = b"".join(out)
+    _, ref_offs = dostats.split_lines(data)
+    rows, ost = oracle.run(oracle.AdMap(aids, camp), data, ref_offs)
+    with make_ctx(n_campaigns=100, ads=(aids, camp), max_batch_bytes=8 << 20) as ctx:
+        ends = ref_offs + [len(data)]
+        for k, a in enumerate(range(0, len(ref_offs), 20_000)):
+            b = min(a + 20_000, len(ref_offs))
+            ctx.submit_raw(data[ends[a]:ends[b]], slot=k & 1)
+        st = ctx.stats()
+        for k, v in ost.items():
+            assert st[k] == v, (k, st[k], v)
+        assert st["events"] == len(ref_offs)
+        assert ctx.drain_buckets() == rows
+
+
+def test_device_sample_follows_a_producer_on_another_stream():
+    """A compact-JSON batch written into its device buffer by a copy queued on a torch side
+    stream behind a long kernel; the compute stream waits for the producer's event and the
+    batch is submitted at once.  The layout sample runs in stream order, so it sees the
+    compact lines (layout 1), not the reordered-key lines the buffer held before, and the
+    counts equal the C oracle's."""
+    import torch
+    dev = torch.device("cuda", 0)
+    gc = GenParams(seed=21, events_per_sec=1000, variant=GEN_COMPACT)
+    gr = GenParams(seed=21, events_per_sec=1000, variant=GEN_REORDER)
+    _, aids = gc.ids()
+    camp = gc.ad_campaign_index()
+    n = 20_000
+    raw_c, off_c = gc.events_host(0, n)
+    raw_r, off_r = gr.events_host(0, n)
+    size = max(raw_c.size, raw_r.size) + 64
+    rows, ost = oracle.run(oracle.AdMap(aids, camp), raw_c.tobytes(), off_c.tolist())
+    with make_ctx(n_campaigns=100, ads=(aids, camp)) as ctx:
+        buf = torch.zeros(size, dtype=torch.uint8, device=dev)
+        obuf = torch.zeros(n, dtype=torch.int32, device=dev)
+        buf[:raw_r.size].copy_(torch.from_numpy(raw_r))          # stale content: another layout
+        obuf.copy_(torch.from_numpy(off_r.view(np.int32)))
+        src_b = torch.from_numpy(raw_c).to(dev)
+        src_o = torch.from_numpy(off_c.view(np.int32)).to(dev)
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(200_000_000)                        # the producer is still queued ...
+            buf[:raw_c.size].copy_(src_b)
+            obuf.copy_(src_o)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        torch.cuda.ExternalStream(ctx.stream(), device=dev).wait_event(ev)
+        ctx.submit_device(buf.data_ptr(), int(raw_c.size), obuf.data_ptr(), n)   # ... when it is submitted
+        assert ctx.launch_info()["layout"] == 1
+        st = ctx.stats()
+        for k, v in ost.items():
+            assert st[k] == v, (k, st[k], v)
+        assert ctx.drain_buckets() == rows
+        torch.cuda.synchronize()
