@@ -801,6 +801,8 @@ def main():
                                "buckets": xinfo["last_buckets"], "cell_bytes": xinfo["last_width"],
                                "whole_ring_u64_bytes": xinfo["full_ring_bytes"]}
     extra = None
+    import threading
+    printed_lock, printed = threading.Lock(), []
     if not args.no_extras:
         free_segments(ctx, segs)
         ctx.close()
@@ -811,11 +813,13 @@ def main():
             # the headline line) forever: after --extras-timeout seconds rank 0 prints the
             # headline with the leg marked timed out and every rank exits
             def give_up():
-                if d.rank == 0:
-                    out["extras"] = {"config3": {"error": "timed out after %d s" % args.extras_timeout}}
-                    print(json.dumps(out), flush=True)
-                os._exit(0)
-            import threading
+                with printed_lock:
+                    if d.rank == 0 and not printed:
+                        out["extras"] = {"config3": {"error": "timed out after %d s" % args.extras_timeout}}
+                        print(json.dumps(out), flush=True)
+                        printed.append(True)
+                # non-zero: the launcher (and CI) must see that a rank was stuck in a collective
+                os._exit(3)
             dog = threading.Timer(args.extras_timeout, give_up)
             dog.daemon = True
             dog.start()
@@ -823,10 +827,12 @@ def main():
             guarded(extra, "config3", lambda: config3_ranks(args, d))
             dog.cancel()
 
-    if d.rank == 0:
-        if extra is not None:
-            out["extras"] = extra
-        print(json.dumps(out), flush=True)
+    with printed_lock:   # (the watchdog may print the line instead, never both)
+        if d.rank == 0 and not printed:
+            if extra is not None:
+                out["extras"] = extra
+            print(json.dumps(out), flush=True)
+            printed.append(True)
     if d.dist:
         d.dist.destroy_process_group()
 

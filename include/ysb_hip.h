@@ -427,9 +427,10 @@ uint32_t    ysb_ad_shard(const char* ad_id, uint32_t len, uint32_t nranks);
  * initialised context reports the same block).  Replaces the key -> subtask mapping of
  * Flink's keyBy(0) hash partitioner (AdvertisingTopologyNative.java:118-119). */
 int         ysb_group_block(uint32_t n_campaigns, int rank, int nranks, uint32_t* lo, uint32_t* hi);
-/* Host router for batches that are not pre-sharded: out_shard[i] = ysb_ad_shard of the
- * raw bytes of line i's top-level "ad_id" string (generator lines: bytes 113..148;
- * other layouts: a key scan); lines without one go to shard 0.  shard_counts (nranks
+/* Host router for batches that are not pre-sharded: out_shard[i] = ysb_ad_shard of line
+ * i's top-level "ad_id" string, its escapes decoded to UTF-8 as org.json and the device
+ * decode them (an escaped key name is found too; generator lines: bytes 113..148; other
+ * layouts: a key scan); lines without one go to shard 0.  shard_counts (nranks
  * entries, may be NULL) receives the lines per shard.  Routing must match the join table:
  * with a sharded table (ysb_load_ad_map_shard) only this hash is exact -- a view routed
  * elsewhere misses and is counted as foreign_shard (an error under YSB_F_STRICT); with the

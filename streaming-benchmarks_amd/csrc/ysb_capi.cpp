@@ -24,6 +24,8 @@ namespace ysb {
 int scan_lds_bytes();
 }
 
+constexpr size_t XEV_KEEP = 64;   // exchange timing pairs pending before they are folded into x_ms
+
 // HBM-resident join table (bucket layout): buckets per key, x4 (8: 2 per key, a 4 GiB
 // table at 10M ads; fewer buckets -> a smaller table, more keys in their second bucket)
 #ifndef YSB_BUCKETS_X4
@@ -1766,6 +1768,7 @@ int ysb_group_unique_id(uint8_t uid[YSB_UNIQUE_ID_BYTES]) {
 }
 
 static int group_setup(ysb_ctx* c, int rank, int nranks);
+static void ungroup(ysb_ctx* c);
 
 int ysb_group_init(ysb_ctx* c, int rank, int nranks, const uint8_t uid[YSB_UNIQUE_ID_BYTES]) {
     if (!c || !uid) return YSB_ERR_ARG;
@@ -1775,8 +1778,13 @@ int ysb_group_init(ysb_ctx* c, int rank, int nranks, const uint8_t uid[YSB_UNIQU
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof id);
     ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
-    if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
-    return group_setup(c, rank, nranks);
+    if (r != ncclSuccess) {
+        c->comm = nullptr;
+        return fail(c, YSB_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    const int rc = group_setup(c, rank, nranks);
+    if (rc) ungroup(c);
+    return rc;
 }
 
 int ysb_group_init_host(ysb_ctx* c, int rank, int nranks, const ysb_collectives* ops) {
@@ -1786,7 +1794,34 @@ int ysb_group_init_host(ysb_ctx* c, int rank, int nranks, const ysb_collectives*
     HIPCHK(c, hipSetDevice(c->device));
     c->hops = *ops;
     c->host_coll = true;
-    return group_setup(c, rank, nranks);
+    const int rc = group_setup(c, rank, nranks);
+    if (rc) ungroup(c);
+    return rc;
+}
+
+// A failed group init leaves the context ungrouped (and a later ysb_group_init possible):
+// the communicator, the exchange buffers and the owned table go; the counts stay.
+static void ungroup(ysb_ctx* c) {
+    if (c->comm) ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+    c->host_coll = false;
+    c->hops = ysb_collectives{};
+    hipFree(c->d_owned);
+    c->d_owned = nullptr;
+    hipFree(c->d_xmax);
+    c->d_xmax = nullptr;
+    hipHostFree(c->h_xmax);
+    c->h_xmax = nullptr;
+    hipFree(c->d_xslots);
+    c->d_xslots = nullptr;
+    for (hipEvent_t& e : c->xplan_ev) {
+        if (e) hipEventDestroy(e);
+        e = nullptr;
+    }
+    c->rank = 0;
+    c->nranks = 1;
+    c->ring_agreed = false;
+    c->x_have_plan = false;
 }
 
 static int group_setup(ysb_ctx* c, int rank, int nranks) {
@@ -1880,6 +1915,18 @@ int ysb_exchange_plan(const uint64_t* slot_max, uint32_t W, uint32_t nranks, uin
 // queues behind the exchange without a gap.  Counts in slots outside that plan, or above
 // what its width sums over the ranks (cap), stay pending for a later exchange; the first
 // call after group init / reset / ring advance is complete.
+// The recorded exchange timing pairs into x_ms (waits for the last of them).
+static int collect_xev(ysb_ctx* c) {
+    for (size_t i = 0; i < c->xev_used; ++i) {
+        float ms = 0;
+        HIPCHK(c, hipEventSynchronize(c->xev[i][1]));
+        HIPCHK(c, hipEventElapsedTime(&ms, c->xev[i][0], c->xev[i][1]));
+        c->x_ms += ms;
+    }
+    c->xev_used = 0;
+    return YSB_OK;
+}
+
 static int exchange(ysb_ctx* c, bool pipelined) {
     if (!grouped(c)) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
     int prc = launch_pending_raw(c);
@@ -1893,12 +1940,18 @@ static int exchange(ysb_ctx* c, bool pipelined) {
     const u32 W = c->cfg.window_ring;
     const u64 cells = (u64)c->c_pad * W;
     const u8* delta = c->delta_bound ? c->d_delta : nullptr;   // (delta_bound 0: the delta ring is all zero)
+    // timing pairs: folded into x_ms once XEV_KEEP are pending (a streaming caller may never
+    // ask for ysb_group_exchange_info); a pair counts only once both events were recorded
+    if (c->xev_used >= XEV_KEEP) {
+        int rc = collect_xev(c);
+        if (rc) return rc;
+    }
     if (c->xev_used == c->xev.size()) {
         std::array<hipEvent_t, 2> ev{};
         for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
         c->xev.push_back(ev);
     }
-    const auto ev = c->xev[c->xev_used++];
+    const auto ev = c->xev[c->xev_used];
     HIPCHK(c, hipEventRecord(ev[0], c->s_comp));
     // this call's plan into buffer nb
     const int nb = c->xb ^ 1;
@@ -1944,6 +1997,7 @@ static int exchange(ysb_ctx* c, bool pipelined) {
         c->delta_bound = 0;
     }
     HIPCHK(c, hipEventRecord(ev[1], c->s_comp));
+    c->xev_used++;
     c->x_count++;
     c->x_bytes += (u64)rows * R * width;
     c->x_last_slots = R;
@@ -1958,13 +2012,8 @@ int ysb_group_exchange_pipelined(ysb_ctx* c) { return c ? exchange(c, true) : YS
 int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
     if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
     int rc = sync_streams(c);
+    if (!rc) rc = collect_xev(c);
     if (rc) return rc;
-    for (size_t i = 0; i < c->xev_used; ++i) {
-        float ms = 0;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->xev[i][0], c->xev[i][1]));
-        c->x_ms += ms;
-    }
-    c->xev_used = 0;
     out->exchanges = c->x_count;
     out->bytes = c->x_bytes;
     out->ms = c->x_ms;

@@ -22,10 +22,10 @@ namespace {
 
 bool is_ws(u8 c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 
-// End of the string whose content starts at p (index of its closing quote), or -1.
-long scan_string(const u8* s, long p, long e) {
+// End of the string whose content starts at p (index of its closing quote q), or -1.
+long scan_string(const u8* s, long p, long e, u8 q = '"') {
     while (p < e) {
-        if (s[p] == '"') return p;
+        if (s[p] == q) return p;
         if (s[p] == '\\') p += 2;
         else ++p;
     }
@@ -55,17 +55,89 @@ long skip_value(const u8* s, long p, long e) {
     return p;
 }
 
+
+// ---- org.json string decoding, as the device decodes a key (ysb_orgjson.h decode_str) ----------
+
+bool hex_digit(u8 c, u32* v) {
+    if (c >= '0' && c <= '9') { *v = c - '0'; return true; }
+    if (c >= 'a' && c <= 'f') { *v = c - 'a' + 10; return true; }
+    if (c >= 'A' && c <= 'F') { *v = c - 'A' + 10; return true; }
+    return false;
+}
+
+// \uXXXX at p (the backslash): Integer.parseInt(XXXX, 16) as a UTF-16 unit -- a leading sign
+// takes three digits (\u-001 is U+FFFF), as JSONTokener.next(4) + parseInt read it.
+bool utf16_unit(const u8* s, long p, long e, bool sign_ok, u32* out) {
+    if (p + 5 >= e || s[p] != '\\' || s[p + 1] != 'u') return false;
+    const u8 d0 = s[p + 2];
+    u32 v = 0, d;
+    if (sign_ok && (d0 == '+' || d0 == '-')) {
+        for (int k = 3; k < 6; ++k) {
+            if (!hex_digit(s[p + k], &d)) return false;
+            v = v << 4 | d;
+        }
+        *out = d0 == '-' ? (0x10000u - v) & 0xFFFFu : v;
+        return true;
+    }
+    for (int k = 2; k < 6; ++k) {
+        if (!hex_digit(s[p + k], &d)) return false;
+        v = v << 4 | d;
+    }
+    *out = v;
+    return true;
+}
+
+void put_utf8(u32 cp, std::string& o) {   // lone surrogates: the 3-byte form
+    if (cp < 0x80) { o += (char)cp; return; }
+    if (cp < 0x800) { o += (char)(0xC0 | (cp >> 6)); o += (char)(0x80 | (cp & 0x3F)); return; }
+    if (cp < 0x10000) {
+        o += (char)(0xE0 | (cp >> 12)); o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F));
+        return;
+    }
+    o += (char)(0xF0 | (cp >> 18)); o += (char)(0x80 | ((cp >> 12) & 0x3F));
+    o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F));
+}
+
+// The string content s[a, b) with its escapes decoded to UTF-8, byte for byte what the
+// device's decode_str produces (so the host route and the device's shard test hash the same
+// key): \b \t \n \f \r, \x -> x, \uXXXX (a high surrogate directly followed by a low one is
+// one code point).  An escape org.json would reject is kept raw: such a line fails to parse
+// on the device, where its shard does not matter.
+std::string decode_escapes(const u8* s, long a, long b) {
+    std::string o;
+    o.reserve((size_t)(b - a));
+    for (long p = a; p < b;) {
+        const u8 c = s[p];
+        if (c != '\\' || p + 1 >= b) { o += (char)c; ++p; continue; }
+        const u8 x = s[p + 1];
+        if (x != 'u') {
+            o += (char)(x == 'b' ? 8 : x == 't' ? 9 : x == 'n' ? 10 : x == 'f' ? 12 : x == 'r' ? 13 : x);
+            p += 2;
+            continue;
+        }
+        u32 cp;
+        if (!utf16_unit(s, p, b, true, &cp)) { o += (char)c; ++p; continue; }
+        p += 6;
+        u32 lo;
+        if (cp >= 0xD800 && cp < 0xDC00 && utf16_unit(s, p, b, false, &lo) && lo >= 0xDC00 && lo < 0xE000) {
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            p += 6;
+        }
+        put_utf8(cp, o);
+    }
+    return o;
+}
+
 }  // namespace
 
-// Raw bytes of the top-level "ad_id" string value of one line.  Escapes are not decoded,
-// so an ad_id written with escapes may be routed to another shard than the one holding its
-// decoded key: with the whole ad map on every rank (ysb_load_ad_map) that only moves load;
-// with a sharded table (ysb_load_ad_map_shard) such a view misses and is counted as
-// foreign_shard -- an error under YSB_F_STRICT, never a silent loss.  Generator lines
-// (data/src/setup/core.clj:90-96) have it at byte 113; other layouts take a small
-// key scan.  Returns false when the line has no string ad_id.
-static bool find_ad_id(const u8* s, long n, long* vs, long* ve) {
+// The top-level "ad_id" string value of one line: its content span [*vs, *ve) and whether
+// it holds escapes (*esc).  Keys are compared decoded, as org.json compares them, so an
+// escaped key name ("ad_id") is found too; strings may be double- or single-quoted.
+// Generator lines (data/src/setup/core.clj:90-96) have the value at byte 113; other
+// layouts take a small key scan.  Returns false when the line has no string ad_id.
+static bool find_ad_id(const u8* s, long n, long* vs, long* ve, bool* esc) {
     static const char canon[] = "\"ad_id\": \"";   // bytes 103..112 of a generator line
+    *esc = false;
     if (n > 150 && std::memcmp(s + 103, canon, 10) == 0 && s[149] == '"' &&
         std::memchr(s + 113, '"', 36) == nullptr && std::memchr(s + 113, '\\', 36) == nullptr &&
         std::memcmp(s, "{\"user_id\": \"", 13) == 0) {
@@ -78,28 +150,31 @@ static bool find_ad_id(const u8* s, long n, long* vs, long* ve) {
             return true;
         }
     }
+    auto has_bs = [&](long a, long b) { return std::memchr(s + a, '\\', (size_t)(b - a)) != nullptr; };
     long p = 0;
     while (p < n && is_ws(s[p])) ++p;
     if (p >= n || s[p] != '{') return false;
     ++p;
     while (true) {
         while (p < n && is_ws(s[p])) ++p;
-        if (p >= n || s[p] != '"') return false;
-        const long ke = scan_string(s, p + 1, n);
+        if (p >= n || (s[p] != '"' && s[p] != '\'')) return false;
+        const long ke = scan_string(s, p + 1, n, s[p]);
         if (ke < 0) return false;
-        const bool is_ad = ke - p - 1 == 5 && std::memcmp(s + p + 1, "ad_id", 5) == 0;
+        bool is_ad = ke - p - 1 == 5 && std::memcmp(s + p + 1, "ad_id", 5) == 0;
+        if (!is_ad && has_bs(p + 1, ke)) is_ad = decode_escapes(s, p + 1, ke) == "ad_id";
         p = ke + 1;
         while (p < n && is_ws(s[p])) ++p;
         if (p >= n || s[p] != ':') return false;
         ++p;
         while (p < n && is_ws(s[p])) ++p;
         if (p >= n) return false;
-        if (s[p] == '"') {
-            const long q = scan_string(s, p + 1, n);
+        if (s[p] == '"' || s[p] == '\'') {
+            const long q = scan_string(s, p + 1, n, s[p]);
             if (q < 0) return false;
             if (is_ad) {
                 *vs = p + 1;
                 *ve = q;
+                *esc = has_bs(p + 1, q);
                 return true;
             }
             p = q + 1;
@@ -108,7 +183,7 @@ static bool find_ad_id(const u8* s, long n, long* vs, long* ve) {
             if (p < 0) return false;
         }
         while (p < n && is_ws(s[p])) ++p;
-        if (p < n && s[p] == ',') { ++p; continue; }
+        if (p < n && (s[p] == ',' || s[p] == ';')) { ++p; continue; }
         return false;   // '}' without an ad_id, or malformed
     }
 }
@@ -134,8 +209,15 @@ int ysb_route_lines(const uint8_t* bytes, uint64_t nbytes, const uint32_t* line_
         const u64 e = i + 1 < n ? (u64)line_off[i + 1] : nbytes;
         u32 r = 0;
         long vs, ve;
-        if (s <= e && e <= nbytes && find_ad_id(bytes + s, (long)(e - s), &vs, &ve))
-            r = ysb_ad_shard(reinterpret_cast<const char*>(bytes + s + vs), (u32)(ve - vs), nranks);
+        bool esc;
+        if (s <= e && e <= nbytes && find_ad_id(bytes + s, (long)(e - s), &vs, &ve, &esc)) {
+            if (!esc) {
+                r = ysb_ad_shard(reinterpret_cast<const char*>(bytes + s + vs), (u32)(ve - vs), nranks);
+            } else {   // the decoded key, as the device hashes it
+                const std::string k = decode_escapes(bytes + s, vs, ve);
+                r = ysb_ad_shard(k.data(), (u32)k.size(), nranks);
+            }
+        }
         out_shard[i] = r;
         if (shard_counts) shard_counts[r]++;
     }

@@ -169,3 +169,32 @@ def test_load_shard_arguments_checked_without_gpu():
     """The sharded loader rejects a bad shard before touching a device."""
     L = _lib.lib()
     assert L.ysb_load_ad_map_shard(None, None, None, None, 0, 0, 1) == -1
+
+
+def test_route_lines_hashes_the_decoded_ad_id():
+    """ysb_route_lines decodes org.json escapes in the ad_id value and the key name (and takes
+    single-quoted strings), so an event routes to the same shard however its ad_id is
+    written -- the shard the device's decoded-key test expects."""
+    import numpy as np
+    from ysb_amd import GenParams, route_lines
+    g = GenParams(seed=3)
+    raw, off = g.events_host(0, 3000)
+    lines = [bytes(raw[a:b]) for a, b in zip(off, list(off[1:]) + [raw.size])]
+
+    def esc(line, mode):
+        i = line.index(b'"ad_id": "')
+        v0 = i + 10
+        val = line[v0:v0 + 36]
+        if mode == 2:
+            return line[:i] + b"'ad_id' : '" + val + b"'" + line[v0 + 37:]
+        ev = b"".join((b"\\u%04X" % c) if k % 3 == 0 else bytes([c]) for k, c in enumerate(val))
+        return line[:i] + (b'"ad\\u005Fid": "' if mode else b'"ad_id": "') + ev + line[v0 + 36:]
+
+    for mode in (0, 1, 2):
+        el = [esc(ln, mode) for ln in lines]
+        for n in (2, 3, 8):
+            a, _ = route_lines(np.frombuffer(b"".join(lines), dtype=np.uint8),
+                               np.cumsum([0] + [len(x) for x in lines[:-1]]), n)
+            b, _ = route_lines(np.frombuffer(b"".join(el), dtype=np.uint8),
+                               np.cumsum([0] + [len(x) for x in el[:-1]]), n)
+            assert np.array_equal(a, b), (mode, n)

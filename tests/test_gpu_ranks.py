@@ -229,3 +229,52 @@ def test_one_rank_group_ring_advance_to_lower_base_moves_to_side_list():
         ctx.group_reduce_scatter()
         got = ctx.drain_buckets()
         assert got == {k: 2 * v for k, v in rows.items()}
+
+
+def _escape_ad(line, mode):
+    """The same event with its ad_id written with \\u escapes (every 5th value byte) and,
+    for mode 1, the key name too ("ad\\u005fid"); mode 2 single-quotes the value."""
+    i = line.index(b'"ad_id": "')
+    v0 = i + 10
+    val = line[v0:v0 + 36]
+    if mode == 2:
+        return line[:i] + b"\"ad_id\": '" + val + b"'" + line[v0 + 37:]
+    ev = b"".join(b"\\u%04x" % c if k % 5 == 0 else bytes([c]) for k, c in enumerate(val))
+    key = b'"ad\\u005fid": "' if mode == 1 else b'"ad_id": "'
+    return line[:i] + key + ev + line[v0 + 36:]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_routed_escaped_ad_ids_join_on_their_shard(world):
+    """ysb_route_lines hashes the DECODED ad_id (and finds an escaped key name), as the
+    device's shard test does: lines whose ad_id is written with \\u escapes, an escaped key or
+    single quotes are routed to the rank that holds their ad in its sharded join table, so no
+    view is foreign_shard and the joined views and counts equal the C oracle's on the whole
+    stream."""
+    import numpy as np
+    from oracle import oracle
+    from ysb_amd import route_lines
+    g = GenParams(seed=77, events_per_sec=1000)
+    _, aids = g.ids()
+    camp = g.ad_campaign_index()
+    raw, off = g.events_host(0, 30_000)
+    lines = [bytes(raw[a:b]) for a, b in zip(off, list(off[1:]) + [raw.size])]
+    lines = [_escape_ad(ln, k % 3) if k % 4 else ln for k, ln in enumerate(lines)]
+    data = b"".join(lines)
+    offs = np.cumsum([0] + [len(x) for x in lines[:-1]]).astype(np.uint32)
+    rows, ost = oracle.run(oracle.AdMap(aids, camp), data, offs.tolist())
+    shard, _ = route_lines(np.frombuffer(data, dtype=np.uint8), offs, world)
+    shard = np.asarray(shard)
+    got, joined = Counter(), 0
+    for r in range(world):
+        mine = [lines[i] for i in np.nonzero(shard == r)[0]]
+        with YsbContext(n_campaigns=100, strict=False) as ctx:
+            ctx.load_ad_map(aids, camp, shard=(r, world))
+            if mine:
+                ctx.submit(b"".join(mine), np.cumsum([0] + [len(x) for x in mine[:-1]]).astype(np.uint32))
+            st = ctx.stats()
+            assert st["foreign_shard"] == 0, (r, st)
+            joined += st["joined"]
+            got.update(ctx.drain_buckets())
+    assert joined == ost["joined"]
+    assert dict(got) == rows
