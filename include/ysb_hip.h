@@ -387,10 +387,12 @@ int         ysb_group_reduce_scatter(ysb_ctx* ctx);
  * sequence of the two calls. */
 int         ysb_group_exchange_pipelined(ysb_ctx* ctx);
 /* Exchange accounting: exchanges run, reduce-scatter input bytes this rank contributed,
- * device time of the exchanges (HIP events on the compute stream around plan, all-reduce,
- * read-back, pack, reduce-scatter and unpack), the last exchange's bucket count and cell
- * width (0: nothing was pending), and what one whole-ring u64 exchange would move.
- * reset != 0 zeroes the totals after reading them. */
+ * device time of the exchanges (HIP events from the plan on the compute stream to the end of
+ * the unpack on the exchange stream: plan, all-reduce(max), read-back, pack, reduce-scatter,
+ * unpack), of their part on the compute stream (critical_ms: plan to pack -- what a step
+ * waits for; the reduce-scatter and the unpack run on a stream of their own, beside the next
+ * launch), the last exchange's bucket count and cell width (0: nothing was pending), and what
+ * one whole-ring u64 exchange would move.  reset != 0 zeroes the totals after reading them. */
 typedef struct ysb_exchange_info {
     uint64_t exchanges;
     uint64_t bytes;
@@ -398,6 +400,7 @@ typedef struct ysb_exchange_info {
     uint32_t last_buckets;
     uint32_t last_width;
     uint64_t full_ring_bytes;
+    double   critical_ms;
 } ysb_exchange_info;
 int         ysb_group_exchange_info(ysb_ctx* ctx, ysb_exchange_info* out, int reset);
 /* The plan every rank derives from the all-reduced per-bucket maxima (host function):

@@ -162,14 +162,23 @@ struct ysb_ctx {
     hipEvent_t xplan_ev[2] = {nullptr, nullptr};
     int xb = 0;
     bool x_have_plan = false;
-    u32* d_xslots = nullptr;
-    void* d_xsend = nullptr;
-    void* d_xrecv = nullptr;
-    u64 xsend_bytes = 0, xrecv_bytes = 0;
+    // plan -> pack run on the compute stream (in order with the scans that add to the rings);
+    // the reduce-scatter and the unpack into the owned table on s_x, beside the next launch.
+    // Two buffer sets (slots, send, receive) alternate; a pack into set k waits for the unpack
+    // that last used it (ev_xdone[k]), the exchange stream for the pack (ev_xpacked[k]).
+    hipStream_t s_x = nullptr;
+    u32* d_xslots = nullptr;                // [2][W]
+    void* d_xsend[2] = {nullptr, nullptr};
+    void* d_xrecv[2] = {nullptr, nullptr};
+    u64 xsend_bytes[2] = {0, 0}, xrecv_bytes[2] = {0, 0};
+    hipEvent_t ev_xpacked[2] = {nullptr, nullptr}, ev_xdone[2] = {nullptr, nullptr};
+    bool xset_used[2] = {false, false};
+    int xk = 0;
     u64 x_count = 0, x_bytes = 0;
     u32 x_last_slots = 0, x_last_width = 0;
-    double x_ms = 0;
-    std::vector<std::array<hipEvent_t, 2>> xev;
+    double x_ms = 0, x_crit_ms = 0;
+    // per exchange {start, packed (compute stream), done (exchange stream)}
+    std::vector<std::array<hipEvent_t, 3>> xev;
     size_t xev_used = 0;
     // truth
     unsigned long long* d_truth = nullptr;
@@ -242,6 +251,7 @@ static void destroy(ysb_ctx* c) {
     if (c->s_comp) hipStreamSynchronize(c->s_comp);
     if (c->s_copy) hipStreamSynchronize(c->s_copy);
     if (c->s_split) hipStreamSynchronize(c->s_split);
+    if (c->s_x) hipStreamSynchronize(c->s_x);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_table);
     hipFree(c->d_ctable);
@@ -281,8 +291,13 @@ static void destroy(ysb_ctx* c) {
     for (hipEvent_t e : c->xplan_ev)
         if (e) hipEventDestroy(e);
     hipFree(c->d_xslots);
-    hipFree(c->d_xsend);
-    hipFree(c->d_xrecv);
+    for (int k = 0; k < 2; ++k) {
+        hipFree(c->d_xsend[k]);
+        hipFree(c->d_xrecv[k]);
+        if (c->ev_xpacked[k]) hipEventDestroy(c->ev_xpacked[k]);
+        if (c->ev_xdone[k]) hipEventDestroy(c->ev_xdone[k]);
+    }
+    if (c->s_x) hipStreamDestroy(c->s_x);
     for (auto& p : c->xev) for (hipEvent_t e : p) hipEventDestroy(e);
     hipFree(c->d_part);
     hipFree(c->d_runs);
@@ -1331,6 +1346,7 @@ static int sync_streams(ysb_ctx* c) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->s_copy));
     HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    if (c->s_x) HIPCHK(c, hipStreamSynchronize(c->s_x));
     poll_ring(c);
     return YSB_OK;
 }
@@ -1705,21 +1721,21 @@ static int coll_max_u64(ysb_ctx* c, unsigned long long* d, u64 n) {
 
 // recv[0..count) <- sum over the ranks of their send blocks [rank * count, (rank + 1) * count),
 // cells of `width` bytes (1, 4 or 8, unsigned).
-static int coll_reduce_scatter(ysb_ctx* c, const void* d_send, void* d_recv, u64 count, u32 width) {
+static int coll_reduce_scatter(ysb_ctx* c, const void* d_send, void* d_recv, u64 count, u32 width, hipStream_t st) {
     if (c->comm) {
         const ncclDataType_t ty = width == 1 ? ncclUint8 : width == 4 ? ncclUint32 : ncclUint64;
-        ncclResult_t r = ncclReduceScatter(d_send, d_recv, (size_t)count, ty, ncclSum, c->comm, c->s_comp);
+        ncclResult_t r = ncclReduceScatter(d_send, d_recv, (size_t)count, ty, ncclSum, c->comm, st);
         if (r != ncclSuccess) return fail(c, YSB_ERR_RCCL, "ncclReduceScatter: %s", ncclGetErrorString(r));
         return YSB_OK;
     }
     const u64 nb = count * width;
     std::vector<u8> hs(nb * (u64)c->nranks), hr(nb);
-    HIPCHK(c, hipMemcpyAsync(hs.data(), d_send, hs.size(), hipMemcpyDeviceToHost, c->s_comp));
-    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    HIPCHK(c, hipMemcpyAsync(hs.data(), d_send, hs.size(), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
     if (c->hops.reduce_scatter_sum(c->hops.user, hs.data(), hr.data(), count, width))
         return fail(c, YSB_ERR_RCCL, "host reduce-scatter failed");
-    HIPCHK(c, hipMemcpyAsync(d_recv, hr.data(), nb, hipMemcpyHostToDevice, c->s_comp));
-    HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    HIPCHK(c, hipMemcpyAsync(d_recv, hr.data(), nb, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipStreamSynchronize(st));
     return YSB_OK;
 }
 
@@ -1818,6 +1834,12 @@ static void ungroup(ysb_ctx* c) {
         if (e) hipEventDestroy(e);
         e = nullptr;
     }
+    for (int k = 0; k < 2; ++k) {
+        if (c->ev_xpacked[k]) hipEventDestroy(c->ev_xpacked[k]);
+        if (c->ev_xdone[k]) hipEventDestroy(c->ev_xdone[k]);
+        c->ev_xpacked[k] = c->ev_xdone[k] = nullptr;
+        c->xset_used[k] = false;
+    }
     c->rank = 0;
     c->nranks = 1;
     c->ring_agreed = false;
@@ -1861,8 +1883,14 @@ static int group_setup(ysb_ctx* c, int rank, int nranks) {
     const u32 W = c->cfg.window_ring;
     HIPCHK(c, hipMalloc(&c->d_xmax, 2 * (u64)W * 8));
     HIPCHK(c, hipHostMalloc(&c->h_xmax, 2 * ((u64)W * 8 + (u64)W * 4)));   // maxima, then the plans' slots
-    HIPCHK(c, hipMalloc(&c->d_xslots, (u64)W * 4));
+    HIPCHK(c, hipMalloc(&c->d_xslots, 2 * (u64)W * 4));
     for (hipEvent_t& e : c->xplan_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (int k = 0; k < 2; ++k) {
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_xpacked[k], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_xdone[k], hipEventDisableTiming));
+        c->xset_used[k] = false;
+    }
+    if (!c->s_x) HIPCHK(c, hipStreamCreateWithFlags(&c->s_x, hipStreamNonBlocking));
     c->x_have_plan = false;
     // every rank's ring must start at the same bucket (the tables are summed cell by
     // cell): agreed here if any rank already knows its base, else at the first exchange
@@ -1872,6 +1900,7 @@ static int group_setup(ysb_ctx* c, int rank, int nranks) {
 static int grow_bytes(ysb_ctx* c, void** buf, u64* have, u64 bytes) {
     if (*have >= bytes) return YSB_OK;
     HIPCHK(c, hipStreamSynchronize(c->s_comp));
+    if (c->s_x) HIPCHK(c, hipStreamSynchronize(c->s_x));
     hipFree(*buf);
     *buf = nullptr;
     *have = 0;
@@ -1918,10 +1947,12 @@ int ysb_exchange_plan(const uint64_t* slot_max, uint32_t W, uint32_t nranks, uin
 // The recorded exchange timing pairs into x_ms (waits for the last of them).
 static int collect_xev(ysb_ctx* c) {
     for (size_t i = 0; i < c->xev_used; ++i) {
-        float ms = 0;
-        HIPCHK(c, hipEventSynchronize(c->xev[i][1]));
-        HIPCHK(c, hipEventElapsedTime(&ms, c->xev[i][0], c->xev[i][1]));
+        float ms = 0, mc = 0;
+        HIPCHK(c, hipEventSynchronize(c->xev[i][2]));
+        HIPCHK(c, hipEventElapsedTime(&ms, c->xev[i][0], c->xev[i][2]));
+        HIPCHK(c, hipEventElapsedTime(&mc, c->xev[i][0], c->xev[i][1]));
         c->x_ms += ms;
+        c->x_crit_ms += mc;
     }
     c->xev_used = 0;
     return YSB_OK;
@@ -1947,7 +1978,7 @@ static int exchange(ysb_ctx* c, bool pipelined) {
         if (rc) return rc;
     }
     if (c->xev_used == c->xev.size()) {
-        std::array<hipEvent_t, 2> ev{};
+        std::array<hipEvent_t, 3> ev{};
         for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
         c->xev.push_back(ev);
     }
@@ -1977,18 +2008,28 @@ static int exchange(ysb_ctx* c, bool pipelined) {
     const unsigned long long cap = width == 8 ? ~0ull / (u64)c->nranks : ((1ull << (8 * width)) - 1) / (u64)c->nranks;
     const u32 rows = c->c_pad, per = c->c_pad / (u32)c->nranks;
     if (R) {
-        int rc = grow_bytes(c, &c->d_xsend, &c->xsend_bytes, (u64)rows * R * width);
-        if (!rc) rc = grow_bytes(c, &c->d_xrecv, &c->xrecv_bytes, (u64)per * R * width);
+        const int k = c->xk;
+        c->xk ^= 1;
+        // set k was last used two exchanges ago: its unpack must be done before it is rewritten
+        if (c->xset_used[k]) HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_xdone[k], 0));
+        int rc = grow_bytes(c, &c->d_xsend[k], &c->xsend_bytes[k], (u64)rows * R * width);
+        if (!rc) rc = grow_bytes(c, &c->d_xrecv[k], &c->xrecv_bytes[k], (u64)per * R * width);
         if (rc) return rc;
+        u32* dslots = c->d_xslots + (u64)k * W;
         // (the slots' pinned area is rewritten two calls later, after xplan_ev of the call
         // in between: this copy has run by then)
-        HIPCHK(c, hipMemcpyAsync(c->d_xslots, slots, (u64)R * 4, hipMemcpyHostToDevice, c->s_comp));
-        launch_xpack(c->d_counts, delta ? c->d_delta : nullptr, W, rows, c->d_xslots, R, c->pend_u64 ? 1 : 0,
-                     c->d_dirty, c->d_xsend, width, pipelined ? cap : ~0ull, c->s_comp);
+        HIPCHK(c, hipMemcpyAsync(dslots, slots, (u64)R * 4, hipMemcpyHostToDevice, c->s_comp));
+        launch_xpack(c->d_counts, delta ? c->d_delta : nullptr, W, rows, dslots, R, c->pend_u64 ? 1 : 0,
+                     c->d_dirty, c->d_xsend[k], width, pipelined ? cap : ~0ull, c->s_comp);
         HIPCHK(c, hipGetLastError());
-        if ((rc = coll_reduce_scatter(c, c->d_xsend, c->d_xrecv, (u64)per * R, width))) return rc;
-        launch_xunpack(c->d_owned, W, per, c->d_xslots, R, c->d_xrecv, width, c->s_comp);
+        HIPCHK(c, hipEventRecord(c->ev_xpacked[k], c->s_comp));
+        // the transfer and the unpack on the exchange stream, beside the next launch
+        HIPCHK(c, hipStreamWaitEvent(c->s_x, c->ev_xpacked[k], 0));
+        if ((rc = coll_reduce_scatter(c, c->d_xsend[k], c->d_xrecv[k], (u64)per * R, width, c->s_x))) return rc;
+        launch_xunpack(c->d_owned, W, per, dslots, R, c->d_xrecv[k], width, c->s_x);
         HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->ev_xdone[k], c->s_x));
+        c->xset_used[k] = true;
     }
     if (!pipelined) {
         // every pending count sat in an exchanged slot: nothing is pending any more
@@ -1997,6 +2038,7 @@ static int exchange(ysb_ctx* c, bool pipelined) {
         c->delta_bound = 0;
     }
     HIPCHK(c, hipEventRecord(ev[1], c->s_comp));
+    HIPCHK(c, hipEventRecord(ev[2], R ? c->s_x : c->s_comp));
     c->xev_used++;
     c->x_count++;
     c->x_bytes += (u64)rows * R * width;
@@ -2017,6 +2059,7 @@ int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
     out->exchanges = c->x_count;
     out->bytes = c->x_bytes;
     out->ms = c->x_ms;
+    out->critical_ms = c->x_crit_ms;
     out->last_buckets = c->x_last_slots;
     out->last_width = c->x_last_width;
     out->full_ring_bytes = (u64)c->c_pad * c->cfg.window_ring * 8;
@@ -2024,6 +2067,7 @@ int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
         c->x_count = 0;
         c->x_bytes = 0;
         c->x_ms = 0;
+        c->x_crit_ms = 0;
     }
     return YSB_OK;
 }

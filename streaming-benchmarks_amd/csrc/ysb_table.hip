@@ -150,41 +150,55 @@ __global__ __launch_bounds__(AUX_TPB) void xplan_kernel(const unsigned long long
         if (lmax[s]) atomicMax(&slot_max[s], lmax[s]);
 }
 
+// The pack and unpack walk the [rows][R] cell array two-dimensionally: one wave per campaign
+// row (grid-stride over rows), its lanes over the plan's slots (a few hundred bytes, cached) --
+// no 64-bit division or modulo per cell, and the packed cells of a row are written contiguously.
+constexpr int XROW_WAVES = AUX_TPB / 64;
+
+template <class T>
+__device__ __forceinline__ void put_cell(void* out, u64 i, unsigned long long v) { static_cast<T*>(out)[i] = (T)v; }
+
 // out[c][k] = pending(c, slots[k]) as `width`-byte cells, the sources zeroed -- except a
 // cell above `cap` (a pipelined exchange whose plan is one call old: the cell grew past what
 // the width can sum over the ranks), which stays pending for a later exchange and sends 0.
-// One thread per output cell: consecutive threads take consecutive slots of a campaign.
+// (On the compute stream, in order with the scans that add to the rings.)
+template <class T>
 __global__ __launch_bounds__(AUX_TPB) void xpack_kernel(unsigned long long* counts, u8* delta, u32 W, u32 rows,
                                                         const u32* slots, u32 R, int force_u64, const u32* dirty,
-                                                        void* out, u32 width, unsigned long long cap) {
+                                                        void* out, unsigned long long cap) {
     const bool r64 = read_u64(force_u64, dirty);
-    const u64 n = (u64)rows * R;
-    for (u64 i = (u64)blockIdx.x * AUX_TPB + threadIdx.x; i < n; i += (u64)gridDim.x * AUX_TPB) {
-        const u32 c = (u32)(i / R), k = (u32)(i % R);
-        const u64 cell = (u64)c * W + slots[k];
-        const unsigned long long d = delta ? delta[cell] : 0ull;
-        const unsigned long long x = r64 ? counts[cell] : 0ull;
-        unsigned long long v = d + x;
-        if (v > cap) {
-            v = 0;
-        } else {
-            if (d) delta[cell] = 0;
-            if (x) counts[cell] = 0;
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (u32 c = blockIdx.x * XROW_WAVES + wave; c < rows; c += gridDim.x * XROW_WAVES) {
+        const u64 row = (u64)c * W, orow = (u64)c * R;
+        for (u32 k = lane; k < R; k += 64) {
+            const u64 cell = row + slots[k];
+            const unsigned long long d = delta ? delta[cell] : 0ull;
+            const unsigned long long x = r64 ? counts[cell] : 0ull;
+            unsigned long long v = d + x;
+            if (v > cap) {
+                v = 0;
+            } else {
+                if (d) delta[cell] = 0;
+                if (x) counts[cell] = 0;
+            }
+            put_cell<T>(out, orow + k, v);
         }
-        if (width == 1) static_cast<u8*>(out)[i] = (u8)v;
-        else if (width == 4) static_cast<u32*>(out)[i] = (u32)v;
-        else static_cast<unsigned long long*>(out)[i] = v;
     }
 }
 
+// owned[c][slots[k]] += in[c][k].  No LDS, so its workgroups fit beside a running scan (it
+// runs on the exchange stream, under the next launch).
+template <class T>
 __global__ __launch_bounds__(AUX_TPB) void xunpack_kernel(unsigned long long* owned, u32 W, u32 rows,
-                                                          const u32* slots, u32 R, const void* in, u32 width) {
-    const u64 n = (u64)rows * R;
-    for (u64 i = (u64)blockIdx.x * AUX_TPB + threadIdx.x; i < n; i += (u64)gridDim.x * AUX_TPB) {
-        const unsigned long long v = width == 1   ? (unsigned long long)static_cast<const u8*>(in)[i]
-                                     : width == 4 ? (unsigned long long)static_cast<const u32*>(in)[i]
-                                                  : static_cast<const unsigned long long*>(in)[i];
-        if (v) owned[(u64)(i / R) * W + slots[i % R]] += v;
+                                                          const u32* slots, u32 R, const void* in) {
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const T* src = static_cast<const T*>(in);
+    for (u32 c = blockIdx.x * XROW_WAVES + wave; c < rows; c += gridDim.x * XROW_WAVES) {
+        const u64 row = (u64)c * W, irow = (u64)c * R;
+        for (u32 k = lane; k < R; k += 64) {
+            const unsigned long long v = src[irow + k];
+            if (v) owned[row + slots[k]] += v;
+        }
     }
 }
 
@@ -218,20 +232,24 @@ void launch_xplan(const unsigned long long* counts, const u8* delta, u32 W, u64 
                        force_u64, dirty, slot_max);
 }
 
+static u64 row_grid(u32 rows) { return std::max<u64>(1, std::min<u64>(((u64)rows + XROW_WAVES - 1) / XROW_WAVES, 8192)); }
+
 void launch_xpack(unsigned long long* counts, u8* delta, u32 W, u32 rows, const u32* slots, u32 R, int force_u64,
                   const u32* dirty, void* out, u32 width, unsigned long long cap, hipStream_t s) {
-    const u64 n = (u64)rows * R;
-    if (!n) return;
-    hipLaunchKernelGGL(xpack_kernel, dim3((unsigned)grid_for(n)), dim3(AUX_TPB), 0, s, counts, delta, W, rows, slots, R,
-                       force_u64, dirty, out, width, cap);
+    if (!rows || !R) return;
+    const dim3 g((unsigned)row_grid(rows)), b(AUX_TPB);
+    if (width == 1) hipLaunchKernelGGL(xpack_kernel<u8>, g, b, 0, s, counts, delta, W, rows, slots, R, force_u64, dirty, out, cap);
+    else if (width == 4) hipLaunchKernelGGL(xpack_kernel<u32>, g, b, 0, s, counts, delta, W, rows, slots, R, force_u64, dirty, out, cap);
+    else hipLaunchKernelGGL(xpack_kernel<unsigned long long>, g, b, 0, s, counts, delta, W, rows, slots, R, force_u64, dirty, out, cap);
 }
 
 void launch_xunpack(unsigned long long* owned, u32 W, u32 rows, const u32* slots, u32 R, const void* in, u32 width,
                     hipStream_t s) {
-    const u64 n = (u64)rows * R;
-    if (!n) return;
-    hipLaunchKernelGGL(xunpack_kernel, dim3((unsigned)grid_for(n)), dim3(AUX_TPB), 0, s, owned, W, rows, slots, R, in,
-                       width);
+    if (!rows || !R) return;
+    const dim3 g((unsigned)row_grid(rows)), b(AUX_TPB);
+    if (width == 1) hipLaunchKernelGGL(xunpack_kernel<u8>, g, b, 0, s, owned, W, rows, slots, R, in);
+    else if (width == 4) hipLaunchKernelGGL(xunpack_kernel<u32>, g, b, 0, s, owned, W, rows, slots, R, in);
+    else hipLaunchKernelGGL(xunpack_kernel<unsigned long long>, g, b, 0, s, owned, W, rows, slots, R, in);
 }
 
 void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_lo, u32 c_off, u32 c_lo, u32 c_hi,

@@ -62,6 +62,8 @@ def workload(name, g, n_campaigns, W, events, seg, table, args):
             "ms_per_step_with_pipelined_exchange": round(piped, 4),
             "exchange_device_ms_per_step": round(x["ms"] / max(x["exchanges"], 1), 4),
             "pipelined_exchange_device_ms_per_step": round(xp["ms"] / max(xp["exchanges"], 1), 4),
+            "exchange_critical_ms_per_step": round(x["critical_ms"] / max(x["exchanges"], 1), 4),
+            "pipelined_exchange_critical_ms_per_step": round(xp["critical_ms"] / max(xp["exchanges"], 1), 4),
             "exchange_bytes_per_step": x["bytes"] // max(x["exchanges"], 1), "buckets": x["last_buckets"],
             "cell_bytes": x["last_width"], "whole_ring_u64_bytes": x["full_ring_bytes"]}
 
