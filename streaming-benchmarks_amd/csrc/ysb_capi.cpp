@@ -163,9 +163,12 @@ struct ysb_ctx {
     int xb = 0;
     bool x_have_plan = false;
     // plan -> pack run on the compute stream (in order with the scans that add to the rings);
-    // the reduce-scatter and the unpack into the owned table on s_x, beside the next launch.
-    // Two buffer sets (slots, send, receive) alternate; a pack into set k waits for the unpack
-    // that last used it (ev_xdone[k]), the exchange stream for the pack (ev_xpacked[k]).
+    // the reduce-scatter on s_x, beside the next launch (at N ranks: the xGMI transfer); the
+    // unpack into the owned table on the compute stream again, at the next exchange (or before
+    // anything reads the owned table) -- beside a running scan it starved it (round 4 A/B).
+    // Two buffer sets (slots, send, receive) alternate; a pack into set k waits for the
+    // reduce-scatter that last used it (ev_xdone[k]), the exchange stream for the pack
+    // (ev_xpacked[k]).
     hipStream_t s_x = nullptr;
     u32* d_xslots = nullptr;                // [2][W]
     void* d_xsend[2] = {nullptr, nullptr};
@@ -174,11 +177,16 @@ struct ysb_ctx {
     hipEvent_t ev_xpacked[2] = {nullptr, nullptr}, ev_xdone[2] = {nullptr, nullptr};
     bool xset_used[2] = {false, false};
     int xk = 0;
+    // the pipelined exchange whose unpack is still to run: its set, slots, width, timing entry
+    int unpack_set = -1;
+    u32 unpack_R = 0, unpack_width = 0;
+    size_t unpack_entry = 0;
     u64 x_count = 0, x_bytes = 0;
     u32 x_last_slots = 0, x_last_width = 0;
     double x_ms = 0, x_crit_ms = 0;
-    // per exchange {start, packed (compute stream), done (exchange stream)}
-    std::vector<std::array<hipEvent_t, 3>> xev;
+    // per exchange {start, packed (compute stream), reduce-scatter done (exchange stream),
+    // unpack start, unpack end (compute stream)}
+    std::vector<std::array<hipEvent_t, 5>> xev;
     size_t xev_used = 0;
     // truth
     unsigned long long* d_truth = nullptr;
@@ -227,6 +235,7 @@ static int sync_streams(ysb_ctx* c);
 static int pull_side_list(ysb_ctx* c);
 static bool grouped(const ysb_ctx* c);
 static int launch_pending_raw(ysb_ctx* c);
+static int finish_unpack(ysb_ctx* c);
 
 int ysb_abi_version(void) { return YSB_ABI_VERSION; }
 
@@ -1342,6 +1351,7 @@ int ysb_submit_device_segments(ysb_ctx* c, const ysb_segment* segs, uint32_t n_s
 
 static int sync_streams(ysb_ctx* c) {
     int rc = launch_pending_raw(c);
+    if (!rc) rc = finish_unpack(c);   // a pipelined exchange's owner block
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->s_copy));
@@ -1840,6 +1850,7 @@ static void ungroup(ysb_ctx* c) {
         c->ev_xpacked[k] = c->ev_xdone[k] = nullptr;
         c->xset_used[k] = false;
     }
+    c->unpack_set = -1;
     c->rank = 0;
     c->nranks = 1;
     c->ring_agreed = false;
@@ -1945,14 +1956,37 @@ int ysb_exchange_plan(const uint64_t* slot_max, uint32_t W, uint32_t nranks, uin
 // what its width sums over the ranks (cap), stay pending for a later exchange; the first
 // call after group init / reset / ring advance is complete.
 // The recorded exchange timing pairs into x_ms (waits for the last of them).
+// The unpack of the last exchange (owner block += received cells), on the compute stream
+// once its reduce-scatter is done; a no-op when none is pending.
+static int finish_unpack(ysb_ctx* c) {
+    if (c->unpack_set < 0) return YSB_OK;
+    const int k = c->unpack_set;
+    c->unpack_set = -1;
+    const u32 W = c->cfg.window_ring, per = c->c_pad / (u32)c->nranks;
+    const auto& ev = c->xev[c->unpack_entry];
+    HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_xdone[k], 0));
+    HIPCHK(c, hipEventRecord(ev[3], c->s_comp));
+    launch_xunpack(c->d_owned, W, per, c->d_xslots + (u64)k * W, c->unpack_R, c->d_xrecv[k], c->unpack_width,
+                   c->s_comp);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(ev[4], c->s_comp));
+    return YSB_OK;
+}
+
+// The recorded exchange timing into x_ms (plan to the end of the reduce-scatter, plus the
+// unpack) and x_crit_ms (the compute stream's share: plan to pack, plus the unpack); waits
+// for the last of them.  Call after finish_unpack.
 static int collect_xev(ysb_ctx* c) {
     for (size_t i = 0; i < c->xev_used; ++i) {
-        float ms = 0, mc = 0;
-        HIPCHK(c, hipEventSynchronize(c->xev[i][2]));
-        HIPCHK(c, hipEventElapsedTime(&ms, c->xev[i][0], c->xev[i][2]));
-        HIPCHK(c, hipEventElapsedTime(&mc, c->xev[i][0], c->xev[i][1]));
-        c->x_ms += ms;
-        c->x_crit_ms += mc;
+        float ms = 0, mc = 0, mu = 0;
+        const auto& ev = c->xev[i];
+        HIPCHK(c, hipEventSynchronize(ev[2]));
+        HIPCHK(c, hipEventSynchronize(ev[4]));
+        HIPCHK(c, hipEventElapsedTime(&ms, ev[0], ev[2]));
+        HIPCHK(c, hipEventElapsedTime(&mc, ev[0], ev[1]));
+        HIPCHK(c, hipEventElapsedTime(&mu, ev[3], ev[4]));
+        c->x_ms += ms + mu;
+        c->x_crit_ms += mc + mu;
     }
     c->xev_used = 0;
     return YSB_OK;
@@ -1961,6 +1995,7 @@ static int collect_xev(ysb_ctx* c) {
 static int exchange(ysb_ctx* c, bool pipelined) {
     if (!grouped(c)) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
     int prc = launch_pending_raw(c);
+    if (!prc) prc = finish_unpack(c);   // the previous (pipelined) exchange's owner block first
     if (prc) return prc;
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->ring_agreed) {
@@ -1973,12 +2008,13 @@ static int exchange(ysb_ctx* c, bool pipelined) {
     const u8* delta = c->delta_bound ? c->d_delta : nullptr;   // (delta_bound 0: the delta ring is all zero)
     // timing pairs: folded into x_ms once XEV_KEEP are pending (a streaming caller may never
     // ask for ysb_group_exchange_info); a pair counts only once both events were recorded
+    int urc = YSB_OK;
     if (c->xev_used >= XEV_KEEP) {
         int rc = collect_xev(c);
         if (rc) return rc;
     }
     if (c->xev_used == c->xev.size()) {
-        std::array<hipEvent_t, 3> ev{};
+        std::array<hipEvent_t, 5> ev{};
         for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
         c->xev.push_back(ev);
     }
@@ -2023,13 +2059,16 @@ static int exchange(ysb_ctx* c, bool pipelined) {
                      c->d_dirty, c->d_xsend[k], width, pipelined ? cap : ~0ull, c->s_comp);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(c->ev_xpacked[k], c->s_comp));
-        // the transfer and the unpack on the exchange stream, beside the next launch
+        // the transfer on the exchange stream, beside the next launch; the unpack follows on
+        // the compute stream (finish_unpack)
         HIPCHK(c, hipStreamWaitEvent(c->s_x, c->ev_xpacked[k], 0));
         if ((rc = coll_reduce_scatter(c, c->d_xsend[k], c->d_xrecv[k], (u64)per * R, width, c->s_x))) return rc;
-        launch_xunpack(c->d_owned, W, per, dslots, R, c->d_xrecv[k], width, c->s_x);
-        HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(c->ev_xdone[k], c->s_x));
         c->xset_used[k] = true;
+        c->unpack_set = k;
+        c->unpack_R = R;
+        c->unpack_width = width;
+        c->unpack_entry = c->xev_used;
     }
     if (!pipelined) {
         // every pending count sat in an exchanged slot: nothing is pending any more
@@ -2039,7 +2078,13 @@ static int exchange(ysb_ctx* c, bool pipelined) {
     }
     HIPCHK(c, hipEventRecord(ev[1], c->s_comp));
     HIPCHK(c, hipEventRecord(ev[2], R ? c->s_x : c->s_comp));
+    if (!R) {   // nothing to unpack: an empty unpack interval
+        HIPCHK(c, hipEventRecord(ev[3], c->s_comp));
+        HIPCHK(c, hipEventRecord(ev[4], c->s_comp));
+    }
     c->xev_used++;
+    // complete: the owners' tables hold everything once the call's work has run
+    if (!pipelined && (urc = finish_unpack(c))) return urc;
     c->x_count++;
     c->x_bytes += (u64)rows * R * width;
     c->x_last_slots = R;

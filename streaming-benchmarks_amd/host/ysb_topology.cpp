@@ -4,6 +4,8 @@
 
 #include <arpa/inet.h>
 #include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <netdb.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -294,15 +296,25 @@ private:
     }
 };
 
-FileBasedDataSource::FileBasedDataSource(const std::string& path, unsigned threads) {
+FileBasedDataSource::FileBasedDataSource(const std::string& path, unsigned threads, bool mmap) {
     fd_ = ::open(path.c_str(), O_RDONLY);
     if (fd_ < 0) throw std::runtime_error("java.io.FileNotFoundException: " + path);
     threads_ = threads ? threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     pool_.reset(new WorkerPool(threads_));
+    struct stat st;
+    if (mmap && ::fstat(fd_, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
+        void* m = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fd_, 0);
+        if (m != MAP_FAILED) {
+            ::madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
+            map_ = static_cast<const uint8_t*>(m);
+            size_ = (uint64_t)st.st_size;
+        }
+    }
 }
 
 FileBasedDataSource::~FileBasedDataSource() {
     pool_.reset();
+    if (map_) ::munmap(const_cast<uint8_t*>(map_), size_);
     if (fd_ >= 0) ::close(fd_);
 }
 
@@ -319,7 +331,17 @@ uint64_t FileBasedDataSource::readBlock(uint8_t* buf, uint64_t cap) {
     uint64_t have = carry_.size();
     std::memcpy(buf, carry_.data(), have);
     carry_.clear();
-    if (!eof_ && have < cap) {
+    if (!eof_ && have < cap && map_) {   // parallel copies out of the mapping (>= 4 MiB each)
+        const uint64_t want = std::min<uint64_t>(cap - have, size_ - std::min(pos_, size_));
+        const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads_, want >> 22));
+        pool_->run(T, [&](unsigned t) {
+            const uint64_t a = want * t / T, b = want * (t + 1) / T;
+            std::memcpy(buf + have + a, map_ + pos_ + a, b - a);
+        });
+        pos_ += want;
+        have += want;
+        if (pos_ >= size_) eof_ = true;
+    } else if (!eof_ && have < cap) {
         const uint64_t want = cap - have;
         const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads_, want >> 22));
         std::vector<uint64_t> got(T, 0);

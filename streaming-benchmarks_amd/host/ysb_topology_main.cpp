@@ -7,7 +7,7 @@
 //   ysb_topology --confPath PATH [--device N] [--sink none|csv:FILE|redis[:HOST[:PORT]]]
 //                [--format json|tbl] [--flush-ms MS] [--batch-mb MB | --batch-bytes B] [--batch-events N]
 //                [--window-ring W] [--require-ip] [--dry-run] [--print-config]
-//                [--replay-rows CSV] [--host-split] [--repeat K] [--io-threads T]
+//                [--replay-rows CSV] [--host-split] [--repeat K] [--io-threads T] [--io mmap|pread]
 //
 // --dry-run reads the config, the map and the events file (FileBasedDataSource) without a
 // GPU and reports what it found; --replay-rows writes the (campaign_id,window_ms,count)
@@ -38,6 +38,7 @@ struct Args {
     bool require_ip = false, dry = false, print_config = false, host_split = false;
     long long repeat = 1;
     unsigned io_threads = 0;
+    bool io_mmap = true;
 };
 
 void usage() {
@@ -45,7 +46,7 @@ void usage() {
                  "usage: ysb_topology --confPath PATH [--device N] [--sink none|csv:FILE|redis[:HOST[:PORT]]]\n"
                  "       [--format json|tbl] [--flush-ms MS] [--batch-mb MB | --batch-bytes B] [--batch-events N]\n"
                  "       [--window-ring W] [--require-ip] [--dry-run] [--print-config] [--replay-rows CSV]\n"
-                 "       [--host-split] [--repeat K] [--io-threads T]\n");
+                 "       [--host-split] [--repeat K] [--io-threads T] [--io mmap|pread]\n");
 }
 
 Args parse(int argc, char** argv) {
@@ -72,6 +73,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--host-split") a.host_split = true;
         else if (k == "--repeat") a.repeat = std::max(1ll, std::atoll(val().c_str()));
         else if (k == "--io-threads") a.io_threads = (unsigned)std::atoll(val().c_str());
+        else if (k == "--io") a.io_mmap = val() != "pread";
         else { usage(); std::exit(2); }
     }
     if (a.conf.empty()) {   // ParameterTool.getRequired("confPath")
@@ -128,7 +130,7 @@ int run(const Args& a) {
     o.requireIp = a.require_ip;
     o.gpuSplit = !a.host_split;
 
-    FileBasedDataSource src(events, a.io_threads);
+    FileBasedDataSource src(events, a.io_threads, a.io_mmap);
     const double t0 = now_s();
     if (a.dry) {   // host half only: map + source, no device
         std::vector<uint8_t> buf(o.batchBytes);

@@ -182,14 +182,35 @@ def test_raw_crlf_and_lone_cr_lines_match_oracle():
         assert ctx.drain_buckets() == rows
 
 
+def _hip():
+    """The HIP runtime libysb_hip.so itself loaded (same instance: its streams and events are
+    the library's)."""
+    import ctypes as C
+    from ysb_amd import lib
+    lib()
+    h = C.CDLL("/opt/rocm/lib/libamdhip64.so.7")
+    for f, args in (("hipStreamCreate", [C.c_void_p]), ("hipStreamDestroy", [C.c_void_p]),
+                    ("hipEventCreate", [C.c_void_p]), ("hipEventDestroy", [C.c_void_p]),
+                    ("hipEventRecord", [C.c_void_p, C.c_void_p]),
+                    ("hipStreamWaitEvent", [C.c_void_p, C.c_void_p, C.c_uint]),
+                    ("hipMemsetAsync", [C.c_void_p, C.c_int, C.c_size_t, C.c_void_p]),
+                    ("hipMemcpyAsync", [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
+                    ("hipStreamSynchronize", [C.c_void_p]), ("hipDeviceSynchronize", [])):
+        getattr(h, f).argtypes = args
+        getattr(h, f).restype = C.c_int
+    return h
+
+
 def test_device_sample_follows_a_producer_on_another_stream():
-    """A compact-JSON batch written into its device buffer by a copy queued on a torch side
-    stream behind a long kernel; the compute stream waits for the producer's event and the
-    batch is submitted at once.  The layout sample runs in stream order, so it sees the
-    compact lines (layout 1), not the reordered-key lines the buffer held before, and the
-    counts equal the C oracle's."""
-    import torch
-    dev = torch.device("cuda", 0)
+    """A compact-JSON batch written into its device buffer by a copy queued on another stream
+    behind ~6 GB of memsets (the producer is still running when the batch is submitted); the
+    compute stream waits for the producer's event (hipStreamWaitEvent(ysb_stream(ctx), ...),
+    the documented contract) and the batch is submitted at once.  The layout sample runs in
+    stream order, so it sees the compact lines (layout 1), not the reordered-key lines the
+    buffer held before, and the counts equal the C oracle's."""
+    import ctypes as C
+    hip = _hip()
+    D2D = 3
     gc = GenParams(seed=21, events_per_sec=1000, variant=GEN_COMPACT)
     gr = GenParams(seed=21, events_per_sec=1000, variant=GEN_REORDER)
     _, aids = gc.ids()
@@ -197,28 +218,33 @@ def test_device_sample_follows_a_producer_on_another_stream():
     n = 20_000
     raw_c, off_c = gc.events_host(0, n)
     raw_r, off_r = gr.events_host(0, n)
-    size = max(raw_c.size, raw_r.size) + 64
     rows, ost = oracle.run(oracle.AdMap(aids, camp), raw_c.tobytes(), off_c.tolist())
     with make_ctx(n_campaigns=100, ads=(aids, camp)) as ctx:
-        buf = torch.zeros(size, dtype=torch.uint8, device=dev)
-        obuf = torch.zeros(n, dtype=torch.int32, device=dev)
-        buf[:raw_r.size].copy_(torch.from_numpy(raw_r))          # stale content: another layout
-        obuf.copy_(torch.from_numpy(off_r.view(np.int32)))
-        src_b = torch.from_numpy(raw_c).to(dev)
-        src_o = torch.from_numpy(off_c.view(np.int32)).to(dev)
-        torch.cuda.synchronize()
-        side = torch.cuda.Stream(device=dev)
-        with torch.cuda.stream(side):
-            torch.cuda._sleep(200_000_000)                        # the producer is still queued ...
-            buf[:raw_c.size].copy_(src_b)
-            obuf.copy_(src_o)
-            ev = torch.cuda.Event()
-            ev.record(side)
-        torch.cuda.ExternalStream(ctx.stream(), device=dev).wait_event(ev)
-        ctx.submit_device(buf.data_ptr(), int(raw_c.size), obuf.data_ptr(), n)   # ... when it is submitted
+        size = max(raw_c.size, raw_r.size) + 64
+        d_b, d_o = ctx.device_alloc(size), ctx.device_alloc(4 * n + 64)
+        s_b, s_o = ctx.device_alloc(size), ctx.device_alloc(4 * n + 64)
+        junk_n = 6 << 30
+        junk = ctx.device_alloc(junk_n)
+        ctx.h2d(d_b, raw_r)                      # stale content: another layout
+        ctx.h2d(d_o, off_r)
+        ctx.h2d(s_b, raw_c)                      # what the producer will copy in
+        ctx.h2d(s_o, off_c)
+        side, ev = C.c_void_p(), C.c_void_p()
+        assert hip.hipStreamCreate(C.byref(side)) == 0 and hip.hipEventCreate(C.byref(ev)) == 0
+        for _ in range(4):                       # the producer is still queued ...
+            assert hip.hipMemsetAsync(C.c_void_p(junk), 0, junk_n, side) == 0
+        assert hip.hipMemcpyAsync(C.c_void_p(d_b), C.c_void_p(s_b), int(raw_c.size), D2D, side) == 0
+        assert hip.hipMemcpyAsync(C.c_void_p(d_o), C.c_void_p(s_o), 4 * n, D2D, side) == 0
+        assert hip.hipEventRecord(ev, side) == 0
+        assert hip.hipStreamWaitEvent(C.c_void_p(ctx.stream()), ev, 0) == 0
+        ctx.submit_device(d_b, int(raw_c.size), d_o, n)   # ... when the batch is submitted
         assert ctx.launch_info()["layout"] == 1
         st = ctx.stats()
         for k, v in ost.items():
             assert st[k] == v, (k, st[k], v)
         assert ctx.drain_buckets() == rows
-        torch.cuda.synchronize()
+        assert hip.hipStreamSynchronize(side) == 0
+        hip.hipEventDestroy(ev)
+        hip.hipStreamDestroy(side)
+        for d in (d_b, d_o, s_b, s_o, junk):
+            ctx.device_free(d)

@@ -154,7 +154,7 @@ def truth_rows(device, g, n, cids, repeat):
 
 
 def native_runner(device=0, file_events=20_000_000, repeat=5, slot_mb=256, host_split=False, workdir=None,
-                  keep=None):
+                  keep=None, io="mmap"):
     made = workdir is None
     path = workdir or tempfile.mkdtemp(prefix="ysb_replay_", dir=os.environ.get("TMPDIR") or "/tmp")
     try:
@@ -168,7 +168,7 @@ def native_runner(device=0, file_events=20_000_000, repeat=5, slot_mb=256, host_
         cids, _ = g.ids()
         out_csv = os.path.join(path, "out.csv")
         cmd = [RUNNER, "--confPath", os.path.join(path, "conf.yaml"), "--device", str(device), "--sink",
-               "csv:" + out_csv, "--batch-mb", str(slot_mb), "--repeat", str(repeat)]
+               "csv:" + out_csv, "--batch-mb", str(slot_mb), "--repeat", str(repeat), "--io", io]
         if host_split:
             cmd += ["--host-split", "--batch-events", str((slot_mb << 20) // 200)]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
@@ -183,7 +183,7 @@ def native_runner(device=0, file_events=20_000_000, repeat=5, slot_mb=256, host_
                 got[(c, int(w))] = int(n)
         want, outside = truth_rows(device, g, file_events, cids, repeat)
         mism = sum(1 for k in set(got) | set(want) if got.get(k, 0) != want.get(k, 0))
-        summary.update({"file_events": file_events, "file_GB": round(os.path.getsize(
+        summary.update({"io": io, "file_events": file_events, "file_GB": round(os.path.getsize(
             os.path.join(path, "kafka-json.txt")) / 1e9, 3),
             "check": {"truth_mismatched_cells": mism, "cells": len(want), "truth_outside_ring": outside,
                       "counted_views": sum(got.values()), "truth_views": sum(want.values())}})
@@ -203,11 +203,12 @@ def main():
     ap.add_argument("--file-events", type=int, default=20_000_000)
     ap.add_argument("--repeat", type=int, default=5)
     ap.add_argument("--host-split", action="store_true")
+    ap.add_argument("--io", default="mmap", choices=["mmap", "pread"])
     a = ap.parse_args()
     if a.mode == "staged":
         out = host_staged(a.device, a.events, a.slot_mb, a.raw)
     else:
-        out = native_runner(a.device, a.file_events, a.repeat, a.slot_mb, a.host_split)
+        out = native_runner(a.device, a.file_events, a.repeat, a.slot_mb, a.host_split, io=a.io)
     print(json.dumps(out), flush=True)
 
 
