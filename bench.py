@@ -344,6 +344,13 @@ def extras(args, device):
     guarded(out, "host_staged", lambda: extra_host_staged(args, device))
     guarded(out, "native_runner", lambda: extra_native_runner(args, device, out.get("host_staged")))
     guarded(out, "config3", lambda: extra_config3(args, device))
+    from ysb_amd import GEN_COMPACT, GEN_REORDER
+    guarded(out, "config3_compact", lambda: extra_config3(
+        args, device, GEN_COMPACT, "compact JSON (no space after ':' and ','), no hint: the layout read from "
+        "each batch's first line"))
+    guarded(out, "config3_reordered_no_hint", lambda: extra_config3(
+        args, device, GEN_REORDER, "the keys in another order (ad_type, event_time, ad_id, ip_address, user_id, "
+        "event_type, page_id), no hint: the learned-order instantiation from each batch's first line"))
     guarded(out, "tbl", lambda: extra_tbl(args, device))
     extra_layouts(args, device, out)
     if args.stream_seconds > 0:
@@ -388,22 +395,28 @@ def extra_native_runner(args, device, staged):
     return r
 
 
-def extra_config3(args, device):
+def extra_config3(args, device, variant=0, what=None):
+    """configs[2] (1M campaigns / 10M ads: the HBM-resident bucket join table, record-mode
+    counting); variant: the same events as another producer writes them (compact JSON,
+    another key order), the layout read from each batch's first line."""
     from ysb_amd import GenParams, YsbContext
     t = time.perf_counter()
-    g = GenParams(seed=42, n_campaigns=1_000_000, ads_per_campaign=10, events_per_sec=args.rate)
+    g = GenParams(seed=42, n_campaigns=1_000_000, ads_per_campaign=10, events_per_sec=args.rate, variant=variant)
     _, ab = g.ids_packed()
     with YsbContext(device=device, n_campaigns=1_000_000, window_ring=128, timing=True,
                     max_batch_bytes=1 << 20, max_batch_events=1 << 12) as ctx:
         ctx.load_ad_map_packed(ab, g.ad_campaign_index_array())
         load_s = time.perf_counter() - t
-        segs = gen_segments(ctx, g, 100_000_000, 16_666_667)   # 6 batches, as the headline
+        # 6 batches, as the headline (other producers' lines up to ~280 B: 7)
+        segs = gen_segments(ctx, g, 100_000_000, 14_285_715 if variant else 16_666_667)
         r = timed_extra("configs[2]: 100M JSON events, 1M campaigns x 10 ads (10M-ad join table and "
-                        "1M x 128-bucket count ring in HBM)", ctx, g, segs, args.extra_steps, args.warmup,
-                        "ysb::scan_kernel<true, false, true, 0>")
+                        "1M x 128-bucket count ring in HBM)" + (", " + what if what else ""), ctx, g, segs,
+                        args.extra_steps, args.warmup, None)
+        lay = ctx.launch_info()["layout"]
+        r["kernel"] = "ysb::scan_kernel<true, false, true, %d>" % lay
         r["ad_map_load_s"] = round(load_s, 2)
         free_segments(ctx, segs)
-    log("extras: config3 %.2f G events/s" % (r["events_per_s"] / 1e9))
+    log("extras: config3%s %.2f G events/s" % (" variant %d" % variant if variant else "", r["events_per_s"] / 1e9))
     return r
 
 

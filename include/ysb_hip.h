@@ -74,7 +74,8 @@ extern "C" {
                                    or ','); the scan tries that layout first and the
                                    generator's (core.clj:90-96) as a later tier.  Counts
                                    are identical either way; only the speed differs.
-                                   Cache-resident join tables only (ignored otherwise). */
+                                   Every join-table layout (since ABI 3 also the HBM-
+                                   resident table's serial-probe / record-mode kernels). */
 #define YSB_F_FLAT_FIRST 0x100u /* layout hint: JSON lines are flat objects in any key
                                    order or spacing (another producer's serializer); the
                                    scan parses every line with its flat-object tier first
@@ -84,20 +85,22 @@ extern "C" {
                                    the learned-order instantiation, which sends lines off
                                    that order to the same flat tier (without
                                    YSB_F_LAYOUT_FIXED).  Counts are identical; takes
-                                   precedence over YSB_F_COMPACT_FIRST.  Cache-resident
-                                   join tables only. */
+                                   precedence over YSB_F_COMPACT_FIRST.  Every join-table
+                                   layout (since ABI 3). */
 #define YSB_F_LAYOUT_AUTO 0x200u /* (the default since ABI 2; the bit is accepted and
                                    ignored) layout read from the data: every submit picks
                                    the scan instantiation from the first line of each batch
                                    -- host batches from the pinned slot, device batches from
-                                   a <= 288-byte device-to-host sample per segment -- the
+                                   a <= 288-byte sample per segment taken on the device in
+                                   stream order (ysb_submit_device) -- the
                                    generator's layout, compact JSON, a learned key order
                                    (the first line's order and spacing, checked in place
                                    on every line), or the flat-object tier first.  Counts
                                    are identical whichever runs.  The explicit hints above
-                                   take precedence.  Cache-resident
-                                   join tables only (the HBM-table and record-mode
-                                   instantiations keep the generator layout first). */
+                                   take precedence.  Every join-table layout: since ABI 3
+                                   the HBM-resident table's serial-probe and record-mode
+                                   kernels (configs[2]) have the layout instantiations
+                                   too. */
 #define YSB_F_LAYOUT_FIXED 0x800u /* no layout sampling: the generator's layout first (or
                                    the explicit hint); device batches are then never read
                                    by the host before their launch */

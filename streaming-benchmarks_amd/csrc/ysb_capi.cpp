@@ -921,8 +921,8 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     launch_scan(p, c->s_comp);
     HIPCHK(c, hipGetLastError());
     if (!p.rec_on) c->pend_u64 = true;   // this launch counts into the u64 ring
-    // (launch_scan: the layout instantiations exist for JSON with the cache-resident table)
-    c->last_launch.layout = (p.tbl || p.rec_on || p.probe_serial) ? 0u : p.layout;
+    // (launch_scan: the layout instantiations exist for every JSON table layout)
+    c->last_launch.layout = p.tbl ? 0u : p.layout;
     c->last_launch.record_mode = p.rec_on ? 1u : 0u;
     c->last_launch.hbm_table = p.probe_serial ? 1u : 0u;
     c->last_launch.tbl = p.tbl ? 1u : 0u;
@@ -1007,11 +1007,12 @@ static int sniff_layout(const ysb_ctx* c, const uint8_t* bytes, u64 nbytes, cons
 
 // Whether batches pick the scan instantiation from their first line (the default): not
 // with YSB_F_COMPACT_FIRST or YSB_F_LAYOUT_FIXED, and only where the layout instantiations
-// exist (JSON, cache-resident join table).  Under YSB_F_FLAT_FIRST the sample only tells
+// exist (JSON: the cache-resident table's and, since round 4, the HBM-resident table's
+// serial-probe and record-mode kernels).  Under YSB_F_FLAT_FIRST the sample only tells
 // whether the batch has one learnable key order (hinted_layout).
 static bool layout_sampling(const ysb_ctx* c) {
     const u32 f = c->cfg.flags;
-    return !(f & (YSB_F_LAYOUT_FIXED | YSB_F_COMPACT_FIRST | YSB_F_FORMAT_TBL)) && !c->ctable_buckets;
+    return !(f & (YSB_F_LAYOUT_FIXED | YSB_F_COMPACT_FIRST | YSB_F_FORMAT_TBL));
 }
 
 // The sampled layout under the flags' hint: YSB_F_FLAT_FIRST keeps the flat-object tier

@@ -2217,9 +2217,19 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
         else if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, true, false>), g, b, Geom<true>::LDS, s, p);
         else hipLaunchKernelGGL((scan_kernel<false, true, false>), g, b, Geom<true>::LDS, s, p);
     } else {
-        if (p.rec_on) hipLaunchKernelGGL((scan_kernel<true, false, true>), g, b, (Geom<false, true>::LDS), s, p);
-        else if (p.probe_serial) hipLaunchKernelGGL((scan_kernel<true, false, false>), g, b, Geom<false>::LDS, s, p);
-        else if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<false, false, false, 1>), g, b, Geom<false>::LDS, s, p);
+        // HBM-resident join table (configs[2]): record mode or serial probes, each with the
+        // layout instantiations too (round 4), so other producers' layouts keep their fast tier
+        if (p.rec_on) {
+            if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<true, false, true, 1>), g, b, (Geom<false, true>::LDS), s, p);
+            else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<true, false, true, 2>), g, b, (Geom<false, true>::LDS), s, p);
+            else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<true, false, true, 3>), g, b, (Geom<false, true>::LDS), s, p);
+            else hipLaunchKernelGGL((scan_kernel<true, false, true>), g, b, (Geom<false, true>::LDS), s, p);
+        } else if (p.probe_serial) {
+            if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<true, false, false, 1>), g, b, Geom<false>::LDS, s, p);
+            else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<true, false, false, 2>), g, b, Geom<false>::LDS, s, p);
+            else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<true, false, false, 3>), g, b, Geom<false>::LDS, s, p);
+            else hipLaunchKernelGGL((scan_kernel<true, false, false>), g, b, Geom<false>::LDS, s, p);
+        } else if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<false, false, false, 1>), g, b, Geom<false>::LDS, s, p);
         else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<false, false, false, 2>), g, b, Geom<false>::LDS, s, p);
         else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<false, false, false, 3>), g, b, Geom<false>::LDS, s, p);
         else hipLaunchKernelGGL((scan_kernel<false, false, false>), g, b, Geom<false>::LDS, s, p);

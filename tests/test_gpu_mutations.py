@@ -160,3 +160,44 @@ def test_random_edits_hbm_table_record_mode_match_oracle():
     for k in STAT_KEYS:
         assert st[k] == est[k], (k, st[k], est[k])
     assert got == exp
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("first,want", [(GEN_COMPACT, 1), (GEN_REORDER, 3), (0, 0)])
+@pytest.mark.parametrize("rec", [True, False])
+def test_hbm_table_layout_instantiations_match_oracle(first, want, rec):
+    """configs[2]'s HBM-resident join table with other producers' layouts (round 4): the
+    batch's first line picks the compact / learned-order / generator instantiation of the
+    record-mode (rec) or serial-probe kernel; 300k lines, a quarter of them from the other
+    producers, 10 % edited -- exact vs the C oracle, and the instantiation is the sampled one."""
+    rng = np.random.default_rng(11 + first)
+    variants = [first] + [v for v in (0, GEN_COMPACT, GEN_REORDER) if v != first]
+    pools = [lines_of(GenParams(seed=71, n_campaigns=600_000, ads_per_campaign=2, events_per_sec=1000,
+                                with_skew=True, variant=v), 300_000) for v in variants]
+    g0 = GenParams(seed=71, n_campaigns=600_000, ads_per_campaign=2)
+    _, aids = g0.ids()
+    camp = g0.ad_campaign_index()
+    pick = rng.random(300_000)
+    lines = [pools[0][i] if pick[i] < 0.75 or i == 0 else pools[1 + (i & 1)][i] for i in range(300_000)]
+    lines = [lines[0]] + mutate(lines[1:], rng, 0.10)
+    data = b"".join(lines)
+    offs = np.cumsum([0] + [len(x) for x in lines[:-1]]).astype(np.uint32)
+    exp, est = oracle.run(oracle.AdMap(aids, camp), data, offs, threads=8)
+    raw = np.frombuffer(data, dtype=np.uint8)
+    with YsbContext(n_campaigns=600_000, window_ring=128, record_count=rec, timing=True,
+                    max_batch_bytes=raw.size + 64, max_batch_events=offs.size + 1) as ctx:
+        ctx.load_ad_map(aids, camp)
+        d_b, d_o = ctx.device_alloc(raw.size + 64), ctx.device_alloc(4 * offs.size + 64)
+        ctx.h2d(d_b, raw)
+        ctx.h2d(d_o, offs)
+        ctx.submit_device(d_b, raw.size, d_o, offs.size)
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+        ctx.kernel_time()
+        info = ctx.launch_info()
+        assert info["hbm_table"] == 1 and info["layout"] == want and info["record_mode"] == int(rec)
+        assert (ctx.path_time()[2] == 1) == rec
+    assert est["parse_errors"] > 1000 and est["views"] > 50_000
+    for k in STAT_KEYS:
+        assert st[k] == est[k], (k, st[k], est[k])
+    assert got == exp
