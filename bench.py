@@ -68,9 +68,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-check", action="store_true", help="skip the generator-truth check")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[2] / .tbl extra measurements")
     ap.add_argument("--extra-steps", type=int, default=20)
-    ap.add_argument("--stream-seconds", type=int, default=125,
-                    help="extras: seconds of real-time sharded streaming (configs[4]; 125 s closes >= 10 windows); "
+    ap.add_argument("--stream-seconds", type=int, default=70,
+                    help="extras: seconds of real-time sharded streaming (configs[4]; 70 s closes >= 5 windows); "
                          "0 skips it")
+    ap.add_argument("--stream-rate", type=int, default=20_000_000,
+                    help="extras: aggregate events/s of the real-time producers (configs[4] under load)")
     ap.add_argument("--dropin-events", type=int, default=100_000_000,
                     help="extras: events through the host-staged (pinned slots, H2D) path")
     ap.add_argument("--runner-file-events", type=int, default=20_000_000,
@@ -483,9 +485,11 @@ def extra_layouts(args, device, out):
 
 
 def extra_stream(args):
-    # configs[4]: real-time producers into double-buffered pinned slots, one context per
+    # configs[4] under load: real-time producers (16 host threads each call) writing
+    # args.stream_rate events/s in all into double-buffered pinned slots, one context per
     # visible GPU (2..8 shards: configs[4]'s 8 GPUs on an 8-GPU node; on a one-GPU box two
-    # contexts share it), one global watermark, p50 / p99 close latency
+    # contexts share it), one global watermark: sustained rate, back-pressure, p50 / p99 close
+    # latency, exact vs the generator truth
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_extra
     try:
@@ -493,8 +497,8 @@ def extra_stream(args):
         visible = torch.cuda.device_count()
     except Exception:   # noqa: BLE001
         visible = 1
-    ns = argparse.Namespace(shards=min(8, max(2, visible)), rate=1_000_000, seconds=args.stream_seconds,
-                            batch_ms=20, ooo_ms=100)
+    ns = argparse.Namespace(shards=min(8, max(2, visible)), rate=args.stream_rate, seconds=args.stream_seconds,
+                            batch_ms=20, ooo_ms=100, threads=16)
     r = bench_extra.stream_sharded(ns)
     log("extras: stream %s" % json.dumps(r["window_close_latency"]))
     return r

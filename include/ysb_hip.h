@@ -488,6 +488,10 @@ int         ysb_gen_ids(const ysb_gen_params* p, char* campaign_ids, char* ad_id
 int         ysb_gen_events_host(const ysb_gen_params* p, uint64_t first, uint64_t n,
                                 uint8_t* out, uint64_t cap, uint32_t* line_off,
                                 uint64_t* nbytes);
+/* The same with `threads` host threads (lengths, their prefix, then the lines in place): a
+ * real-time producer fast enough to load the streaming path (configs[4] under load). */
+int         ysb_gen_events_host_mt(const ysb_gen_params* p, uint64_t first, uint64_t n, uint8_t* out,
+                                   uint64_t cap, uint32_t* line_off, uint64_t* nbytes, uint32_t threads);
 /* Same on the device (d_out / d_line_off are HBM); synchronous. */
 int         ysb_gen_events_device(ysb_ctx* ctx, const ysb_gen_params* p, uint64_t first,
                                   uint64_t n, uint8_t* d_out, uint64_t cap,

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -2264,6 +2265,49 @@ int ysb_gen_events_host(const ysb_gen_params* p, uint64_t first, uint64_t n, uin
         o += len;
     }
     *nbytes = o;
+    return YSB_OK;
+}
+
+int ysb_gen_events_host_mt(const ysb_gen_params* p, uint64_t first, uint64_t n, uint8_t* out, uint64_t cap,
+                           uint32_t* line_off, uint64_t* nbytes, uint32_t threads) {
+    if (!gen_ok(p) || (n && (!out || !line_off)) || !nbytes) return fail(nullptr, YSB_ERR_ARG, "bad generator arguments");
+    const u32 T = (u32)std::max<u64>(1, std::min<u64>({(u64)std::max(threads, 1u), (u64)64, n / 4096 + 1}));
+    if (T == 1) return ysb_gen_events_host(p, first, n, out, cap, line_off, nbytes);
+    const GenSpec s = spec_of(p, p->ad_subset);
+    // lengths (line_off as scratch) and per-thread sums, the bases, then the lines in place
+    std::vector<u64> sum(T + 1, 0);
+    auto span = [&](u32 t, u64* a, u64* b) { *a = n * t / T; *b = n * (t + 1) / T; };
+    std::vector<std::thread> th;
+    for (u32 t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            u64 a, b, acc = 0;
+            span(t, &a, &b);
+            for (u64 i = a; i < b; ++i) {
+                const u32 l = gen_line_len(s, first + i, gen_event(s, first + i));
+                line_off[i] = l;
+                acc += l;
+            }
+            sum[t + 1] = acc;
+        });
+    for (auto& x : th) x.join();
+    th.clear();
+    for (u32 t = 0; t < T; ++t) sum[t + 1] += sum[t];
+    if (sum[T] > cap) return fail(nullptr, YSB_ERR_CAPACITY, "generator output exceeds %llu bytes", (unsigned long long)cap);
+    if (sum[T] > 0xFFFFFFFFull + 1) return fail(nullptr, YSB_ERR_CAPACITY, "batch exceeds 4 GiB (u32 offsets)");
+    for (u32 t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            u64 a, b, o = sum[t];
+            span(t, &a, &b);
+            char line[320];
+            for (u64 i = a; i < b; ++i) {
+                const u32 len = gen_line_write(s, first + i, gen_event(s, first + i), line);
+                line_off[i] = (u32)o;
+                std::memcpy(out + o, line, len);
+                o += len;
+            }
+        });
+    for (auto& x : th) x.join();
+    *nbytes = sum[T];
     return YSB_OK;
 }
 

@@ -145,6 +145,7 @@ SIGNATURES = {
     "ysb_gen_default": (None, [C.POINTER(YsbGenParams)]),
     "ysb_gen_ids": (_I, [C.POINTER(YsbGenParams), _P, _P]),
     "ysb_gen_events_host": (_I, [C.POINTER(YsbGenParams), _U64, _U64, _PU8, _U64, _PU32, C.POINTER(_U64)]),
+    "ysb_gen_events_host_mt": (_I, [C.POINTER(YsbGenParams), _U64, _U64, _PU8, _U64, _PU32, C.POINTER(_U64), _U32]),
     "ysb_gen_events_device": (_I, [_P, C.POINTER(YsbGenParams), _U64, _U64, _PU8, _U64, _PU32, C.POINTER(_U64)]),
     "ysb_gen_max_line_bytes": (_U64, [C.POINTER(YsbGenParams)]),
     "ysb_truth_accumulate": (_I, [_P, C.POINTER(YsbGenParams), _U64, _U64]),

@@ -87,6 +87,15 @@ class GenParams:
                                         C.c_void_p(off.ctypes.data), C.byref(nb)))
         return out[:nb.value], off[:n]
 
+    def write_host(self, first, n, out, off, threads=1):
+        """Events [first, first+n) written straight into out (a uint8 array or view, e.g. a
+        pinned slot) with their offsets in off (uint32); threads > 1: ysb_gen_events_host_mt.
+        Returns the bytes written."""
+        nb = C.c_uint64()
+        check(lib().ysb_gen_events_host_mt(C.byref(self.c), first, n, C.c_void_p(out.ctypes.data), out.size,
+                                           C.c_void_p(off.ctypes.data), C.byref(nb), max(1, int(threads))))
+        return nb.value
+
     def dump(self, n_events, directory):
         check(lib().ysb_gen_dump(C.byref(self.c), n_events, str(directory).encode()))
 

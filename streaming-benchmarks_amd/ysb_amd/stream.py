@@ -169,6 +169,11 @@ class StreamingOperator:
         self.batches = 0
         self.flushes = 0
         self.open_at_end = 0
+        # back-pressure: submits forced by a full slot (before the batch interval), and the
+        # time spent waiting for the other slot's H2D before it could be refilled
+        self.full_submits = 0
+        self.wait_ms = 0.0
+        self.wait_max_ms = 0.0
 
     # the book's fields, as attributes of the operator (reports, tests)
     seen_buckets = property(lambda self: self.book.seen_buckets)
@@ -229,6 +234,17 @@ class StreamingOperator:
     def due(self):
         return self.fill_events > 0 and self.clock() - self.batch_open_ms >= self.batch_interval_ms
 
+    def full(self, line_bytes):
+        """The open slot cannot take another line of line_bytes (or another event)."""
+        fb, fe = self.free_space()
+        return fe == 0 or fb < line_bytes
+
+    def submit_full(self):
+        """Submits a slot that filled up before its batch interval (counted as back-pressure)."""
+        if self.fill_events:
+            self.full_submits += 1
+            self.submit()
+
     # -- submission / watermark --------------------------------------------------------
     def submit(self):
         if self.fill_events == 0:
@@ -239,7 +255,11 @@ class StreamingOperator:
         self.events += self.fill_events
         self.batches += 1
         self.slot ^= 1
+        t0 = time.perf_counter()
         self.s.wait(self.slot)          # the other slot's H2D is done: it may be refilled
+        w = (time.perf_counter() - t0) * 1e3
+        self.wait_ms += w
+        self.wait_max_ms = max(self.wait_max_ms, w)
         self.fill_bytes = self.fill_events = 0
         if t is not None:
             self.max_time = t if self.max_time is None else max(self.max_time, t)
@@ -322,6 +342,9 @@ class ShardedStreamingOperator:
     totals = property(lambda self: self.book.totals)
     events = property(lambda self: sum(s.events for s in self.shards))
     batches = property(lambda self: sum(s.batches for s in self.shards))
+    full_submits = property(lambda self: sum(s.full_submits for s in self.shards))
+    wait_ms = property(lambda self: sum(s.wait_ms for s in self.shards))
+    wait_max_ms = property(lambda self: max(s.wait_max_ms for s in self.shards))
 
     # -- input ---------------------------------------------------------------------------
     def append(self, raw, offs):

@@ -218,3 +218,18 @@ def test_layout_sampling_decisions():
                 g.replace(b'"1.2.3.4"', b'1234'),                    # a non-string value
                 b"", b"not json"):
         assert layout_of_line(bad)[0] == 2, bad
+
+
+def test_threaded_host_generator_is_byte_identical():
+    """ysb_gen_events_host_mt (the loaded streaming leg's producer) writes the same bytes and
+    offsets as the single-threaded generator, for every variant and with skew."""
+    import numpy as np
+    from ysb_amd import GEN_COMPACT, GEN_REORDER, GenParams
+    for variant in (0, GEN_COMPACT, GEN_REORDER):
+        g = GenParams(seed=13, events_per_sec=20_000_000, with_skew=True, n_users=100, variant=variant)
+        raw, offs = g.events_host(1000, 50_000)
+        out = np.zeros(50_000 * g.max_line_bytes(), dtype=np.uint8)
+        off = np.zeros(50_000, dtype=np.uint32)
+        for threads in (1, 3, 16):
+            nb = g.write_host(1000, 50_000, out, off, threads)
+            assert nb == raw.size and np.array_equal(out[:nb], raw) and np.array_equal(off, offs), (variant, threads)

@@ -365,18 +365,18 @@ def stream(args):
 def stream_sharded(args):
     """configs[4] with N shards: N contexts (one per GPU, round robin over the visible
     devices; on a one-GPU box N contexts share it), each fed in real time by its ad_id
-    shard's producer (rate / N events per second each), one global watermark."""
+    shard's producer (rate / N events per second each), one global watermark.  Producers
+    write straight into the pinned slots with --threads host threads each
+    (ysb_gen_events_host_mt); a slot that fills before its tick is submitted at once
+    (full_submits, back-pressure), and the time spent waiting for a slot's H2D is reported."""
     from ysb_amd import shard_ads
     from ysb_amd.stream import ShardedStreamingOperator, SlotContext
-    import ctypes as C
-    from ysb_amd._lib import lib as _l
     n = args.shards
-    ndev = C.c_int(0)
     try:
         import torch
-        ndev.value = max(1, torch.cuda.device_count())
-    except Exception:
-        ndev.value = 1
+        ndev = max(1, torch.cuda.device_count())
+    except Exception:   # noqa: BLE001
+        ndev = 1
     rate = args.rate
     t0_ms = (int(time.time() * 1000) // 10000 + 1) * 10000 - 2000
     base = GenParams(seed=7, n_campaigns=100, ads_per_campaign=10, events_per_sec=rate)
@@ -384,9 +384,10 @@ def stream_sharded(args):
     subsets = shard_ads(aids, n)
     gens = [GenParams(seed=7, event_stream=1 + r, n_campaigns=100, ads_per_campaign=10, events_per_sec=rate // n,
                       ad_subset=subsets[r], with_skew=True, n_users=100, t0_ms=t0_ms) for r in range(n)]
+    line = gens[0].max_line_bytes()
     per_batch = max(1, rate // n * args.batch_ms // 1000)
-    cap_b = per_batch * gens[0].max_line_bytes() * 2
-    ctxs = [YsbContext(device=r % ndev.value, n_campaigns=100, window_ring=16, max_batch_bytes=cap_b,
+    cap_b = per_batch * line * 2
+    ctxs = [YsbContext(device=r % ndev, n_campaigns=100, window_ring=16, max_batch_bytes=cap_b,
                        max_batch_events=per_batch * 2) for r in range(n)]
     for c in ctxs:
         c.load_ad_map(aids, base.ad_campaign_index())
@@ -397,34 +398,39 @@ def stream_sharded(args):
                                   flush_every=max(1, 1000 // args.batch_ms), max_out_of_orderness_ms=args.ooo_ms)
     n_total = rate // n * args.seconds
     produced = [0] * n
+    threads = max(1, args.threads)
+    behind_max = 0.0
 
     def producer(r):
         def fill(bv, ov, cap_bb, cap_e):
             due = int((clock() - t0_ms) * (rate // n) / 1000)
-            m = min(cap_e, cap_bb // gens[r].max_line_bytes(), max(0, min(due, n_total) - produced[r]))
+            m = min(cap_e, cap_bb // line, max(0, min(due, n_total) - produced[r]))
             if m <= 0:
                 return 0, 0
-            raw, offs = gens[r].events_host(produced[r], m)
-            bv[:raw.size] = raw
-            ov[:m] = offs
+            nb = gens[r].write_host(produced[r], m, bv[:cap_bb], ov[:m], threads)
             produced[r] += m
-            return raw.size, m
+            return nb, m
         return fill
     last_tick = clock()
     last_log = time.time()
+    t_start = time.perf_counter()
     while min(produced) < n_total:
         for r in range(n):
             op.fill_with(r, producer(r))
+            if op.shards[r].full(line):
+                op.shards[r].submit_full()
+        behind_max = max(behind_max, clock() - (t0_ms + min(produced) * 1000.0 / (rate // n)))
         if clock() - last_tick >= args.batch_ms:
             op.tick()
             last_tick = clock()
-        else:
+        elif rate < 5_000_000:
             time.sleep(0.001)
         if time.time() - last_log >= 30:   # progress (a long run stays visibly alive)
             last_log = time.time()
             log("stream_sharded: %.0f s, %d events, %d flushes" % (last_log - wall0 / 1000.0, sum(produced),
                                                                     op.flushes))
     op.close()
+    el = time.perf_counter() - t_start
     # the reference counts: the generator truth of every event each producer made, straight
     # from the RNG (ysb_truth_accumulate: no bytes, no parsing -- independent of the path
     # under test), in a ring wide enough for the late events (<= 60 s, core.clj:166-174)
@@ -432,7 +438,8 @@ def stream_sharded(args):
     ref, outside = {}, 0
     for r in range(n):
         with YsbContext(n_campaigns=100, window_ring=64, ring_base_bucket=t0_ms // 10000 - 8) as c2:
-            c2.truth_accumulate(gens[r], 0, produced[r])
+            for f in range(0, produced[r], 100_000_000):
+                c2.truth_accumulate(gens[r], f, min(100_000_000, produced[r] - f))
             truth, lo = c2.truth_read()
             _, ttotal, _ = c2.truth_compare()
             outside += ttotal - int(truth.sum())
@@ -442,10 +449,14 @@ def stream_sharded(args):
         c.close()
     lat = op.latency_summary()
     return {"config": "configs[4] with %d shards (%d GPU(s) visible): real-time producers, %d events/s in all, "
-                      "skew +-50 ms, late p=1e-5 (core.clj:166-174); %d ms ticks, one global watermark; %d s"
-                      % (n, ndev.value, rate, args.batch_ms, args.seconds),
-            "shards": n, "devices": ndev.value, "events": op.events, "batches": op.batches, "flushes": op.flushes,
-            "window_close_latency": lat, "open_at_end": op.open_at_end,
+                      "skew +-50 ms, late p=1e-5 (core.clj:166-174); %d ms ticks, one global watermark; %d s; "
+                      "producers: ysb_gen_events_host_mt with %d threads each, straight into the pinned slots"
+                      % (n, ndev, rate, args.batch_ms, args.seconds, threads),
+            "shards": n, "devices": ndev, "target_events_per_s": rate,
+            "sustained_events_per_s": round(op.events / el, 1), "events": op.events, "batches": op.batches,
+            "flushes": op.flushes, "window_close_latency": lat, "open_at_end": op.open_at_end,
+            "producer_max_behind_ms": round(behind_max, 1), "slot_full_submits": op.full_submits,
+            "slot_wait_ms_total": round(op.wait_ms, 1), "slot_wait_max_ms": round(op.wait_max_ms, 2),
             "exact_vs_generator_truth": op.totals == ref and outside == 0, "rows": len(ref),
             "truth_outside_ring": outside}
 
@@ -469,6 +480,7 @@ def main():
     ap.add_argument("--shape", default="reorder", choices=["generator", "compact", "reorder", "spaced", "extra", "escaped"],
                     help="general: how the generator's lines are re-laid")
     ap.add_argument("--shards", type=int, default=2, help="stream_sharded: contexts (one per GPU)")
+    ap.add_argument("--threads", type=int, default=16, help="stream_sharded: host threads per producer call")
     ap.add_argument("--hint", default="none", choices=["none", "compact", "flat", "auto"],
                     help="general: layout hint (YSB_F_COMPACT_FIRST / YSB_F_FLAT_FIRST / YSB_F_LAYOUT_AUTO, host batches)")
     args = ap.parse_args()
