@@ -91,6 +91,8 @@ struct ysb_ctx {
     u32 c_pad = 0;                        // campaigns padded to the group size
     unsigned long long* d_counts = nullptr;   // [c_pad][W]
     unsigned long long* d_owned = nullptr;    // [c_pad / nranks][W] after reduce-scatter
+    u8* d_owned8 = nullptr;                   // ... its saturating u8 accumulator (xunpack), folded before reads
+    bool owned8_dirty = false;
     unsigned long long* d_rs_tmp = nullptr;
     bool ring_agreed = false;                 // ranks' ring bases checked equal
     TableRow* d_rows = nullptr;               // drain compaction output
@@ -267,6 +269,7 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_ctable);
     hipFree(c->d_counts);
     hipFree(c->d_owned);
+    hipFree(c->d_owned8);
     hipFree(c->d_rs_tmp);
     hipFree(c->d_rows);
     hipFree(c->d_rows_n);
@@ -756,6 +759,15 @@ static int grow_u32(ysb_ctx* c, u32** buf, u64* have, u64 words) {
     *have = 0;
     HIPCHK(c, hipMalloc(buf, words * 4));
     *have = words;
+    return YSB_OK;
+}
+
+// The owned table's u8 accumulator into it (queued on the compute stream), cleared.
+static int fold_owned(ysb_ctx* c) {
+    if (!c->d_owned8 || !c->owned8_dirty) return YSB_OK;
+    launch_fold(c->d_owned, c->d_owned8, (u64)c->c_pad / (u64)c->nranks * c->cfg.window_ring, c->s_comp);
+    HIPCHK(c, hipGetLastError());
+    c->owned8_dirty = false;
     return YSB_OK;
 }
 
@@ -1465,6 +1477,7 @@ static int ring_rows(ysb_ctx* c, i64 blo, i64 bhi, bool clear, std::map<std::pai
     const i64 a = std::max<i64>(blo, lo), b = std::min<i64>(bhi, lo + (i64)W);
     if (a >= b) return YSB_OK;
     const u32 nb = (u32)(b - a);
+    if ((frc = fold_owned(c))) return frc;
     struct Tab { unsigned long long* t; u32 rows, off; };
     std::vector<Tab> tabs{{c->d_counts, c->cfg.n_campaigns, 0u}};
     if (c->d_owned) {
@@ -1606,6 +1619,8 @@ int ysb_reset(ysb_ctx* c) {
     c->pend_u64 = false;
     c->x_have_plan = false;
     if (c->d_owned) HIPCHK(c, hipMemset(c->d_owned, 0, cells / c->nranks * 8));
+    if (c->d_owned8) HIPCHK(c, hipMemset(c->d_owned8, 0, cells / c->nranks));
+    c->owned8_dirty = false;
     if (c->d_truth) HIPCHK(c, hipMemset(c->d_truth, 0, cells * 8));
     if (c->d_truth_out) HIPCHK(c, hipMemset(c->d_truth_out, 0, 8));
     HIPCHK(c, hipMemset(c->d_ovf_count, 0, 16));
@@ -1836,6 +1851,9 @@ static void ungroup(ysb_ctx* c) {
     c->hops = ysb_collectives{};
     hipFree(c->d_owned);
     c->d_owned = nullptr;
+    hipFree(c->d_owned8);
+    c->d_owned8 = nullptr;
+    c->owned8_dirty = false;
     hipFree(c->d_xmax);
     c->d_xmax = nullptr;
     hipHostFree(c->h_xmax);
@@ -1893,6 +1911,8 @@ static int group_setup(ysb_ctx* c, int rank, int nranks) {
     const u64 per = (u64)c->c_pad / nranks * c->cfg.window_ring;
     HIPCHK(c, hipMalloc(&c->d_owned, per * 8));
     HIPCHK(c, hipMemset(c->d_owned, 0, per * 8));
+    HIPCHK(c, hipMalloc(&c->d_owned8, per));
+    HIPCHK(c, hipMemset(c->d_owned8, 0, per));
     const u32 W = c->cfg.window_ring;
     HIPCHK(c, hipMalloc(&c->d_xmax, 2 * (u64)W * 8));
     HIPCHK(c, hipHostMalloc(&c->h_xmax, 2 * ((u64)W * 8 + (u64)W * 4)));   // maxima, then the plans' slots
@@ -1968,9 +1988,10 @@ static int finish_unpack(ysb_ctx* c) {
     const auto& ev = c->xev[c->unpack_entry];
     HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_xdone[k], 0));
     HIPCHK(c, hipEventRecord(ev[3], c->s_comp));
-    launch_xunpack(c->d_owned, W, per, c->d_xslots + (u64)k * W, c->unpack_R, c->d_xrecv[k], c->unpack_width,
-                   c->s_comp);
+    launch_xunpack(c->d_owned, c->d_owned8, W, per, c->d_xslots + (u64)k * W, c->unpack_R, c->d_xrecv[k],
+                   c->unpack_width, c->s_comp);
     HIPCHK(c, hipGetLastError());
+    c->owned8_dirty = true;
     HIPCHK(c, hipEventRecord(ev[4], c->s_comp));
     return YSB_OK;
 }
@@ -2155,6 +2176,7 @@ int ysb_group_checksum(ysb_ctx* c, int what, uint32_t nranks, uint64_t* out) {
         u32 lo = 0, hi = 0;
         ysb_group_block(C, c->rank, c->nranks, &lo, &hi);
         const u32 per = c->c_pad / (u32)c->nranks;   // row i of the owned table: campaign rank * per + i
+        if ((rc = fold_owned(c))) return rc;
         return sum(c->d_owned, per, (u32)c->rank * per, lo, hi, &out[0]);
     }
     return fail(c, YSB_ERR_ARG, "unknown checksum %d", what);

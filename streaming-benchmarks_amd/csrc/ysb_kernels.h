@@ -214,13 +214,13 @@ void launch_fold(unsigned long long* counts, u8* delta, u64 cells, hipStream_t s
 // xplan: slot_max[s] = max over campaigns of the pending count in ring slot s (atomicMax:
 // zero slot_max first).  xpack: the pending cells of slots[0..R) as a dense [rows][R] array
 // of `width`-byte cells (1, 4 or 8), the sources zeroed.  xunpack: owned[c][slots[k]] +=
-// in[c][k] for the owner block's rows.
+// in[c][k] for the owner block's rows (through the saturating u8 accumulator owned8).
 void launch_xplan(const unsigned long long* counts, const u8* delta, u32 W, u64 cells, int force_u64,
                   const u32* dirty, unsigned long long* slot_max, hipStream_t s);
 void launch_xpack(unsigned long long* counts, u8* delta, u32 W, u32 rows, const u32* slots, u32 R, int force_u64,
                   const u32* dirty, void* out, u32 width, unsigned long long cap, hipStream_t s);
-void launch_xunpack(unsigned long long* owned, u32 W, u32 rows, const u32* slots, u32 R, const void* in, u32 width,
-                    hipStream_t s);
+void launch_xunpack(unsigned long long* owned, u8* owned8, u32 W, u32 rows, const u32* slots, u32 R, const void* in,
+                    u32 width, hipStream_t s);
 // Linear checksum of a campaign-major [rows][W] u64 table (row i = campaign c_off + i) over
 // the campaigns [c_lo, c_hi): *out += SUM count * cell_weight(campaign, bucket) (mod 2^64).
 void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_lo, u32 c_off, u32 c_lo, u32 c_hi,

@@ -186,10 +186,14 @@ __global__ __launch_bounds__(AUX_TPB) void xpack_kernel(unsigned long long* coun
     }
 }
 
-// owned[c][slots[k]] += in[c][k].  No LDS, so its workgroups fit beside a running scan (it
-// runs on the exchange stream, under the next launch).
+// owned[c][slots[k]] += in[c][k], through a u8 accumulator of the owned table's layout
+// (saturating, as the record-mode delta ring: a cell whose byte would pass 255 adds the whole
+// sum to the u64 owned table and restarts at 0; launch_fold moves the bytes into it before the
+// owned table is read).  configs[2]'s ~0.3 views per cell and exchange then cost a byte of
+// read-modify-write per cell instead of 8 (the owned table's 1.6 GB per exchange at one rank).
+// The unpack is the owned table's only writer (one thread per cell: plain adds).
 template <class T>
-__global__ __launch_bounds__(AUX_TPB) void xunpack_kernel(unsigned long long* owned, u32 W, u32 rows,
+__global__ __launch_bounds__(AUX_TPB) void xunpack_kernel(unsigned long long* owned, u8* owned8, u32 W, u32 rows,
                                                           const u32* slots, u32 R, const void* in) {
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const T* src = static_cast<const T*>(in);
@@ -197,7 +201,15 @@ __global__ __launch_bounds__(AUX_TPB) void xunpack_kernel(unsigned long long* ow
         const u64 row = (u64)c * W, irow = (u64)c * R;
         for (u32 k = lane; k < R; k += 64) {
             const unsigned long long v = src[irow + k];
-            if (v) owned[row + slots[k]] += v;
+            if (!v) continue;
+            const u64 cell = row + slots[k];
+            const unsigned long long sum = owned8[cell] + v;
+            if (sum > 255u) {
+                owned[cell] += sum;
+                owned8[cell] = 0;
+            } else {
+                owned8[cell] = (u8)sum;
+            }
         }
     }
 }
@@ -243,13 +255,13 @@ void launch_xpack(unsigned long long* counts, u8* delta, u32 W, u32 rows, const 
     else hipLaunchKernelGGL(xpack_kernel<unsigned long long>, g, b, 0, s, counts, delta, W, rows, slots, R, force_u64, dirty, out, cap);
 }
 
-void launch_xunpack(unsigned long long* owned, u32 W, u32 rows, const u32* slots, u32 R, const void* in, u32 width,
-                    hipStream_t s) {
+void launch_xunpack(unsigned long long* owned, u8* owned8, u32 W, u32 rows, const u32* slots, u32 R, const void* in,
+                    u32 width, hipStream_t s) {
     if (!rows || !R) return;
     const dim3 g((unsigned)row_grid(rows)), b(AUX_TPB);
-    if (width == 1) hipLaunchKernelGGL(xunpack_kernel<u8>, g, b, 0, s, owned, W, rows, slots, R, in);
-    else if (width == 4) hipLaunchKernelGGL(xunpack_kernel<u32>, g, b, 0, s, owned, W, rows, slots, R, in);
-    else hipLaunchKernelGGL(xunpack_kernel<unsigned long long>, g, b, 0, s, owned, W, rows, slots, R, in);
+    if (width == 1) hipLaunchKernelGGL(xunpack_kernel<u8>, g, b, 0, s, owned, owned8, W, rows, slots, R, in);
+    else if (width == 4) hipLaunchKernelGGL(xunpack_kernel<u32>, g, b, 0, s, owned, owned8, W, rows, slots, R, in);
+    else hipLaunchKernelGGL(xunpack_kernel<unsigned long long>, g, b, 0, s, owned, owned8, W, rows, slots, R, in);
 }
 
 void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_lo, u32 c_off, u32 c_lo, u32 c_hi,
