@@ -480,6 +480,9 @@ typedef struct ysb_gen_params {
 #define YSB_GEN_MORE_AD_TYPES 2u
 #define YSB_GEN_COMPACT       4u
 #define YSB_GEN_REORDER       8u
+#define YSB_GEN_MIXED        16u  /* four producers interleaved line by line: each event's layout drawn
+                                     from {the generator's, compact, reordered keys, random ip with 8
+                                     ad_types}; the same events and truth */
 
 void        ysb_gen_default(ysb_gen_params* p);
 /* Campaign and ad UUIDs, 36 bytes each, no separators (ad a -> campaign a / ads_per_campaign). */

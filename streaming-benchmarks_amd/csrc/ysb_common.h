@@ -104,8 +104,18 @@ enum : u32 {
     GEN_V_MORE_AD_TYPES = 2u,  // ad_type one of 8 (adds native-video / interstitial / rewarded)
     GEN_V_COMPACT = 4u,        // no space after ':' and ',' (compact JSON)
     GEN_V_REORDER = 8u,        // the seven pairs in another (fixed) key order
+    GEN_V_MIXED = 16u,         // four producers interleaved line by line: each event's layout is
+                               // one of {generator, compact, reordered, random ip + 8 ad_types},
+                               // drawn per event (the mutation tests' interleave, unmutated)
 };
-enum : u32 { S_IP = 9 };
+enum : u32 { S_IP = 9, S_MIX = 10 };
+
+// The layout variant of event i (GEN_V_MIXED: drawn per event; else the spec's).
+YSB_HD u32 event_variant(const GenSpec& s, u64 i) {
+    if (!(s.variant & GEN_V_MIXED)) return s.variant;
+    const u32 k = (u32)(draw(stream_key(s.ev_seed, S_MIX), i) >> 62);
+    return k == 0 ? 0u : k == 1 ? (u32)GEN_V_COMPACT : k == 2 ? (u32)GEN_V_REORDER : (u32)(GEN_V_RANDOM_IP | GEN_V_MORE_AD_TYPES);
+}
 
 struct GenEvent {
     u32 ad, ad_type, event_type;
@@ -117,7 +127,7 @@ YSB_HD GenEvent gen_event(const GenSpec& s, u64 i) {
     u64 c = draw(stream_key(s.ev_seed, S_CHOICE), i);
     u32 idx = (u32)(((c >> 32) * (u64)s.n_pick) >> 32);   // rand-nth ads (core.clj:92)
     e.ad = s.subset ? s.subset[idx] : idx;
-    e.ad_type = (u32)(c & 0xFFFF) % ((s.variant & GEN_V_MORE_AD_TYPES) ? 8u : 5u);   // rand-nth ad-types (:93)
+    e.ad_type = (u32)(c & 0xFFFF) % ((event_variant(s, i) & GEN_V_MORE_AD_TYPES) ? 8u : 5u);   // rand-nth ad-types (:93)
     e.event_type = (u32)((c >> 16) & 0xFFFF) % 3u;         // rand-nth event-types (:94)
     i64 t = s.t0_ms + (i64)((i * 1000ULL) / s.events_per_sec);   // (+ start-time (* n 10)) (:95)
     if (s.with_skew) {                                      // make-kafka-event-at (:166-174)
@@ -156,8 +166,9 @@ YSB_HD u32 gen_line_len(const GenSpec& s, u64 i, const GenEvent& e) {
     const u32 var = ad_type_len(e.ad_type) + event_type_len(e.event_type) + dec_len(e.time_ms);
     if (s.tbl) return 3u * 36u + 5u + 1u + var;
     u32 n = (u32)LINE_FIXED + var;
-    if (s.variant & GEN_V_RANDOM_IP) n += ip_len(gen_ip(s, i)) - 7u;
-    if (s.variant & GEN_V_COMPACT) n -= 13u;   // 7 ": " and 6 ", " lose their space
+    const u32 v = event_variant(s, i);
+    if (v & GEN_V_RANDOM_IP) n += ip_len(gen_ip(s, i)) - 7u;
+    if (v & GEN_V_COMPACT) n -= 13u;   // 7 ": " and 6 ", " lose their space
     return n;
 }
 
@@ -170,14 +181,14 @@ YSB_HD char* put_str(char* o, const char* s, u32 n) {
 // in the generator's order or (GEN_V_REORDER) in the order ad_type, event_time, ad_id,
 // ip_address, user_id, event_type, page_id; the separators with or without their space;
 // the ip a random dotted quad.  Same pieces, so gen_line_len holds for every variant.
-YSB_HD u32 gen_line_write_variant(const GenSpec& s, u64 i, const GenEvent& e, char* out) {
-    const bool cp = (s.variant & GEN_V_COMPACT) != 0;
+YSB_HD u32 gen_line_write_variant(const GenSpec& s, u64 i, const GenEvent& e, char* out, u32 variant) {
+    const bool cp = (variant & GEN_V_COMPACT) != 0;
     const char* sep = cp ? "\",\"" : "\", \"";       // between a value and the next key
     const char* col = cp ? "\":\"" : "\": \"";       // between a key and its value
     const u32 ls = cp ? 3u : 4u;
     const u32 order_gen[7] = {0, 1, 2, 3, 4, 5, 6};
     const u32 order_re[7] = {3, 5, 2, 6, 0, 4, 1};
-    const u32* order = (s.variant & GEN_V_REORDER) ? order_re : order_gen;
+    const u32* order = (variant & GEN_V_REORDER) ? order_re : order_gen;
     char* o = out;
     u64 hi, lo;
     *o++ = '{';
@@ -223,7 +234,7 @@ YSB_HD u32 gen_line_write_variant(const GenSpec& s, u64 i, const GenEvent& e, ch
         default:
             o = put_str(o, "ip_address", 10);
             o = put_str(o, col, ls);
-            if (s.variant & GEN_V_RANDOM_IP) {
+            if (variant & GEN_V_RANDOM_IP) {
                 const u32 ip = gen_ip(s, i);
                 for (int q = 0; q < 4; ++q) {
                     if (q) *o++ = '.';
@@ -268,7 +279,8 @@ YSB_HD u32 gen_line_write(const GenSpec& s, u64 i, const GenEvent& e, char* out)
         *o++ = '\n';
         return (u32)(o - out);
     }
-    if (s.variant & (GEN_V_RANDOM_IP | GEN_V_COMPACT | GEN_V_REORDER)) return gen_line_write_variant(s, i, e, out);
+    const u32 v = event_variant(s, i);
+    if (v & (GEN_V_RANDOM_IP | GEN_V_COMPACT | GEN_V_REORDER)) return gen_line_write_variant(s, i, e, out, v);
     o = put_str(o, YSB_P0, LEN_P0);
     if (s.n_users == 0) uuid_words(stream_key(s.ev_seed, S_USER), i, &hi, &lo);
     else uuid_words(stream_key(s.ev_seed, S_USER), draw(stream_key(s.ev_seed, S_USERPOOL), i) % s.n_users, &hi, &lo);

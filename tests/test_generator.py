@@ -233,3 +233,24 @@ def test_threaded_host_generator_is_byte_identical():
         for threads in (1, 3, 16):
             nb = g.write_host(1000, 50_000, out, off, threads)
             assert nb == raw.size and np.array_equal(out[:nb], raw) and np.array_equal(off, offs), (variant, threads)
+
+
+def test_mixed_variant_interleaves_four_producers_per_event():
+    """GEN_MIXED: line i is exactly line i of one of the four producers' generators (the
+    generator's layout, compact, reordered keys, random ip with 8 ad_types), each about a
+    quarter of the lines -- the same events, so the same truth."""
+    import numpy as np
+    from ysb_amd import GEN_COMPACT, GEN_MIXED, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER, GenParams
+
+    def lines(v):
+        raw, off = GenParams(seed=17, events_per_sec=1000, with_skew=True, variant=v).events_host(0, 4000)
+        b = raw.tobytes()
+        return [b[a:e] for a, e in zip(off, list(off[1:]) + [len(b)])]
+    mixed = lines(GEN_MIXED)
+    pools = [lines(v) for v in (0, GEN_COMPACT, GEN_REORDER, GEN_RANDOM_IP | GEN_MORE_AD_TYPES)]
+    hits = np.zeros(4, dtype=int)
+    for i, ln in enumerate(mixed):
+        m = [k for k in range(4) if pools[k][i] == ln]
+        assert len(m) == 1, (i, ln)
+        hits[m[0]] += 1
+    assert hits.min() > 800, hits
