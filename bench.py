@@ -446,7 +446,10 @@ def extra_layouts(args, device, out):
     from ysb_amd import GEN_COMPACT, GEN_MIXED, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER, GenParams, YsbContext
     for key, variant, cf, what in (("mixed_layouts", GEN_MIXED, False,
                                     "four producers interleaved line by line (the generator's layout, compact JSON, "
-                                    "reordered keys, random ip with 8 ad_types; a quarter each), no hint"),("random_ip", GEN_RANDOM_IP, False, "random dotted-quad ip_address"),
+                                    "reordered keys, random ip with 8 ad_types; a quarter each), no hint"),
+                                   ("mixed_layouts_flat_tier", GEN_MIXED, "flat_fixed",
+                                    "four producers interleaved line by line, YSB_F_FLAT_FIRST with YSB_F_LAYOUT_FIXED: "
+                                    "the flat-object tier parses every line"),("random_ip", GEN_RANDOM_IP, False, "random dotted-quad ip_address"),
                                    ("random_ip_8_ad_types", GEN_RANDOM_IP | GEN_MORE_AD_TYPES, False,
                                     "random dotted-quad ip_address and 8 ad_types"),
                                    ("compact_json", GEN_COMPACT, True,
