@@ -23,6 +23,8 @@
 // moves.  Any other line goes to a deferred list that defer_kernel parses with the
 // general org.json parser (ysb_orgjson.h).  scan_kernel<*, true> does the same for the
 // fork's pipe-delimited rows (tbl_stage1/2, deferred rows through process_tbl_line).
+#include <type_traits>
+
 #include "ysb_kernels.h"
 
 namespace ysb {
@@ -902,6 +904,9 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
 }
 
 // ---- the general path's flat tier --------------------------------------------------------
+#ifndef YSB_FLAT_LDS
+#define YSB_FLAT_LDS 1   // round 4: flat_parse_lds for the flat-first / learned-order instantiations
+#endif
 // A flat object of plain double-quoted string pairs whose keys are all DeserializeBolt's
 // -- in any order, with any whitespace nextClean skips, ',' or ';' between pairs and a
 // separator allowed before '}' -- is decided here with word-at-a-time string scans over
@@ -1029,6 +1034,132 @@ __device__ __forceinline__ bool flat_parse_fast(const S& src, int s, int e, u32 
     return (seen & need) == need;
 }
 
+// 36 value bytes (w[0..8]) are plain string bytes: no quote, backslash or byte < 0x20.
+// Fast test: every byte in [0x2D, 0x7F) and not a backslash (UUID text always is); else
+// the exact flags.
+__device__ __forceinline__ bool plain36(const u32 (&w)[10]) {
+    u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        lo &= w[k] + 0x53535353u;   // bit 7 set per byte iff byte >= 0x2D (bytes < 0x80: no carries)
+        hi |= w[k];
+        bs |= zero_bytes(w[k] ^ 0x5C5C5C5Cu);
+    }
+    if (((lo & 0x80808080u) == 0x80808080u) & ((hi & 0x80808080u) == 0u) & (bs == 0u)) return true;
+    u32 f = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f |= ft_flags(w[k]);
+    return f == 0u;
+}
+
+// Round 4: the flat-first / learned-order instantiations' flat tier on the staged LDS line
+// (flat_parse_fast's subset and decisions), with the common forms taken branch-free:
+//   * the key named from the four realigned words at its text (load_span: five aligned
+//     reads) by compares and selects -- no if-chain, so lanes whose lines carry different
+//     keys at the same pair (several producers interleaved) do not serialise on it;
+//   * the key's closing quote and `": "` / `":"` read from the same words;
+//   * an id value (ad / user / page) as one 10-word span: 36 plain bytes by plain36's
+//     cheap test, its closing quote and the separator after it (`", "` / `","` / `"}`);
+//   * any other value by ft_string_end and one word for its separator.
+// Every other form (other whitespace, ';', a key that is not DeserializeBolt's, an id that
+// is not 36 plain bytes) takes the same per-byte steps as flat_parse_fast: a divergent slow
+// branch that the common lines never enter.
+__device__ __forceinline__ bool flat_parse_lds(const LdsSrc& src, int s, int e, u32 require, Span& ad, Span& et,
+                                               Span& tm, u32 (&adw)[9]) {
+    u32 c = 0;
+    int kq;                                           // the next key's opening quote
+    if ((src.load4(s) & 0xFFFFu) == w4('{', '"', 0, 0) && s + 1 < e) {
+        kq = s + 1;
+    } else {
+        int p = ft_clean<LdsSrc, true>(src, s, e, c);
+        if (p < 0 || c != '{') return false;
+        p = ft_clean<LdsSrc, true>(src, p + 1, e, c);
+        if (p < 0) return false;
+        if (c == '}') return (require | K_AD | K_ETYPE | K_ETIME) == 0u;   // {} (never: the chain's keys are required)
+        if (c != '"') return false;
+        kq = p;
+    }
+    u32 seen = 0;
+    bool closed = false;
+#pragma unroll 1
+    for (int k = 0; k < 9 && !closed; ++k) {          // at most 7 keys + one extra field: 8 pairs
+        u32 kw[4];
+        load_span(src, kq + 1, kw);
+        const bool isAD = kw[0] == w4('a', 'd', '_', 'i') && (kw[1] & 0xFFFFu) == w4('d', '"', 0, 0);
+        const bool is7 = (kw[1] == w4('_', 'i', 'd', '"') && (kw[0] == w4('u', 's', 'e', 'r') || kw[0] == w4('p', 'a', 'g', 'e'))) ||
+                         (kw[0] == w4('a', 'd', '_', 't') && kw[1] == w4('y', 'p', 'e', '"'));
+        const bool ev = kw[0] == w4('e', 'v', 'e', 'n');
+        const u32 k2 = kw[2] & 0xFFFFFFu;
+        const bool isET = ev && kw[1] == w4('t', '_', 't', 'y') && k2 == (w4('p', 'e', '"', 0) & 0xFFFFFFu);
+        const bool isTM = ev && kw[1] == w4('t', '_', 't', 'i') && k2 == (w4('m', 'e', '"', 0) & 0xFFFFFFu);
+        const bool isIP = kw[0] == w4('i', 'p', '_', 'a') && kw[1] == w4('d', 'd', 'r', 'e') && k2 == (w4('s', 's', '"', 0) & 0xFFFFFFu);
+        u32 id = isAD ? K_AD : isET ? K_ETYPE : isTM ? K_ETIME : isIP ? K_IP : 0u;
+        if (is7) id = kw[0] == w4('u', 's', 'e', 'r') ? K_USER : kw[0] == w4('p', 'a', 'g', 'e') ? K_PAGE : K_ADTYPE;
+        // the key's closing quote at kq + 1 + kl; the 4 bytes after it
+        const u32 x = isAD ? __builtin_amdgcn_alignbyte(kw[2], kw[1], 2) : is7 ? kw[2] : __builtin_amdgcn_alignbyte(kw[3], kw[2], 3);
+        const int ke = kq + 1 + (isAD ? 5 : is7 ? 7 : 10);
+        int vq;                                       // the value's opening quote
+        if (id != 0u && (x & 0xFFFFFFu) == (w4(':', ' ', '"', 0) & 0xFFFFFFu) && ke + 3 < e) {
+            vq = ke + 3;
+        } else if (id != 0u && (x & 0xFFFFu) == (w4(':', '"', 0, 0) & 0xFFFFu) && ke + 2 < e) {
+            vq = ke + 2;
+        } else {                                      // slow: another key, other whitespace
+            int kend = ke;
+            if (id == 0u) {   // a producer's extra field: at most one, a plain string key
+                kend = ft_string_end(src, kq + 1, e);
+                if (kend < 0 || (seen & K_OTHER) != 0u) return false;
+                id = K_OTHER;
+            }
+            int p = ft_clean<LdsSrc, true>(src, kend + 1, e, c);
+            if (p < 0 || c != ':') return false;
+            p = ft_clean<LdsSrc, true>(src, p + 1, e, c);
+            if (p < 0 || c != '"') return false;
+            vq = p;
+        }
+        if ((seen & id) != 0u) return false;          // a repeated key: putOnce throws
+        seen |= id;
+        int ve = -1;
+        u32 y = 0;                                    // the closing quote and the 3 bytes after it
+        if (id & (K_AD | K_USER | K_PAGE)) {
+            u32 w[10];
+            load_span(src, vq + 1, w);
+            if (plain36(w) && vq + 37 < e && (w[9] & 0xFFu) == '"') {
+                ve = vq + 37;
+                y = w[9];
+                if (id == K_AD) {
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) adw[j] = w[j];
+                }
+            }
+        }
+        if (ve < 0) {
+            ve = ft_string_end(src, vq + 1, e);
+            if (ve < 0) return false;
+            y = src.load4(ve);
+        }
+        const Span sp{vq + 1, ve, 0};
+        if (id == K_AD) ad = sp;
+        else if (id == K_ETYPE) et = sp;
+        else if (id == K_ETIME) tm = sp;
+        // ', "' / ',"' and the next key, or '}'
+        if (y == w4('"', ',', ' ', '"') && ve + 3 < e) { kq = ve + 3; continue; }
+        if ((y & 0xFFFFFFu) == (w4('"', ',', '"', 0) & 0xFFFFFFu) && ve + 2 < e) { kq = ve + 2; continue; }
+        if ((y & 0xFFFFu) == w4('"', '}', 0, 0) && ve + 1 < e) { closed = true; continue; }
+        int p = ft_clean<LdsSrc, true>(src, ve + 1, e, c);
+        if (p < 0) return false;
+        if (c == '}') { closed = true; continue; }
+        if (c != ',' && c != ';') return false;
+        p = ft_clean<LdsSrc, true>(src, p + 1, e, c);  // the next key, or '}' after a separator
+        if (p < 0) return false;
+        if (c == '}') { closed = true; continue; }
+        if (c != '"') return false;
+        kq = p;
+    }
+    // (a ninth pair is a repeat: putOnce would throw -- not closed, not taken)
+    const u32 need = require | K_AD | K_ETYPE | K_ETIME;
+    return closed && (seen & need) == need;
+}
+
 // FAST (the flat-first instantiation only): the whitespace skips' first step outside their
 // loops, and the id values (ad / user / page) checked as 36-byte UUIDs in one step before
 // the string scan -- the same decisions, fewer divergent loop trips.
@@ -1083,11 +1214,25 @@ template <class S, bool FAST = false>
 __device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 require, CanonA& a, CanonB& b) {
     Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
     bool okp;
-    if constexpr (FAST) okp = flat_parse_fast(src, ls, le, require, ad, et, tm);
-    else okp = flat_parse<S, FAST>(src, ls, le, require, ad, et, tm);
-    if (!okp || ad.e - ad.s != 36) return false;
+#if YSB_FLAT_LDS
+    if constexpr (FAST && std::is_same<S, LdsSrc>::value) {
+        u32 adw[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) a.kw[k] = src.load4(ad.s + 4 * k);
+        for (int k = 0; k < 9; ++k) adw[k] = 0u;
+        okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
+        if (!okp || ad.e - ad.s != 36) return false;
+        const bool fast_ad = adw[0] | adw[1] | adw[8];   // the id fast path kept the ad_id's words
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a.kw[k] = fast_ad ? adw[k] : src.load4(ad.s + 4 * k);
+    } else
+#endif
+    {
+        if constexpr (FAST) okp = flat_parse_fast(src, ls, le, require, ad, et, tm);
+        else okp = flat_parse<S, FAST>(src, ls, le, require, ad, et, tm);
+        if (!okp || ad.e - ad.s != 36) return false;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a.kw[k] = src.load4(ad.s + 4 * k);
+    }
     a.t0 = tm.s - ls;
     b.tlen = tm.e - tm.s;
 #pragma unroll
@@ -1132,24 +1277,6 @@ struct KeyLit {
         return make_words<4>(buf, 0, n);
     }
 };
-
-// 36 value bytes (w[0..8]) are plain string bytes: no quote, backslash or byte < 0x20.
-// Fast test: every byte in [0x2D, 0x7F) and not a backslash (UUID text always is); else
-// the exact flags.
-__device__ __forceinline__ bool plain36(const u32 (&w)[10]) {
-    u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        lo &= w[k] + 0x53535353u;   // bit 7 set per byte iff byte >= 0x2D (bytes < 0x80: no carries)
-        hi |= w[k];
-        bs |= zero_bytes(w[k] ^ 0x5C5C5C5Cu);
-    }
-    if (((lo & 0x80808080u) == 0x80808080u) & ((hi & 0x80808080u) == 0u) & (bs == 0u)) return true;
-    u32 f = 0;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f |= ft_flags(w[k]);
-    return f == 0u;
-}
 
 // One pair of a learned order: the key literal at p, its value, the separator after it
 // (", " + the next key's quote, or the closing quote + '}' when `last`).  p moves to the
