@@ -1010,12 +1010,50 @@ static int learn_layout(const u8* l, u64 len, u32 require_mask, LearnDesc* d) {
     return 3;
 }
 
-// The layout of a host batch from its first line (held in the pinned slot).
+// The batch's layout from SAMPLE_LINES of its lines (round 4; until round 3 the first line
+// only): line 0 and one line at a hashed position in each of the other strata of
+// [0, n).  If at least SAMPLE_AGREE of them name the same layout (for 3 the same key order
+// and spacing), that one; otherwise several producers are interleaved and the flat-object
+// tier, which takes every layout alike, runs first (2).  Only a choice of instantiation:
+// every instantiation counts every line exactly.
+constexpr u32 SAMPLE_LINES = 16, SAMPLE_AGREE = 12;
+
+static u64 sample_index(u64 n, u32 j) {
+    if (j == 0 || n <= SAMPLE_LINES) return std::min<u64>(j, n ? n - 1 : 0);
+    const u64 a = n * j / SAMPLE_LINES, b = n * (j + 1) / SAMPLE_LINES;   // stratum j
+    return a + mix64(0x51ED27u + j) % std::max<u64>(1, b - a);
+}
+
+static int decide_layout(const ysb_ctx* c, const std::vector<std::pair<const u8*, u64>>& lines, LearnDesc* d) {
+    const u32 req = (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu;
+    std::vector<std::pair<int, LearnDesc>> got;
+    for (const auto& l : lines) {
+        LearnDesc di{};
+        const int lay = learn_layout(l.first, l.second, req, &di);
+        got.push_back({lay, lay == 3 ? di : LearnDesc{}});
+    }
+    if (got.empty()) return 0;
+    for (const auto& g : got) {   // the most frequent (layout, order) of the sample
+        u32 k = 0;
+        for (const auto& h : got) k += h.first == g.first && std::memcmp(&h.second, &g.second, sizeof(LearnDesc)) == 0;
+        if (k >= std::min<u32>(SAMPLE_AGREE, (u32)got.size())) {
+            *d = g.second;
+            return g.first;
+        }
+    }
+    return 2;
+}
+
+// A host batch (held in the pinned slot).
 static int sniff_layout(const ysb_ctx* c, const uint8_t* bytes, u64 nbytes, const u32* off, u64 n, LearnDesc* d) {
-    const u64 s = off[0];
-    const u64 e = n > 1 ? (u64)off[1] : nbytes;
-    if (s >= e || e > nbytes) return 0;
-    return learn_layout(bytes + s, e - s, (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu, d);
+    std::vector<std::pair<const u8*, u64>> lines;
+    for (u32 j = 0; j < SAMPLE_LINES && j < n; ++j) {
+        const u64 i = sample_index(n, j);
+        const u64 s = off[i], e = i + 1 < n ? (u64)off[i + 1] : nbytes;
+        if (s >= e || e > nbytes) return 0;   // bad offsets: the scan defers them anyway
+        lines.push_back({bytes + s, std::min<u64>(e - s, SAMPLE_BYTES)});
+    }
+    return decide_layout(c, lines, d);
 }
 
 // Whether batches pick the scan instantiation from their first line (the default): not
@@ -1036,17 +1074,16 @@ static int hinted_layout(const ysb_ctx* c, int sampled) {
     return sampled;
 }
 
-// Device batches: the first line of every segment, copied by sample_kernel on the compute
-// stream -- in stream order, so after whatever produced the batch there (the caller's
-// contract: a device batch is complete when submitted, or its producer is ordered before
-// ysb_stream(ctx)) -- into one of two pinned buffers.  Which sample decides: this launch's
-// own when the compute stream was idle at the submit (the copy finishes in microseconds) or
-// no earlier sample exists; otherwise the previous launch's, read without waiting for the
-// device (one launch late: a producer writes one layout, and counts do not depend on the
-// choice).  One layout for the launch: the segments' common one, else the flat-object tier
-// first (it takes every layout).
+// Device batches: SAMPLE_LINES lines spread over the launch's segments (as sniff_layout
+// spreads them over a host batch), copied by sample_kernel on the compute stream -- in
+// stream order, so after whatever produced the batch there (the caller's contract: a device
+// batch is complete when submitted, or its producer is ordered before ysb_stream(ctx)) --
+// into one of two pinned buffers.  Which sample decides: this launch's own when the compute
+// stream was idle at the submit (the copy finishes in microseconds) or no earlier sample
+// exists; otherwise the previous launch's, read without waiting for the device (one launch
+// late: a producer writes one layout, and counts do not depend on the choice).
 static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, LearnDesc* d) {
-    const u64 buf = (u64)MAX_SEGS * SAMPLE_STRIDE;
+    const u64 buf = (u64)SAMPLE_LINES * SAMPLE_STRIDE;
     if (!c->h_sample) {
         HIPCHK(c, hipHostMalloc(&c->h_sample, 2 * buf));
         for (hipEvent_t& e : c->ev_sample) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1054,14 +1091,18 @@ static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, L
     const bool idle = hipStreamQuery(c->s_comp) == hipSuccess;
     const int k = c->sample_cur;
     c->sample_cur ^= 1;
+    u64 total = 0;
+    for (u32 i = 0; i < nseg; ++i) total += segs[i].n_events;
     SampleSegs ss{};
     u32 n = 0;
-    for (u32 i = 0; i < nseg && n < (u32)MAX_SEGS; ++i) {
-        if (!segs[i].n_events) continue;
+    for (u32 j = 0; j < SAMPLE_LINES && j < total; ++j) {
+        u64 g = sample_index(total, j), i = 0;   // global line -> (segment, line)
+        while (g >= segs[i].n_events) g -= segs[i++].n_events;
         ss.bytes[n] = segs[i].d_bytes;
         ss.off[n] = segs[i].d_line_off;
         ss.nbytes[n] = segs[i].nbytes;
         ss.n[n] = segs[i].n_events;
+        ss.line[n] = g;
         ++n;
     }
     launch_sample(ss, n, c->h_sample + (u64)k * buf, c->s_comp);
@@ -1071,23 +1112,15 @@ static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, L
     const int use = (!idle && c->sample_nseg[k ^ 1]) ? k ^ 1 : k;
     HIPCHK(c, hipEventSynchronize(c->ev_sample[use]));
     const u8* h = c->h_sample + (u64)use * buf;
-    const u32 req = (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu;
-    int lay = -1;
+    std::vector<std::pair<const u8*, u64>> lines;
     for (u32 i = 0; i < c->sample_nseg[use]; ++i) {
-        const u8* s = h + (u64)i * SAMPLE_STRIDE;
+        const u8* sp = h + (u64)i * SAMPLE_STRIDE;
         u32 hd[3];
-        std::memcpy(hd, s, 12);
+        std::memcpy(hd, sp, 12);
         if (!hd[2]) return 0;   // bad offsets: the scan defers them anyway
-        LearnDesc di{};
-        const int l = learn_layout(s + 16, hd[1], req, &di);
-        if (lay < 0) {
-            lay = l;
-            *d = di;
-        } else if (lay != l || (l == 3 && std::memcmp(&di, d, sizeof di) != 0)) {
-            lay = 2;
-        }
+        lines.push_back({sp + 16, hd[1]});
     }
-    return lay < 0 ? 0 : lay;
+    return decide_layout(c, lines, d);
 }
 
 // With YSB_F_TIMING: an event pair around a slot's H2D copy (ysb_copy_time), else none.
@@ -1215,12 +1248,24 @@ static int launch_pending_raw(ysb_ctx* c) {
     return rc;
 }
 
-// The layout of a raw batch from its first line (host bytes: up to the first terminator).
+// The layout of a raw batch (host bytes): its first line and the first complete line after
+// each of SAMPLE_LINES - 1 spread byte positions, decided as sniff_layout decides.
 static int sniff_raw(const ysb_ctx* c, const u8* b, u64 nbytes, LearnDesc* d) {
-    const u64 lim = std::min<u64>(nbytes, 4096);
-    u64 e = 0;
-    while (e < lim && b[e] != '\n' && b[e] != '\r') ++e;
-    return learn_layout(b, std::min<u64>(e + 1, nbytes), (c->cfg.flags & YSB_F_REQUIRE_IP) ? 0x7Fu : 0x3Fu, d);
+    auto line_at = [&](u64 p) -> std::pair<const u8*, u64> {   // the line starting at p
+        const u64 lim = std::min<u64>(nbytes, p + SAMPLE_BYTES);
+        u64 e = p;
+        while (e < lim && b[e] != '\n' && b[e] != '\r') ++e;
+        return {b + p, std::min<u64>(e + 1, nbytes) - p};
+    };
+    std::vector<std::pair<const u8*, u64>> lines{line_at(0)};
+    for (u32 j = 1; j < SAMPLE_LINES; ++j) {
+        u64 p = nbytes * j / SAMPLE_LINES;
+        const u64 lim = std::min<u64>(nbytes, p + 4096);
+        while (p < lim && b[p] != '\n') ++p;   // the next line after a '\n' (a lone '\r' only ends lines elsewhere)
+        if (p + 1 >= lim) continue;
+        lines.push_back(line_at(p + 1));
+    }
+    return decide_layout(c, lines, d);
 }
 
 int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) {

@@ -232,16 +232,19 @@ void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_
 u64 split_chunks(u64 nbytes);
 hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64 cap, unsigned long long* d_n,
                               hipStream_t s);
-// Layout sampling of device launches: each segment's first line, copied on the device (in
-// stream order after the batch's producer) into pinned host memory, SAMPLE_STRIDE bytes per
-// segment: u32 {line start, sampled length, valid, 0}, then <= SAMPLE_BYTES line bytes.
+// Layout sampling of device launches: sampled lines (spread over the launch's segments),
+// copied on the device (in stream order after the batch's producer) into pinned host memory,
+// SAMPLE_STRIDE bytes per line: u32 {line start, sampled length, valid, 0}, then
+// <= SAMPLE_BYTES line bytes.
 constexpr u32 SAMPLE_BYTES = 288;   // a line of the scan's tile capacity
 constexpr u32 SAMPLE_STRIDE = 16 + SAMPLE_BYTES;
-struct SampleSegs {
-    const u8* bytes[MAX_SEGS];
-    const u32* off[MAX_SEGS];
-    u64 nbytes[MAX_SEGS];
-    u64 n[MAX_SEGS];   // >= 1
+constexpr int SAMPLE_MAX = 16;
+struct SampleSegs {                  // per sampled line: its batch and its index there
+    const u8* bytes[SAMPLE_MAX];
+    const u32* off[SAMPLE_MAX];
+    u64 nbytes[SAMPLE_MAX];
+    u64 n[SAMPLE_MAX];   // >= 1
+    u64 line[SAMPLE_MAX];
 };
 void launch_sample(const SampleSegs& s, u32 nseg, u8* out, hipStream_t st);
 

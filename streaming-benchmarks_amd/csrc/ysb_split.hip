@@ -124,8 +124,8 @@ __global__ __launch_bounds__(SPLIT_TPB) void split_write_kernel(const u8* b, u64
     }
 }
 
-// The first line of every segment of a device launch, for the host's layout sampling
-// (ysb_capi.cpp sample_device_layout): block i writes out[i * SAMPLE_STRIDE] = {line start,
+// The sampled lines of a device launch, for the host's layout sampling (ysb_capi.cpp
+// sample_device_layout): block i copies line s.line[i] of its batch: out[i * SAMPLE_STRIDE] = {line start,
 // sampled length, valid} and then the line's first <= SAMPLE_BYTES bytes.  It runs on the
 // compute stream, so it reads the batch after whatever produced it there; out is pinned host
 // memory (no copy of its own).
@@ -134,8 +134,9 @@ __global__ __launch_bounds__(64) void sample_kernel(SampleSegs s, u8* out) {
     const u32 i = blockIdx.x;
     u8* o = out + (u64)i * SAMPLE_STRIDE;
     if (threadIdx.x == 0) {
-        const u32 o0 = s.off[i][0];
-        const u64 end = s.n[i] > 1 ? (u64)s.off[i][1] : s.nbytes[i];
+        const u64 li = s.line[i];
+        const u32 o0 = s.off[i][li];
+        const u64 end = li + 1 < s.n[i] ? (u64)s.off[i][li + 1] : s.nbytes[i];
         const bool valid = o0 <= end && end <= s.nbytes[i];
         const u32 len = valid ? (u32)(end - o0 < SAMPLE_BYTES ? end - o0 : SAMPLE_BYTES) : 0u;
         hdr[0] = o0;

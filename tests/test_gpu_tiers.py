@@ -237,11 +237,13 @@ def test_learned_order_with_off_order_lines(require_ip):
         lambda ln: ln + b' trailing',                                               # text after '}'
         lambda ln: ln.replace(b'{"ad_type"', b'{ "ad_type"', 1),                    # space after '{'
     ]
+    # one line in ten off the order (the layout sample -- 16 lines, 12 must agree -- still
+    # names the learned order; with 4 producers interleaved it picks the flat tier instead)
     lines = [la[0]]
     for i in range(1, 4000):
-        if i % 5 == 0:
-            lines.append(breaks[(i // 5) % len(breaks)](la[i]))
-        elif i % 5 == 1:
+        if i % 20 == 0:
+            lines.append(breaks[(i // 20) % len(breaks)](la[i]))
+        elif i % 20 == 10:
             lines.append(lb[i])                                                     # generator order
         else:
             lines.append(la[i])
@@ -423,3 +425,35 @@ def test_extra_field_edge_lines_match_oracle(hint):
         assert got == exp, lines[0]
         for k, v in est.items():
             assert st[k] == v, (k, lines[0])
+
+
+def test_mixed_producers_sample_the_flat_tier():
+    """Four producers interleaved line by line (GEN_MIXED): the 16-line layout sample finds no
+    layout 12 of them agree on, so the flat-object tier (it takes every layout alike) runs
+    first -- host, device and raw batches, exact vs the oracle, nothing deferred."""
+    from ysb_amd import GEN_MIXED
+    g = GenParams(seed=53, n_campaigns=40, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
+                  variant=GEN_MIXED)
+    _, aids = g.ids()
+    raw, offs = g.events_host(0, 80_000)
+    exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), raw, offs)
+    for how in ("host", "device", "raw"):
+        with YsbContext(n_campaigns=40, window_ring=256, max_batch_bytes=raw.size + 64,
+                        max_batch_events=offs.size + 1) as ctx:
+            ctx.load_ad_map(aids, g.ad_campaign_index())
+            if how == "device":
+                d_b, d_o = ctx.device_alloc(raw.size + 64), ctx.device_alloc(4 * offs.size + 64)
+                ctx.h2d(d_b, raw)
+                ctx.h2d(d_o, offs)
+                ctx.submit_device(d_b, raw.size, d_o, offs.size)
+            elif how == "raw":
+                ctx.submit_raw(raw)
+            else:
+                ctx.submit(raw, offs)
+            got = ctx.drain_buckets()
+            st = ctx.stats()
+            assert ctx.launch_info()["layout"] == 2, how
+        assert got == exp, how
+        for k, v in est.items():
+            assert st[k] == v, (how, k)
+        assert st["deferred"] == 0, how
