@@ -907,6 +907,9 @@ __device__ __forceinline__ bool process_line(const S& src, int s, int e, const S
 #ifndef YSB_FLAT_LDS
 #define YSB_FLAT_LDS 1   // round 4: flat_parse_lds for the flat-first / learned-order instantiations
 #endif
+#ifndef YSB_FLAT_VOCAB
+#define YSB_FLAT_VOCAB 1   // round 4: flat_parse_lds names short values from the generator's vocabularies
+#endif
 // A flat object of plain double-quoted string pairs whose keys are all DeserializeBolt's
 // -- in any order, with any whitespace nextClean skips, ',' or ';' between pairs and a
 // separator allowed before '}' -- is decided here with word-at-a-time string scans over
@@ -1052,6 +1055,40 @@ __device__ __forceinline__ bool plain36(const u32 (&w)[10]) {
     return f == 0u;
 }
 
+// The length of a short value named from its vocabulary -- the generator's closed sets
+// (core.clj:68-69,96,181): an ad_type of the five, an event_type of the three, a 13-digit
+// event_time, ip "1.2.3.4" -- from the words at its first byte (A: >= 5 realigned words), or 0
+// when it is none of them (the caller then scans for its closing quote).  Every byte up to the
+// closing quote is compared (or shown to be a digit), so a value named is a plain string.
+// KI: learn_key's index (3 ad_type, 4 event_type, 5 event_time, 6 ip_address).
+template <int KI>
+__device__ __forceinline__ int vocab_len(const u32* A) {
+    if constexpr (KI == 3) {
+        if (A[0] == w4('b', 'a', 'n', 'n') && (A[1] & 0xFFFFFFu) == (w4('e', 'r', '"', 0) & 0xFFFFFFu)) return 6;
+        if (A[0] == w4('m', 'a', 'i', 'l') && (A[1] & 0xFFu) == '"') return 4;
+        if (A[0] == w4('m', 'o', 'd', 'a') && (A[1] & 0xFFFFu) == w4('l', '"', 0, 0)) return 5;
+        if (A[0] == w4('m', 'o', 'b', 'i') && (A[1] & 0xFFFFFFu) == (w4('l', 'e', '"', 0) & 0xFFFFFFu)) return 6;
+        if (A[0] == w4('s', 'p', 'o', 'n') && A[1] == w4('s', 'o', 'r', 'e') && A[2] == w4('d', '-', 's', 'e') &&
+            A[3] == w4('a', 'r', 'c', 'h') && (A[4] & 0xFFu) == '"')
+            return 16;
+        return 0;
+    } else if constexpr (KI == 4) {
+        if (A[0] == w4('v', 'i', 'e', 'w') && (A[1] & 0xFFu) == '"') return 4;
+        if (A[0] == w4('c', 'l', 'i', 'c') && (A[1] & 0xFFFFu) == w4('k', '"', 0, 0)) return 5;
+        if (A[0] == w4('p', 'u', 'r', 'c') && A[1] == w4('h', 'a', 's', 'e') && (A[2] & 0xFFu) == '"') return 8;
+        return 0;
+    } else if constexpr (KI == 5) {
+        u32 bad = 0;
+        swar_digits4(A[0], bad);
+        swar_digits4(A[1], bad);
+        swar_digits4(A[2], bad);
+        bad |= ((A[3] & 0xFFu) - '0') > 9u;
+        return (bad == 0u && ((A[3] >> 8) & 0xFFu) == '"') ? 13 : 0;
+    } else {
+        return (A[0] == w4('1', '.', '2', '.') && A[1] == w4('3', '.', '4', '"')) ? 7 : 0;
+    }
+}
+
 // Round 4: the flat-first / learned-order instantiations' flat tier on the staged LDS line
 // (flat_parse_fast's subset and decisions), with the common forms taken branch-free:
 //   * the key named from the four realigned words at its text (load_span: five aligned
@@ -1120,6 +1157,27 @@ __device__ __forceinline__ bool flat_parse_lds(const LdsSrc& src, int s, int e, 
         seen |= id;
         int ve = -1;
         u32 y = 0;                                    // the closing quote and the 3 bytes after it
+#if YSB_FLAT_VOCAB
+        u32 w[10];                                    // the value's words, for every key
+        load_span(src, vq + 1, w);
+        if (id & (K_AD | K_USER | K_PAGE)) {
+            if (plain36(w) && vq + 37 < e && (w[9] & 0xFFu) == '"') {
+                ve = vq + 37;
+                y = w[9];
+                if (id == K_AD) {
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) adw[j] = w[j];
+                }
+            }
+        } else {                                      // round 4: a short value named from its vocabulary
+            const int la = id == K_ADTYPE ? vocab_len<3>(w) : id == K_ETYPE ? vocab_len<4>(w)
+                         : id == K_ETIME ? vocab_len<5>(w) : id == K_IP ? vocab_len<6>(w) : 0;
+            if (la && vq + 1 + la < e) {
+                ve = vq + 1 + la;
+                y = src.load4(ve);
+            }
+        }
+#else
         if (id & (K_AD | K_USER | K_PAGE)) {
             u32 w[10];
             load_span(src, vq + 1, w);
@@ -1132,6 +1190,7 @@ __device__ __forceinline__ bool flat_parse_lds(const LdsSrc& src, int s, int e, 
                 }
             }
         }
+#endif
         if (ve < 0) {
             ve = ft_string_end(src, vq + 1, e);
             if (ve < 0) return false;
@@ -1254,6 +1313,10 @@ __device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 requ
 // (JSONObject(JSONTokener) on this subset: nextClean, nextString, putOnce, ',' / '}');
 // any other line goes on to the flat tier, then the general parser.
 
+#ifndef YSB_LEARN_VOCAB
+#define YSB_LEARN_VOCAB 1   // round 4: learned-order short values named from the generator's vocabularies first
+#endif
+
 // key index -> its text (ScanParams.learn_order)
 __host__ __device__ constexpr const char* learn_key(int i) {
     return i == 0 ? "user_id" : i == 1 ? "page_id" : i == 2 ? "ad_id" : i == 3 ? "ad_type" : i == 4 ? "event_type"
@@ -1277,6 +1340,15 @@ struct KeyLit {
         return make_words<4>(buf, 0, n);
     }
 };
+
+// the closing quote of the learned order's value at v named by vocab_len, or -1
+template <int KI>
+__device__ __forceinline__ int vocab_value_end(const LdsSrc& src, int v) {
+    u32 A[5];
+    load_span(src, v, A);
+    const int la = vocab_len<KI>(A);
+    return la ? v + la : -1;
+}
 
 // One pair of a learned order: the key literal at p, its value, the separator after it
 // (", " + the next key's quote, or the closing quote + '}' when `last`).  p moves to the
@@ -1305,7 +1377,12 @@ __device__ __forceinline__ bool learned_pair(const LdsSrc& src, int& p, int e, b
             for (int k = 0; k < 9; ++k) kw[k] = w[k];
         }
     } else {
+#if YSB_LEARN_VOCAB
+        ve = vocab_value_end<KI>(src, v);         // round 4: the value named, not scanned
+        if (__builtin_expect(ve < 0, 0)) ve = ft_string_end(src, v, e);
+#else
         ve = ft_string_end(src, v, e);
+#endif
         ok &= ve >= v;
         const u32 x = src.load4(ok ? ve : v);
         ok &= last ? (x & 0xFFFFu) == w4('"', '}', 0, 0) : (x & SEPM) == SEP;
