@@ -389,13 +389,14 @@ int         ysb_group_reduce_scatter(ysb_ctx* ctx);
  * everything (do one before reading the owned tables).  Every rank must use the same
  * sequence of the two calls. */
 int         ysb_group_exchange_pipelined(ysb_ctx* ctx);
-/* Exchange accounting: exchanges run, reduce-scatter input bytes this rank contributed,
- * device time of the exchanges (HIP events from the plan on the compute stream to the end of
- * the unpack on the exchange stream: plan, all-reduce(max), read-back, pack, reduce-scatter,
- * unpack), of their part on the compute stream (critical_ms: plan to pack -- what a step
- * waits for; the reduce-scatter and the unpack run on a stream of their own, beside the next
- * launch), the last exchange's bucket count and cell width (0: nothing was pending), and what
- * one whole-ring u64 exchange would move.  reset != 0 zeroes the totals after reading them. */
+/* Exchange accounting: exchanges run, reduce-scatter input bytes this rank contributed
+ * (campaign rows x the bucket count rounded up to a multiple of 4 x the cell width), device
+ * time of the exchanges (HIP events: plan, all-reduce(max), read-back, pack, reduce-scatter,
+ * unpack), of their part on the compute stream (critical_ms: plan to pack, plus the unpack --
+ * what the launches queue behind; the reduce-scatter runs on a stream of its own beside the
+ * next launch, and the unpack is enqueued on the compute stream at the next exchange or read),
+ * the last exchange's bucket count and cell width (0: nothing was pending), and what one
+ * whole-ring u64 exchange would move.  reset != 0 zeroes the totals after reading them. */
 typedef struct ysb_exchange_info {
     uint64_t exchanges;
     uint64_t bytes;

@@ -2111,6 +2111,10 @@ static int exchange(ysb_ctx* c, bool pipelined) {
         return fail(c, YSB_ERR_CAPACITY, "pending counts too large to sum over %d ranks", c->nranks);
     const unsigned long long cap = width == 8 ? ~0ull / (u64)c->nranks : ((1ull << (8 * width)) - 1) / (u64)c->nranks;
     const u32 rows = c->c_pad, per = c->c_pad / (u32)c->nranks;
+    const u32 nslots = R;
+    // the slot list padded to whole words (W is a power of two >= 16: R4 <= W); a pad slot
+    // sends 0 and receives nothing (ysb_table.hip XSLOT_PAD)
+    while (R % 4) slots[R++] = 0xFFFFFFFFu;
     if (R) {
         const int k = c->xk;
         c->xk ^= 1;
@@ -2155,7 +2159,7 @@ static int exchange(ysb_ctx* c, bool pipelined) {
     if (!pipelined && (urc = finish_unpack(c))) return urc;
     c->x_count++;
     c->x_bytes += (u64)rows * R * width;
-    c->x_last_slots = R;
+    c->x_last_slots = nslots;
     c->x_last_width = R ? width : 0;
     return YSB_OK;
 }

@@ -126,6 +126,38 @@ __global__ __launch_bounds__(AUX_TPB) void xplan_kernel(const unsigned long long
         for (u32 s = threadIdx.x; s < W; s += AUX_TPB) lmax[s] = 0;
     __syncthreads();
     const bool r64 = read_u64(force_u64, dirty);
+    if (!r64 && in_lds && delta) {
+        // Round 4: the grid stride (a multiple of W / 16 vectors: AUX_TPB = 256 >= 4096 / 16)
+        // keeps a thread on the same 16 slots, so their maxima stay in registers and reach
+        // LDS once per thread -- not an LDS atomic per nonzero cell (configs[2]: ~30 %).
+        u32 m[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m[j] = 0;
+        const u64 q0 = (u64)blockIdx.x * AUX_TPB + threadIdx.x, st = (u64)gridDim.x * AUX_TPB;
+        const uint4* dv = reinterpret_cast<const uint4*>(delta);
+        auto fold = [&](const uint4 d) {
+            const u32 dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) m[j] = max(m[j], (dw[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+        };
+        u64 q = q0;
+        for (; q + 7 * st < vecs; q += 8 * st) {   // eight loads in flight
+            uint4 d[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) d[u] = dv[q + u * st];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) fold(d[u]);
+        }
+        for (; q < vecs; q += st) fold(dv[q]);
+        const u32 s0 = (u32)((16 * q0) & (u64)(W - 1));
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (m[j]) atomicMax(&lmax[s0 + j], (unsigned long long)m[j]);
+        __syncthreads();
+        for (u32 s = threadIdx.x; s < W; s += AUX_TPB)
+            if (lmax[s]) atomicMax(&slot_max[s], lmax[s]);
+        return;
+    }
     for (u64 q = (u64)blockIdx.x * AUX_TPB + threadIdx.x; q < vecs; q += (u64)gridDim.x * AUX_TPB) {
         const u64 i0 = 16 * q;
         const u32 s0 = (u32)(i0 & (u64)(W - 1));
@@ -158,6 +190,9 @@ constexpr int XROW_WAVES = AUX_TPB / 64;
 template <class T>
 __device__ __forceinline__ void put_cell(void* out, u64 i, unsigned long long v) { static_cast<T*>(out)[i] = (T)v; }
 
+// The plan's slot list is padded to a multiple of 4 with 0xFFFFFFFF (any slot >= W: a cell
+// that sends 0 and receives nothing), so a packed u8 row is whole words.
+
 // out[c][k] = pending(c, slots[k]) as `width`-byte cells, the sources zeroed -- except a
 // cell above `cap` (a pipelined exchange whose plan is one call old: the cell grew past what
 // the width can sum over the ranks), which stays pending for a later exchange and sends 0.
@@ -171,6 +206,10 @@ __global__ __launch_bounds__(AUX_TPB) void xpack_kernel(unsigned long long* coun
     for (u32 c = blockIdx.x * XROW_WAVES + wave; c < rows; c += gridDim.x * XROW_WAVES) {
         const u64 row = (u64)c * W, orow = (u64)c * R;
         for (u32 k = lane; k < R; k += 64) {
+            if (slots[k] >= W) {
+                put_cell<T>(out, orow + k, 0);
+                continue;
+            }
             const u64 cell = row + slots[k];
             const unsigned long long d = delta ? delta[cell] : 0ull;
             const unsigned long long x = r64 ? counts[cell] : 0ull;
@@ -201,7 +240,7 @@ __global__ __launch_bounds__(AUX_TPB) void xunpack_kernel(unsigned long long* ow
         const u64 row = (u64)c * W, irow = (u64)c * R;
         for (u32 k = lane; k < R; k += 64) {
             const unsigned long long v = src[irow + k];
-            if (!v) continue;
+            if (!v || slots[k] >= W) continue;
             const u64 cell = row + slots[k];
             const unsigned long long sum = owned8[cell] + v;
             if (sum > 255u) {
@@ -209,6 +248,188 @@ __global__ __launch_bounds__(AUX_TPB) void xunpack_kernel(unsigned long long* ow
                 owned8[cell] = 0;
             } else {
                 owned8[cell] = (u8)sum;
+            }
+        }
+    }
+}
+
+// Round 4: the u8 pack and unpack (configs[2]: ~100 slots x 1M campaigns per exchange) a word
+// of 4 cells per lane: a row's L = R / 4 words over L lanes, 64 / L rows per wave.  Four
+// consecutive, aligned slots (the common case: the plan is the live bucket range) move as one
+// u32 load / store of the ring; any other group, a cell above cap, or the u64 ring in play
+// (r64) takes the per-cell steps of xpack_kernel / xunpack_kernel for its 4 cells.
+struct XLanes {
+    u32 L, rpw, sub, j;
+    __device__ XLanes(u32 R, u32 lane) : L(R / 4) {
+        rpw = L <= 64 ? 64 / L : 1;
+        sub = L <= 64 ? lane / L : 0;
+        j = lane - sub * (L <= 64 ? L : 0);
+    }
+};
+
+__device__ __forceinline__ bool run4(const uint4 sk) {
+    return (sk.x & 3u) == 0u && sk.y == sk.x + 1 && sk.z == sk.x + 2 && sk.w == sk.x + 3;
+}
+
+__global__ __launch_bounds__(AUX_TPB) void xpack8_kernel(unsigned long long* counts, u8* delta, u32 W, u32 rows,
+                                                         const u32* slots, u32 R, int force_u64, const u32* dirty,
+                                                         u32* out, unsigned long long cap) {
+    const bool r64 = read_u64(force_u64, dirty);
+    const XLanes X(R, threadIdx.x & 63);
+    if (X.sub >= X.rpw) return;
+    const u32 wave = threadIdx.x >> 6;
+    const u32 c8 = cap < 255ull ? (u32)cap : 255u;
+    const u32 c0 = (blockIdx.x * XROW_WAVES + wave) * X.rpw + X.sub, cst = gridDim.x * XROW_WAVES * X.rpw;
+    if (X.L <= 64 && !r64) {
+        // the common case: a lane keeps one word of the row (its slots loaded once), four
+        // rows' loads in flight per step
+        const uint4 sk = reinterpret_cast<const uint4*>(slots)[X.j];
+        if (run4(sk)) {
+            u32 c = c0;
+            for (; c < rows; c += 4 * cst) {
+                u32 d[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const u32 cu = c + u * cst;
+                    d[u] = cu < rows ? *reinterpret_cast<const u32*>(delta + (u64)cu * W + sk.x) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const u32 cu = c + u * cst;
+                    if (cu >= rows) continue;
+                    u32 word = d[u];
+                    const u32 hi = max(max(word & 0xFFu, (word >> 8) & 0xFFu), max((word >> 16) & 0xFFu, word >> 24));
+                    if (hi <= c8) {
+                        if (word) *reinterpret_cast<u32*>(delta + (u64)cu * W + sk.x) = 0;
+                    } else {   // a cell above cap stays pending and sends 0
+                        u32 keep = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            const u32 v = (word >> (8 * b)) & 0xFFu;
+                            if (v > c8) keep |= v << (8 * b);
+                        }
+                        *reinterpret_cast<u32*>(delta + (u64)cu * W + sk.x) = keep;
+                        word &= ~keep;
+                    }
+                    out[(u64)cu * X.L + X.j] = word;
+                }
+            }
+            return;
+        }
+    }
+    for (u32 c = c0; c < rows; c += cst) {
+        const u64 row = (u64)c * W;
+        for (u32 j = X.j; j < X.L; j += (X.L <= 64 ? X.L : 64)) {
+            const uint4 sk = reinterpret_cast<const uint4*>(slots)[j];
+            u32 word = 0;
+            bool done = false;
+            if (!r64 && run4(sk)) {
+                u32* dp = reinterpret_cast<u32*>(delta + row + sk.x);
+                const u32 d = *dp;
+                const u32 hi = max(max(d & 0xFFu, (d >> 8) & 0xFFu), max((d >> 16) & 0xFFu, d >> 24));
+                if (hi <= c8) {
+                    word = d;
+                    if (d) *dp = 0;
+                    done = true;
+                }
+            }
+            if (!done) {
+                const u32 sl[4] = {sk.x, sk.y, sk.z, sk.w};
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    if (sl[b] >= W) continue;
+                    const u64 cell = row + sl[b];
+                    const unsigned long long d = delta[cell];
+                    const unsigned long long x = r64 ? counts[cell] : 0ull;
+                    const unsigned long long v = d + x;
+                    if (v > cap) continue;   // stays pending, sends 0
+                    if (d) delta[cell] = 0;
+                    if (x) counts[cell] = 0;
+                    word |= (u32)v << (8 * b);
+                }
+            }
+            out[(u64)c * X.L + j] = word;
+        }
+    }
+}
+
+__global__ __launch_bounds__(AUX_TPB) void xunpack8_kernel(unsigned long long* owned, u8* owned8, u32 W, u32 rows,
+                                                           const u32* slots, u32 R, const u32* in) {
+    const XLanes X(R, threadIdx.x & 63);
+    if (X.sub >= X.rpw) return;
+    const u32 wave = threadIdx.x >> 6;
+    const u32 c0 = (blockIdx.x * XROW_WAVES + wave) * X.rpw + X.sub, cst = gridDim.x * XROW_WAVES * X.rpw;
+    if (X.L <= 64) {
+        // the common case: a lane keeps one word of the row, four rows' loads in flight per step
+        const uint4 sk = reinterpret_cast<const uint4*>(slots)[X.j];
+        if (run4(sk)) {
+            for (u32 c = c0; c < rows; c += 4 * cst) {
+                u32 v[4], o[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const u32 cu = c + u * cst;
+                    v[u] = cu < rows ? in[(u64)cu * X.L + X.j] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const u32 cu = c + u * cst;
+                    o[u] = v[u] ? *reinterpret_cast<const u32*>(owned8 + (u64)cu * W + sk.x) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (!v[u]) continue;
+                    const u64 row = (u64)(c + u * cst) * W;
+                    const u32 t = (o[u] & 0x7F7F7F7Fu) + (v[u] & 0x7F7F7F7Fu);
+                    if ((((o[u] & v[u]) | ((o[u] | v[u]) & ~t)) & 0x80808080u) == 0u) {
+                        *reinterpret_cast<u32*>(owned8 + row + sk.x) = o[u] + v[u];
+                        continue;
+                    }
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {   // a byte would pass 255: its sum to the u64 table
+                        const u32 vb = (v[u] >> (8 * b)) & 0xFFu;
+                        const u64 cell = row + sk.x + b;
+                        const u32 sum = ((o[u] >> (8 * b)) & 0xFFu) + vb;
+                        if (sum > 255u) {
+                            owned[cell] += sum;
+                            owned8[cell] = 0;
+                        } else {
+                            owned8[cell] = (u8)sum;
+                        }
+                    }
+                }
+            }
+            return;
+        }
+    }
+    for (u32 c = c0; c < rows; c += cst) {
+        const u64 row = (u64)c * W;
+        for (u32 j = X.j; j < X.L; j += (X.L <= 64 ? X.L : 64)) {
+            const u32 v = in[(u64)c * X.L + j];
+            if (!v) continue;
+            const uint4 sk = reinterpret_cast<const uint4*>(slots)[j];
+            if (run4(sk)) {
+                u32* op = reinterpret_cast<u32*>(owned8 + row + sk.x);
+                const u32 o = *op;
+                // per-byte carry out of o + v: none -> the bytes add as one word
+                const u32 t = (o & 0x7F7F7F7Fu) + (v & 0x7F7F7F7Fu);
+                if ((((o & v) | ((o | v) & ~t)) & 0x80808080u) == 0u) {
+                    *op = o + v;
+                    continue;
+                }
+            }
+            const u32 sl[4] = {sk.x, sk.y, sk.z, sk.w};
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const u32 vb = (v >> (8 * b)) & 0xFFu;
+                if (!vb || sl[b] >= W) continue;
+                const u64 cell = row + sl[b];
+                const u32 sum = owned8[cell] + vb;
+                if (sum > 255u) {
+                    owned[cell] += sum;
+                    owned8[cell] = 0;
+                } else {
+                    owned8[cell] = (u8)sum;
+                }
             }
         }
     }
@@ -240,17 +461,25 @@ void launch_xplan(const unsigned long long* counts, const u8* delta, u32 W, u64 
                   const u32* dirty, unsigned long long* slot_max, hipStream_t s) {
     const u64 vecs = cells / 16;
     if (!vecs) return;
-    hipLaunchKernelGGL(xplan_kernel, dim3((unsigned)grid_for(vecs, 2048)), dim3(AUX_TPB), 0, s, counts, delta, W, vecs,
+    // 512 workgroups: each ends with one global atomicMax per live slot (configs[2]: ~100 slots)
+    hipLaunchKernelGGL(xplan_kernel, dim3((unsigned)grid_for(vecs, 512)), dim3(AUX_TPB), 0, s, counts, delta, W, vecs,
                        force_u64, dirty, slot_max);
 }
 
-static u64 row_grid(u32 rows) { return std::max<u64>(1, std::min<u64>(((u64)rows + XROW_WAVES - 1) / XROW_WAVES, 8192)); }
+static u64 row_grid(u32 rows, u32 rpw = 1) {
+    const u64 waves = ((u64)rows + rpw - 1) / rpw;
+    return std::max<u64>(1, std::min<u64>((waves + XROW_WAVES - 1) / XROW_WAVES, 8192));
+}
+static u32 rows_per_wave(u32 R) { return R / 4 <= 64 ? 64 / (R / 4) : 1; }
 
 void launch_xpack(unsigned long long* counts, u8* delta, u32 W, u32 rows, const u32* slots, u32 R, int force_u64,
                   const u32* dirty, void* out, u32 width, unsigned long long cap, hipStream_t s) {
     if (!rows || !R) return;
     const dim3 g((unsigned)row_grid(rows)), b(AUX_TPB);
-    if (width == 1) hipLaunchKernelGGL(xpack_kernel<u8>, g, b, 0, s, counts, delta, W, rows, slots, R, force_u64, dirty, out, cap);
+    if (width == 1 && delta && R % 4 == 0)
+        hipLaunchKernelGGL(xpack8_kernel, dim3((unsigned)row_grid(rows, rows_per_wave(R))), b, 0, s, counts, delta, W,
+                           rows, slots, R, force_u64, dirty, static_cast<u32*>(out), cap);
+    else if (width == 1) hipLaunchKernelGGL(xpack_kernel<u8>, g, b, 0, s, counts, delta, W, rows, slots, R, force_u64, dirty, out, cap);
     else if (width == 4) hipLaunchKernelGGL(xpack_kernel<u32>, g, b, 0, s, counts, delta, W, rows, slots, R, force_u64, dirty, out, cap);
     else hipLaunchKernelGGL(xpack_kernel<unsigned long long>, g, b, 0, s, counts, delta, W, rows, slots, R, force_u64, dirty, out, cap);
 }
@@ -259,7 +488,10 @@ void launch_xunpack(unsigned long long* owned, u8* owned8, u32 W, u32 rows, cons
                     u32 width, hipStream_t s) {
     if (!rows || !R) return;
     const dim3 g((unsigned)row_grid(rows)), b(AUX_TPB);
-    if (width == 1) hipLaunchKernelGGL(xunpack_kernel<u8>, g, b, 0, s, owned, owned8, W, rows, slots, R, in);
+    if (width == 1 && R % 4 == 0)
+        hipLaunchKernelGGL(xunpack8_kernel, dim3((unsigned)row_grid(rows, rows_per_wave(R))), b, 0, s, owned, owned8, W,
+                           rows, slots, R, static_cast<const u32*>(in));
+    else if (width == 1) hipLaunchKernelGGL(xunpack_kernel<u8>, g, b, 0, s, owned, owned8, W, rows, slots, R, in);
     else if (width == 4) hipLaunchKernelGGL(xunpack_kernel<u32>, g, b, 0, s, owned, owned8, W, rows, slots, R, in);
     else hipLaunchKernelGGL(xunpack_kernel<unsigned long long>, g, b, 0, s, owned, owned8, W, rows, slots, R, in);
 }
