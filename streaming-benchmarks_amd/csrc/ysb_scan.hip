@@ -1219,6 +1219,102 @@ __device__ __forceinline__ bool flat_parse_lds(const LdsSrc& src, int s, int e, 
     return closed && (seen & need) == need;
 }
 
+#ifndef YSB_FLAT_BL
+#define YSB_FLAT_BL 1   // round 4: flat_parse_bl before flat_parse_lds in the flat-first / learned-order tier
+#endif
+// Round 4: flat_parse_lds's common forms with no branch per pair -- for batches whose lines
+// carry different key orders (several producers interleaved), where every per-pair branch
+// of a per-lane walk diverges.  Per pair, for every lane at once: the key named (as in
+// flat_parse_lds), `": "` / `":"`, the value -- an id as 36 plain bytes by plain36's cheap
+// test, any other value named from its vocabulary or, when it is none of them, by the
+// string scan -- and `", "` / `","` / `"}` after it; the loop runs while any lane is open
+// (a uniform exit).  A lane meets no slow step here: any other form (another key, a repeat,
+// other spacing, a value that is not 36 / vocabulary / plain, a missing field) only clears
+// its `ok`, and the caller hands the line to flat_parse_lds, which decides it.  true: the
+// line is in that common subset with every field of `require` (and the three the topology
+// reads) -- a subset of flat_parse_lds's, with the same spans.
+__device__ __forceinline__ bool flat_parse_bl(const LdsSrc& src, int s, int e, u32 require, Span& ad, Span& et,
+                                              Span& tm, u32 (&adw)[9]) {
+    bool ok = (src.load4(s) & 0xFFFFu) == w4('{', '"', 0, 0) && s + 1 < e;
+    bool closed = false;
+    int kq = s + 1;
+    u32 seen = 0;
+    int ads = s, ets = s, ete = s, tms = s, tme = s;
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) {
+        const bool act = ok && !closed;
+        if (__ballot(act) == 0ull) break;
+        if (!act) kq = s + 1;                         // an idle lane reads inside its line
+        u32 kw[4];
+        load_span(src, kq + 1, kw);
+        const bool isAD = kw[0] == w4('a', 'd', '_', 'i') && (kw[1] & 0xFFFFu) == w4('d', '"', 0, 0);
+        const bool is7 = (kw[1] == w4('_', 'i', 'd', '"') && (kw[0] == w4('u', 's', 'e', 'r') || kw[0] == w4('p', 'a', 'g', 'e'))) ||
+                         (kw[0] == w4('a', 'd', '_', 't') && kw[1] == w4('y', 'p', 'e', '"'));
+        const bool ev = kw[0] == w4('e', 'v', 'e', 'n');
+        const u32 k2 = kw[2] & 0xFFFFFFu;
+        const bool isET = ev && kw[1] == w4('t', '_', 't', 'y') && k2 == (w4('p', 'e', '"', 0) & 0xFFFFFFu);
+        const bool isTM = ev && kw[1] == w4('t', '_', 't', 'i') && k2 == (w4('m', 'e', '"', 0) & 0xFFFFFFu);
+        const bool isIP = kw[0] == w4('i', 'p', '_', 'a') && kw[1] == w4('d', 'd', 'r', 'e') && k2 == (w4('s', 's', '"', 0) & 0xFFFFFFu);
+        u32 id = isAD ? K_AD : isET ? K_ETYPE : isTM ? K_ETIME : isIP ? K_IP : 0u;
+        if (is7) id = kw[0] == w4('u', 's', 'e', 'r') ? K_USER : kw[0] == w4('p', 'a', 'g', 'e') ? K_PAGE : K_ADTYPE;
+        const u32 x = isAD ? __builtin_amdgcn_alignbyte(kw[2], kw[1], 2) : is7 ? kw[2] : __builtin_amdgcn_alignbyte(kw[3], kw[2], 3);
+        const int ke = kq + 1 + (isAD ? 5 : is7 ? 7 : 10);
+        const bool sp3 = (x & 0xFFFFFFu) == (w4(':', ' ', '"', 0) & 0xFFFFFFu);
+        const bool sp2 = (x & 0xFFFFu) == (w4(':', '"', 0, 0) & 0xFFFFu);
+        const int vq = sp3 ? ke + 3 : ke + 2;
+        bool g = act && id != 0u && (sp3 || sp2) && vq < e && (seen & id) == 0u;
+        u32 w[10];
+        load_span(src, vq + 1, w);
+        int ve;
+        u32 y;
+        if (id & (K_AD | K_USER | K_PAGE)) {
+            u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                lo &= w[j] + 0x53535353u;
+                hi |= w[j];
+                bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
+            }
+            g = g && (lo & 0x80808080u) == 0x80808080u && (hi & 0x80808080u) == 0u && bs == 0u &&
+                (w[9] & 0xFFu) == '"';
+            ve = vq + 37;
+            y = w[9];
+        } else {
+            int la = id == K_ADTYPE ? vocab_len<3>(w) : id == K_ETYPE ? vocab_len<4>(w)
+                   : id == K_ETIME ? vocab_len<5>(w) : id == K_IP ? vocab_len<6>(w) : 0;
+            if (__builtin_expect(g && la == 0, 0)) {  // a value outside the vocabularies
+                const int q = ft_string_end(src, vq + 1, e);
+                la = q > vq ? q - vq - 1 : 0;
+            }
+            g = g && la > 0;
+            ve = vq + 1 + la;
+            y = src.load4(ve);
+        }
+        ads = g && id == K_AD ? vq + 1 : ads;
+        ets = g && id == K_ETYPE ? vq + 1 : ets;
+        ete = g && id == K_ETYPE ? ve : ete;
+        tms = g && id == K_ETIME ? vq + 1 : tms;
+        tme = g && id == K_ETIME ? ve : tme;
+        seen |= g ? id : 0u;
+        const bool n3 = y == w4('"', ',', ' ', '"') && ve + 3 < e;
+        const bool n2 = (y & 0xFFFFFFu) == (w4('"', ',', '"', 0) & 0xFFFFFFu) && ve + 2 < e;
+        const bool cl = (y & 0xFFFFu) == w4('"', '}', 0, 0) && ve + 1 < e;
+        g = g && (n3 || n2 || cl);
+        if (act) {
+            ok = g;
+            closed = cl;
+            kq = n3 ? ve + 3 : ve + 2;
+        }
+    }
+    const u32 need = require | K_AD | K_ETYPE | K_ETIME;
+    if (!(ok && closed && (seen & need) == need)) return false;
+    ad = Span{ads, ads + 36, 0};
+    et = Span{ets, ete, 0};
+    tm = Span{tms, tme, 0};
+    load_span(src, ads, adw);
+    return true;
+}
+
 // FAST (the flat-first instantiation only): the whitespace skips' first step outside their
 // loops, and the id values (ad / user / page) checked as 36-byte UUIDs in one step before
 // the string scan -- the same decisions, fewer divergent loop trips.
@@ -1278,7 +1374,12 @@ __device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 requ
         u32 adw[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) adw[k] = 0u;
+#if YSB_FLAT_BL
+        okp = flat_parse_bl(src, ls, le, require, ad, et, tm, adw);
+        if (__builtin_expect(!okp, 0)) okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
+#else
         okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
+#endif
         if (!okp || ad.e - ad.s != 36) return false;
         const bool fast_ad = adw[0] | adw[1] | adw[8];   // the id fast path kept the ad_id's words
 #pragma unroll
