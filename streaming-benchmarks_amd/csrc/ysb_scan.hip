@@ -1089,6 +1089,37 @@ __device__ __forceinline__ int vocab_len(const u32* A) {
     }
 }
 
+// vocab_len<3..6> for a lane's key id (K_ADTYPE / K_ETYPE / K_ETIME / K_IP, else 0) with no
+// branch: every candidate compared with bitwise ands, the length selected (lanes whose
+// lines carry different keys at the same pair, and the if-chains' per-candidate blocks,
+// cost flat_parse_bl a branch and its exec-mask steps each).
+__device__ __forceinline__ int vocab_len_any(u32 id, const u32 (&A)[10]) {
+    const u32 a1l8 = A[1] & 0xFFu, a1l16 = A[1] & 0xFFFFu, a1l24 = A[1] & 0xFFFFFFu;
+    // ad_type
+    const bool t6 = (A[0] == w4('b', 'a', 'n', 'n')) & (a1l24 == (w4('e', 'r', '"', 0) & 0xFFFFFFu));
+    const bool t4 = (A[0] == w4('m', 'a', 'i', 'l')) & (a1l8 == '"');
+    const bool t5 = (A[0] == w4('m', 'o', 'd', 'a')) & (a1l16 == w4('l', '"', 0, 0));
+    const bool t6b = (A[0] == w4('m', 'o', 'b', 'i')) & (a1l24 == (w4('l', 'e', '"', 0) & 0xFFFFFFu));
+    const bool t16 = (A[0] == w4('s', 'p', 'o', 'n')) & (A[1] == w4('s', 'o', 'r', 'e')) & (A[2] == w4('d', '-', 's', 'e')) &
+                     (A[3] == w4('a', 'r', 'c', 'h')) & ((A[4] & 0xFFu) == '"');
+    const int lat = (t6 | t6b) ? 6 : t4 ? 4 : t5 ? 5 : t16 ? 16 : 0;
+    // event_type
+    const bool e4 = (A[0] == w4('v', 'i', 'e', 'w')) & (a1l8 == '"');
+    const bool e5 = (A[0] == w4('c', 'l', 'i', 'c')) & (a1l16 == w4('k', '"', 0, 0));
+    const bool e8 = (A[0] == w4('p', 'u', 'r', 'c')) & (A[1] == w4('h', 'a', 's', 'e')) & ((A[2] & 0xFFu) == '"');
+    const int lae = e4 ? 4 : e5 ? 5 : e8 ? 8 : 0;
+    // event_time: 13 digits
+    u32 bad = 0;
+    swar_digits4(A[0], bad);
+    swar_digits4(A[1], bad);
+    swar_digits4(A[2], bad);
+    bad |= ((A[3] & 0xFFu) - '0') > 9u;
+    const int lam = (bad == 0u) & (((A[3] >> 8) & 0xFFu) == '"') ? 13 : 0;
+    // ip_address
+    const int lai = (A[0] == w4('1', '.', '2', '.')) & (A[1] == w4('3', '.', '4', '"')) ? 7 : 0;
+    return id == K_ADTYPE ? lat : id == K_ETYPE ? lae : id == K_ETIME ? lam : id == K_IP ? lai : 0;
+}
+
 // Round 4: the flat-first / learned-order instantiations' flat tier on the staged LDS line
 // (flat_parse_fast's subset and decisions), with the common forms taken branch-free:
 //   * the key named from the four realigned words at its text (load_span: five aligned
@@ -1220,7 +1251,16 @@ __device__ __forceinline__ bool flat_parse_lds(const LdsSrc& src, int s, int e, 
 }
 
 #ifndef YSB_FLAT_BL
-#define YSB_FLAT_BL 1   // round 4: flat_parse_bl before flat_parse_lds in the flat-first / learned-order tier
+#define YSB_FLAT_BL 2   // round 4: flat_parse_bl2 (1: flat_parse_bl) before flat_parse_lds in the flat-first / learned-order tier
+#endif
+#ifndef YSB_BL_NOVOCAB
+#define YSB_BL_NOVOCAB 0   // A/B: flat_parse_bl's short values by a 20-byte flag search instead of the vocabularies
+#endif
+#ifndef YSB_BL_VANY
+#define YSB_BL_VANY 0      // A/B: flat_parse_bl's vocabularies compared with no branch (vocab_len_any)
+#endif
+#ifndef YSB_BL_YREG
+#define YSB_BL_YREG 0      // A/B: flat_parse_bl's separator after a short value from the value's words
 #endif
 // Round 4: flat_parse_lds's common forms with no branch per pair -- for batches whose lines
 // carry different key orders (several producers interleaved), where every per-pair branch
@@ -1262,7 +1302,11 @@ __device__ __forceinline__ bool flat_parse_bl(const LdsSrc& src, int s, int e, u
         const bool sp3 = (x & 0xFFFFFFu) == (w4(':', ' ', '"', 0) & 0xFFFFFFu);
         const bool sp2 = (x & 0xFFFFu) == (w4(':', '"', 0, 0) & 0xFFFFu);
         const int vq = sp3 ? ke + 3 : ke + 2;
+#if YSB_BL_VANY
+        bool g = act & (id != 0u) & (sp3 | sp2) & (vq < e) & ((seen & id) == 0u);
+#else
         bool g = act && id != 0u && (sp3 || sp2) && vq < e && (seen & id) == 0u;
+#endif
         u32 w[10];
         load_span(src, vq + 1, w);
         int ve;
@@ -1275,20 +1319,51 @@ __device__ __forceinline__ bool flat_parse_bl(const LdsSrc& src, int s, int e, u
                 hi |= w[j];
                 bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
             }
+#if YSB_BL_VANY
+            g = g & ((lo & 0x80808080u) == 0x80808080u) & ((hi & 0x80808080u) == 0u) & (bs == 0u) &
+                ((w[9] & 0xFFu) == '"');
+#else
             g = g && (lo & 0x80808080u) == 0x80808080u && (hi & 0x80808080u) == 0u && bs == 0u &&
                 (w[9] & 0xFFu) == '"';
+#endif
             ve = vq + 37;
             y = w[9];
         } else {
+#if YSB_BL_NOVOCAB
+            // the first quote, backslash or control byte of the value's first 20 bytes
+            u32 fl = 0;
+#pragma unroll
+            for (int j = 4; j >= 0; --j) {
+                const u32 z = ft_flags(w[j]);   // the four bytes' flags as bits 0..3
+                fl = (fl << 4) | ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+            }
+            const int fq = fl ? (int)__builtin_ctz(fl) : 32;
+            const u32 qb = fq < 20 ? (w[fq >> 2] >> (8 * (fq & 3))) & 0xFFu : 0u;
+            int la = (fq < 20 && qb == '"') ? fq : 0;
+#elif YSB_BL_VANY
+            int la = vocab_len_any(id, w);
+#else
             int la = id == K_ADTYPE ? vocab_len<3>(w) : id == K_ETYPE ? vocab_len<4>(w)
                    : id == K_ETIME ? vocab_len<5>(w) : id == K_IP ? vocab_len<6>(w) : 0;
+#endif
             if (__builtin_expect(g && la == 0, 0)) {  // a value outside the vocabularies
                 const int q = ft_string_end(src, vq + 1, e);
                 la = q > vq ? q - vq - 1 : 0;
             }
             g = g && la > 0;
             ve = vq + 1 + la;
+#if YSB_BL_YREG
+            if (__builtin_expect(la > 16, 0)) {
+                y = src.load4(ve);
+            } else {                                  // the 4 bytes at la from the value's words
+                const int i = la >> 2;
+                const u32 lo = i == 0 ? w[0] : i == 1 ? w[1] : i == 2 ? w[2] : i == 3 ? w[3] : w[4];
+                const u32 hi = i == 0 ? w[1] : i == 1 ? w[2] : i == 2 ? w[3] : i == 3 ? w[4] : w[5];
+                y = __builtin_amdgcn_alignbyte(hi, lo, (u32)(la & 3));
+            }
+#else
             y = src.load4(ve);
+#endif
         }
         ads = g && id == K_AD ? vq + 1 : ads;
         ets = g && id == K_ETYPE ? vq + 1 : ets;
@@ -1296,10 +1371,17 @@ __device__ __forceinline__ bool flat_parse_bl(const LdsSrc& src, int s, int e, u
         tms = g && id == K_ETIME ? vq + 1 : tms;
         tme = g && id == K_ETIME ? ve : tme;
         seen |= g ? id : 0u;
+#if YSB_BL_VANY
+        const bool n3 = (y == w4('"', ',', ' ', '"')) & (ve + 3 < e);
+        const bool n2 = ((y & 0xFFFFFFu) == (w4('"', ',', '"', 0) & 0xFFFFFFu)) & (ve + 2 < e);
+        const bool cl = ((y & 0xFFFFu) == w4('"', '}', 0, 0)) & (ve + 1 < e);
+        g = g & (n3 | n2 | cl);
+#else
         const bool n3 = y == w4('"', ',', ' ', '"') && ve + 3 < e;
         const bool n2 = (y & 0xFFFFFFu) == (w4('"', ',', '"', 0) & 0xFFFFFFu) && ve + 2 < e;
         const bool cl = (y & 0xFFFFu) == w4('"', '}', 0, 0) && ve + 1 < e;
         g = g && (n3 || n2 || cl);
+#endif
         if (act) {
             ok = g;
             closed = cl;
@@ -1308,6 +1390,122 @@ __device__ __forceinline__ bool flat_parse_bl(const LdsSrc& src, int s, int e, u
     }
     const u32 need = require | K_AD | K_ETYPE | K_ETIME;
     if (!(ok && closed && (seen & need) == need)) return false;
+    ad = Span{ads, ads + 36, 0};
+    et = Span{ets, ete, 0};
+    tm = Span{tms, tme, 0};
+    load_span(src, ads, adw);
+    return true;
+}
+
+// flat_parse_bl with its per-lane conditions as u32 values instead of bools (YSB_FLAT_BL 2).
+// A bool is a lane mask in scalar registers: every && / || / ! of two bools is a scalar
+// instruction, and every bool carried across the loop's blocks is merged by three more --
+// issue slots the wave spends beside its VALU work.  Here a pair's checks OR into one u32
+// (`bad`: 0 = the pair is in the common forms), the lane state is a u32 (1 open, 2 closed,
+// 0 out: the caller's flat_parse_lds decides the line) and each decision is one compare.
+__device__ __forceinline__ int bl2_vocab(u32 id, const u32 (&A)[10]) {
+    int la = 0;
+    if (id == K_ADTYPE) {
+        const u32 dBN = (A[0] ^ w4('b', 'a', 'n', 'n')) | ((A[1] ^ w4('e', 'r', '"', 0)) & 0xFFFFFFu);
+        const u32 dML = (A[0] ^ w4('m', 'a', 'i', 'l')) | ((A[1] ^ '"') & 0xFFu);
+        const u32 dMD = (A[0] ^ w4('m', 'o', 'd', 'a')) | ((A[1] ^ w4('l', '"', 0, 0)) & 0xFFFFu);
+        const u32 dMB = (A[0] ^ w4('m', 'o', 'b', 'i')) | ((A[1] ^ w4('l', 'e', '"', 0)) & 0xFFFFFFu);
+        const u32 dSP = (A[0] ^ w4('s', 'p', 'o', 'n')) | (A[1] ^ w4('s', 'o', 'r', 'e')) | (A[2] ^ w4('d', '-', 's', 'e')) |
+                        (A[3] ^ w4('a', 'r', 'c', 'h')) | ((A[4] ^ '"') & 0xFFu);
+        la = dBN == 0u ? 6 : dML == 0u ? 4 : dMD == 0u ? 5 : dMB == 0u ? 6 : dSP == 0u ? 16 : 0;
+    } else if (id == K_ETYPE) {
+        const u32 dV = (A[0] ^ w4('v', 'i', 'e', 'w')) | ((A[1] ^ '"') & 0xFFu);
+        const u32 dC = (A[0] ^ w4('c', 'l', 'i', 'c')) | ((A[1] ^ w4('k', '"', 0, 0)) & 0xFFFFu);
+        const u32 dP = (A[0] ^ w4('p', 'u', 'r', 'c')) | (A[1] ^ w4('h', 'a', 's', 'e')) | ((A[2] ^ '"') & 0xFFu);
+        la = dV == 0u ? 4 : dC == 0u ? 5 : dP == 0u ? 8 : 0;
+    } else if (id == K_ETIME) {
+        u32 bad = 0;
+        swar_digits4(A[0], bad);
+        swar_digits4(A[1], bad);
+        swar_digits4(A[2], bad);
+        bad |= (((A[3] & 0xFFu) - '0') > 9u ? 1u : 0u) | (((A[3] >> 8) & 0xFFu) ^ '"');
+        la = bad == 0u ? 13 : 0;
+    } else if (id == K_IP) {
+        la = ((A[0] ^ w4('1', '.', '2', '.')) | (A[1] ^ w4('3', '.', '4', '"'))) == 0u ? 7 : 0;
+    }
+    return la;
+}
+
+__device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, u32 require, Span& ad, Span& et,
+                                               Span& tm, u32 (&adw)[9]) {
+    // (u32)(a - b) >> 31: 1 when a < b (positions < 2^31)
+    u32 st = (((src.load4(s) & 0xFFFFu) ^ w4('{', '"', 0, 0)) | ((u32)(e - 2 - s) >> 31)) == 0u ? 1u : 0u;
+    int kq = s + 1;
+    u32 seen = 0;
+    int ads = s, ets = s, ete = s, tms = s, tme = s;
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) {
+        if (__ballot(st == 1u) == 0ull) break;
+        const u32 open = st == 1u ? 1u : 0u;
+        kq = open ? kq : s + 1;                       // an idle lane reads inside its line
+        u32 kw[4];
+        load_span(src, kq + 1, kw);
+        const u32 d7 = kw[1] ^ w4('_', 'i', 'd', '"');
+        const u32 dEV = kw[0] ^ w4('e', 'v', 'e', 'n');
+        const u32 k2 = kw[2] & 0xFFFFFFu;
+        const u32 dAD = (kw[0] ^ w4('a', 'd', '_', 'i')) | ((kw[1] ^ w4('d', '"', 0, 0)) & 0xFFFFu);
+        const u32 dUS = (kw[0] ^ w4('u', 's', 'e', 'r')) | d7;
+        const u32 dPG = (kw[0] ^ w4('p', 'a', 'g', 'e')) | d7;
+        const u32 dAT = (kw[0] ^ w4('a', 'd', '_', 't')) | (kw[1] ^ w4('y', 'p', 'e', '"'));
+        const u32 dET = dEV | (kw[1] ^ w4('t', '_', 't', 'y')) | (k2 ^ (w4('p', 'e', '"', 0) & 0xFFFFFFu));
+        const u32 dTM = dEV | (kw[1] ^ w4('t', '_', 't', 'i')) | (k2 ^ (w4('m', 'e', '"', 0) & 0xFFFFFFu));
+        const u32 dIP = (kw[0] ^ w4('i', 'p', '_', 'a')) | (kw[1] ^ w4('d', 'd', 'r', 'e')) | (k2 ^ (w4('s', 's', '"', 0) & 0xFFFFFFu));
+        const u32 id = dAD == 0u ? K_AD : dUS == 0u ? K_USER : dPG == 0u ? K_PAGE : dAT == 0u ? K_ADTYPE
+                     : dET == 0u ? K_ETYPE : dTM == 0u ? K_ETIME : dIP == 0u ? K_IP : 0u;
+        const u32 k7 = id & (K_USER | K_PAGE | K_ADTYPE);
+        const u32 x = id == K_AD ? __builtin_amdgcn_alignbyte(kw[2], kw[1], 2) : k7 ? kw[2] : __builtin_amdgcn_alignbyte(kw[3], kw[2], 3);
+        const int ke = kq + 1 + (id == K_AD ? 5 : k7 ? 7 : 10);
+        const u32 s3 = (x ^ w4(':', ' ', '"', 0)) & 0xFFFFFFu;
+        const u32 s2 = (x ^ w4(':', '"', 0, 0)) & 0xFFFFu;
+        const int vq = ke + (s3 == 0u ? 3 : 2);
+        u32 bad = min(s3, s2) | (id == 0u ? 1u : 0u) | (seen & id) | ((u32)(e - 1 - vq) >> 31);
+        u32 w[10];
+        load_span(src, vq + 1, w);
+        int ve;
+        u32 y;
+        if (id & (K_AD | K_USER | K_PAGE)) {
+            u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                lo &= w[j] + 0x53535353u;
+                hi |= w[j];
+                bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
+            }
+            bad |= ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs | ((w[9] ^ '"') & 0xFFu);
+            ve = vq + 37;
+            y = w[9];
+        } else {
+            int la = bl2_vocab(id, w);
+            if (__builtin_expect((bad | (u32)la) == 0u, 0)) {   // a value outside the vocabularies
+                const int q = ft_string_end(src, vq + 1, e);
+                la = q > vq ? q - vq - 1 : 0;
+            }
+            bad |= la == 0 ? 1u : 0u;
+            ve = vq + 1 + la;
+            y = src.load4(ve);
+        }
+        const u32 n3 = y ^ w4('"', ',', ' ', '"');
+        const u32 n2 = (y ^ w4('"', ',', '"', 0)) & 0xFFFFFFu;
+        const u32 cl = (y ^ w4('"', '}', 0, 0)) & 0xFFFFu;
+        const int nk = n3 == 0u ? ve + 3 : n2 == 0u ? ve + 2 : ve + 1;   // the next key's quote / the '}'
+        bad |= (n3 == 0u || n2 == 0u || cl == 0u) ? ((u32)(e - 1 - nk) >> 31) : 1u;
+        const u32 idg = (open != 0u && bad == 0u) ? id : 0u;
+        ads = idg == K_AD ? vq + 1 : ads;
+        ets = idg == K_ETYPE ? vq + 1 : ets;
+        ete = idg == K_ETYPE ? ve : ete;
+        tms = idg == K_ETIME ? vq + 1 : tms;
+        tme = idg == K_ETIME ? ve : tme;
+        seen |= idg;
+        st = open == 0u ? st : bad != 0u ? 0u : cl == 0u ? 2u : 1u;
+        kq = nk;
+    }
+    const u32 need = require | K_AD | K_ETYPE | K_ETIME;
+    if (((st ^ 2u) | ((seen & need) ^ need)) != 0u) return false;
     ad = Span{ads, ads + 36, 0};
     et = Span{ets, ete, 0};
     tm = Span{tms, tme, 0};
@@ -1374,7 +1572,10 @@ __device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 requ
         u32 adw[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) adw[k] = 0u;
-#if YSB_FLAT_BL
+#if YSB_FLAT_BL == 2
+        okp = flat_parse_bl2(src, ls, le, require, ad, et, tm, adw);
+        if (__builtin_expect(!okp, 0)) okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
+#elif YSB_FLAT_BL
         okp = flat_parse_bl(src, ls, le, require, ad, et, tm, adw);
         if (__builtin_expect(!okp, 0)) okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
 #else
@@ -1492,9 +1693,100 @@ __device__ __forceinline__ bool learned_pair(const LdsSrc& src, int& p, int e, b
     return ok;
 }
 
+#ifndef YSB_LEARN_U32
+#define YSB_LEARN_U32 1   // round 4: learned_pair's checks as one u32 (no scalar lane-mask logic, see flat_parse_bl2)
+#endif
+// learned_pair with its checks ORed into a u32 (0 = the pair is in the learned form).
+template <int KI, bool CP>
+__device__ __forceinline__ u32 learned_pair_u(const LdsSrc& src, int& p, int e, bool last, u32 (&kw)[9], int& vs,
+                                              int& ve) {
+    using K = KeyLit<KI, CP>;
+    constexpr WordTpl<4> T = K::tpl();
+    constexpr u32 SEP = CP ? w4('"', ',', '"', 0) : w4('"', ',', ' ', '"');
+    constexpr u32 SEPM = CP ? 0x00FFFFFFu : 0xFFFFFFFFu;
+    constexpr int SEPL = CP ? 3 : 4;
+    u32 kwd[4];
+    load_span(src, p, kwd);
+    u32 bad = words_diff(kwd, T);
+    const int v = p + K::LEN;
+    vs = v;
+    if constexpr (KI <= 2) {
+        u32 w[10];
+        load_span(src, v, w);
+        u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            lo &= w[j] + 0x53535353u;
+            hi |= w[j];
+            bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
+        }
+        u32 pb = ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs;
+        if (__builtin_expect(pb != 0u, 0)) {   // not UUID-like: the exact plain-string flags
+            pb = 0;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) pb |= ft_flags(w[j]);
+        }
+        bad |= pb | (last ? (w[9] ^ w4('"', '}', 0, 0)) & 0xFFFFu : (w[9] ^ SEP) & SEPM);
+        ve = v + 36;
+        if constexpr (KI == 2) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) kw[k] = w[k];
+        }
+    } else {
+        u32 A[5];
+        load_span(src, v, A);
+        u32 A10[10];
+#pragma unroll
+        for (int j = 0; j < 10; ++j) A10[j] = j < 5 ? A[j] : 0u;
+        const u32 id = KI == 3 ? K_ADTYPE : KI == 4 ? K_ETYPE : KI == 5 ? K_ETIME : K_IP;
+        const int la = bl2_vocab(id, A10);
+        ve = v + la;
+        if (__builtin_expect(la == 0, 0)) ve = ft_string_end(src, v, e);
+        bad |= (u32)(ve - v) >> 31;              // ve < v: no closing quote
+        const u32 x = src.load4(ve >= v ? ve : v);
+        bad |= last ? (x ^ w4('"', '}', 0, 0)) & 0xFFFFu : (x ^ SEP) & SEPM;
+    }
+    p = last ? ve + 1 : ve + SEPL;
+    return bad;
+}
+
 template <bool CP>
 __device__ __forceinline__ bool learned_parse(const LdsSrc& src, int s, int e, const ScanParams& P, CanonA& a,
                                               CanonB& b) {
+#if YSB_LEARN_U32
+    u32 bad = (src.load4(s) & 0xFFFFu) ^ w4('{', '"', 0, 0);
+    int p = s + 2;
+    int ets = s, ete = s, tms = s, tme = s;
+    u32 kw[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) kw[k] = 0u;
+    const int n = (int)P.learn_n;
+#pragma unroll 1
+    for (int k = 0; k < n; ++k) {
+        const bool last = k + 1 == n;
+        int vs = 0, ve = 0;
+        u32 pb;
+        switch ((P.learn_code >> (3 * k)) & 7u) {   // uniform: a scalar branch
+        case 0: pb = learned_pair_u<0, CP>(src, p, e, last, kw, vs, ve); break;
+        case 1: pb = learned_pair_u<1, CP>(src, p, e, last, kw, vs, ve); break;
+        case 2: pb = learned_pair_u<2, CP>(src, p, e, last, kw, vs, ve); break;
+        case 3: pb = learned_pair_u<3, CP>(src, p, e, last, kw, vs, ve); break;
+        case 4: pb = learned_pair_u<4, CP>(src, p, e, last, kw, vs, ve); ets = vs; ete = ve; break;
+        case 5: pb = learned_pair_u<5, CP>(src, p, e, last, kw, vs, ve); tms = vs; tme = ve; break;
+        default: pb = learned_pair_u<6, CP>(src, p, e, last, kw, vs, ve); break;
+        }
+        bad |= pb;
+        p = bad == 0u ? p : s + 2;   // a failed lane keeps reading inside its line (result ignored)
+    }
+    bad |= (u32)(e - 1 - p) >> 31;   // the '}' (every compared byte lies before it)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a.kw[k] = kw[k];
+    a.t0 = tms - s;
+    b.tlen = tme - tms;
+    load_span(src, tms, b.td);
+    b.view = ete - ets == 4 && src.load4(ets) == VIEW_W;
+    return bad == 0u;
+#else
     bool ok = (src.load4(s) & 0xFFFFu) == w4('{', '"', 0, 0);
     int p = s + 2;
     int ets = s, ete = s, tms = s, tme = s;
@@ -1527,6 +1819,7 @@ __device__ __forceinline__ bool learned_parse(const LdsSrc& src, int s, int e, c
     load_span(src, tms, b.td);
     b.view = ete - ets == 4 && src.load4(ets) == VIEW_W;
     return ok;
+#endif
 }
 
 // The deferred-line kernel's use: true = decided here (ok = counted); false = nothing
