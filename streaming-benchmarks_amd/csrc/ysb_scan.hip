@@ -1259,6 +1259,9 @@ __device__ __forceinline__ bool flat_parse_lds(const LdsSrc& src, int s, int e, 
 #ifndef YSB_BL_VANY
 #define YSB_BL_VANY 0      // A/B: flat_parse_bl's vocabularies compared with no branch (vocab_len_any)
 #endif
+#ifndef YSB_BL2_FSEARCH
+#define YSB_BL2_FSEARCH 0  // A/B: flat_parse_bl2's values outside the vocabularies by a 20-byte flag search first
+#endif
 #ifndef YSB_BL_YREG
 #define YSB_BL_YREG 0      // A/B: flat_parse_bl's separator after a short value from the value's words
 #endif
@@ -1482,8 +1485,26 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
         } else {
             int la = bl2_vocab(id, w);
             if (__builtin_expect((bad | (u32)la) == 0u, 0)) {   // a value outside the vocabularies
+#if YSB_BL2_FSEARCH
+                // its closing quote among the first 20 bytes (the first quote, backslash or
+                // control byte is a quote), else the string scan
+                u32 fl = 0;
+#pragma unroll
+                for (int j = 4; j >= 0; --j) {
+                    const u32 z = ft_flags(w[j]);
+                    fl = (fl << 4) | ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+                }
+                const int fq = fl ? (int)__builtin_ctz(fl) : 31;
+                const u32 wq = fq >> 2 == 0 ? w[0] : fq >> 2 == 1 ? w[1] : fq >> 2 == 2 ? w[2] : fq >> 2 == 3 ? w[3] : w[4];
+                la = (fq < 20 && ((wq >> (8 * (fq & 3))) & 0xFFu) == '"') ? fq : 0;
+                if (fl == 0u) {
+                    const int q = ft_string_end(src, vq + 1, e);
+                    la = q > vq ? q - vq - 1 : 0;
+                }
+#else
                 const int q = ft_string_end(src, vq + 1, e);
                 la = q > vq ? q - vq - 1 : 0;
+#endif
             }
             bad |= la == 0 ? 1u : 0u;
             ve = vq + 1 + la;
