@@ -1259,6 +1259,9 @@ __device__ __forceinline__ bool flat_parse_lds(const LdsSrc& src, int s, int e, 
 #ifndef YSB_BL_VANY
 #define YSB_BL_VANY 0      // A/B: flat_parse_bl's vocabularies compared with no branch (vocab_len_any)
 #endif
+#ifndef YSB_BL2_NOBRANCH
+#define YSB_BL2_NOBRANCH 0  // A/B: flat_parse_bl2 checks a value both ways (id, vocabulary) with no branch
+#endif
 #ifndef YSB_BL2_FSEARCH
 #define YSB_BL2_FSEARCH 0  // A/B: flat_parse_bl2's values outside the vocabularies by a 20-byte flag search first
 #endif
@@ -1471,7 +1474,32 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
         load_span(src, vq + 1, w);
         int ve;
         u32 y;
+#if YSB_BL2_NOBRANCH
+        {
+            // both value forms for every lane, no branch (lanes with different keys at this pair)
+            u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                lo &= w[j] + 0x53535353u;
+                hi |= w[j];
+                bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
+            }
+            const u32 bid = ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs | ((w[9] ^ '"') & 0xFFu);
+            int la = vocab_len_any(id, w);
+            const u32 isid = id & (K_AD | K_USER | K_PAGE);
+            if (__builtin_expect((bad | isid | (u32)la) == 0u, 0)) {   // a value outside the vocabularies
+                const int q = ft_string_end(src, vq + 1, e);
+                la = q > vq ? q - vq - 1 : 0;
+            }
+            bad |= isid ? bid : (la == 0 ? 1u : 0u);
+            ve = isid ? vq + 37 : vq + 1 + la;
+            const u32 yl = src.load4(ve);
+            y = isid ? w[9] : yl;
+        }
+        if (false) {
+#else
         if (id & (K_AD | K_USER | K_PAGE)) {
+#endif
             u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
 #pragma unroll
             for (int j = 0; j < 9; ++j) {
@@ -1482,7 +1510,11 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
             bad |= ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs | ((w[9] ^ '"') & 0xFFu);
             ve = vq + 37;
             y = w[9];
-        } else {
+        } else
+#if YSB_BL2_NOBRANCH
+        if (false)
+#endif
+        {
             int la = bl2_vocab(id, w);
             if (__builtin_expect((bad | (u32)la) == 0u, 0)) {   // a value outside the vocabularies
 #if YSB_BL2_FSEARCH
