@@ -89,13 +89,15 @@ extern "C" {
                                    layout (since ABI 3). */
 #define YSB_F_LAYOUT_AUTO 0x200u /* (the default since ABI 2; the bit is accepted and
                                    ignored) layout read from the data: every submit picks
-                                   the scan instantiation from the first line of each batch
-                                   -- host batches from the pinned slot, device batches from
-                                   a <= 288-byte sample per segment taken on the device in
-                                   stream order (ysb_submit_device) -- the
-                                   generator's layout, compact JSON, a learned key order
-                                   (the first line's order and spacing, checked in place
-                                   on every line), or the flat-object tier first.  Counts
+                                   the scan instantiation from 16 stratified lines of the
+                                   launch (since ABI 3; ABI 2: the first line) -- host
+                                   batches from the pinned slot, device batches from
+                                   <= 288-byte samples taken on the device in stream order
+                                   (ysb_submit_device) -- the generator's layout, compact
+                                   JSON, a learned key order (the sampled order and
+                                   spacing, checked in place on every line), when 12 of
+                                   the 16 agree; else (interleaved producers) the
+                                   flat-object tier first.  Counts
                                    are identical whichever runs.  The explicit hints above
                                    take precedence.  Every join-table layout: since ABI 3
                                    the HBM-resident table's serial-probe and record-mode
@@ -245,8 +247,9 @@ int         ysb_split_lines_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_
 /* Device-resident batch (HBM pointers, e.g. from ysb_device_alloc). Asynchronous.  The batch
  * must be complete when submitted, or its producer ordered before the compute stream
  * (hipStreamWaitEvent(ysb_stream(ctx), ...), or produced on that stream).  Unless
- * YSB_F_LAYOUT_FIXED, the first line of every segment is copied into pinned memory by a small
- * kernel on the compute stream (so after that producer) to pick the scan's instantiation: the
+ * YSB_F_LAYOUT_FIXED, 16 stratified lines of the launch (ABI 2: each segment's first line) are
+ * copied into pinned memory by a small kernel on the compute stream (so after that producer)
+ * to pick the scan's instantiation (12 of 16 must agree, else the flat tier first): the
  * launch's own sample when the compute stream is idle at the submit (the host waits for that
  * copy, microseconds), else the previous launch's (no wait for the device: one launch late --
  * counts never depend on the choice). */
