@@ -1089,37 +1089,6 @@ __device__ __forceinline__ int vocab_len(const u32* A) {
     }
 }
 
-// vocab_len<3..6> for a lane's key id (K_ADTYPE / K_ETYPE / K_ETIME / K_IP, else 0) with no
-// branch: every candidate compared with bitwise ands, the length selected (lanes whose
-// lines carry different keys at the same pair, and the if-chains' per-candidate blocks,
-// cost flat_parse_bl a branch and its exec-mask steps each).
-__device__ __forceinline__ int vocab_len_any(u32 id, const u32 (&A)[10]) {
-    const u32 a1l8 = A[1] & 0xFFu, a1l16 = A[1] & 0xFFFFu, a1l24 = A[1] & 0xFFFFFFu;
-    // ad_type
-    const bool t6 = (A[0] == w4('b', 'a', 'n', 'n')) & (a1l24 == (w4('e', 'r', '"', 0) & 0xFFFFFFu));
-    const bool t4 = (A[0] == w4('m', 'a', 'i', 'l')) & (a1l8 == '"');
-    const bool t5 = (A[0] == w4('m', 'o', 'd', 'a')) & (a1l16 == w4('l', '"', 0, 0));
-    const bool t6b = (A[0] == w4('m', 'o', 'b', 'i')) & (a1l24 == (w4('l', 'e', '"', 0) & 0xFFFFFFu));
-    const bool t16 = (A[0] == w4('s', 'p', 'o', 'n')) & (A[1] == w4('s', 'o', 'r', 'e')) & (A[2] == w4('d', '-', 's', 'e')) &
-                     (A[3] == w4('a', 'r', 'c', 'h')) & ((A[4] & 0xFFu) == '"');
-    const int lat = (t6 | t6b) ? 6 : t4 ? 4 : t5 ? 5 : t16 ? 16 : 0;
-    // event_type
-    const bool e4 = (A[0] == w4('v', 'i', 'e', 'w')) & (a1l8 == '"');
-    const bool e5 = (A[0] == w4('c', 'l', 'i', 'c')) & (a1l16 == w4('k', '"', 0, 0));
-    const bool e8 = (A[0] == w4('p', 'u', 'r', 'c')) & (A[1] == w4('h', 'a', 's', 'e')) & ((A[2] & 0xFFu) == '"');
-    const int lae = e4 ? 4 : e5 ? 5 : e8 ? 8 : 0;
-    // event_time: 13 digits
-    u32 bad = 0;
-    swar_digits4(A[0], bad);
-    swar_digits4(A[1], bad);
-    swar_digits4(A[2], bad);
-    bad |= ((A[3] & 0xFFu) - '0') > 9u;
-    const int lam = (bad == 0u) & (((A[3] >> 8) & 0xFFu) == '"') ? 13 : 0;
-    // ip_address
-    const int lai = (A[0] == w4('1', '.', '2', '.')) & (A[1] == w4('3', '.', '4', '"')) ? 7 : 0;
-    return id == K_ADTYPE ? lat : id == K_ETYPE ? lae : id == K_ETIME ? lam : id == K_IP ? lai : 0;
-}
-
 // Round 4: the flat-first / learned-order instantiations' flat tier on the staged LDS line
 // (flat_parse_fast's subset and decisions), with the common forms taken branch-free:
 //   * the key named from the four realigned words at its text (load_span: five aligned
@@ -1251,164 +1220,10 @@ __device__ __forceinline__ bool flat_parse_lds(const LdsSrc& src, int s, int e, 
 }
 
 #ifndef YSB_FLAT_BL
-#define YSB_FLAT_BL 2   // round 4: flat_parse_bl2 (1: flat_parse_bl) before flat_parse_lds in the flat-first / learned-order tier
+#define YSB_FLAT_BL 1   // round 4: flat_parse_bl2 before flat_parse_lds in the flat-first / learned-order tier
 #endif
-#ifndef YSB_BL_NOVOCAB
-#define YSB_BL_NOVOCAB 0   // A/B: flat_parse_bl's short values by a 20-byte flag search instead of the vocabularies
-#endif
-#ifndef YSB_BL_VANY
-#define YSB_BL_VANY 0      // A/B: flat_parse_bl's vocabularies compared with no branch (vocab_len_any)
-#endif
-#ifndef YSB_BL2_NOBRANCH
-#define YSB_BL2_NOBRANCH 0  // A/B: flat_parse_bl2 checks a value both ways (id, vocabulary) with no branch
-#endif
-#ifndef YSB_BL2_FSEARCH
-#define YSB_BL2_FSEARCH 0  // A/B: flat_parse_bl2's values outside the vocabularies by a 20-byte flag search first
-#endif
-#ifndef YSB_BL_YREG
-#define YSB_BL_YREG 0      // A/B: flat_parse_bl's separator after a short value from the value's words
-#endif
-// Round 4: flat_parse_lds's common forms with no branch per pair -- for batches whose lines
-// carry different key orders (several producers interleaved), where every per-pair branch
-// of a per-lane walk diverges.  Per pair, for every lane at once: the key named (as in
-// flat_parse_lds), `": "` / `":"`, the value -- an id as 36 plain bytes by plain36's cheap
-// test, any other value named from its vocabulary or, when it is none of them, by the
-// string scan -- and `", "` / `","` / `"}` after it; the loop runs while any lane is open
-// (a uniform exit).  A lane meets no slow step here: any other form (another key, a repeat,
-// other spacing, a value that is not 36 / vocabulary / plain, a missing field) only clears
-// its `ok`, and the caller hands the line to flat_parse_lds, which decides it.  true: the
-// line is in that common subset with every field of `require` (and the three the topology
-// reads) -- a subset of flat_parse_lds's, with the same spans.
-__device__ __forceinline__ bool flat_parse_bl(const LdsSrc& src, int s, int e, u32 require, Span& ad, Span& et,
-                                              Span& tm, u32 (&adw)[9]) {
-    bool ok = (src.load4(s) & 0xFFFFu) == w4('{', '"', 0, 0) && s + 1 < e;
-    bool closed = false;
-    int kq = s + 1;
-    u32 seen = 0;
-    int ads = s, ets = s, ete = s, tms = s, tme = s;
-#pragma unroll 1
-    for (int k = 0; k < 8; ++k) {
-        const bool act = ok && !closed;
-        if (__ballot(act) == 0ull) break;
-        if (!act) kq = s + 1;                         // an idle lane reads inside its line
-        u32 kw[4];
-        load_span(src, kq + 1, kw);
-        const bool isAD = kw[0] == w4('a', 'd', '_', 'i') && (kw[1] & 0xFFFFu) == w4('d', '"', 0, 0);
-        const bool is7 = (kw[1] == w4('_', 'i', 'd', '"') && (kw[0] == w4('u', 's', 'e', 'r') || kw[0] == w4('p', 'a', 'g', 'e'))) ||
-                         (kw[0] == w4('a', 'd', '_', 't') && kw[1] == w4('y', 'p', 'e', '"'));
-        const bool ev = kw[0] == w4('e', 'v', 'e', 'n');
-        const u32 k2 = kw[2] & 0xFFFFFFu;
-        const bool isET = ev && kw[1] == w4('t', '_', 't', 'y') && k2 == (w4('p', 'e', '"', 0) & 0xFFFFFFu);
-        const bool isTM = ev && kw[1] == w4('t', '_', 't', 'i') && k2 == (w4('m', 'e', '"', 0) & 0xFFFFFFu);
-        const bool isIP = kw[0] == w4('i', 'p', '_', 'a') && kw[1] == w4('d', 'd', 'r', 'e') && k2 == (w4('s', 's', '"', 0) & 0xFFFFFFu);
-        u32 id = isAD ? K_AD : isET ? K_ETYPE : isTM ? K_ETIME : isIP ? K_IP : 0u;
-        if (is7) id = kw[0] == w4('u', 's', 'e', 'r') ? K_USER : kw[0] == w4('p', 'a', 'g', 'e') ? K_PAGE : K_ADTYPE;
-        const u32 x = isAD ? __builtin_amdgcn_alignbyte(kw[2], kw[1], 2) : is7 ? kw[2] : __builtin_amdgcn_alignbyte(kw[3], kw[2], 3);
-        const int ke = kq + 1 + (isAD ? 5 : is7 ? 7 : 10);
-        const bool sp3 = (x & 0xFFFFFFu) == (w4(':', ' ', '"', 0) & 0xFFFFFFu);
-        const bool sp2 = (x & 0xFFFFu) == (w4(':', '"', 0, 0) & 0xFFFFu);
-        const int vq = sp3 ? ke + 3 : ke + 2;
-#if YSB_BL_VANY
-        bool g = act & (id != 0u) & (sp3 | sp2) & (vq < e) & ((seen & id) == 0u);
-#else
-        bool g = act && id != 0u && (sp3 || sp2) && vq < e && (seen & id) == 0u;
-#endif
-        u32 w[10];
-        load_span(src, vq + 1, w);
-        int ve;
-        u32 y;
-        if (id & (K_AD | K_USER | K_PAGE)) {
-            u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
-#pragma unroll
-            for (int j = 0; j < 9; ++j) {
-                lo &= w[j] + 0x53535353u;
-                hi |= w[j];
-                bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
-            }
-#if YSB_BL_VANY
-            g = g & ((lo & 0x80808080u) == 0x80808080u) & ((hi & 0x80808080u) == 0u) & (bs == 0u) &
-                ((w[9] & 0xFFu) == '"');
-#else
-            g = g && (lo & 0x80808080u) == 0x80808080u && (hi & 0x80808080u) == 0u && bs == 0u &&
-                (w[9] & 0xFFu) == '"';
-#endif
-            ve = vq + 37;
-            y = w[9];
-        } else {
-#if YSB_BL_NOVOCAB
-            // the first quote, backslash or control byte of the value's first 20 bytes
-            u32 fl = 0;
-#pragma unroll
-            for (int j = 4; j >= 0; --j) {
-                const u32 z = ft_flags(w[j]);   // the four bytes' flags as bits 0..3
-                fl = (fl << 4) | ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-            }
-            const int fq = fl ? (int)__builtin_ctz(fl) : 32;
-            const u32 qb = fq < 20 ? (w[fq >> 2] >> (8 * (fq & 3))) & 0xFFu : 0u;
-            int la = (fq < 20 && qb == '"') ? fq : 0;
-#elif YSB_BL_VANY
-            int la = vocab_len_any(id, w);
-#else
-            int la = id == K_ADTYPE ? vocab_len<3>(w) : id == K_ETYPE ? vocab_len<4>(w)
-                   : id == K_ETIME ? vocab_len<5>(w) : id == K_IP ? vocab_len<6>(w) : 0;
-#endif
-            if (__builtin_expect(g && la == 0, 0)) {  // a value outside the vocabularies
-                const int q = ft_string_end(src, vq + 1, e);
-                la = q > vq ? q - vq - 1 : 0;
-            }
-            g = g && la > 0;
-            ve = vq + 1 + la;
-#if YSB_BL_YREG
-            if (__builtin_expect(la > 16, 0)) {
-                y = src.load4(ve);
-            } else {                                  // the 4 bytes at la from the value's words
-                const int i = la >> 2;
-                const u32 lo = i == 0 ? w[0] : i == 1 ? w[1] : i == 2 ? w[2] : i == 3 ? w[3] : w[4];
-                const u32 hi = i == 0 ? w[1] : i == 1 ? w[2] : i == 2 ? w[3] : i == 3 ? w[4] : w[5];
-                y = __builtin_amdgcn_alignbyte(hi, lo, (u32)(la & 3));
-            }
-#else
-            y = src.load4(ve);
-#endif
-        }
-        ads = g && id == K_AD ? vq + 1 : ads;
-        ets = g && id == K_ETYPE ? vq + 1 : ets;
-        ete = g && id == K_ETYPE ? ve : ete;
-        tms = g && id == K_ETIME ? vq + 1 : tms;
-        tme = g && id == K_ETIME ? ve : tme;
-        seen |= g ? id : 0u;
-#if YSB_BL_VANY
-        const bool n3 = (y == w4('"', ',', ' ', '"')) & (ve + 3 < e);
-        const bool n2 = ((y & 0xFFFFFFu) == (w4('"', ',', '"', 0) & 0xFFFFFFu)) & (ve + 2 < e);
-        const bool cl = ((y & 0xFFFFu) == w4('"', '}', 0, 0)) & (ve + 1 < e);
-        g = g & (n3 | n2 | cl);
-#else
-        const bool n3 = y == w4('"', ',', ' ', '"') && ve + 3 < e;
-        const bool n2 = (y & 0xFFFFFFu) == (w4('"', ',', '"', 0) & 0xFFFFFFu) && ve + 2 < e;
-        const bool cl = (y & 0xFFFFu) == w4('"', '}', 0, 0) && ve + 1 < e;
-        g = g && (n3 || n2 || cl);
-#endif
-        if (act) {
-            ok = g;
-            closed = cl;
-            kq = n3 ? ve + 3 : ve + 2;
-        }
-    }
-    const u32 need = require | K_AD | K_ETYPE | K_ETIME;
-    if (!(ok && closed && (seen & need) == need)) return false;
-    ad = Span{ads, ads + 36, 0};
-    et = Span{ets, ete, 0};
-    tm = Span{tms, tme, 0};
-    load_span(src, ads, adw);
-    return true;
-}
-
-// flat_parse_bl with its per-lane conditions as u32 values instead of bools (YSB_FLAT_BL 2).
-// A bool is a lane mask in scalar registers: every && / || / ! of two bools is a scalar
-// instruction, and every bool carried across the loop's blocks is merged by three more --
-// issue slots the wave spends beside its VALU work.  Here a pair's checks OR into one u32
-// (`bad`: 0 = the pair is in the common forms), the lane state is a u32 (1 open, 2 closed,
-// 0 out: the caller's flat_parse_lds decides the line) and each decision is one compare.
+// vocab_len's sets for a key id known only at run time (K_ADTYPE / K_ETYPE / K_ETIME / K_IP,
+// else 0), each candidate's bytes compared as u32 differences (no bool logic, see below).
 __device__ __forceinline__ int bl2_vocab(u32 id, const u32 (&A)[10]) {
     int la = 0;
     if (id == K_ADTYPE) {
@@ -1437,6 +1252,21 @@ __device__ __forceinline__ int bl2_vocab(u32 id, const u32 (&A)[10]) {
     return la;
 }
 
+// Round 4 (YSB_FLAT_BL): flat_parse_lds's common forms with no slow branch per pair -- for
+// batches whose lines carry different key orders (several producers interleaved), where
+// every per-pair branch of a per-lane walk diverges.  Per pair, for every lane at once: the
+// key named (as in flat_parse_lds), `": "` / `":"`, the value -- an id as 36 plain bytes by
+// plain36's cheap test, any other value named from its vocabulary or, when it is none of
+// them, by the string scan -- and `", "` / `","` / `"}` after it; the loop runs while any
+// lane is open (a uniform exit).  Any other form (another key, a repeat, other spacing, a
+// value that is not 36 / vocabulary / plain, a missing field) only marks the lane out, and
+// the caller hands the line to flat_parse_lds, which decides it: a subset of its lines, the
+// same spans.
+// A bool is a lane mask in scalar registers: every && / || / ! of two bools is a scalar
+// instruction, and every bool carried across the loop's blocks is merged by three more --
+// issue slots the wave spends beside its VALU work.  Here a pair's checks OR into one u32
+// (`bad`: 0 = the pair is in the common forms), the lane state is a u32 (1 open, 2 closed,
+// 0 out: the caller's flat_parse_lds decides the line) and each decision is one compare.
 __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, u32 require, Span& ad, Span& et,
                                                Span& tm, u32 (&adw)[9]) {
     // (u32)(a - b) >> 31: 1 when a < b (positions < 2^31)
@@ -1474,32 +1304,7 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
         load_span(src, vq + 1, w);
         int ve;
         u32 y;
-#if YSB_BL2_NOBRANCH
-        {
-            // both value forms for every lane, no branch (lanes with different keys at this pair)
-            u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
-#pragma unroll
-            for (int j = 0; j < 9; ++j) {
-                lo &= w[j] + 0x53535353u;
-                hi |= w[j];
-                bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
-            }
-            const u32 bid = ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs | ((w[9] ^ '"') & 0xFFu);
-            int la = vocab_len_any(id, w);
-            const u32 isid = id & (K_AD | K_USER | K_PAGE);
-            if (__builtin_expect((bad | isid | (u32)la) == 0u, 0)) {   // a value outside the vocabularies
-                const int q = ft_string_end(src, vq + 1, e);
-                la = q > vq ? q - vq - 1 : 0;
-            }
-            bad |= isid ? bid : (la == 0 ? 1u : 0u);
-            ve = isid ? vq + 37 : vq + 1 + la;
-            const u32 yl = src.load4(ve);
-            y = isid ? w[9] : yl;
-        }
-        if (false) {
-#else
         if (id & (K_AD | K_USER | K_PAGE)) {
-#endif
             u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
 #pragma unroll
             for (int j = 0; j < 9; ++j) {
@@ -1510,33 +1315,11 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
             bad |= ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs | ((w[9] ^ '"') & 0xFFu);
             ve = vq + 37;
             y = w[9];
-        } else
-#if YSB_BL2_NOBRANCH
-        if (false)
-#endif
-        {
+        } else {
             int la = bl2_vocab(id, w);
             if (__builtin_expect((bad | (u32)la) == 0u, 0)) {   // a value outside the vocabularies
-#if YSB_BL2_FSEARCH
-                // its closing quote among the first 20 bytes (the first quote, backslash or
-                // control byte is a quote), else the string scan
-                u32 fl = 0;
-#pragma unroll
-                for (int j = 4; j >= 0; --j) {
-                    const u32 z = ft_flags(w[j]);
-                    fl = (fl << 4) | ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-                }
-                const int fq = fl ? (int)__builtin_ctz(fl) : 31;
-                const u32 wq = fq >> 2 == 0 ? w[0] : fq >> 2 == 1 ? w[1] : fq >> 2 == 2 ? w[2] : fq >> 2 == 3 ? w[3] : w[4];
-                la = (fq < 20 && ((wq >> (8 * (fq & 3))) & 0xFFu) == '"') ? fq : 0;
-                if (fl == 0u) {
-                    const int q = ft_string_end(src, vq + 1, e);
-                    la = q > vq ? q - vq - 1 : 0;
-                }
-#else
                 const int q = ft_string_end(src, vq + 1, e);
                 la = q > vq ? q - vq - 1 : 0;
-#endif
             }
             bad |= la == 0 ? 1u : 0u;
             ve = vq + 1 + la;
@@ -1625,11 +1408,8 @@ __device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 requ
         u32 adw[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) adw[k] = 0u;
-#if YSB_FLAT_BL == 2
+#if YSB_FLAT_BL
         okp = flat_parse_bl2(src, ls, le, require, ad, et, tm, adw);
-        if (__builtin_expect(!okp, 0)) okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
-#elif YSB_FLAT_BL
-        okp = flat_parse_bl(src, ls, le, require, ad, et, tm, adw);
         if (__builtin_expect(!okp, 0)) okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
 #else
         okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
