@@ -1055,6 +1055,35 @@ __device__ __forceinline__ bool plain36(const u32 (&w)[10]) {
     return f == 0u;
 }
 
+#ifndef YSB_PLAIN_XAD
+#define YSB_PLAIN_XAD 1   // round 4: plain36_bad's backslash test as an xor and an add per word (A/B +2 % flat tier)
+#endif
+// plain36's fast test as a u32 (0 = every byte of w[0..8] in [0x2D, 0x7F) and not a
+// backslash); nonzero says only that the fast test failed (the exact flags decide).
+// YSB_PLAIN_XAD: with every byte < 0x80 (the `hi` term), (w ^ 0x5C5C5C5C) + 0x7F7F7F7F sets
+// bit 7 of a byte iff it is not '\\' and w + 0x53535353 iff it is >= 0x2D, with no carry
+// between bytes -- two adds (one v_xad_u32) and two ands per word instead of a zero-byte test.
+__device__ __forceinline__ u32 plain36_bad(const u32 (&w)[10]) {
+#if YSB_PLAIN_XAD
+    u32 acc = 0xFFFFFFFFu, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        acc &= (w[j] + 0x53535353u) & ((w[j] ^ 0x5C5C5C5Cu) + 0x7F7F7F7Fu);
+        hi |= w[j];
+    }
+    return ((acc & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u);
+#else
+    u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        lo &= w[j] + 0x53535353u;
+        hi |= w[j];
+        bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
+    }
+    return ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs;
+#endif
+}
+
 // The length of a short value named from its vocabulary -- the generator's closed sets
 // (core.clj:68-69,96,181): an ad_type of the five, an event_type of the three, a 13-digit
 // event_time, ip "1.2.3.4" -- from the words at its first byte (A: >= 5 realigned words), or 0
@@ -1305,14 +1334,7 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
         int ve;
         u32 y;
         if (id & (K_AD | K_USER | K_PAGE)) {
-            u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
-#pragma unroll
-            for (int j = 0; j < 9; ++j) {
-                lo &= w[j] + 0x53535353u;
-                hi |= w[j];
-                bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
-            }
-            bad |= ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs | ((w[9] ^ '"') & 0xFFu);
+            bad |= plain36_bad(w) | ((w[9] ^ '"') & 0xFFu);
             ve = vq + 37;
             y = w[9];
         } else {
@@ -1546,14 +1568,7 @@ __device__ __forceinline__ u32 learned_pair_u(const LdsSrc& src, int& p, int e, 
     if constexpr (KI <= 2) {
         u32 w[10];
         load_span(src, v, w);
-        u32 lo = 0xFFFFFFFFu, hi = 0, bs = 0;
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-            lo &= w[j] + 0x53535353u;
-            hi |= w[j];
-            bs |= zero_bytes(w[j] ^ 0x5C5C5C5Cu);
-        }
-        u32 pb = ((lo & 0x80808080u) ^ 0x80808080u) | (hi & 0x80808080u) | bs;
+        u32 pb = plain36_bad(w);
         if (__builtin_expect(pb != 0u, 0)) {   // not UUID-like: the exact plain-string flags
             pb = 0;
 #pragma unroll
