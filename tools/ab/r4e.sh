@@ -10,4 +10,4 @@ timeout -k 10 200 python3 tools/extra_one.py config3_reorder > $O/config3_reorde
 timeout -k 10 200 python3 tools/extra_one.py mixed > $O/mixed.json 2> $O/mixed.err || exit 1
 timeout -k 10 200 python3 tools/extra_one.py reorder_flat_fixed > $O/reorder_flat_fixed.json 2> $O/reorder_flat_fixed.err || exit 1
 cat $O/reorder.json $O/config3_reorder.json $O/mixed.json $O/reorder_flat_fixed.json
-bash tools/r4d.sh
+bash tools/ab/r4d.sh
