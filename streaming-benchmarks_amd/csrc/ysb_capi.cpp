@@ -2060,6 +2060,28 @@ static int collect_xev(ysb_ctx* c) {
     return YSB_OK;
 }
 
+// The plan's ascending slot list widened to whole aligned groups of four: every run of
+// consecutive slots grows to [floor4(first), ceil4(last + 1)) (W is a power of two >= 16, so
+// the groups never pass W), so the u8 pack / unpack move each group as one u32 of the ring
+// (ysb_table.hip xpack8_kernel: a group that is not four consecutive aligned slots takes
+// per-cell steps).  An added slot held no pending count anywhere when the plan was made: it
+// sends zeros -- or, in a pipelined exchange whose plan is one call old, a count that arrived
+// since, within the width's cap like any planned slot.  At most three extra slots per run
+// end.  In place (the list has W entries); returns the new length, a multiple of 4.
+static u32 align_slot_runs(u32* slots, u32 R, u32 W) {
+    std::vector<u32> out;
+    out.reserve(R + 8);
+    for (u32 i = 0; i < R;) {
+        u32 j = i + 1;
+        while (j < R && slots[j] == slots[j - 1] + 1) ++j;
+        const u32 a = slots[i] & ~3u, b = std::min<u32>((slots[j - 1] + 4) & ~3u, W);
+        for (u32 sl = std::max<u32>(a, out.empty() ? 0u : out.back() + 1); sl < b; ++sl) out.push_back(sl);
+        i = j;
+    }
+    std::copy(out.begin(), out.end(), slots);
+    return (u32)out.size();
+}
+
 static int exchange(ysb_ctx* c, bool pipelined) {
     if (!grouped(c)) return fail(c, YSB_ERR_STATE, "ysb_group_init has not been called");
     int prc = launch_pending_raw(c);
@@ -2112,9 +2134,7 @@ static int exchange(ysb_ctx* c, bool pipelined) {
     const unsigned long long cap = width == 8 ? ~0ull / (u64)c->nranks : ((1ull << (8 * width)) - 1) / (u64)c->nranks;
     const u32 rows = c->c_pad, per = c->c_pad / (u32)c->nranks;
     const u32 nslots = R;
-    // the slot list padded to whole words (W is a power of two >= 16: R4 <= W); a pad slot
-    // sends 0 and receives nothing (ysb_table.hip XSLOT_PAD)
-    while (R % 4) slots[R++] = 0xFFFFFFFFu;
+    R = align_slot_runs(slots, R, W);
     if (R) {
         const int k = c->xk;
         c->xk ^= 1;

@@ -188,8 +188,10 @@ def test_one_rank_group_range_exchange_config3_sized():
             assert x["exchanges"] == k + 1
             assert x["last_width"] == 1, x            # ~0.2 views per cell per step
             assert 0 < x["last_buckets"] <= 128
-        per_step = 200_000 * ((x["last_buckets"] + 3) // 4 * 4)   # rows of whole words
-        assert x["bytes"] == 3 * per_step and x["ms"] > 0
+        # rows of whole aligned 4-slot groups: each run of buckets widened by < 4 slots per end
+        assert x["bytes"] % (3 * 200_000) == 0 and x["ms"] > 0
+        row = x["bytes"] // (3 * 200_000)
+        assert row % 4 == 0 and x["last_buckets"] <= row <= x["last_buckets"] + 6
         assert x["full_ring_bytes"] == 200_000 * 128 * 8
         _, _, nrec = ctx.path_time()
         assert nrec == 3                               # every launch in record mode
