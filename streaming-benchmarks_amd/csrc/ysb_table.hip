@@ -190,8 +190,9 @@ constexpr int XROW_WAVES = AUX_TPB / 64;
 template <class T>
 __device__ __forceinline__ void put_cell(void* out, u64 i, unsigned long long v) { static_cast<T*>(out)[i] = (T)v; }
 
-// The plan's slot list is padded to a multiple of 4 with 0xFFFFFFFF (any slot >= W: a cell
-// that sends 0 and receives nothing), so a packed u8 row is whole words.
+// The host widens the plan's runs of slots to aligned groups of four (ysb_capi.cpp
+// align_slot_runs), so a packed u8 row is whole words; a slot >= W in the list would be a
+// cell that sends 0 and receives nothing.
 
 // out[c][k] = pending(c, slots[k]) as `width`-byte cells, the sources zeroed -- except a
 // cell above `cap` (a pipelined exchange whose plan is one call old: the cell grew past what
