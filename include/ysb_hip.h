@@ -393,7 +393,8 @@ int         ysb_group_reduce_scatter(ysb_ctx* ctx);
  * sequence of the two calls. */
 int         ysb_group_exchange_pipelined(ysb_ctx* ctx);
 /* Exchange accounting: exchanges run, reduce-scatter input bytes this rank contributed
- * (campaign rows x the bucket count rounded up to a multiple of 4 x the cell width), device
+ * (campaign rows x the planned buckets, each run widened to aligned groups of 4 ring slots,
+ * x the cell width), device
  * time of the exchanges (HIP events: plan, all-reduce(max), read-back, pack, reduce-scatter,
  * unpack), of their part on the compute stream (critical_ms: plan to pack, plus the unpack --
  * what the launches queue behind; the reduce-scatter runs on a stream of its own beside the
