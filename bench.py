@@ -443,10 +443,16 @@ def extra_layouts(args, device, out):
     vocabulary path's generic-value branches), compact JSON and another key order -- with
     the layout read from each batch's first line (the default), with an explicit hint, and
     (_fixed) with neither."""
-    from ysb_amd import GEN_COMPACT, GEN_MIXED, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER, GenParams, YsbContext
+    from ysb_amd import (GEN_COMPACT, GEN_MIXED, GEN_MIXED_BLOCKS, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER,
+                         GenParams, YsbContext)
     for key, variant, cf, what in (("mixed_layouts", GEN_MIXED, False,
                                     "four producers interleaved line by line (the generator's layout, compact JSON, "
-                                    "reordered keys, random ip with 8 ad_types; a quarter each), no hint"),
+                                    "reordered keys, random ip with 8 ad_types; a quarter each), no hint: the "
+                                    "per-tile dispatch (layout 4), every tile mixed"),
+                                   ("mixed_blocks", GEN_MIXED_BLOCKS, False,
+                                    "the same four producers in runs of 256 events (a consumer's batches from "
+                                    "several partitions), no hint: the per-tile dispatch, a tile of one producer "
+                                    "takes that producer's path"),
                                    ("mixed_layouts_flat_tier", GEN_MIXED, "flat_fixed",
                                     "four producers interleaved line by line, YSB_F_FLAT_FIRST with YSB_F_LAYOUT_FIXED: "
                                     "the flat-object tier parses every line"),("random_ip", GEN_RANDOM_IP, False, "random dotted-quad ip_address"),

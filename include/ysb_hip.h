@@ -89,15 +89,15 @@ extern "C" {
                                    layout (since ABI 3). */
 #define YSB_F_LAYOUT_AUTO 0x200u /* (the default since ABI 2; the bit is accepted and
                                    ignored) layout read from the data: every submit picks
-                                   the scan instantiation from 16 stratified lines of the
+                                   the scan instantiation from 64 stratified lines of the
                                    launch (since ABI 3; ABI 2: the first line) -- host
                                    batches from the pinned slot, device batches from
                                    <= 288-byte samples taken on the device in stream order
                                    (ysb_submit_device) -- the generator's layout, compact
                                    JSON, a learned key order (the sampled order and
-                                   spacing, checked in place on every line), when 12 of
-                                   the 16 agree; else (interleaved producers) the
-                                   flat-object tier first.  Counts
+                                   spacing, checked in place on every line), when 46 of
+                                   the 64 agree; else (several producers) the per-tile
+                                   dispatch (layout 4).  Counts
                                    are identical whichever runs.  The explicit hints above
                                    take precedence.  Every join-table layout: since ABI 3
                                    the HBM-resident table's serial-probe and record-mode
@@ -247,9 +247,9 @@ int         ysb_split_lines_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_
 /* Device-resident batch (HBM pointers, e.g. from ysb_device_alloc). Asynchronous.  The batch
  * must be complete when submitted, or its producer ordered before the compute stream
  * (hipStreamWaitEvent(ysb_stream(ctx), ...), or produced on that stream).  Unless
- * YSB_F_LAYOUT_FIXED, 16 stratified lines of the launch (ABI 2: each segment's first line) are
+ * YSB_F_LAYOUT_FIXED, 64 stratified lines of the launch (ABI 2: each segment's first line) are
  * copied into pinned memory by a small kernel on the compute stream (so after that producer)
- * to pick the scan's instantiation (12 of 16 must agree, else the flat tier first): the
+ * to pick the scan's instantiation (46 of 64 must agree, else the per-tile dispatch): the
  * launch's own sample when the compute stream is idle at the submit (the host waits for that
  * copy, microseconds), else the previous launch's (no wait for the device: one launch late --
  * counts never depend on the choice). */
@@ -317,8 +317,8 @@ int         ysb_copy_time(ysb_ctx* ctx, double* total_ms, uint64_t* copies, uint
  * collects both), and the launches so far that used record mode. */
 int         ysb_path_time(ysb_ctx* ctx, double* total_ms, uint64_t* launches, uint64_t* record_launches);
 /* The scan instantiation the last launch ran: the JSON layout tried first (0 the
- * generator's, 1 compact JSON, 2 the flat-object tier; what layout sampling or a hint
- * chose), record-mode counting, the HBM-resident join table (bucket layout, serial
+ * generator's, 1 compact JSON, 2 the flat-object tier, 3 a learned key order, 4 the per-tile
+ * dispatch for several producers in one batch; what layout sampling or a hint chose), record-mode counting, the HBM-resident join table (bucket layout, serial
  * probes), the .tbl format -- each 0 or 1. */
 typedef struct ysb_launch_desc {
     uint32_t layout;
@@ -488,6 +488,7 @@ typedef struct ysb_gen_params {
 #define YSB_GEN_MIXED        16u  /* four producers interleaved line by line: each event's layout drawn
                                      from {the generator's, compact, reordered keys, random ip with 8
                                      ad_types}; the same events and truth */
+#define YSB_GEN_MIXED_BLOCKS 32u  /* the same four producers in runs of 256 events (drawn per run) */
 
 void        ysb_gen_default(ysb_gen_params* p);
 /* Campaign and ad UUIDs, 36 bytes each, no separators (ad a -> campaign a / ads_per_campaign). */

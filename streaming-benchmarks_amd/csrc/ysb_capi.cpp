@@ -682,7 +682,7 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     p.probe_serial = c->ctable_buckets ? 1u : 0u;
     p.layout = (c->cfg.flags & YSB_F_FLAT_FIRST) ? 2u : (c->cfg.flags & YSB_F_COMPACT_FIRST) ? 1u : 0u;
     if (c->submit_layout >= 0) p.layout = (u32)c->submit_layout;
-    if (p.layout == 3) {
+    if (p.layout == 3 || p.layout == 4) {   // (4: learn_n 0 when the sample named no learned order)
         p.learn_code = 0;
         for (u32 i = 0; i < c->submit_learn.n; ++i) p.learn_code |= c->submit_learn.order[i] << (3 * i);
         p.learn_n = c->submit_learn.n;
@@ -1016,7 +1016,15 @@ static int learn_layout(const u8* l, u64 len, u32 require_mask, LearnDesc* d) {
 // and spacing), that one; otherwise several producers are interleaved and the flat-object
 // tier, which takes every layout alike, runs first (2).  Only a choice of instantiation:
 // every instantiation counts every line exactly.
-constexpr u32 SAMPLE_LINES = 16, SAMPLE_AGREE = 12;
+// 46 of 64 (72 %): a producer writing most of the batch keeps its instantiation (its lines at
+// full speed, the others through the tiers); a batch half of one layout (four producers, two
+// of them in the generator's layout) reaches 46 of 64 in ~0.03 % of samples (with 32 lines
+// and 23 of them: 0.4 %, which a bench seed hit)
+constexpr u32 SAMPLE_LINES = 64, SAMPLE_AGREE = 46;
+static_assert(SAMPLE_LINES <= (u32)SAMPLE_MAX, "device samples: one SampleSegs entry per line");
+#ifndef YSB_MIXED_TILE
+#define YSB_MIXED_TILE 1   // round 4: a sample without a majority layout takes the per-tile dispatch (4), not the flat tier (2)
+#endif
 
 static u64 sample_index(u64 n, u32 j) {
     if (j == 0 || n <= SAMPLE_LINES) return std::min<u64>(j, n ? n - 1 : 0);
@@ -1033,6 +1041,7 @@ static int decide_layout(const ysb_ctx* c, const std::vector<std::pair<const u8*
         got.push_back({lay, lay == 3 ? di : LearnDesc{}});
     }
     if (got.empty()) return 0;
+    u32 best_learned = 0;
     for (const auto& g : got) {   // the most frequent (layout, order) of the sample
         u32 k = 0;
         for (const auto& h : got) k += h.first == g.first && std::memcmp(&h.second, &g.second, sizeof(LearnDesc)) == 0;
@@ -1040,8 +1049,19 @@ static int decide_layout(const ysb_ctx* c, const std::vector<std::pair<const u8*
             *d = g.second;
             return g.first;
         }
+        if (g.first == 3 && k > best_learned) {   // the most frequent learned order, for layout 4
+            best_learned = k;
+            *d = g.second;
+        }
     }
+#if YSB_MIXED_TILE
+    // several producers: the per-tile dispatch (4) -- tiles of one producer take its path
+    // (the learned order: the sample's most frequent one), mixed tiles the flat tier
+    if (!best_learned) *d = LearnDesc{};
+    return 4;
+#else
     return 2;
+#endif
 }
 
 // A host batch (held in the pinned slot).
@@ -1070,7 +1090,7 @@ static bool layout_sampling(const ysb_ctx* c) {
 // first unless the first line names a key order (3: the learned-order instantiation, whose
 // lines off that order go to the same flat tier).
 static int hinted_layout(const ysb_ctx* c, int sampled) {
-    if ((c->cfg.flags & YSB_F_FLAT_FIRST) && sampled >= 0 && sampled != 3) return 2;
+    if ((c->cfg.flags & YSB_F_FLAT_FIRST) && sampled >= 0 && sampled != 3 && sampled != 4) return 2;
     return sampled;
 }
 
@@ -2318,7 +2338,8 @@ static GenSpec spec_of(const ysb_gen_params* p, const u32* subset) {
 
 static bool gen_ok(const ysb_gen_params* p) {
     return p && p->n_campaigns && p->ads_per_campaign && p->events_per_sec && p->format <= YSB_GEN_TBL &&
-           p->variant <= (YSB_GEN_RANDOM_IP | YSB_GEN_MORE_AD_TYPES | YSB_GEN_COMPACT | YSB_GEN_REORDER | YSB_GEN_MIXED) &&
+           p->variant <= (YSB_GEN_RANDOM_IP | YSB_GEN_MORE_AD_TYPES | YSB_GEN_COMPACT | YSB_GEN_REORDER | YSB_GEN_MIXED |
+                          YSB_GEN_MIXED_BLOCKS) &&
            (!p->ad_subset || p->n_ad_subset) && (u64)p->n_campaigns * p->ads_per_campaign < (1ull << 32);
 }
 

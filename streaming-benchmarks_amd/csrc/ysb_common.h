@@ -107,13 +107,17 @@ enum : u32 {
     GEN_V_MIXED = 16u,         // four producers interleaved line by line: each event's layout is
                                // one of {generator, compact, reordered, random ip + 8 ad_types},
                                // drawn per event (the mutation tests' interleave, unmutated)
+    GEN_V_MIXED_BLOCKS = 32u,  // the same four producers in runs of 256 events (a consumer's
+                               // batches from several partitions): drawn per run
 };
 enum : u32 { S_IP = 9, S_MIX = 10 };
 
-// The layout variant of event i (GEN_V_MIXED: drawn per event; else the spec's).
+// The layout variant of event i (GEN_V_MIXED: drawn per event; GEN_V_MIXED_BLOCKS: per run of
+// 256 events; else the spec's).
 YSB_HD u32 event_variant(const GenSpec& s, u64 i) {
-    if (!(s.variant & GEN_V_MIXED)) return s.variant;
-    const u32 k = (u32)(draw(stream_key(s.ev_seed, S_MIX), i) >> 62);
+    if (!(s.variant & (GEN_V_MIXED | GEN_V_MIXED_BLOCKS))) return s.variant;
+    const u64 unit = (s.variant & GEN_V_MIXED_BLOCKS) ? i >> 8 : i;
+    const u32 k = (u32)(draw(stream_key(s.ev_seed, S_MIX), unit) >> 62);
     return k == 0 ? 0u : k == 1 ? (u32)GEN_V_COMPACT : k == 2 ? (u32)GEN_V_REORDER : (u32)(GEN_V_RANDOM_IP | GEN_V_MORE_AD_TYPES);
 }
 

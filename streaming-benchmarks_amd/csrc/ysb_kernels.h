@@ -238,7 +238,7 @@ hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64
 // <= SAMPLE_BYTES line bytes.
 constexpr u32 SAMPLE_BYTES = 288;   // a line of the scan's tile capacity
 constexpr u32 SAMPLE_STRIDE = 16 + SAMPLE_BYTES;
-constexpr int SAMPLE_MAX = 16;
+constexpr int SAMPLE_MAX = 64;
 struct SampleSegs {                  // per sampled line: its batch and its index there
     const u8* bytes[SAMPLE_MAX];
     const u32* off[SAMPLE_MAX];

@@ -2124,8 +2124,39 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 // a line off the learned order: the flat tier (any order or spacing)
                 if (__builtin_expect(!ok1, 0)) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb);
             }
+            else if constexpr (LAY == 4) {}   // below, once the wave's mode is known
             else if constexpr (YSB_VOCAB != 0) ok1 = vocab_stage1<LAY == 1>(lsrc, ls, le, ca);
             else ok1 = canon_stage1<false>(lsrc, ls, le, ca);
+        }
+        // LAY 4 (round 4, several producers in one batch): per-tile dispatch.  Each lane names
+        // its line's class from its first 12 bytes (the generator's `{"user_id": ` / compact
+        // `{"user_id":"` / anything else); one ballot per class makes the tile's mode, uniform
+        // in the wave: all one canonical class -> that vocabulary path, all "else" with a
+        // sampled learned order -> the learned-order parse, a tile of mixed classes -> the
+        // flat tier.  Lanes a producer's path rejects take the flat tier after it (`fl`).
+        // Tiles of one producer (producers writing in runs of lines) run at its speed.
+        int mode = 0;
+        bool fl = false;
+        if constexpr (LAY == 4) {
+            u32 cls = 0;
+            if (elig) {
+                const u32 h2 = lsrc.load4(ls + 8);
+                const bool up = lsrc.load4(ls) == w4('{', '"', 'u', 's') && lsrc.load4(ls + 4) == w4('e', 'r', '_', 'i') &&
+                                (h2 & 0xFFFFFFu) == (w4('d', '"', ':', 0) & 0xFFFFFFu);
+                cls = up && (h2 >> 24) == ' ' ? 1u : up && (h2 >> 24) == '"' ? 2u : 3u;
+            }
+            const u64 b1 = __ballot(cls == 1u), b2 = __ballot(cls == 2u), b3 = __ballot(cls == 3u);
+            mode = (b2 | b3) == 0ull ? 1 : (b1 | b3) == 0ull ? 2 : ((b1 | b2) == 0ull && P.learn_n) ? 3 : 4;
+            if (elig) {
+                if (mode == 1) ok1 = vocab_stage1<false>(lsrc, ls, le, ca);
+                else if (mode == 2) ok1 = vocab_stage1<true>(lsrc, ls, le, ca);
+                else if (mode == 3) {
+                    ok1 = P.learn_cp ? learned_parse<true>(lsrc, ls, le, P, ca, cb) : learned_parse<false>(lsrc, ls, le, P, ca, cb);
+                    fl = !ok1;
+                } else {
+                    fl = true;
+                }
+            }
         }
         bool pend = false, dfr = false, tok = false;
         i64 bucket = 0;
@@ -2133,6 +2164,12 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
         if (li < cur.count) {
             if constexpr (TBL) ok2 = ok1 && tbl_stage2(lsrc, ls, le, ca, cb);
             else if constexpr (LAY == 2 || LAY == 3) ok2 = ok1;
+            else if constexpr (LAY == 4) {
+                if (mode == 1) ok2 = ok1 && vocab_stage2<false>(lsrc, ls, le, ca, cb);
+                else if (mode == 2) ok2 = ok1 && vocab_stage2<true>(lsrc, ls, le, ca, cb);
+                else ok2 = ok1;
+                if (mode <= 2) fl = elig && !ok2;
+            }
             else if constexpr (YSB_VOCAB != 0) ok2 = ok1 && vocab_stage2<LAY == 1>(lsrc, ls, le, ca, cb);
             else ok2 = ok1 && canon_stage2<false>(lsrc, ls, le, ca, cb);
         }
@@ -2178,6 +2215,18 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
 #else
         (void)elig;
 #endif
+        if constexpr (LAY == 4) {
+            if (elig && fl) {   // the flat tier: a mixed tile's lines, and the lanes its path rejected
+                CanonA c2;
+                CanonB b2;
+                b2.view = false;
+                if (flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, c2, b2)) {
+                    ca = c2;
+                    cb = b2;
+                    ok2 = true;
+                }
+            }
+        }
         dfr = li < cur.count && !ok2;   // bad offsets, other layouts, escapes, over-size tiles
         pend = ok2 && cb.view;                                             // EventFilterBolt
         // RedisJoinBolt's lookup (36-byte keys), views only (a third of the lanes:
@@ -2669,15 +2718,18 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
             if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<true, false, true, 1>), g, b, (Geom<false, true>::LDS), s, p);
             else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<true, false, true, 2>), g, b, (Geom<false, true>::LDS), s, p);
             else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<true, false, true, 3>), g, b, (Geom<false, true>::LDS), s, p);
+            else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<true, false, true, 4>), g, b, (Geom<false, true>::LDS), s, p);
             else hipLaunchKernelGGL((scan_kernel<true, false, true>), g, b, (Geom<false, true>::LDS), s, p);
         } else if (p.probe_serial) {
             if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<true, false, false, 1>), g, b, Geom<false>::LDS, s, p);
             else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<true, false, false, 2>), g, b, Geom<false>::LDS, s, p);
             else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<true, false, false, 3>), g, b, Geom<false>::LDS, s, p);
+            else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<true, false, false, 4>), g, b, Geom<false>::LDS, s, p);
             else hipLaunchKernelGGL((scan_kernel<true, false, false>), g, b, Geom<false>::LDS, s, p);
         } else if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<false, false, false, 1>), g, b, Geom<false>::LDS, s, p);
         else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<false, false, false, 2>), g, b, Geom<false>::LDS, s, p);
         else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<false, false, false, 3>), g, b, Geom<false>::LDS, s, p);
+        else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<false, false, false, 4>), g, b, Geom<false>::LDS, s, p);
         else hipLaunchKernelGGL((scan_kernel<false, false, false>), g, b, Geom<false>::LDS, s, p);
     }
 }

@@ -202,8 +202,8 @@ class YsbContext:
         return t.value, k.value, r.value
 
     def launch_info(self):
-        """The scan instantiation of the last launch: layout (0 generator, 1 compact, 2 flat),
-        record_mode, hbm_table, tbl."""
+        """The scan instantiation of the last launch: layout (0 generator, 1 compact, 2 flat,
+        3 learned order, 4 per-tile dispatch), record_mode, hbm_table, tbl."""
         d = YsbLaunchDesc()
         self._c(lib().ysb_launch_info(self._h, C.byref(d)))
         return {n: getattr(d, n) for n, _ in YsbLaunchDesc._fields_}

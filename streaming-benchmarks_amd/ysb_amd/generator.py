@@ -12,7 +12,7 @@ from ._lib import YsbGenParams, check, lib
 
 AD_TYPES = ("banner", "modal", "sponsored-search", "mail", "mobile")   # core.clj:68
 MORE_AD_TYPES = AD_TYPES + ("native-video", "interstitial", "rewarded")  # GEN_MORE_AD_TYPES
-GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_COMPACT, GEN_REORDER, GEN_MIXED = 1, 2, 4, 8, 16
+GEN_RANDOM_IP, GEN_MORE_AD_TYPES, GEN_COMPACT, GEN_REORDER, GEN_MIXED, GEN_MIXED_BLOCKS = 1, 2, 4, 8, 16, 32
 EVENT_TYPES = ("view", "click", "purchase")                            # core.clj:69
 
 

@@ -254,3 +254,28 @@ def test_mixed_variant_interleaves_four_producers_per_event():
         assert len(m) == 1, (i, ln)
         hits[m[0]] += 1
     assert hits.min() > 800, hits
+
+
+def test_mixed_blocks_variant_runs_of_one_producer():
+    """GEN_MIXED_BLOCKS: the four producers of GEN_MIXED in runs of 256 events -- every line
+    is exactly that line of one producer's generator, one producer per run, each producer
+    running some of the runs (the same events, so the same truth)."""
+    from ysb_amd import GEN_COMPACT, GEN_MIXED_BLOCKS, GEN_MORE_AD_TYPES, GEN_RANDOM_IP, GEN_REORDER, GenParams
+
+    def lines(v):
+        raw, off = GenParams(seed=17, events_per_sec=1000, with_skew=True, variant=v).events_host(0, 8192)
+        b = raw.tobytes()
+        return [b[a:e] for a, e in zip(off, list(off[1:]) + [len(b)])]
+    mixed = lines(GEN_MIXED_BLOCKS)
+    pools = [lines(v) for v in (0, GEN_COMPACT, GEN_REORDER, GEN_RANDOM_IP | GEN_MORE_AD_TYPES)]
+    runs = []
+    for r in range(len(mixed) // 256):
+        owners = set()
+        for i in range(256 * r, 256 * (r + 1)):
+            m = [k for k in range(4) if pools[k][i] == mixed[i]]
+            assert m, (i, mixed[i])
+            owners.add(m[0] if len(m) == 1 else -1)
+        owners.discard(-1)   # a line two producers write alike (none expected)
+        assert len(owners) == 1, (r, owners)
+        runs.append(owners.pop())
+    assert len(set(runs)) == 4, runs

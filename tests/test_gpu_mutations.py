@@ -178,7 +178,7 @@ def test_hbm_table_layout_instantiations_match_oracle(first, want, rec):
     _, aids = g0.ids()
     camp = g0.ad_campaign_index()
     pick = rng.random(300_000)
-    # 94 % in the first producer's layout (the 16-line layout sample, 12 of which must agree,
+    # 94 % in the first producer's layout (the 64-line layout sample, 46 of which must agree,
     # names it), the rest from the others, 3 % edited
     lines = [pools[0][i] if pick[i] < 0.94 or i == 0 else pools[1 + (i & 1)][i] for i in range(300_000)]
     lines = [lines[0]] + mutate(lines[1:], rng, 0.03)

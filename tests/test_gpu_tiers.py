@@ -237,7 +237,7 @@ def test_learned_order_with_off_order_lines(require_ip):
         lambda ln: ln + b' trailing',                                               # text after '}'
         lambda ln: ln.replace(b'{"ad_type"', b'{ "ad_type"', 1),                    # space after '{'
     ]
-    # one line in ten off the order (the layout sample -- 16 lines, 12 must agree -- still
+    # one line in ten off the order (the layout sample -- 64 lines, 46 must agree -- still
     # names the learned order; with 4 producers interleaved it picks the flat tier instead)
     lines = [la[0]]
     for i in range(1, 4000):
@@ -427,13 +427,16 @@ def test_extra_field_edge_lines_match_oracle(hint):
             assert st[k] == v, (k, lines[0])
 
 
-def test_mixed_producers_sample_the_flat_tier():
-    """Four producers interleaved line by line (GEN_MIXED): the 16-line layout sample finds no
-    layout 12 of them agree on, so the flat-object tier (it takes every layout alike) runs
-    first -- host, device and raw batches, exact vs the oracle, nothing deferred."""
-    from ysb_amd import GEN_MIXED
+@pytest.mark.parametrize("blocks", [False, True])
+def test_mixed_producers_take_the_per_tile_dispatch(blocks):
+    """Four producers interleaved line by line (GEN_MIXED) or in runs of 256 lines
+    (GEN_MIXED_BLOCKS): the 64-line layout sample finds no layout 46 of them agree on, so the
+    per-tile dispatch runs (layout 4: a tile of one producer takes its path -- the
+    vocabulary paths, the learned order -- a mixed tile the flat tier) -- host, device and raw
+    batches, exact vs the oracle, nothing deferred."""
+    from ysb_amd import GEN_MIXED, GEN_MIXED_BLOCKS
     g = GenParams(seed=53, n_campaigns=40, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
-                  variant=GEN_MIXED)
+                  variant=GEN_MIXED_BLOCKS if blocks else GEN_MIXED)
     _, aids = g.ids()
     raw, offs = g.events_host(0, 80_000)
     exp, est = oracle.run(oracle.AdMap(aids, g.ad_campaign_index()), raw, offs)
@@ -452,7 +455,7 @@ def test_mixed_producers_sample_the_flat_tier():
                 ctx.submit(raw, offs)
             got = ctx.drain_buckets()
             st = ctx.stats()
-            assert ctx.launch_info()["layout"] == 2, how
+            assert ctx.launch_info()["layout"] == 4, how
         assert got == exp, how
         for k, v in est.items():
             assert st[k] == v, (how, k)

@@ -1,6 +1,7 @@
 """Runs one of bench.py's extra legs by itself (profiling passes, A/B runs):
     python tools/extra_one.py config3|config3_compact|config3_reorder|tbl|stream|host_staged|native_runner|
-                              reorder|reorder_fixed|reorder_flat|reorder_flat_fixed|compact|mixed|mixed_flat_fixed
+                              reorder|reorder_fixed|reorder_flat|reorder_flat_fixed|compact|mixed|mixed_flat_fixed|
+                              mixed_blocks|mixed_blocks_flat_fixed
                               [bench.py options]"""
 import json
 import os
@@ -28,13 +29,15 @@ def layout(args, variant, **kw):
 if __name__ == "__main__":
     leg = sys.argv[1]
     args = bench.parse_args(sys.argv[2:])
-    from ysb_amd import GEN_COMPACT, GEN_MIXED, GEN_REORDER
+    from ysb_amd import GEN_COMPACT, GEN_MIXED, GEN_MIXED_BLOCKS, GEN_REORDER
     fn = {"config3": lambda: bench.extra_config3(args, 0), "tbl": lambda: bench.extra_tbl(args, 0),
           "config3_compact": lambda: bench.extra_config3(args, 0, GEN_COMPACT, "compact"),
           "config3_reorder": lambda: bench.extra_config3(args, 0, GEN_REORDER, "reordered keys"),
           "host_staged": lambda: bench.extra_host_staged(args, 0),
           "native_runner": lambda: bench.extra_native_runner(args, 0, None),
           "mixed": lambda: layout(args, GEN_MIXED),
+          "mixed_blocks": lambda: layout(args, GEN_MIXED_BLOCKS),
+          "mixed_blocks_flat_fixed": lambda: layout(args, GEN_MIXED_BLOCKS, flat_first=True, layout_auto=False),
           "mixed_flat_fixed": lambda: layout(args, GEN_MIXED, flat_first=True, layout_auto=False),
           "stream": lambda: bench.extra_stream(args),
           "reorder": lambda: layout(args, GEN_REORDER),
