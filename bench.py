@@ -448,7 +448,7 @@ def extra_layouts(args, device, out):
     for key, variant, cf, what in (("mixed_layouts", GEN_MIXED, False,
                                     "four producers interleaved line by line (the generator's layout, compact JSON, "
                                     "reordered keys, random ip with 8 ad_types; a quarter each), no hint: the "
-                                    "per-tile dispatch (layout 4), every tile mixed"),
+                                    "flat tier (the sample's adjacent lines differ)"),
                                    ("mixed_blocks", GEN_MIXED_BLOCKS, False,
                                     "the same four producers in runs of 256 events (a consumer's batches from "
                                     "several partitions), no hint: the per-tile dispatch, a tile of one producer "

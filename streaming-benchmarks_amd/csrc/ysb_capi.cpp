@@ -1026,10 +1026,16 @@ static_assert(SAMPLE_LINES <= (u32)SAMPLE_MAX, "device samples: one SampleSegs e
 #define YSB_MIXED_TILE 1   // round 4: a sample without a majority layout takes the per-tile dispatch (4), not the flat tier (2)
 #endif
 
+// Sample line j: pairs of adjacent lines, one pair per stratum of [0, n) in SAMPLE_LINES / 2
+// strata (lines 0 and 1, then a hashed position in each other stratum and the line after it)
+// -- so the sample also tells producers writing in runs (adjacent lines alike) from a
+// line-by-line interleave.
 static u64 sample_index(u64 n, u32 j) {
-    if (j == 0 || n <= SAMPLE_LINES) return std::min<u64>(j, n ? n - 1 : 0);
-    const u64 a = n * j / SAMPLE_LINES, b = n * (j + 1) / SAMPLE_LINES;   // stratum j
-    return a + mix64(0x51ED27u + j) % std::max<u64>(1, b - a);
+    if (n <= SAMPLE_LINES) return std::min<u64>(j, n ? n - 1 : 0);
+    const u64 P = SAMPLE_LINES / 2, q = j >> 1;
+    const u64 a = n * q / P, b = n * (q + 1) / P;   // stratum q
+    const u64 base = q == 0 ? 0 : a + mix64(0x51ED27u + q) % std::max<u64>(1, b - a - 1);
+    return std::min<u64>(base + (j & 1u), n - 1);
 }
 
 static int decide_layout(const ysb_ctx* c, const std::vector<std::pair<const u8*, u64>>& lines, LearnDesc* d) {
@@ -1055,13 +1061,20 @@ static int decide_layout(const ysb_ctx* c, const std::vector<std::pair<const u8*
         }
     }
 #if YSB_MIXED_TILE
-    // several producers: the per-tile dispatch (4) -- tiles of one producer take its path
-    // (the learned order: the sample's most frequent one), mixed tiles the flat tier
-    if (!best_learned) *d = LearnDesc{};
-    return 4;
-#else
-    return 2;
+    // several producers.  Writing in runs (3 of 4 adjacent sample pairs alike): the per-tile
+    // dispatch (4) -- tiles of one producer take its path (the learned order: the sample's
+    // most frequent one), mixed tiles the flat tier; interleaved line by line: every tile
+    // would be mixed, so the flat tier without the dispatch (2)
+    u32 pairs = 0, alike = 0;
+    for (size_t i = 0; i + 1 < got.size(); i += 2, ++pairs)
+        alike += got[i].first == got[i + 1].first &&
+                 std::memcmp(&got[i].second, &got[i + 1].second, sizeof(LearnDesc)) == 0;
+    if (4 * alike >= 3 * pairs) {
+        if (!best_learned) *d = LearnDesc{};
+        return 4;
+    }
 #endif
+    return 2;
 }
 
 // A host batch (held in the pinned slot).
@@ -1277,14 +1290,23 @@ static int sniff_raw(const ysb_ctx* c, const u8* b, u64 nbytes, LearnDesc* d) {
         while (e < lim && b[e] != '\n' && b[e] != '\r') ++e;
         return {b + p, std::min<u64>(e + 1, nbytes) - p};
     };
-    std::vector<std::pair<const u8*, u64>> lines{line_at(0)};
-    for (u32 j = 1; j < SAMPLE_LINES; ++j) {
-        u64 p = nbytes * j / SAMPLE_LINES;
+    // pairs of adjacent lines (as sample_index): the first two, then the two after a '\n' at
+    // each other stratum's start (a lone '\r' only ends lines elsewhere)
+    auto next_start = [&](u64 p) -> u64 {   // past the '\n' at or after p (nbytes: none near)
         const u64 lim = std::min<u64>(nbytes, p + 4096);
-        while (p < lim && b[p] != '\n') ++p;   // the next line after a '\n' (a lone '\r' only ends lines elsewhere)
-        if (p + 1 >= lim) continue;
-        lines.push_back(line_at(p + 1));
+        while (p < lim && b[p] != '\n') ++p;
+        return p + 1 < lim ? p + 1 : nbytes;
+    };
+    std::vector<std::pair<const u8*, u64>> lines;
+    for (u32 q = 0; q < SAMPLE_LINES / 2; ++q) {
+        const u64 s0 = q == 0 ? 0 : next_start(nbytes * q / (SAMPLE_LINES / 2));
+        if (s0 >= nbytes) continue;
+        const u64 s1 = next_start(s0);
+        if (s1 >= nbytes) continue;   // a pair or nothing
+        lines.push_back(line_at(s0));
+        lines.push_back(line_at(s1));
     }
+    if (lines.empty()) lines.push_back(line_at(0));
     return decide_layout(c, lines, d);
 }
 

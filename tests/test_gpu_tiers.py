@@ -430,9 +430,10 @@ def test_extra_field_edge_lines_match_oracle(hint):
 @pytest.mark.parametrize("blocks", [False, True])
 def test_mixed_producers_take_the_per_tile_dispatch(blocks):
     """Four producers interleaved line by line (GEN_MIXED) or in runs of 256 lines
-    (GEN_MIXED_BLOCKS): the 64-line layout sample finds no layout 46 of them agree on, so the
-    per-tile dispatch runs (layout 4: a tile of one producer takes its path -- the
-    vocabulary paths, the learned order -- a mixed tile the flat tier) -- host, device and raw
+    (GEN_MIXED_BLOCKS): the 64-line layout sample (32 pairs of adjacent lines) finds no layout
+    46 of them agree on.  In runs (adjacent lines alike) the per-tile dispatch runs (layout 4:
+    a tile of one producer takes its path -- the vocabulary paths, the learned order -- a
+    mixed tile the flat tier); line by line, the flat tier (layout 2) -- host, device and raw
     batches, exact vs the oracle, nothing deferred."""
     from ysb_amd import GEN_MIXED, GEN_MIXED_BLOCKS
     g = GenParams(seed=53, n_campaigns=40, ads_per_campaign=10, events_per_sec=1000, with_skew=True,
@@ -455,7 +456,8 @@ def test_mixed_producers_take_the_per_tile_dispatch(blocks):
                 ctx.submit(raw, offs)
             got = ctx.drain_buckets()
             st = ctx.stats()
-            assert ctx.launch_info()["layout"] == 4, how
+            # runs: adjacent sample lines alike -> the per-tile dispatch; line by line -> the flat tier
+            assert ctx.launch_info()["layout"] == (4 if blocks else 2), how
         assert got == exp, how
         for k, v in est.items():
             assert st[k] == v, (how, k)
