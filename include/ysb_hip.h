@@ -97,7 +97,9 @@ extern "C" {
                                    JSON, a learned key order (the sampled order and
                                    spacing, checked in place on every line), when 46 of
                                    the 64 agree; else (several producers) the per-tile
-                                   dispatch (layout 4).  Counts
+                                   dispatch (layout 4) when the sample's adjacent lines
+                                   are mostly alike (producers writing in runs), the
+                                   flat-object tier (2) when they are not.  Counts
                                    are identical whichever runs.  The explicit hints above
                                    take precedence.  Every join-table layout: since ABI 3
                                    the HBM-resident table's serial-probe and record-mode
@@ -249,7 +251,7 @@ int         ysb_split_lines_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_
  * (hipStreamWaitEvent(ysb_stream(ctx), ...), or produced on that stream).  Unless
  * YSB_F_LAYOUT_FIXED, 64 stratified lines of the launch (ABI 2: each segment's first line) are
  * copied into pinned memory by a small kernel on the compute stream (so after that producer)
- * to pick the scan's instantiation (46 of 64 must agree, else the per-tile dispatch): the
+ * to pick the scan's instantiation (46 of 64 must agree, else the per-tile dispatch or the flat tier): the
  * launch's own sample when the compute stream is idle at the submit (the host waits for that
  * copy, microseconds), else the previous launch's (no wait for the device: one launch late --
  * counts never depend on the choice). */
