@@ -203,3 +203,34 @@ def test_hbm_table_layout_instantiations_match_oracle(first, want, rec):
     for k in STAT_KEYS:
         assert st[k] == est[k], (k, st[k], est[k])
     assert got == exp
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("rec", [True, False])
+def test_hbm_table_producers_in_runs_take_the_per_tile_dispatch(rec):
+    """configs[2]'s HBM-resident join table, four producers writing in runs of 256 lines
+    (GEN_MIXED_BLOCKS), 3 % of the lines edited: the per-tile dispatch instantiation of the
+    record-mode (rec) / serial-probe kernel (layout 4) -- exact vs the C oracle."""
+    from ysb_amd import GEN_MIXED_BLOCKS
+    rng = np.random.default_rng(5)
+    g = GenParams(seed=73, n_campaigns=600_000, ads_per_campaign=2, events_per_sec=1000, with_skew=True,
+                  variant=GEN_MIXED_BLOCKS)
+    _, aids = g.ids()
+    camp = g.ad_campaign_index()
+    lines = lines_of(g, 200_000)
+    lines = lines[:1] + mutate(lines[1:], rng, 0.03)
+    data = b"".join(lines)
+    offs = np.cumsum([0] + [len(x) for x in lines[:-1]]).astype(np.uint32)
+    exp, est = oracle.run(oracle.AdMap(aids, camp), data, offs, threads=8)
+    raw = np.frombuffer(data, dtype=np.uint8)
+    with YsbContext(n_campaigns=600_000, window_ring=128, record_count=rec, max_batch_bytes=raw.size + 64,
+                    max_batch_events=offs.size + 1) as ctx:
+        ctx.load_ad_map(aids, camp)
+        ctx.submit(raw, offs)
+        got = ctx.drain_buckets()
+        st = ctx.stats()
+        info = ctx.launch_info()
+        assert info["hbm_table"] == 1 and info["layout"] == 4 and info["record_mode"] == int(rec)
+    for k in STAT_KEYS:
+        assert st[k] == est[k], (k, st[k], est[k])
+    assert got == exp
