@@ -354,6 +354,14 @@ __global__ __launch_bounds__(AUX_TPB) void xpack8_kernel(unsigned long long* cou
     }
 }
 
+// Bytes of o + v (four u8 lanes) that carry out of their lane: bit 7 of each byte set where
+// the byte sum passes 255.  t holds the sums of the low seven bits, so bit 7 of t is the carry
+// INTO bit 7; the carry out of bit 7 is the majority of o7, v7 and that carry.
+__device__ __forceinline__ u32 byte_carry(u32 o, u32 v) {
+    const u32 t = (o & 0x7F7F7F7Fu) + (v & 0x7F7F7F7Fu);
+    return ((o & v) | ((o ^ v) & t)) & 0x80808080u;
+}
+
 __global__ __launch_bounds__(AUX_TPB) void xunpack8_kernel(unsigned long long* owned, u8* owned8, u32 W, u32 rows,
                                                            const u32* slots, u32 R, const u32* in) {
     const XLanes X(R, threadIdx.x & 63);
@@ -380,8 +388,7 @@ __global__ __launch_bounds__(AUX_TPB) void xunpack8_kernel(unsigned long long* o
                 for (int u = 0; u < 4; ++u) {
                     if (!v[u]) continue;
                     const u64 row = (u64)(c + u * cst) * W;
-                    const u32 t = (o[u] & 0x7F7F7F7Fu) + (v[u] & 0x7F7F7F7Fu);
-                    if ((((o[u] & v[u]) | ((o[u] | v[u]) & ~t)) & 0x80808080u) == 0u) {
+                    if (!byte_carry(o[u], v[u])) {
                         *reinterpret_cast<u32*>(owned8 + row + sk.x) = o[u] + v[u];
                         continue;
                     }
@@ -411,9 +418,8 @@ __global__ __launch_bounds__(AUX_TPB) void xunpack8_kernel(unsigned long long* o
             if (run4(sk)) {
                 u32* op = reinterpret_cast<u32*>(owned8 + row + sk.x);
                 const u32 o = *op;
-                // per-byte carry out of o + v: none -> the bytes add as one word
-                const u32 t = (o & 0x7F7F7F7Fu) + (v & 0x7F7F7F7Fu);
-                if ((((o & v) | ((o | v) & ~t)) & 0x80808080u) == 0u) {
+                // no byte of o + v carries out: the bytes add as one word
+                if (!byte_carry(o, v)) {
                     *op = o + v;
                     continue;
                 }
