@@ -143,16 +143,9 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        # this rank's GPU: LOCAL_RANK, unless the launcher left each process fewer visible
-        # devices (e.g. one per rank through HIP_VISIBLE_DEVICES): then the k-th visible one
+        # this rank's GPU: LOCAL_RANK until resolve_device() (not in a dry run: nothing here
+        # touches a GPU)
         self.device = self.local
-        try:
-            import torch
-            nvis = torch.cuda.device_count()   # counts devices without initialising one
-            if 0 < nvis <= self.local:
-                self.device = self.local % nvis
-        except Exception:
-            pass
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
@@ -161,6 +154,15 @@ class Dist:
             self.dist = dist
         if n != self.world:
             log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (n, self.world))
+
+    def resolve_device(self):
+        """LOCAL_RANK, unless the launcher left each process fewer visible devices (e.g. one per
+        rank through HIP_VISIBLE_DEVICES): then the k-th visible one -- counted by the library
+        (hipGetDeviceCount), not by torch, whose ROCm build may not see a GPU HIP sees."""
+        from ysb_amd import device_count, rank_device
+        self.n_visible = device_count()
+        self.device = rank_device(self.local, self.n_visible)
+        return self.device
 
     def barrier(self):
         if self.dist:
@@ -503,11 +505,8 @@ def extra_stream(args):
     # latency, exact vs the generator truth
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_extra
-    try:
-        import torch
-        visible = torch.cuda.device_count()
-    except Exception:   # noqa: BLE001
-        visible = 1
+    from ysb_amd import device_count
+    visible = device_count()
     ns = argparse.Namespace(shards=min(8, max(2, visible)), rate=args.stream_rate, seconds=args.stream_seconds,
                             batch_ms=20, ooo_ms=100, threads=16)
     r = bench_extra.stream_sharded(ns)
@@ -695,6 +694,7 @@ def main():
     if args.dry_run:
         dry_run(d, args)
         return
+    d.resolve_device()
     from ysb_amd import GenParams, YsbContext, shard_ads
 
     base = GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate)

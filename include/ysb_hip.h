@@ -32,8 +32,12 @@ extern "C" {
  *    ysb_sync's sticky YSB_ERR_CAPACITY, the collective ysb_ring_advance after
  *    ysb_group_init, ysb_gen_params.variant
  * 3: raw batches with the line split on the GPU (ysb_submit_raw, ysb_split_lines_device),
- *    ysb_slot_capacity, ysb_copy_time; device batches' layout sampled in stream order */
-#define YSB_ABI_VERSION 3
+ *    ysb_slot_capacity, ysb_copy_time; device batches' layout sampled in stream order
+ * 4: ysb_device_count; a busy stream's device batches take the sampled layout only when two
+ *    samples agree (else the per-tile dispatch, never a host wait for the launch queued
+ *    last); a raw batch that cannot launch is a sticky error (ysb_stream returns NULL);
+ *    raw batches hold at most max(max_batch_events, max_batch_bytes / 32) lines */
+#define YSB_ABI_VERSION 4
 
 /* status codes */
 #define YSB_OK            0
@@ -177,6 +181,10 @@ typedef struct ysb_count {
 
 int         ysb_abi_version(void);
 void        ysb_config_default(ysb_config* cfg);
+/* The HIP devices this process sees (hipGetDeviceCount; 0 when there is none or the runtime
+ * fails).  A launcher maps rank -> device with it (one context per GPU, the reference's one
+ * subtask per slot) without a framework's device query. */
+int         ysb_device_count(void);
 
 /* Replaces CampaignProcessorCommon(String)/prepare() (CampaignProcessorCommon.java:30-55)
  * and RedisJoinBolt.open() (AdvertisingTopologyNative.java:451-458). */
@@ -235,12 +243,15 @@ int         ysb_slot_capacity(ysb_ctx* ctx, uint64_t* max_bytes, uint64_t* max_e
  * (ysb_split.hip) where BufferedReader.readLine ends a line -- '\n', "\r\n" or a lone '\r';
  * a last line without a terminator is a line, a terminator that ends the batch starts none --
  * so the caller (FileBasedDataSource.run, AdvertisingTopologyNative.java:144-165) only reads
- * the file into the pinned slot (max_batch_bytes; max_batch_events does not apply).
+ * the file into the pinned slot (max_batch_bytes bytes, at most max(max_batch_events,
+ * max_batch_bytes / 32) lines: the device keeps 4 B per line start, not per byte).
  * Asynchronous and double-buffered like ysb_submit: H2D on the copy stream, the split on a
  * stream of its own; the batch's scan is launched once its line count is back, at the next
  * call on the context (the next submit, ysb_sync, ...), so a caller that fills the other slot
  * in between keeps the copy engine busy; ysb_wait(ctx, slot) before the slot's pinned buffer
- * is rewritten.  An error of that deferred launch is returned by the call that performs it. */
+ * is rewritten.  A batch that cannot launch (more lines than the slot holds: YSB_ERR_CAPACITY,
+ * or a HIP failure) is dropped, and its error is returned by the call that performs the
+ * launch and by every later call that orders work after it, until ysb_reset. */
 int         ysb_submit_raw(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes);
 /* The same split of a device-resident batch (16-byte aligned, < 4 GiB): d_off[0..*n) <- its
  * line starts (YSB_ERR_CAPACITY, *n = the lines, if more than cap).  Synchronous. */
@@ -251,10 +262,15 @@ int         ysb_split_lines_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_
  * (hipStreamWaitEvent(ysb_stream(ctx), ...), or produced on that stream).  Unless
  * YSB_F_LAYOUT_FIXED, 64 stratified lines of the launch (ABI 2: each segment's first line) are
  * copied into pinned memory by a small kernel on the compute stream (so after that producer)
- * to pick the scan's instantiation (46 of 64 must agree, else the per-tile dispatch or the flat tier): the
- * launch's own sample when the compute stream is idle at the submit (the host waits for that
- * copy, microseconds), else the previous launch's (no wait for the device: one launch late --
- * counts never depend on the choice). */
+ * to pick the scan's instantiation (46 of 64 must agree, else the per-tile dispatch or the flat
+ * tier): the launch's own sample when the compute stream is idle at the submit (the host waits
+ * for that copy, microseconds); else the previous launch's sample if the one before it decided
+ * the same (the host waits for that copy, which is queued behind the launch before the
+ * previous one -- never for the launch just queued), and the per-tile dispatch when the two
+ * disagree (producers alternating by batch: every producer's tiles still take its own path) or
+ * no earlier sample exists.  A producer that changes its layout on a busy stream therefore
+ * runs one launch through the old instantiation, then the dispatch until two samples agree;
+ * counts never depend on the choice (ysb_launch_info tells which ran). */
 int         ysb_submit_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes,
                               const uint32_t* d_line_off, uint64_t n_events);
 /* Several device-resident batches in ONE kernel launch.  Each segment is a batch as
@@ -338,7 +354,8 @@ int         ysb_launch_info(ysb_ctx* ctx, ysb_launch_desc* out);
  * rule (ip_address must be among the keys). */
 int         ysb_layout_of_line(const uint8_t* line, uint64_t len, int require_ip, uint32_t order[8],
                                uint32_t* n, uint32_t* compact);
-/* The compute stream (hipStream_t) for callers that want to order work with it. */
+/* The compute stream (hipStream_t) for callers that want to order work with it (a pending
+ * raw batch is launched first); NULL if that launch failed (ysb_last_error). */
 void*       ysb_stream(ysb_ctx* ctx);
 
 /* ---- device memory helpers (so host code needs no framework for HBM buffers) ----------- */

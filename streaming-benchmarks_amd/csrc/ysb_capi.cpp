@@ -23,6 +23,11 @@ extern "C" {
 
 int ysb_abi_version(void) { return YSB_ABI_VERSION; }
 
+int ysb_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 void ysb_config_default(ysb_config* c) {
     std::memset(c, 0, sizeof *c);
     c->time_divisor_ms = 10000;
@@ -700,6 +705,7 @@ int ysb_stats_get(ysb_ctx* c, ysb_stats* s) {
 
 int ysb_reset(ysb_ctx* c) {
     if (!c) return YSB_ERR_ARG;
+    c->raw_fail = 0;   // a raw batch that could not launch was dropped: counting starts over
     int rc = sync_streams(c);
     if (rc) return rc;
     const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
@@ -773,7 +779,9 @@ int ysb_launch_info(ysb_ctx* c, ysb_launch_desc* out) {
 
 void* ysb_stream(ysb_ctx* c) {
     if (!c) return nullptr;
-    launch_pending_raw(c);   // work the caller orders after it follows every submitted batch
+    // work the caller orders after it follows every submitted batch; NULL if one could not
+    // launch (ysb_last_error says why)
+    if (launch_pending_raw(c)) return nullptr;
     return (void*)c->s_comp;
 }
 

@@ -68,6 +68,9 @@ struct ysb_ctx {
     hipEvent_t ev_sample[2] = {nullptr, nullptr};
     u32 sample_nseg[2] = {0, 0};
     int sample_cur = 0;
+    // the layout decided from buffer k's sample (-1: not decided yet) and its key order
+    int sample_dec[2] = {-1, -1};
+    LearnDesc sample_learn[2]{};
     u32* h_used = nullptr;       // pinned: the out-of-ring map's fill level after a launch ...
     hipEvent_t ev_used = nullptr; // ... readable once this has completed
     bool used_pending = false;
@@ -75,13 +78,16 @@ struct ysb_ctx {
     // s_split after the slot's H2D, into d_roff[slot]; the scan is launched once the line
     // count is back (launch_pending_raw, at the next call), so the next H2D queues first
     hipStream_t s_split = nullptr;
-    u32* d_roff[2] = {nullptr, nullptr};        // max_batch_bytes + 1 starts per slot
+    u32* d_roff[2] = {nullptr, nullptr};        // raw_lines_cap starts per slot
+    u64 raw_lines_cap = 0;                      // lines a raw batch may hold (raw_line_cap)
     u32* d_split_chunk = nullptr;               // per-chunk counts, then bases
     u64 split_chunk_words = 0;
     unsigned long long* d_rawn = nullptr;       // [2] lines of the slot's raw batch
     unsigned long long* h_rawn = nullptr;       // pinned mirror
     hipEvent_t ev_raw[2] = {nullptr, nullptr};  // split done and its count read back
     int raw_pend = -1;                          // the slot whose raw batch awaits its launch
+    int raw_fail = 0;                           // a raw batch that could not launch: sticky until ysb_reset
+    std::string raw_fail_msg;
     u64 raw_nbytes[2] = {0, 0};
     int raw_layout[2] = {-1, -1};               // its first line's layout (sampled on the host)
     LearnDesc raw_learn[2]{};

@@ -288,12 +288,19 @@ int finish_unpack(ysb_ctx* c) {
 }
 
 // The recorded exchange timing into x_ms (plan to the end of the reduce-scatter, plus the
-// unpack) and x_crit_ms (the compute stream's share: plan to pack, plus the unpack); waits
-// for the last of them.  Call after finish_unpack.
-static int collect_xev(ysb_ctx* c) {
+// unpack) and x_crit_ms (the compute stream's share: plan to pack, plus the unpack).  Call
+// after finish_unpack.  wait: every entry, waiting for the last of them (an info request);
+// otherwise only the entries whose events have completed -- the rest stay pending, so the
+// host never waits behind the launches it has queued (the pipelined exchange's periodic fold).
+static int collect_xev(ysb_ctx* c, bool wait) {
+    size_t keep = 0;
     for (size_t i = 0; i < c->xev_used; ++i) {
-        float ms = 0, mc = 0, mu = 0;
         const auto& ev = c->xev[i];
+        if (!wait && (hipEventQuery(ev[2]) != hipSuccess || hipEventQuery(ev[4]) != hipSuccess)) {
+            std::swap(c->xev[keep++], c->xev[i]);   // pending entries keep their order
+            continue;
+        }
+        float ms = 0, mc = 0, mu = 0;
         HIPCHK(c, hipEventSynchronize(ev[2]));
         HIPCHK(c, hipEventSynchronize(ev[4]));
         HIPCHK(c, hipEventElapsedTime(&ms, ev[0], ev[2]));
@@ -302,7 +309,7 @@ static int collect_xev(ysb_ctx* c) {
         c->x_ms += ms + mu;
         c->x_crit_ms += mc + mu;
     }
-    c->xev_used = 0;
+    c->xev_used = keep;
     return YSB_OK;
 }
 
@@ -346,7 +353,7 @@ static int exchange(ysb_ctx* c, bool pipelined) {
     // ask for ysb_group_exchange_info); a pair counts only once both events were recorded
     int urc = YSB_OK;
     if (c->xev_used >= XEV_KEEP) {
-        int rc = collect_xev(c);
+        int rc = collect_xev(c, false);
         if (rc) return rc;
     }
     if (c->xev_used == c->xev.size()) {
@@ -437,7 +444,7 @@ int ysb_group_exchange_pipelined(ysb_ctx* c) { return c ? exchange(c, true) : YS
 int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
     if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
     int rc = sync_streams(c);
-    if (!rc) rc = collect_xev(c);
+    if (!rc) rc = collect_xev(c, true);
     if (rc) return rc;
     out->exchanges = c->x_count;
     out->bytes = c->x_bytes;

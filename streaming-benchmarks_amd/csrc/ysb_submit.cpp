@@ -436,10 +436,42 @@ static int hinted_layout(const ysb_ctx* c, int sampled) {
 // spreads them over a host batch), copied by sample_kernel on the compute stream -- in
 // stream order, so after whatever produced the batch there (the caller's contract: a device
 // batch is complete when submitted, or its producer is ordered before ysb_stream(ctx)) --
-// into one of two pinned buffers.  Which sample decides: this launch's own when the compute
-// stream was idle at the submit (the copy finishes in microseconds) or no earlier sample
-// exists; otherwise the previous launch's, read without waiting for the device (one launch
-// late: a producer writes one layout, and counts do not depend on the choice).
+// into one of two pinned buffers, alternating by launch.  Which layout runs:
+//  * compute stream idle at the submit: this launch's own sample (the copy takes microseconds);
+//  * busy: the previous launch's sample (queued behind the launch before it, so the host waits
+//    for that one, never for the launch it is queueing behind) -- if it and the sample before
+//    it decided the same layout (or there is no decided sample before it), that one; if they
+//    disagree (producers alternating by batch,
+//    or a producer that just changed its layout), the per-tile dispatch (4), which takes every
+//    producer's tiles at that producer's speed, until two samples agree again;
+//  * busy with no earlier sample (the first launch queued behind other work): the per-tile
+//    dispatch, without a wait.
+// So a producer that changes its layout costs one launch of the wrong instantiation and then
+// dispatch launches until it settles; counts never depend on the choice.
+static bool same_decision(int a, const LearnDesc& la, int b, const LearnDesc& lb) {
+    return a == b && (a != 3 || std::memcmp(&la, &lb, sizeof(LearnDesc)) == 0);
+}
+
+static int decide_sample(ysb_ctx* c, int k) {
+    if (c->sample_dec[k] >= 0) return YSB_OK;
+    HIPCHK(c, hipEventSynchronize(c->ev_sample[k]));
+    const u8* h = c->h_sample + (u64)k * SAMPLE_LINES * SAMPLE_STRIDE;
+    std::vector<std::pair<const u8*, u64>> lines;
+    LearnDesc d{};
+    int lay = -1;
+    for (u32 i = 0; i < c->sample_nseg[k]; ++i) {
+        const u8* sp = h + (u64)i * SAMPLE_STRIDE;
+        u32 hd[3];
+        std::memcpy(hd, sp, 12);
+        if (!hd[2]) { lay = 0; break; }   // bad offsets: the scan defers them anyway
+        lines.push_back({sp + 16, hd[1]});
+    }
+    if (lay < 0) lay = decide_layout(c, lines, &d);
+    c->sample_dec[k] = lay;
+    c->sample_learn[k] = lay == 3 || lay == 4 ? d : LearnDesc{};
+    return YSB_OK;
+}
+
 static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, LearnDesc* d) {
     const u64 buf = (u64)SAMPLE_LINES * SAMPLE_STRIDE;
     if (!c->h_sample) {
@@ -449,6 +481,15 @@ static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, L
     const bool idle = hipStreamQuery(c->s_comp) == hipSuccess;
     const int k = c->sample_cur;
     c->sample_cur ^= 1;
+    // buffer k still holds the sample of the launch before the previous one: its decision (if
+    // the copy is done -- it is whenever the previous launch waited for a sample) is the
+    // older of the two the busy rule compares
+    if (c->sample_nseg[k] && c->sample_dec[k] < 0 && hipEventQuery(c->ev_sample[k]) == hipSuccess) {
+        int rc = decide_sample(c, k);
+        if (rc) return rc;
+    }
+    const int older = c->sample_nseg[k] ? c->sample_dec[k] : -1;
+    const LearnDesc older_learn = c->sample_learn[k];
     u64 total = 0;
     for (u32 i = 0; i < nseg; ++i) total += segs[i].n_events;
     SampleSegs ss{};
@@ -467,18 +508,27 @@ static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, L
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev_sample[k], c->s_comp));
     c->sample_nseg[k] = n;
-    const int use = (!idle && c->sample_nseg[k ^ 1]) ? k ^ 1 : k;
-    HIPCHK(c, hipEventSynchronize(c->ev_sample[use]));
-    const u8* h = c->h_sample + (u64)use * buf;
-    std::vector<std::pair<const u8*, u64>> lines;
-    for (u32 i = 0; i < c->sample_nseg[use]; ++i) {
-        const u8* sp = h + (u64)i * SAMPLE_STRIDE;
-        u32 hd[3];
-        std::memcpy(hd, sp, 12);
-        if (!hd[2]) return 0;   // bad offsets: the scan defers them anyway
-        lines.push_back({sp + 16, hd[1]});
+    c->sample_dec[k] = -1;
+    int rc;
+    if (idle) {   // this launch's own sample
+        if ((rc = decide_sample(c, k))) return rc;
+        *d = c->sample_learn[k];
+        return c->sample_dec[k];
     }
-    return decide_layout(c, lines, d);
+    const int p = k ^ 1;   // the previous launch's sample
+    if (!c->sample_nseg[p]) {   // none: no wait, the dispatch
+        *d = LearnDesc{};
+        return 4;
+    }
+    if ((rc = decide_sample(c, p))) return rc;
+    // (no older decision -- the first two launches -- trusts the previous sample alone)
+    if (older < 0 || same_decision(older, older_learn, c->sample_dec[p], c->sample_learn[p])) {
+        *d = c->sample_learn[p];
+        return c->sample_dec[p];
+    }
+    // two samples disagree: the per-tile dispatch (with the newer sample's learned order, if any)
+    *d = c->sample_dec[p] == 3 || c->sample_dec[p] == 4 ? c->sample_learn[p] : LearnDesc{};
+    return 4;
 }
 
 // With YSB_F_TIMING: an event pair around a slot's H2D copy (ysb_copy_time), else none.
@@ -565,13 +615,21 @@ int ysb_wait(ysb_ctx* c, int slot) {
 
 // ---- raw batches (ysb_submit_raw): the line split on the GPU ----------------------------------
 
+// Lines a raw batch may hold: max_batch_events, or one per 32 bytes of the slot if that is
+// more (an event line is > 60 bytes; the device's line-start array is 4 B per line, not per
+// byte); at most one per byte.  A batch with more lines fails its launch (YSB_ERR_CAPACITY).
+static u64 raw_line_cap(const ysb_config& cfg) {
+    return std::min<u64>(cfg.max_batch_bytes + 1, std::max<u64>(cfg.max_batch_events, cfg.max_batch_bytes / 32) + 1);
+}
+
 static int ensure_raw(ysb_ctx* c) {
     if (c->h_rawn) return YSB_OK;
     HIPCHK(c, hipSetDevice(c->device));
+    c->raw_lines_cap = raw_line_cap(c->cfg);
     for (int s = 0; s < 2; ++s) {   // (a failed earlier attempt may have left some of these)
         hipFree(c->d_roff[s]);
         c->d_roff[s] = nullptr;
-        HIPCHK(c, hipMalloc(&c->d_roff[s], (c->cfg.max_batch_bytes + 1) * 4));   // n <= nbytes lines
+        HIPCHK(c, hipMalloc(&c->d_roff[s], c->raw_lines_cap * 4));
         if (!c->ev_raw[s]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_raw[s], hipEventDisableTiming));
     }
     if (!c->s_split) HIPCHK(c, hipStreamCreateWithFlags(&c->s_split, hipStreamNonBlocking));
@@ -588,21 +646,37 @@ static int ensure_raw(ysb_ctx* c) {
 }
 
 // The raw batch waiting for its launch (if any): its line count is back from the device
-// (ev_raw), so its scan is enqueued now -- the order of submission is kept.
+// (ev_raw), so its scan is enqueued now -- the order of submission is kept.  A batch that
+// cannot launch (more lines than raw_lines_cap, a failed enqueue) is dropped and its error
+// is sticky: every later call on the context that would order work after it returns it,
+// until ysb_reset -- counts after a lost batch are not the stream's.
 int launch_pending_raw(ysb_ctx* c) {
+    if (c->raw_fail) return fail(c, c->raw_fail, "%s", c->raw_fail_msg.c_str());
     if (c->raw_pend < 0) return YSB_OK;
     const int slot = c->raw_pend;
+    int rc = YSB_OK;
+    if (hipSetDevice(c->device) != hipSuccess || hipEventSynchronize(c->ev_raw[slot]) != hipSuccess ||
+        hipStreamWaitEvent(c->s_comp, c->ev_raw[slot], 0) != hipSuccess) {
+        rc = fail(c, YSB_ERR_HIP, "raw batch (slot %d): waiting for its line split failed", slot);
+    } else if (c->h_rawn[slot] > c->raw_lines_cap) {
+        rc = fail(c, YSB_ERR_CAPACITY, "raw batch (slot %d): %llu lines, more than the %llu its slot holds "
+                  "(max(max_batch_events, max_batch_bytes / 32))", slot, (unsigned long long)c->h_rawn[slot],
+                  (unsigned long long)c->raw_lines_cap);
+    } else {
+        const ysb_segment sg{c->d_bytes[slot], c->raw_nbytes[slot], c->d_roff[slot], c->h_rawn[slot]};
+        c->submit_layout = c->raw_layout[slot];
+        c->submit_learn = c->raw_learn[slot];
+        rc = enqueue_scan(c, &sg, 1);
+        c->submit_layout = -1;
+    }
+    // the slot's device buffers are free again once this launch (or nothing) has run
+    if (hipEventRecord(c->ev_kdone[slot], c->s_comp) != hipSuccess && !rc)
+        rc = fail(c, YSB_ERR_HIP, "hipEventRecord failed");
     c->raw_pend = -1;
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipEventSynchronize(c->ev_raw[slot]));
-    HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_raw[slot], 0));
-    const ysb_segment sg{c->d_bytes[slot], c->raw_nbytes[slot], c->d_roff[slot], c->h_rawn[slot]};
-    c->submit_layout = c->raw_layout[slot];
-    c->submit_learn = c->raw_learn[slot];
-    const int rc = enqueue_scan(c, &sg, 1);
-    c->submit_layout = -1;
-    // the slot's device buffers are free again once this launch has run
-    HIPCHK(c, hipEventRecord(c->ev_kdone[slot], c->s_comp));
+    if (rc) {
+        c->raw_fail = rc;
+        c->raw_fail_msg = c->err;
+    }
     return rc;
 }
 
@@ -667,7 +741,7 @@ int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) 
     if (nbytes) {
         // the line count goes straight to pinned memory (read at the launch)
         HIPCHK(c, launch_split_lines(c->d_bytes[slot], nbytes, c->d_split_chunk, c->d_roff[slot],
-                                     c->cfg.max_batch_bytes + 1, c->h_rawn + slot, c->s_split));
+                                     c->raw_lines_cap, c->h_rawn + slot, c->s_split));
     } else {
         c->h_rawn[slot] = 0;
     }

@@ -97,6 +97,7 @@ _PU32 = C.c_void_p
 # name -> (restype, argtypes); every function include/ysb_hip.h declares.
 SIGNATURES = {
     "ysb_abi_version": (_I, []),
+    "ysb_device_count": (_I, []),
     "ysb_config_default": (None, [C.POINTER(YsbConfig)]),
     "ysb_open": (_I, [C.POINTER(_P), _I, C.POINTER(YsbConfig)]),
     "ysb_close": (_I, [_P]),

@@ -20,6 +20,22 @@ def _ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None else C.c_void_p(0)
 
 
+def device_count():
+    """The HIP devices this process sees (ysb_device_count: hipGetDeviceCount, no framework's
+    device query -- a torch build that cannot see the GPU does not change it)."""
+    return int(lib().ysb_device_count())
+
+
+def rank_device(local_rank, n_visible):
+    """The device a rank uses (one context per GPU): its LOCAL_RANK, unless the launcher left
+    each process fewer visible devices (e.g. one per rank through HIP_VISIBLE_DEVICES): then
+    the (LOCAL_RANK mod n_visible)-th.  With none visible the local rank is kept, so the
+    context's open fails loudly instead of silently sharing device 0."""
+    if n_visible <= 0:
+        return local_rank
+    return local_rank if local_rank < n_visible else local_rank % n_visible
+
+
 class YsbContext:
     def __init__(self, device=0, n_campaigns=100, time_divisor_ms=10000, window_ring=1024,
                  max_batch_events=1 << 20, max_batch_bytes=256 << 20, ring_base_bucket=None,
@@ -209,7 +225,10 @@ class YsbContext:
         return {n: getattr(d, n) for n, _ in YsbLaunchDesc._fields_}
 
     def stream(self):
-        return lib().ysb_stream(self._h)
+        s = lib().ysb_stream(self._h)
+        if not s:   # a pending raw batch could not launch (sticky until reset)
+            raise _lib.YsbError(-3, (lib().ysb_last_error(self._h) or b"").decode())
+        return s
 
     # -- device memory -----------------------------------------------------------------
     def device_alloc(self, nbytes):

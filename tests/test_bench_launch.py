@@ -48,3 +48,21 @@ def test_bench_launcher_stops_the_ranks_when_one_fails():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--dry-run"], capture_output=True, text=True,
                        timeout=180, env=env)
     assert r.returncode == 3 and "stopping the others" in r.stderr
+
+
+def test_rank_device_mapping():
+    """LOCAL_RANK -> device (bench.Dist.resolve_device over the library's hipGetDeviceCount):
+    the local rank on a node that shows every GPU, modulo the visible ones when the launcher
+    shows each process fewer, and the local rank itself when none is visible (the context's
+    open then fails loudly instead of every rank sharing device 0)."""
+    from ysb_amd import rank_device
+    assert [rank_device(r, 8) for r in range(8)] == list(range(8))
+    assert [rank_device(r, 1) for r in range(4)] == [0, 0, 0, 0]
+    assert [rank_device(r, 2) for r in range(4)] == [0, 1, 0, 1]
+    assert rank_device(5, 0) == 5
+
+
+def test_device_count_without_a_gpu_is_zero():
+    """ysb_device_count on this CPU-only container: 0, no exception, no framework needed."""
+    from ysb_amd import device_count
+    assert device_count() == 0

@@ -86,7 +86,7 @@ def test_struct_layouts_match_ctypes(tmp_path):
 
 def test_abi_version_and_defaults():
     L = _lib.lib()
-    assert L.ysb_abi_version() == 3
+    assert L.ysb_abi_version() == 4
     cfg = _lib.YsbConfig()
     L.ysb_config_default(C.byref(cfg))
     assert cfg.time_divisor_ms == 10000          # CampaignProcessorCommon.java:28

@@ -280,3 +280,60 @@ def test_routed_escaped_ad_ids_join_on_their_shard(world):
             got.update(ctx.drain_buckets())
     assert joined == ost["joined"]
     assert dict(got) == rows
+
+
+def _buggy_word_add(o, v):
+    """Round 4's carry test in xunpack8: True when it let a byte pair add as a
+    word although the byte sum passes 255."""
+    t = (o & 0x7F) + (v & 0x7F)
+    return (((o & v) | ((o | v) & ~t)) & 0x80) == 0 and o + v > 255
+
+
+def test_owned_u8_accumulator_carries_across_exchanges_without_reads():
+    """Four complete exchanges of the same batch with NO read of the owned table in between
+    (no drain or checksum folds the u8 accumulator): ~83 views per cell and exchange, so the
+    owned bytes pass 127 and then 255 with the incoming byte below 128 -- the case round 4's
+    per-byte carry test missed (256 counts lost, one leaked into the next cell).  The drain
+    after the fourth equals 4 x the C oracle's counts; the test first checks that its own
+    cells do hit that case."""
+    from oracle import oracle
+    g, aids, camp = rank_params(1, 0, rate=2500)
+    raw, offs = g.events_host(0, 300_000)
+    rows, _ = oracle.run(oracle.AdMap(aids, camp), raw, offs)
+    hits = 0
+    for v in rows.values():
+        o = 0
+        for _ in range(4):
+            if o + v > 255:
+                hits += _buggy_word_add(o, v)
+                o = 0
+            else:
+                o += v
+    assert hits > 0 and max(rows.values()) <= 255
+    with YsbContext(device=0, n_campaigns=100, window_ring=64, max_batch_bytes=raw.size + 64,
+                    max_batch_events=offs.size + 1) as ctx:
+        ctx.load_ad_map(aids, camp)
+        ctx.group_init(0, 1, YsbContext.group_unique_id())
+        for k in range(4):
+            ctx.submit(raw, offs, slot=k & 1)
+            ctx.group_reduce_scatter()
+            assert ctx.exchange_info()["last_width"] == 1
+        assert ctx.drain_buckets() == {key: 4 * v for key, v in rows.items()}
+
+
+def test_device_count_does_not_depend_on_torch(monkeypatch):
+    """bench.py maps LOCAL_RANK -> device with the library's hipGetDeviceCount, so a torch
+    build that cannot see the GPU (seen on this pool: "No HIP GPUs are available" while HIP
+    worked) cannot put every rank on device 0."""
+    import torch
+    import bench
+    from ysb_amd import device_count
+    n = device_count()
+    assert n >= 1
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    for local in (0, n - 1, n, 3 * n + 1):
+        monkeypatch.setenv("LOCAL_RANK", str(local))
+        d = bench.Dist(1)
+        assert d.resolve_device() == (local if local < n else local % n)
+        assert d.n_visible == n

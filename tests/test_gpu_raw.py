@@ -207,7 +207,9 @@ def test_device_sample_follows_a_producer_on_another_stream():
     compute stream waits for the producer's event (hipStreamWaitEvent(ysb_stream(ctx), ...),
     the documented contract) and the batch is submitted at once.  The layout sample runs in
     stream order, so it sees the compact lines (layout 1), not the reordered-key lines the
-    buffer held before, and the counts equal the C oracle's."""
+    buffer held before, and the counts equal the C oracle's.  Since
+    ABI 4 the first launch on a busy stream takes the per-tile dispatch instead of waiting for
+    its own sample; an idle stream's launch then reads its own sample (compact: layout 1)."""
     import ctypes as C
     hip = _hip()
     D2D = 3
@@ -238,13 +240,111 @@ def test_device_sample_follows_a_producer_on_another_stream():
         assert hip.hipEventRecord(ev, side) == 0
         assert hip.hipStreamWaitEvent(C.c_void_p(ctx.stream()), ev, 0) == 0
         ctx.submit_device(d_b, int(raw_c.size), d_o, n)   # ... when the batch is submitted
-        assert ctx.launch_info()["layout"] == 1
+        # the stream is busy and no earlier sample exists: the per-tile dispatch, no host wait
+        # (ABI 4; it takes the compact lines' tiles by their own path)
+        assert ctx.launch_info()["layout"] == 4
         st = ctx.stats()
         for k, v in ost.items():
             assert st[k] == v, (k, st[k], v)
         assert ctx.drain_buckets() == rows
         assert hip.hipStreamSynchronize(side) == 0
+        ctx.reset()
+        ctx.submit_device(d_b, int(raw_c.size), d_o, n)   # idle stream: its own sample
+        assert ctx.launch_info()["layout"] == 1
+        assert ctx.drain_buckets() == rows
         hip.hipEventDestroy(ev)
         hip.hipStreamDestroy(side)
         for d in (d_b, d_o, s_b, s_o, junk):
             ctx.device_free(d)
+
+
+def _producer_batches(n):
+    """The same events as three producers write them (the generator's layout, reordered keys,
+    compact JSON), each a device batch, with the C oracle's counts of each."""
+    from ysb_amd import GEN_REORDER as R, GEN_COMPACT as CP
+    out = []
+    for v in (0, R, CP):
+        g = GenParams(seed=33, events_per_sec=2000, variant=v)
+        raw, off = g.events_host(0, n)
+        out.append((raw, off))
+    g0 = GenParams(seed=33, events_per_sec=2000)
+    _, aids = g0.ids()
+    return out, aids, g0.ad_campaign_index()
+
+
+@pytest.mark.parametrize("busy", [True, False])
+def test_alternating_producers_on_a_busy_stream(busy):
+    """Device batches whose producers alternate per batch (generator layout, reordered keys,
+    compact JSON, twice round) submitted back to back.  busy: a 2 GB memset is queued on the
+    compute stream before every submit, so each launch is decided on the previous launch's
+    sample: the first launch takes the per-tile dispatch (no earlier
+    sample, no host wait), the second the previous sample's layout (nothing older to compare),
+    every later one the dispatch (the last two samples disagree).  Idle (a sync after each
+    submit): every launch reads its own sample -- 0, 3, 1.  Counts equal the C oracle's on
+    the whole stream either way."""
+    import ctypes as C
+    hip = _hip()
+    n = 60_000
+    batches, aids, camp = _producer_batches(n)
+    seq = [0, 1, 2, 0, 1, 2]
+    allraw = b"".join(batches[i][0].tobytes() for i in seq)
+    offs, base = [], 0
+    for i in seq:
+        offs.extend(int(o) + base for o in batches[i][1])
+        base += batches[i][0].size
+    rows, ost = oracle.run(oracle.AdMap(aids, camp), allraw, offs, threads=8)
+    with make_ctx(n_campaigns=100, ads=(aids, camp)) as ctx:
+        dev = []
+        for raw, off in batches:
+            d_b, d_o = ctx.device_alloc(raw.size + 64), ctx.device_alloc(4 * n + 64)
+            ctx.h2d(d_b, raw)
+            ctx.h2d(d_o, off)
+            dev.append((d_b, int(raw.size), d_o))
+        junk_n = 2 << 30
+        junk = ctx.device_alloc(junk_n)
+        stream = C.c_void_p(ctx.stream())
+        ctx.sync()
+        layouts = []
+        for i in seq:
+            if busy:
+                assert hip.hipMemsetAsync(C.c_void_p(junk), 0, junk_n, stream) == 0
+            d_b, nb, d_o = dev[i]
+            ctx.submit_device(d_b, nb, d_o, n)
+            layouts.append(ctx.launch_info()["layout"])
+            if not busy:
+                ctx.sync()
+        st = ctx.stats()
+        got = ctx.drain_buckets()
+        for d_b, _, d_o in dev:
+            ctx.device_free(d_b)
+            ctx.device_free(d_o)
+        ctx.device_free(junk)
+    assert layouts == ([4, 0, 4, 4, 4, 4] if busy else [0, 3, 1, 0, 3, 1]), layouts
+    for k, v in ost.items():
+        assert st[k] == v, (k, st[k], v)
+    assert st["deferred"] == 0
+    assert got == rows
+
+
+def test_raw_batch_over_its_line_capacity_is_a_sticky_error():
+    """A raw batch with more lines than its slot holds (max(max_batch_events,
+    max_batch_bytes / 32): here 40,000 blank lines in a 1 MiB slot that holds 32,769) is
+    dropped at its launch with YSB_ERR_CAPACITY; the error is returned by every later call that
+    would order work after it (ysb_sync, ysb_stream gives NULL) until ysb_reset, after which
+    batches count again (a failed deferred launch was silently lost)."""
+    from ysb_amd import YsbError
+    from ysb_amd._lib import lib
+    raw, offs = gd.events("gen_s7")
+    with make_ctx(max_batch_bytes=1 << 20, max_batch_events=1000) as ctx:
+        ctx.submit_raw(b"\n" * 40_000, slot=0)
+        with pytest.raises(YsbError) as e:
+            ctx.sync()
+        assert e.value.code == -4 and "lines" in str(e.value)
+        with pytest.raises(YsbError):
+            ctx.submit(raw, offs, slot=1)
+        assert lib().ysb_stream(ctx._h) is None
+        with pytest.raises(YsbError):
+            ctx.sync()
+        ctx.reset()
+        ctx.submit_raw(raw, slot=1)
+        check_against(ctx, *gd.expected("gen_s7"))

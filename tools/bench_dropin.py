@@ -29,6 +29,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "streaming-benchmarks_amd"))
 
 import numpy as np  # noqa: E402
@@ -62,6 +63,9 @@ def host_staged(device=0, events=100_000_000, slot_mb=256, raw=False, rate=100_0
             ctx.device_free(d_o)
             sizes.append(nb)
         addr = [sc.slot_views(s)[0] for s in (0, 1)]
+        import numa_info
+        where = {"gpu": numa_info.gpu_node(device), "slot0": numa_info.placement(addr[0], sizes[0]),
+                 "slot1_pages_by_node": numa_info.page_nodes(addr[1], sizes[1])}
 
         def submit(s):
             if raw:
@@ -101,7 +105,7 @@ def host_staged(device=0, events=100_000_000, slot_mb=256, raw=False, rate=100_0
             "scan_ms_per_batch": round(kms / max(launches, 1), 4),
             "copy_busy_frac": round(cms * 1e-3 / el, 4),
             "scan_hidden_frac": round(1.0 - max(0.0, el * 1e3 - cms) / max(kms, 1e-9), 4),
-            "json_bytes_per_event": round(nbytes / n, 3),
+            "json_bytes_per_event": round(nbytes / n, 3), "placement": where,
             "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": counted,
                       "events": st["events"], "parse_errors": st["parse_errors"], "join_misses": st["join_misses"],
                       "deferred": st["deferred"]},

@@ -372,11 +372,8 @@ def stream_sharded(args):
     from ysb_amd import shard_ads
     from ysb_amd.stream import ShardedStreamingOperator, SlotContext
     n = args.shards
-    try:
-        import torch
-        ndev = max(1, torch.cuda.device_count())
-    except Exception:   # noqa: BLE001
-        ndev = 1
+    from ysb_amd import device_count
+    ndev = max(1, device_count())   # hipGetDeviceCount (torch's count may be 0 where HIP sees GPUs)
     rate = args.rate
     t0_ms = (int(time.time() * 1000) // 10000 + 1) * 10000 - 2000
     base = GenParams(seed=7, n_campaigns=100, ads_per_campaign=10, events_per_sec=rate)
