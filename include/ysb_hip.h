@@ -50,6 +50,7 @@ extern "C" {
 #define YSB_ERR_NOMEM    (-7)  /* host or device allocation failed         */
 #define YSB_ERR_DATA     (-8)  /* strict mode: the batch held records the
                                   reference would have thrown on           */
+#define YSB_PENDING        1   /* ysb_flush_end(wait = 0): not complete yet (not an error) */
 
 /* ysb_config.flags */
 #define YSB_F_TIMING       0x1u /* record HIP events around every scan launch */
@@ -112,6 +113,11 @@ extern "C" {
 #define YSB_F_LAYOUT_FIXED 0x800u /* no layout sampling: the generator's layout first (or
                                    the explicit hint); device batches are then never read
                                    by the host before their launch */
+#define YSB_F_H2D_SDMA 0x1000u   /* the slots' host-to-device copies by the DMA engine
+                                   (hipMemcpyAsync) instead of a copy kernel reading the
+                                   pinned slot (the default since ABI 4): on this pool DMA
+                                   copies run at half rate in episodes after the GPU idled
+                                   ("H2D") */
 #define YSB_F_STRICT 0x400u      /* ysb_sync (and the calls built on it) return YSB_ERR_DATA
                                    once a record the reference would have thrown on was seen
                                    (parse_errors / time_errors: JSONObject / getString /
@@ -309,6 +315,21 @@ int         ysb_sync(ysb_ctx* ctx);
  * additive, exactly like the HINCRBY they feed). */
 int         ysb_drain(ysb_ctx* ctx, int64_t bucket_lo, int64_t bucket_hi, int clear,
                       ysb_count* out, uint64_t cap, uint64_t* n_out);
+/* Asynchronous flush for streaming callers: CampaignProcessorCommon's flusher thread
+ * (CampaignProcessorCommon.java:35-55, 91-98) writes every second while records keep flowing.
+ * ysb_flush_begin enqueues, behind every batch submitted so far (a pending raw batch is launched
+ * first), the compaction of the ring's nonzero (campaign, bucket) cells of [bucket_lo,
+ * bucket_hi) straight into pinned host rows, clearing them on the device, and returns without
+ * waiting: the stream keeps running.  Up to 4 flushes may be outstanding.  ysb_flush_end
+ * returns the oldest one's rows sorted by (campaign, window): with wait = 0 it returns
+ * YSB_PENDING if the device has not reached it yet; out = NULL: *n_out = rows needed (the rows
+ * stay until they are taken).  A flush holds at most min(n_campaigns * window_ring, 2^20) rows:
+ * cells beyond that keep their counts for the next flush (*more = 1).  Counts outside the ring
+ * (the out-of-ring map and the side list) are not part of an asynchronous flush -- ysb_drain
+ * reports them; deltas are additive, so a caller that sums flushes and drains has every count
+ * exactly once.  Not after ysb_group_init (YSB_ERR_STATE). */
+int         ysb_flush_begin(ysb_ctx* ctx, int64_t bucket_lo, int64_t bucket_hi);
+int         ysb_flush_end(ysb_ctx* ctx, int wait, ysb_count* out, uint64_t cap, uint64_t* n_out, int* more);
 int         ysb_stats_get(ysb_ctx* ctx, ysb_stats* out);
 /* Zero counts, side list and stats; the ad table is kept. */
 int         ysb_reset(ysb_ctx* ctx);

@@ -114,6 +114,12 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_rawn);
     hipHostFree(c->h_rawn);
     for (auto& p : c->cev) for (hipEvent_t e : p) hipEventDestroy(e);
+    for (auto& f : c->fl) {
+        hipHostFree(f.h_rows);
+        hipHostFree(f.h_n);
+        if (f.ev) hipEventDestroy(f.ev);
+    }
+    hipFree(c->d_fl_n);
     if (c->s_split) hipStreamDestroy(c->s_split);
     if (c->s_comp) hipStreamDestroy(c->s_comp);
     if (c->s_copy) hipStreamDestroy(c->s_copy);
@@ -609,6 +615,86 @@ static int ring_rows(ysb_ctx* c, i64 blo, i64 bhi, bool clear, std::map<std::pai
     return YSB_OK;
 }
 
+// ---- asynchronous flush (CampaignProcessorCommon's flusher thread, :35-55, 91-98) --------------
+
+constexpr u64 FLUSH_MAX_ROWS = 1u << 20;
+
+int ysb_flush_begin(ysb_ctx* c, int64_t blo, int64_t bhi) {
+    if (!c) return YSB_ERR_ARG;
+    if (grouped(c)) return fail(c, YSB_ERR_STATE, "ysb_flush_begin after ysb_group_init: use ysb_drain");
+    if (c->fl_n == ysb_ctx::FLUSH_SLOTS)
+        return fail(c, YSB_ERR_STATE, "%d flushes outstanding: ysb_flush_end first", ysb_ctx::FLUSH_SLOTS);
+    int rc = launch_pending_raw(c);   // every batch submitted so far is counted before the compaction
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    const u32 W = c->cfg.window_ring;
+    const int k = (c->fl_head + c->fl_n) % ysb_ctx::FLUSH_SLOTS;
+    auto& f = c->fl[k];
+    if (!c->d_fl_n) {
+        HIPCHK(c, hipMalloc(&c->d_fl_n, 4 * ysb_ctx::FLUSH_SLOTS));
+        HIPCHK(c, hipMemset(c->d_fl_n, 0, 4 * ysb_ctx::FLUSH_SLOTS));
+    }
+    if (!f.h_rows) {   // every nonzero cell of the ring fits (up to FLUSH_MAX_ROWS)
+        f.cap = std::min<u64>((u64)c->cfg.n_campaigns * W, FLUSH_MAX_ROWS);
+        HIPCHK(c, hipHostMalloc(&f.h_rows, f.cap * sizeof(TableRow)));
+        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&f.hd_rows), f.h_rows, 0));
+        HIPCHK(c, hipHostMalloc(&f.h_n, 16));
+        HIPCHK(c, hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
+    }
+    // the ring's base: known once the first launch's auto-base is back (a copy of 16 bytes)
+    poll_ring(c);
+    if (!c->ring_known && c->ring_query_pending) {
+        HIPCHK(c, hipEventSynchronize(c->ev_ring));
+        poll_ring(c);
+    }
+    if ((rc = fold_delta(c))) return rc;   // record mode's pending bytes into the u64 ring (stream order)
+    HIPCHK(c, hipMemsetAsync(c->d_fl_n + k, 0, 4, c->s_comp));
+    if (c->ring_known) {
+        const i64 a = std::max<i64>(blo, c->ring_lo), b = std::min<i64>(bhi, c->ring_lo + (i64)W);
+        if (a < b)   // straight into the pinned rows; a cell past cap keeps its count (next flush)
+            launch_compact(c->d_counts, c->cfg.n_campaigns, W, a, (u32)(b - a), 0, false, true, f.hd_rows,
+                           c->d_fl_n + k, (u32)f.cap, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipMemcpyAsync(f.h_n, c->d_fl_n + k, 4, hipMemcpyDeviceToHost, c->s_comp));
+    HIPCHK(c, hipEventRecord(f.ev, c->s_comp));
+    c->fl_n++;
+    return YSB_OK;
+}
+
+int ysb_flush_end(ysb_ctx* c, int wait, ysb_count* out, uint64_t cap, uint64_t* n_out, int* more) {
+    if (!c || !n_out) return c ? fail(c, YSB_ERR_ARG, "n_out is NULL") : YSB_ERR_ARG;
+    if (!c->fl_n) return fail(c, YSB_ERR_STATE, "no flush begun");
+    HIPCHK(c, hipSetDevice(c->device));
+    auto& f = c->fl[c->fl_head];
+    if (!wait) {
+        const hipError_t q = hipEventQuery(f.ev);
+        if (q == hipErrorNotReady) return YSB_PENDING;
+        if (q != hipSuccess) return fail(c, YSB_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(q));
+    }
+    HIPCHK(c, hipEventSynchronize(f.ev));
+    const u64 written = *f.h_n;
+    const u64 n = std::min<u64>(written, f.cap);
+    *n_out = n;
+    if (more) *more = written > f.cap ? 1 : 0;
+    if (!out) return YSB_OK;   // (the rows stay: call again with a buffer)
+    if (cap < n) return fail(c, YSB_ERR_CAPACITY, "flush needs %llu rows, cap %llu", (unsigned long long)n,
+                             (unsigned long long)cap);
+    std::vector<TableRow> rows(f.h_rows, f.h_rows + n);
+    std::sort(rows.begin(), rows.end(), [](const TableRow& x, const TableRow& y) {
+        return x.campaign != y.campaign ? x.campaign < y.campaign : x.bucket < y.bucket;
+    });
+    for (u64 i = 0; i < n; ++i) {
+        out[i].campaign = rows[i].campaign;
+        out[i].reserved = 0;
+        out[i].window_ms = rows[i].bucket * c->cfg.time_divisor_ms;
+        out[i].count = rows[i].count;
+    }
+    c->fl_head = (c->fl_head + 1) % ysb_ctx::FLUSH_SLOTS;
+    c->fl_n--;
+    return YSB_OK;
+}
+
 int ysb_drain(ysb_ctx* c, int64_t blo, int64_t bhi, int clear, ysb_count* out, uint64_t cap, uint64_t* n_out) {
     if (!c || !n_out) return c ? fail(c, YSB_ERR_ARG, "n_out is NULL") : YSB_ERR_ARG;
     int rc = ysb_sync(c);
@@ -708,6 +794,7 @@ int ysb_reset(ysb_ctx* c) {
     c->raw_fail = 0;   // a raw batch that could not launch was dropped: counting starts over
     int rc = sync_streams(c);
     if (rc) return rc;
+    c->fl_head = c->fl_n = 0;   // outstanding asynchronous flushes are dropped
     const u64 cells = (u64)c->c_pad * c->cfg.window_ring;
     HIPCHK(c, hipMemset(c->d_counts, 0, cells * 8));
     if (c->d_delta) HIPCHK(c, hipMemset(c->d_delta, 0, c->delta_cells));

@@ -130,6 +130,8 @@ struct ysb_ctx {
     // slots
     u8* h_bytes[2] = {nullptr, nullptr};
     u32* h_off[2] = {nullptr, nullptr};
+    u8* hd_bytes[2] = {nullptr, nullptr};      // the pinned slots' device-visible addresses (the CU copy)
+    u32* hd_off[2] = {nullptr, nullptr};
     u8* d_bytes[2] = {nullptr, nullptr};
     u32* d_off[2] = {nullptr, nullptr};
     hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_kdone[2] = {nullptr, nullptr};
@@ -203,6 +205,20 @@ struct ysb_ctx {
     // unpack start, unpack end (compute stream)}
     std::vector<std::array<hipEvent_t, 5>> xev;
     size_t xev_used = 0;
+    // asynchronous flushes (ysb_flush_begin / ysb_flush_end): a ring of FLUSH_SLOTS pinned row
+    // buffers the compaction kernel writes straight into, each with its device-side count
+    // copied back and an event; fl_head the oldest outstanding, fl_n how many
+    struct FlushSlot {
+        TableRow* h_rows = nullptr;   // pinned (device-visible: written by the kernel)
+        TableRow* hd_rows = nullptr;  // ... its device address
+        u32* h_n = nullptr;           // pinned: the rows the kernel wrote
+        u64 cap = 0;
+        hipEvent_t ev = nullptr;
+    };
+    static constexpr int FLUSH_SLOTS = 4;
+    FlushSlot fl[FLUSH_SLOTS];
+    int fl_head = 0, fl_n = 0;
+    u32* d_fl_n = nullptr;                 // [FLUSH_SLOTS] device counters
     // truth
     unsigned long long* d_truth = nullptr;
     unsigned long long* d_truth_out = nullptr;

@@ -230,6 +230,8 @@ void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_
 // the line starts of b[0, nbytes) (b 16-byte aligned, nbytes < 4 GiB), *d_n <- n.  chunk:
 // split_chunks(nbytes) u32 of scratch.  Asynchronous on s.
 u64 split_chunks(u64 nbytes);
+// the slots' host -> device copy by a kernel (ysb_split.hip): src a device-visible pinned host pointer
+void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t s);
 hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64 cap, unsigned long long* d_n,
                               hipStream_t s);
 // Layout sampling of device launches: sampled lines (spread over the launch's segments),

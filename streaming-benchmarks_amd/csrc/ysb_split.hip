@@ -28,6 +28,42 @@ constexpr int SPLIT_STEPS = 16;                                   // 16-byte vec
 constexpr u64 SPLIT_CHUNK = (u64)SPLIT_TPB * 16 * SPLIT_STEPS;    // 64 KiB
 constexpr int SPLIT_PREFIX_TPB = 1024;
 
+// ---- host -> device copy by the CUs (the slots' H2D) ---------------------------------------
+// A pinned host slot is visible to the device at its own address (hipHostMalloc); this kernel
+// streams it into HBM with 16-byte nontemporal loads and stores, H2D_UNROLL vectors in flight
+// per lane.  Why not the DMA engine (hipMemcpyAsync): measured on this pool
+// (profiles/r05_h2d_*), SDMA copies of a slot run at 56.5 GB/s or at exactly half that in
+// episodes that follow a stretch of GPU idleness and last until compute work wakes the chip
+// (the drop-in path's one short scan per 4.5 ms copy does not); a copy done by the CUs keeps
+// the GPU active and ran at 55-56 GB/s in every measurement, episodes included.
+constexpr int H2D_TPB = 256, H2D_UNROLL = 4;
+
+typedef u32 h2d_v4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(H2D_TPB) void h2d_copy_kernel(const h2d_v4* __restrict__ src, h2d_v4* __restrict__ dst,
+                                                           u64 vecs) {
+    const u64 stride = (u64)gridDim.x * H2D_TPB;
+    u64 i = (u64)blockIdx.x * H2D_TPB + threadIdx.x;
+    for (; i + (H2D_UNROLL - 1) * stride < vecs; i += H2D_UNROLL * stride) {
+        h2d_v4 v[H2D_UNROLL];
+#pragma unroll
+        for (int u = 0; u < H2D_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < H2D_UNROLL; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+    }
+    for (; i < vecs; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+// bytes rounded up to whole 16-byte vectors: both buffers have >= 64 bytes of slack
+void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t s) {
+    const u64 vecs = (bytes + 15) / 16;
+    if (!vecs) return;
+    // one workgroup per CU (4 waves): ~4 MiB in flight, far above PCIe's bandwidth x latency
+    const u64 grid = std::max<u64>(1, std::min<u64>((u64)cus, (vecs + H2D_TPB - 1) / H2D_TPB));
+    hipLaunchKernelGGL(h2d_copy_kernel, dim3((unsigned)grid), dim3(H2D_TPB), 0, s, static_cast<const h2d_v4*>(src),
+                       static_cast<h2d_v4*>(dst), vecs);
+}
+
 u64 split_chunks(u64 nbytes) { return (nbytes + SPLIT_CHUNK - 1) / SPLIT_CHUNK; }
 
 // high bit of every zero byte of x (exact, no carries between bytes)

@@ -553,8 +553,19 @@ static int ensure_slots(ysb_ctx* c) {
         HIPCHK(c, hipHostMalloc(&c->h_off[s], c->cfg.max_batch_events * 4 + 64));
         HIPCHK(c, hipMalloc(&c->d_bytes[s], c->cfg.max_batch_bytes + 64));
         HIPCHK(c, hipMalloc(&c->d_off[s], c->cfg.max_batch_events * 4 + 64));
+        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hd_bytes[s]), c->h_bytes[s], 0));
+        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hd_off[s]), c->h_off[s], 0));
     }
     return YSB_OK;
+}
+
+// A slot's host -> device copy on the copy stream: by the CUs from the pinned slot's device
+// address (launch_h2d_copy, the default: ysb_split.hip says why), or by the DMA engine with
+// YSB_F_H2D_SDMA.
+static hipError_t h2d(ysb_ctx* c, void* dst, const void* dsrc, const void* hsrc, u64 bytes) {
+    if (c->cfg.flags & YSB_F_H2D_SDMA) return hipMemcpyAsync(dst, hsrc, bytes, hipMemcpyHostToDevice, c->s_copy);
+    launch_h2d_copy(dst, dsrc, bytes, c->cus, c->s_copy);
+    return hipGetLastError();
 }
 
 int ysb_slot_buffers(ysb_ctx* c, int slot, uint8_t** bytes, uint32_t** line_off) {
@@ -587,8 +598,8 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
     hipEvent_t* ce = nullptr;
     if ((rc = copy_events(c, &ce, nbytes + n * 4))) return rc;
     if (ce) HIPCHK(c, hipEventRecord(ce[0], c->s_copy));
-    if (nbytes) HIPCHK(c, hipMemcpyAsync(c->d_bytes[slot], c->h_bytes[slot], nbytes, hipMemcpyHostToDevice, c->s_copy));
-    if (n) HIPCHK(c, hipMemcpyAsync(c->d_off[slot], c->h_off[slot], n * 4, hipMemcpyHostToDevice, c->s_copy));
+    if (nbytes) HIPCHK(c, h2d(c, c->d_bytes[slot], c->hd_bytes[slot], c->h_bytes[slot], nbytes));
+    if (n) HIPCHK(c, h2d(c, c->d_off[slot], c->hd_off[slot], c->h_off[slot], n * 4));
     if (ce) HIPCHK(c, hipEventRecord(ce[1], c->s_copy));
     HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
     HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_h2d[slot], 0));
@@ -734,7 +745,7 @@ int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) 
     hipEvent_t* ce = nullptr;
     if ((rc = copy_events(c, &ce, nbytes))) return rc;
     if (ce) HIPCHK(c, hipEventRecord(ce[0], c->s_copy));
-    if (nbytes) HIPCHK(c, hipMemcpyAsync(c->d_bytes[slot], c->h_bytes[slot], nbytes, hipMemcpyHostToDevice, c->s_copy));
+    if (nbytes) HIPCHK(c, h2d(c, c->d_bytes[slot], c->hd_bytes[slot], c->h_bytes[slot], nbytes));
     if (ce) HIPCHK(c, hipEventRecord(ce[1], c->s_copy));
     HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
     HIPCHK(c, hipStreamWaitEvent(c->s_split, c->ev_h2d[slot], 0));

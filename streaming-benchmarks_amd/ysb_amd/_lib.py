@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(PKG_ROOT, "lib", "libysb_hip%s.so" % (
     "_" + os.environ["YSB_LIB_VARIANT"] if os.environ.get("YSB_LIB_VARIANT") else ""))
 
 YSB_OK = 0
+YSB_PENDING = 1
 ERRORS = {-1: "YSB_ERR_ARG", -2: "YSB_ERR_HIP", -3: "YSB_ERR_STATE", -4: "YSB_ERR_CAPACITY",
           -5: "YSB_ERR_FORMAT", -6: "YSB_ERR_RCCL", -7: "YSB_ERR_NOMEM", -8: "YSB_ERR_DATA"}
 
@@ -30,6 +31,7 @@ YSB_F_FLAT_FIRST = 0x100
 YSB_F_LAYOUT_AUTO = 0x200   # the default since ABI 2 (accepted, ignored)
 YSB_F_STRICT = 0x400
 YSB_F_LAYOUT_FIXED = 0x800
+YSB_F_H2D_SDMA = 0x1000
 YSB_SUM_TRUTH_BLOCKS = 0
 YSB_SUM_PENDING_BLOCKS = 1
 YSB_SUM_OWNED = 2
@@ -118,6 +120,8 @@ SIGNATURES = {
     "ysb_sync": (_I, [_P]),
     "ysb_drain": (_I, [_P, _I64, _I64, _I, C.POINTER(YsbCount), _U64, C.POINTER(_U64)]),
     "ysb_stats_get": (_I, [_P, C.POINTER(YsbStats)]),
+    "ysb_flush_begin": (_I, [_P, _I64, _I64]),
+    "ysb_flush_end": (_I, [_P, _I, C.POINTER(YsbCount), _U64, C.POINTER(_U64), C.POINTER(_I)]),
     "ysb_reset": (_I, [_P]),
     "ysb_ring_range": (_I, [_P, C.POINTER(_I64), C.POINTER(_U32)]),
     "ysb_ring_advance": (_I, [_P, _I64]),

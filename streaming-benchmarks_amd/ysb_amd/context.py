@@ -41,7 +41,7 @@ class YsbContext:
                  max_batch_events=1 << 20, max_batch_bytes=256 << 20, ring_base_bucket=None,
                  overflow_capacity=1 << 20, timing=False, require_ip=False, lds_count=True,
                  sparse_fast_join=False, input_format="json", record_count=None, compact_first=False,
-                 flat_first=False, layout_auto=True, strict=False):
+                 flat_first=False, layout_auto=True, strict=False, h2d_sdma=False):
         L = lib()
         cfg = YsbConfig()
         L.ysb_config_default(C.byref(cfg))
@@ -60,6 +60,7 @@ class YsbContext:
                  | (_lib.YSB_F_FLAT_FIRST if flat_first else 0)
                  | (0 if layout_auto else _lib.YSB_F_LAYOUT_FIXED)
                  | (_lib.YSB_F_STRICT if strict else 0)
+                 | (_lib.YSB_F_H2D_SDMA if h2d_sdma else 0)
                  | (0 if record_count is None else
                     _lib.YSB_F_RECORD_COUNT if record_count else _lib.YSB_F_NO_RECORD_COUNT))
         if input_format not in ("json", "tbl"):
@@ -180,6 +181,23 @@ class YsbContext:
         rows = (YsbCount * max(n.value, 1))()
         self._c(lib().ysb_drain(self._h, bucket_lo, bucket_hi, int(clear), rows, n.value, C.byref(n)))
         return {(rows[i].campaign, rows[i].window_ms): rows[i].count for i in range(n.value)}
+
+    def flush_begin(self, bucket_lo=INT64_MIN, bucket_hi=(1 << 63) - 1):
+        """ysb_flush_begin: the ring's deltas of [bucket_lo, bucket_hi) compacted behind every
+        submitted batch, without waiting."""
+        self._c(lib().ysb_flush_begin(self._h, bucket_lo, bucket_hi))
+
+    def flush_end(self, wait=True):
+        """The oldest begun flush as ({(campaign, window_ms): count}, more), or None while it is
+        pending (wait=False)."""
+        n, more = C.c_uint64(), C.c_int()
+        rc = lib().ysb_flush_end(self._h, int(wait), None, 0, C.byref(n), C.byref(more))
+        if rc == _lib.YSB_PENDING:
+            return None
+        self._c(rc)
+        rows = (YsbCount * max(n.value, 1))()
+        self._c(lib().ysb_flush_end(self._h, 1, rows, n.value, C.byref(n), C.byref(more)))
+        return {(rows[i].campaign, rows[i].window_ms): rows[i].count for i in range(n.value)}, bool(more.value)
 
     def drain_buckets(self, **kw):
         """Same as drain() keyed by (campaign, bucket) instead of window_ms."""

@@ -240,3 +240,67 @@ def test_sharded_streaming_n_contexts_exact(n):
     assert op.events == n * per_tick * ticks
     lat = op.latency_summary()
     assert lat["windows"] >= 1 and lat["p99_ms"] < 1000
+
+
+def test_async_flushes_sum_to_the_drain_without_stopping_the_stream():
+    """ysb_flush_begin / ysb_flush_end (ABI 4): a flush begun after each of 8 device batches
+    submitted back to back, taken without waiting where it is done and in order otherwise, plus
+    one final drain, equal the C oracle's counts exactly -- each delta in exactly one flush or
+    the drain; at most 4 flushes outstanding; a pending flush reports YSB_PENDING, not an error."""
+    import numpy as np
+    from oracle import oracle
+    from ysb_amd import YsbError
+    g = GenParams(seed=61, events_per_sec=20_000)
+    _, aids = g.ids()
+    camp = g.ad_campaign_index()
+    n, parts = 400_000, 8
+    raw, offs = g.events_host(0, n)
+    rows, ost = oracle.run(oracle.AdMap(aids, camp), raw, offs, threads=8)
+    ends = [int(x) for x in offs] + [int(raw.size)]
+    got, flushes = {}, []
+    with YsbContext(device=0, n_campaigns=100, window_ring=64) as ctx:
+        ctx.load_ad_map(aids, camp)
+        bufs = []
+        for p in range(parts):
+            a, b = p * n // parts, (p + 1) * n // parts
+            piece = raw[ends[a]:ends[b]]
+            d_b, d_o = ctx.device_alloc(piece.size + 64), ctx.device_alloc(4 * (b - a) + 64)
+            ctx.h2d(d_b, piece)
+            ctx.h2d(d_o, (np.asarray(ends[a:b], dtype=np.int64) - ends[a]).astype(np.uint32))
+            bufs.append((d_b, int(piece.size), d_o, b - a))
+        ctx.sync()
+
+        def take(wait):
+            r = ctx.flush_end(wait=wait)
+            if r is None:
+                return False
+            assert not r[1]
+            flushes.append(len(r[0]))
+            for k, v in r[0].items():
+                got[k] = got.get(k, 0) + v
+            return True
+        pending = 0
+        for d_b, nb, d_o, m in bufs:
+            ctx.submit_device(d_b, nb, d_o, m)
+            ctx.flush_begin()
+            pending += 1
+            if pending == 4:
+                with pytest.raises(YsbError):
+                    ctx.flush_begin()
+                assert take(True)
+                pending -= 1
+            while pending and take(False):
+                pending -= 1
+        while pending:
+            assert take(True)
+            pending -= 1
+        for k, v in ctx.drain(clear=True).items():
+            got[k] = got.get(k, 0) + v
+        st = ctx.stats()
+        for d_b, _, d_o, _ in bufs:
+            ctx.device_free(d_b)
+            ctx.device_free(d_o)
+    assert len(flushes) == parts and sum(flushes) > 0
+    assert {(c, w // 10000): v for (c, w), v in got.items()} == rows
+    for k, v in ost.items():
+        assert st[k] == v, (k, st[k], v)

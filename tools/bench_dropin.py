@@ -42,14 +42,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def host_staged(device=0, events=100_000_000, slot_mb=256, raw=False, rate=100_000):
+def host_staged(device=0, events=100_000_000, slot_mb=256, raw=False, rate=100_000, h2d_sdma=False):
     from ysb_amd import GenParams, YsbContext
     from ysb_amd.stream import SlotContext
     g = GenParams(seed=42, events_per_sec=rate)
     _, aids = g.ids()
     per = int((slot_mb << 20) // g.max_line_bytes())
     with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True, max_batch_bytes=slot_mb << 20,
-                    max_batch_events=per, ring_base_bucket=g.c.t0_ms // 10000 - 8) as ctx:
+                    max_batch_events=per, ring_base_bucket=g.c.t0_ms // 10000 - 8, h2d_sdma=h2d_sdma) as ctx:
         ctx.load_ad_map(aids, g.ad_campaign_index())
         sc = SlotContext(ctx)
         sizes = []

@@ -25,6 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--events", type=int, default=30_000_000)
     ap.add_argument("--skip-headline", action="store_true")
+    ap.add_argument("--sdma", action="store_true", help="after the headline: DMA-engine / copy-kernel legs interleaved")
+    ap.add_argument("--zc", action="store_true", help="after the headline: staged / zero-copy legs interleaved")
     ap.add_argument("--pre", default=None,
                     help="one precondition only, then the offsets leg: torch | segments | pageable | oracle | none")
     a = ap.parse_args()
@@ -55,6 +57,15 @@ def main():
         out["cpu_baseline_value"] = cpu["value"]
         out["nodes_after_headline"] = numa_info.node_meminfo()
         out["after_headline"] = brief(bench_dropin.host_staged(0, a.events))
+    if a.zc:   # staged and zero-copy legs interleaved in the same (slow-prone) period
+        import zerocopy_probe
+        for k in range(3):
+            out["zc_staged_%d" % k] = brief(bench_dropin.host_staged(0, a.events))
+            out["zc_zero_copy_%d" % k] = zerocopy_probe.zero_copy(a.events)
+    if a.sdma:   # the DMA engine and the copy kernel interleaved in the same period
+        for k in range(3):
+            out["sdma_%d" % k] = brief(bench_dropin.host_staged(0, a.events, h2d_sdma=True))
+            out["kernel_%d" % k] = brief(bench_dropin.host_staged(0, a.events))
     out["again"] = brief(bench_dropin.host_staged(0, a.events))
     out["raw_again"] = brief(bench_dropin.host_staged(0, a.events, raw=True))
     print(json.dumps(out), flush=True)
