@@ -500,7 +500,8 @@ typedef struct ysb_gen_params {
     int64_t  t0_ms;             /* event_time of event 0                              */
     uint64_t events_per_sec;    /* event time advances 1000/rate ms per event;
                                    100 reproduces catch-up mode (10 ms, core.clj:95)   */
-    uint32_t with_skew;         /* +-50 ms skew, 1e-5 late by <60 s (core.clj:166-174) */
+    uint32_t with_skew;         /* 1: +-50 ms skew, 1e-5 late by <60 s (core.clj:166-174);
+                                   2: the skew only (out of order, never late)         */
     uint32_t n_users;           /* 0: a fresh user/page UUID per event (core.clj:79-80);
                                    k: draw from a pool of k (core.clj:187-188)         */
     const uint32_t* ad_subset;  /* optional: draw ads only from these indices (shards) */

@@ -137,7 +137,7 @@ YSB_HD GenEvent gen_event(const GenSpec& s, u64 i) {
     if (s.with_skew) {                                      // make-kafka-event-at (:166-174)
         u64 r = draw(stream_key(s.ev_seed, S_SKEW), i);
         t += 50 - (i64)(r % 100);
-        if (((r >> 17) % 100000ULL) == 0) t -= (i64)((r >> 40) % 60000ULL);
+        if (s.with_skew == 1 && ((r >> 17) % 100000ULL) == 0) t -= (i64)((r >> 40) % 60000ULL);   // 2: skew only
     }
     e.time_ms = t;
     return e;

@@ -1,6 +1,7 @@
 // ysb_topology.cpp -- implementation of ysb_topology.hpp (see there for what each class
 // restates from the reference).
 #include "ysb_topology.hpp"
+#include "worker_pool.hpp"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -237,64 +238,6 @@ AdCampaignMap AdCampaignMap::fromFile(const std::string& path) {
 }
 
 // ---- FileBasedDataSource -----------------------------------------------------------------------
-
-class WorkerPool {
-public:
-    explicit WorkerPool(unsigned n) {
-        for (unsigned t = 1; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
-    }
-    ~WorkerPool() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& x : th_) x.join();
-    }
-    unsigned size() const { return (unsigned)th_.size() + 1; }
-    // f(t) for t in [0, n), n <= size(); t = 0 on the calling thread
-    void run(unsigned n, const std::function<void(unsigned)>& f) {
-        if (n <= 1) { f(0u); return; }
-        {
-            std::lock_guard<std::mutex> g(m_);
-            job_ = &f;
-            active_ = n;
-            left_ = n - 1;
-            ++gen_;
-        }
-        cv_.notify_all();
-        f(0u);
-        std::unique_lock<std::mutex> g(m_);
-        done_.wait(g, [this] { return left_ == 0; });
-        job_ = nullptr;
-    }
-
-private:
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    const std::function<void(unsigned)>* job_ = nullptr;
-    unsigned active_ = 0, left_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-    void loop(unsigned t) {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(unsigned)>* f;
-            {
-                std::unique_lock<std::mutex> g(m_);
-                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                if (t >= active_) continue;
-                f = job_;
-            }
-            (*f)(t);
-            std::lock_guard<std::mutex> g(m_);
-            if (--left_ == 0) done_.notify_all();
-        }
-    }
-};
 
 FileBasedDataSource::FileBasedDataSource(const std::string& path, unsigned threads, bool mmap) {
     fd_ = ::open(path.c_str(), O_RDONLY);
@@ -650,7 +593,7 @@ std::string randomUuid() {
 RedisWindowWriter::RedisWindowWriter(const std::string& host, int port) : r_(new RespClient(host, port)) {}
 RedisWindowWriter::~RedisWindowWriter() = default;
 
-void RedisWindowWriter::writeWindows(const std::vector<WindowDelta>& rows) {
+void RedisWindowWriter::writeWindows(const std::vector<WindowDelta>& rows, int64_t nowMs) {
     // the (campaign, window) keys and campaigns not cached yet, each once, in first-seen
     // order (sets beside the vectors: a config-3 flush holds millions of rows)
     std::vector<std::pair<std::string, std::string>> need_w;
@@ -694,7 +637,9 @@ void RedisWindowWriter::writeWindows(const std::vector<WindowDelta>& rows) {
     }
     // round trip 2: the deltas (:84, :87-88)
     const std::string now = std::to_string(
-        std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch()).count());
+        nowMs >= 0 ? nowMs
+                   : (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+                         std::chrono::system_clock::now().time_since_epoch()).count());
     for (const WindowDelta& d : rows) {
         if (!d.count) continue;
         const std::string& w = windowUuid_[std::make_pair(d.campaign, std::to_string(d.windowMs))];

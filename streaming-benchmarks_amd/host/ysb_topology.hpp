@@ -171,8 +171,9 @@ class RedisWindowWriter {
 public:
     RedisWindowWriter(const std::string& host, int port);
     ~RedisWindowWriter();
-    // writeWindow for every delta of one flush, in two pipelined round trips.
-    void writeWindows(const std::vector<WindowDelta>& rows);
+    // writeWindow for every delta of one flush, in two pipelined round trips; time_updated is
+    // nowMs (the wall clock when negative; a streaming replay passes its replay clock).
+    void writeWindows(const std::vector<WindowDelta>& rows, int64_t nowMs = -1);
     uint64_t roundTrips() const { return trips_; }
 
 private:

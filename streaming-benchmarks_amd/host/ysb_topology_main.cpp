@@ -16,13 +16,16 @@
 // splits the lines on the host instead (ysb_submit with offsets).  --repeat K reads the file
 // K times (a replay source; the counts are K times the file's).  The last stdout line is a
 // JSON summary.
+#include <algorithm>
 #include <chrono>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include "ysb_stream.hpp"
 #include "ysb_topology.hpp"
 
 using namespace ysb::topology;
@@ -39,6 +42,10 @@ struct Args {
     long long repeat = 1;
     unsigned io_threads = 0;
     bool io_mmap = true;
+    // streaming mode (configs[4]): --stream plus its options (ysb_stream.hpp)
+    bool stream = false;
+    StreamOptions so;
+    std::string stream_csv;   // per-(campaign, window) totals of everything written
 };
 
 void usage() {
@@ -46,7 +53,11 @@ void usage() {
                  "usage: ysb_topology --confPath PATH [--device N] [--sink none|csv:FILE|redis[:HOST[:PORT]]]\n"
                  "       [--format json|tbl] [--flush-ms MS] [--batch-mb MB | --batch-bytes B] [--batch-events N]\n"
                  "       [--window-ring W] [--require-ip] [--dry-run] [--print-config] [--replay-rows CSV]\n"
-                 "       [--host-split] [--repeat K] [--io-threads T] [--io mmap|pread]\n");
+                 "       [--host-split] [--repeat K] [--io-threads T] [--io mmap|pread]\n"
+                 "   or: ysb_topology --stream [--sink none|csv:FILE|redis[:HOST[:PORT]]] [--shards N] [--device D]\n"
+                 "       [--seed S] [--campaigns C] [--ads-per-campaign A] [--event-rate E] [--speedup F]\n"
+                 "       [--cycle-ms MS] [--flush-ms MS] [--batch-ms MS] [--ooo-ms MS] [--seconds S]\n"
+                 "       [--batch-mb MB] [--window-ring W] [--skew 0|1|2] [--io-threads T] [--totals CSV]\n");
 }
 
 Args parse(int argc, char** argv) {
@@ -74,7 +85,28 @@ Args parse(int argc, char** argv) {
         else if (k == "--repeat") a.repeat = std::max(1ll, std::atoll(val().c_str()));
         else if (k == "--io-threads") a.io_threads = (unsigned)std::atoll(val().c_str());
         else if (k == "--io") a.io_mmap = val() != "pread";
+        else if (k == "--stream") a.stream = true;
+        else if (k == "--shards") a.so.shards = std::atoi(val().c_str());
+        else if (k == "--seed") a.so.seed = std::strtoull(val().c_str(), nullptr, 10);
+        else if (k == "--campaigns") a.so.campaigns = (uint32_t)std::atoll(val().c_str());
+        else if (k == "--ads-per-campaign") a.so.adsPerCampaign = (uint32_t)std::atoll(val().c_str());
+        else if (k == "--event-rate") a.so.eventRate = std::atof(val().c_str());
+        else if (k == "--speedup") a.so.speedup = std::atof(val().c_str());
+        else if (k == "--cycle-ms") a.so.cycleMs = std::atoll(val().c_str());
+        else if (k == "--batch-ms") a.so.batchMs = std::atoll(val().c_str());
+        else if (k == "--ooo-ms") a.so.oooMs = std::atoll(val().c_str());
+        else if (k == "--seconds") a.so.seconds = std::atof(val().c_str());
+        else if (k == "--skew") a.so.skew = std::atoi(val().c_str());
+        else if (k == "--totals") a.stream_csv = val();
         else { usage(); std::exit(2); }
+    }
+    if (a.stream) {   // the generator's ids and events: no config file needed
+        a.so.device = a.device;
+        a.so.flushMs = a.flush_ms;
+        a.so.slotBytes = (uint64_t)a.batch_bytes;
+        a.so.windowRing = a.window_ring == 1024 ? 64 : a.window_ring;
+        a.so.threads = a.io_threads;
+        return a;
     }
     if (a.conf.empty()) {   // ParameterTool.getRequired("confPath")
         std::fprintf(stderr, "No data for required key 'confPath'\n");
@@ -232,11 +264,88 @@ int run(const Args& a) {
     return s.overflow_dropped ? 3 : 0;
 }
 
+double pct(std::vector<double> v, double q) {
+    if (v.empty()) return 0;
+    std::sort(v.begin(), v.end());
+    const double pos = q / 100.0 * (double)(v.size() - 1);
+    const size_t lo = (size_t)pos, hi = std::min(v.size() - 1, lo + 1);
+    return v[lo] + (v[hi] - v[lo]) * (pos - (double)lo);
+}
+
+std::string dist(const std::vector<double>& v, double scale) {
+    char b[256];
+    std::snprintf(b, sizeof b, "{\"n\": %zu, \"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}", v.size(),
+                  pct(v, 50) * scale, pct(v, 99) * scale, v.empty() ? 0.0 : *std::max_element(v.begin(), v.end()) * scale);
+    return b;
+}
+
+// Streaming mode (BASELINE configs[4]): ysb_stream.hpp.
+int run_stream(const Args& a) {
+    StreamingJob job(a.so);
+    const double t0 = now_s();
+    job.prepare();
+    const double prep_s = now_s() - t0;
+    std::unique_ptr<RedisWindowWriter> redis;
+    if (a.sink.rfind("redis", 0) == 0) {
+        std::string host = "localhost";
+        int port = 6379;
+        const std::string rest = a.sink.size() > 6 ? a.sink.substr(6) : "";
+        if (!rest.empty()) {
+            const size_t c = rest.rfind(':');
+            host = c == std::string::npos ? rest : rest.substr(0, c);
+            if (c != std::string::npos) port = std::atoi(rest.c_str() + c + 1);
+        }
+        redis.reset(new RedisWindowWriter(host, port));
+    } else if (a.sink != "none" && a.sink.rfind("csv:", 0) != 0) {
+        usage();
+        return 2;
+    }
+    CsvWindowSink totals;
+    const std::string csv_path = a.sink.rfind("csv:", 0) == 0 ? a.sink.substr(4) : a.stream_csv;
+    const StreamReport r = job.run([&](const FlushRows& f, int64_t now) {
+        if (redis) redis->writeWindows(f.rows, now);
+        totals.add(f.rows);
+    });
+    if (!csv_path.empty()) totals.write(csv_path);
+    const double f = 1.0 / a.so.speedup;   // replay ms -> wall ms
+    std::string cyc = "[", part = "[";
+    for (size_t i = 0; i < r.cycles.size(); ++i) {
+        cyc += (i ? ", " : "") + std::to_string(r.cycles[i]);
+        part += (i ? ", " : "") + std::to_string(r.partialLines[i]);
+    }
+    cyc += "]";
+    part += "]";
+    std::printf("{\"mode\": \"stream\", \"shards\": %d, \"events\": %llu, \"batches\": %llu, \"wall_s\": %.3f, "
+                "\"events_per_s\": %.1f, \"target_events_per_s\": %.1f, \"copy_GBs\": %.2f, \"copy_busy_frac\": %.4f, "
+                "\"slot_waits\": %llu, \"slot_wait_ms\": %.2f, \"slot_wait_max_ms\": %.3f, \"max_behind_ms\": %.2f, "
+                "\"flushes\": %llu, \"rows_written\": %llu, \"ring_advances\": %llu, "
+                "\"window_close_ms\": %s, \"window_close_wall_ms\": %s, \"get_stats_ms\": %s, "
+                "\"get_stats_wall_ms_after_window_end\": %s, \"open_at_end\": %llu, \"final_watermark_ms\": %lld, "
+                "\"speedup\": %.3f, \"event_rate\": %.1f, \"cycle_ms\": %lld, \"flush_ms\": %lld, \"batch_ms\": %lld, "
+                "\"ooo_ms\": %lld, \"skew\": %d, \"seed\": %llu, \"campaigns\": %u, \"ads_per_campaign\": %u, "
+                "\"t0_ms\": %lld, \"lines_per_cycle\": %llu, \"cycles\": %s, \"partial_lines\": %s, "
+                "\"overflow_dropped\": %llu, \"parse_errors\": %llu, \"join_misses\": %llu, \"prepare_s\": %.2f, "
+                "\"sink\": %s}\n",
+                a.so.shards, (unsigned long long)r.events, (unsigned long long)r.batches, r.wallSeconds, r.eventsPerSecond,
+                r.targetEventsPerSecond, r.copyGBs, r.copyBusyFrac, (unsigned long long)r.slotWaits, r.slotWaitMs,
+                r.slotWaitMaxMs, r.maxBehindMs, (unsigned long long)r.flushes, (unsigned long long)r.rowsWritten,
+                (unsigned long long)r.ringAdvances, dist(r.closeReplayMs, 1.0).c_str(), dist(r.closeReplayMs, f).c_str(),
+                dist(r.cwReplayMs, 1.0).c_str(),
+                dist([&] { std::vector<double> v; for (double x : r.cwReplayMs) v.push_back(x - 10000.0); return v; }(), f).c_str(),
+                (unsigned long long)r.openAtEnd, (long long)r.finalWatermarkMs, a.so.speedup, a.so.eventRate, (long long)a.so.cycleMs,
+                (long long)a.so.flushMs, (long long)a.so.batchMs, (long long)a.so.oooMs, a.so.skew,
+                (unsigned long long)a.so.seed, a.so.campaigns, a.so.adsPerCampaign, (long long)a.so.t0Ms,
+                (unsigned long long)r.linesPerCycle, cyc.c_str(), part.c_str(), (unsigned long long)r.overflowDropped,
+                (unsigned long long)r.parseErrors, (unsigned long long)r.joinMisses, prep_s, json_str(a.sink).c_str());
+    return r.overflowDropped ? 3 : 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     const Args a = parse(argc, argv);
     try {
+        if (a.stream) return run_stream(a);
         return run(a);
     } catch (const std::exception& e) {   // the job fails, as the reference's uncaught exceptions do
         std::fprintf(stderr, "ysb_topology: %s\n", e.what());

@@ -30,7 +30,8 @@ class GenParams:
         self.c.ads_per_campaign = ads_per_campaign
         self.c.t0_ms = t0_ms
         self.c.events_per_sec = events_per_sec
-        self.c.with_skew = int(bool(with_skew))
+        # True / 1: +-50 ms skew and 1e-5 late events (core.clj:166-174); 2: the skew only
+        self.c.with_skew = with_skew if isinstance(with_skew, int) and not isinstance(with_skew, bool) else int(bool(with_skew))
         self.c.n_users = n_users
         self.c.event_stream = event_stream
         if fmt not in ("json", "tbl"):

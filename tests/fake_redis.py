@@ -3,6 +3,8 @@
 Redis command reference for string / hash / list / set keys."""
 from __future__ import annotations
 
+import collections
+import itertools
 import socketserver
 import threading
 
@@ -104,18 +106,18 @@ class _Handler(socketserver.StreamRequestHandler):
                 v = int(h.get(a[1], "0")) + int(a[2])
                 h[a[1]] = str(v)
                 return _int(v)
-            if cmd == "LPUSH":
-                lst = typed(a[0], list)
+            if cmd == "LPUSH":   # (a deque: O(1) at the head; the time_updated list grows long)
+                lst = typed(a[0], collections.deque)
                 for v in a[1:]:
-                    lst.insert(0, v)
+                    lst.appendleft(v)
                 return _int(len(lst))
             if cmd == "LLEN":
                 return _int(len(kv.get(a[0], [])))
             if cmd == "LRANGE":
-                lst = kv.get(a[0], [])
+                lst = kv.get(a[0], collections.deque())
                 lo, hi = int(a[1]), int(a[2])
                 hi = len(lst) - 1 if hi < 0 else hi
-                return _arr(lst[lo:hi + 1])
+                return _arr(list(itertools.islice(lst, lo, hi + 1)))
             return b"-ERR unknown command '%s'\r\n" % cmd.encode()
         except TypeError:
             return b"-WRONGTYPE Operation against a key holding the wrong kind of value\r\n"

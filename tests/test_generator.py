@@ -77,6 +77,24 @@ def test_skew_semantics():
     assert 0 <= late <= 10
 
 
+def test_skew_only_mode_is_never_late():
+    """with_skew=2: the same +-50 ms skew draws, no late events (the streaming leg's
+    out-of-order workload); with_skew=1 on the same seed differs only on its late events."""
+    n = 200_000
+    a = GenParams(seed=5, events_per_sec=1000, with_skew=2)
+    b = GenParams(seed=5, events_per_sec=1000, with_skew=True)
+    ra, oa = a.events_host(0, n)
+    rb, ob = b.events_host(0, n)
+    ta, tb = [], []
+    for raw, off, out in ((bytes(ra), oa, ta), (bytes(rb), ob, tb)):
+        for i in range(n):
+            j = raw.index(b'"event_time": "', off[i]) + 15
+            out.append(int(raw[j:raw.index(b'"', j)]) - (1_700_000_000_000 + i))
+    assert all(-49 <= d <= 50 for d in ta)
+    diff = [i for i in range(n) if ta[i] != tb[i]]
+    assert 0 < len(diff) <= 10 and all(tb[i] < ta[i] for i in diff)
+
+
 def test_first_offset_and_subsets():
     g = GenParams(seed=9)
     d1, o1 = g.events_host(0, 100)
