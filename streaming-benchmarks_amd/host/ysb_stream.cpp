@@ -82,7 +82,8 @@ StreamingJob::~StreamingJob() {
 }
 
 // The shard's replay cycle: generated on its GPU (ysb_gen_events_device, the data/ generator)
-// in pieces, copied to host memory, indexed.
+// in pieces and copied to host memory -- or, ctx NULL (the CPU self-check), by the host
+// generator -- then indexed.
 static void build_cycle(ysb_ctx* ctx, const ysb_gen_params& g, const StreamOptions& o,
                         ReplayCycle& c, WorkerPool& pool) {
     const uint64_t n = (uint64_t)(o.eventRate * (double)o.cycleMs / 1000.0);
@@ -92,23 +93,36 @@ static void build_cycle(ysb_ctx* ctx, const ysb_gen_params& g, const StreamOptio
     c.start.assign(n + 1, 0);
     void *d_b = nullptr, *d_o = nullptr;
     const uint64_t piece = std::min<uint64_t>(n, GEN_PIECE);
-    check_ctx(ysb_device_alloc(ctx, piece * maxLine + 64, &d_b), ctx, "ysb_device_alloc");
-    check_ctx(ysb_device_alloc(ctx, piece * 4 + 64, &d_o), ctx, "ysb_device_alloc");
+    std::vector<uint8_t> hbuf;
+    if (ctx) {
+        check_ctx(ysb_device_alloc(ctx, piece * maxLine + 64, &d_b), ctx, "ysb_device_alloc");
+        check_ctx(ysb_device_alloc(ctx, piece * 4 + 64, &d_o), ctx, "ysb_device_alloc");
+    } else {
+        hbuf.resize(piece * maxLine + 64);
+    }
     std::vector<uint32_t> off(piece);
     for (uint64_t first = 0; first < n; first += piece) {
         const uint64_t m = std::min(piece, n - first);
         uint64_t nb = 0;
-        check_ctx(ysb_gen_events_device(ctx, &g, first, m, (uint8_t*)d_b, piece * maxLine, (uint32_t*)d_o, &nb), ctx,
-                  "ysb_gen_events_device");
         const uint64_t base = c.bytes.size();
-        c.bytes.resize(base + nb);
-        check_ctx(ysb_memcpy_d2h(ctx, c.bytes.data() + base, d_b, nb), ctx, "ysb_memcpy_d2h");
-        check_ctx(ysb_memcpy_d2h(ctx, off.data(), d_o, m * 4), ctx, "ysb_memcpy_d2h");
+        if (ctx) {
+            check_ctx(ysb_gen_events_device(ctx, &g, first, m, (uint8_t*)d_b, piece * maxLine, (uint32_t*)d_o, &nb), ctx,
+                      "ysb_gen_events_device");
+            c.bytes.resize(base + nb);
+            check_ctx(ysb_memcpy_d2h(ctx, c.bytes.data() + base, d_b, nb), ctx, "ysb_memcpy_d2h");
+            check_ctx(ysb_memcpy_d2h(ctx, off.data(), d_o, m * 4), ctx, "ysb_memcpy_d2h");
+        } else {
+            if (ysb_gen_events_host_mt(&g, first, m, hbuf.data(), hbuf.size(), off.data(), &nb, pool.size()) != YSB_OK)
+                throw std::runtime_error(std::string("ysb_gen_events_host_mt: ") + ysb_last_error(nullptr));
+            c.bytes.insert(c.bytes.end(), hbuf.begin(), hbuf.begin() + (ptrdiff_t)nb);
+        }
         for (uint64_t i = 0; i < m; ++i) c.start[first + i] = base + off[i];
     }
     c.start[n] = c.bytes.size();
-    ysb_device_free(ctx, d_b);
-    ysb_device_free(ctx, d_o);
+    if (ctx) {
+        ysb_device_free(ctx, d_b);
+        ysb_device_free(ctx, d_o);
+    }
     // each line's 13 time digits: their offset and the leading nine as a number
     c.timePos.assign(n, 0);
     std::vector<int64_t> up(n), tm(n);
@@ -155,6 +169,72 @@ static void build_cycle(ysb_ctx* ctx, const ysb_gen_params& g, const StreamOptio
         c.batches.push_back({a, b, nominal(b - 1), mx});
         a = b;
     }
+}
+
+// Batch b of cycle `cycle` into dst: its lines copied in parallel pieces, every event_time moved
+// by cycle * cycleMs -- the nine leading digits replaced from a per-cycle table of the few
+// values they take (the four trailing digits do not change: cycleMs is a multiple of 10 000).
+static uint64_t fill_batch(const ReplayCycle& c, const ReplayCycle::Batch& b, uint64_t cycle, int64_t cycleMs,
+                           uint8_t* dst, WorkerPool& pool, unsigned T) {
+    const int64_t shift = (int64_t)cycle * (cycleMs / BUCKET_MS);
+    std::vector<char> table(9ull * c.nUpper);
+    for (uint32_t k = 0; k < c.nUpper; ++k) {
+        int64_t v = c.upperMin + k + shift;
+        for (int d = 8; d >= 0; --d) {
+            table[9ull * k + d] = (char)('0' + v % 10);
+            v /= 10;
+        }
+    }
+    const uint64_t base = c.start[b.a], nb = c.start[b.b] - base;
+    const uint64_t lines = b.b - b.a;
+    const unsigned tn = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(std::min(T, pool.size()), nb >> 22));
+    pool.run(tn, [&](unsigned t) {
+        const uint64_t la = b.a + lines * t / tn, lb = b.a + lines * (t + 1) / tn;
+        const uint64_t pa = c.start[la], pb = c.start[lb];
+        std::memcpy(dst + (pa - base), c.bytes.data() + pa, pb - pa);
+        if (shift)
+            for (uint64_t i = la; i < lb; ++i)
+                std::memcpy(dst + (c.start[i] - base) + c.timePos[i], &table[9ull * c.upper[i]], 9);
+    });
+    return nb;
+}
+
+std::string StreamingJob::replaySelfCheck(const StreamOptions& o, const std::vector<uint64_t>& cycles) {
+    ysb_gen_params g;
+    ysb_gen_default(&g);
+    g.seed = o.seed;
+    g.n_campaigns = o.campaigns;
+    g.ads_per_campaign = o.adsPerCampaign;
+    g.t0_ms = o.t0Ms;
+    g.events_per_sec = (uint64_t)o.eventRate;
+    g.with_skew = (uint32_t)o.skew;
+    g.event_stream = 1;
+    const unsigned T = o.threads ? o.threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    WorkerPool pool(T);
+    ReplayCycle c;
+    build_cycle(nullptr, g, o, c, pool);
+    std::vector<uint8_t> buf(o.slotBytes + 64), ref(o.slotBytes + 64);
+    std::vector<uint32_t> off(c.lines() + 1);
+    uint64_t lines = 0, bad = 0, batches = 0;
+    for (uint64_t cy : cycles) {
+        ysb_gen_params gc = g;
+        gc.t0_ms = o.t0Ms + (int64_t)cy * o.cycleMs;   // the generator's own lines of that cycle
+        for (const auto& b : c.batches) {
+            const uint64_t nb = fill_batch(c, b, cy, o.cycleMs, buf.data(), pool, T);
+            uint64_t rb = 0;
+            if (ysb_gen_events_host(&gc, b.a, b.b - b.a, ref.data(), ref.size(), off.data(), &rb) != YSB_OK)
+                throw std::runtime_error("ysb_gen_events_host failed");
+            if (rb != nb || std::memcmp(buf.data(), ref.data(), nb) != 0) ++bad;
+            lines += b.b - b.a;
+            ++batches;
+        }
+    }
+    char o2[256];
+    std::snprintf(o2, sizeof o2, "{\"mode\": \"stream-self-check\", \"lines_per_cycle\": %llu, \"batches\": %llu, "
+                  "\"lines\": %llu, \"mismatched_batches\": %llu, \"upper_values\": %u}",
+                  (unsigned long long)c.lines(), (unsigned long long)batches, (unsigned long long)lines,
+                  (unsigned long long)bad, c.nUpper);
+    return o2;
 }
 
 void StreamingJob::prepare() {
@@ -317,29 +397,7 @@ StreamReport StreamingJob::run(const FlushSink& sink) {
     std::vector<std::string> patch;   // the nine leading time digits of each code, this cycle
 
     auto fill = [&](Shard* s, const ReplayCycle::Batch& b, uint8_t* dst) -> uint64_t {
-        const ReplayCycle& c = s->cyc;
-        const int64_t shift = (int64_t)s->cycle * (o_.cycleMs / BUCKET_MS);
-        // per cycle: the digits of every leading-nine value + shift (tiny table)
-        std::vector<char> table(9ull * c.nUpper);
-        for (uint32_t k = 0; k < c.nUpper; ++k) {
-            int64_t v = c.upperMin + k + shift;
-            for (int d = 8; d >= 0; --d) {
-                table[9ull * k + d] = (char)('0' + v % 10);
-                v /= 10;
-            }
-        }
-        const uint64_t base = c.start[b.a], nb = c.start[b.b] - base;
-        const uint64_t lines = b.b - b.a;
-        const unsigned tn = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(T, nb >> 22));
-        pool.run(tn, [&](unsigned t) {
-            const uint64_t la = b.a + lines * t / tn, lb = b.a + lines * (t + 1) / tn;
-            const uint64_t pa = c.start[la], pb = c.start[lb];
-            std::memcpy(dst + (pa - base), c.bytes.data() + pa, pb - pa);
-            if (shift)
-                for (uint64_t i = la; i < lb; ++i)
-                    std::memcpy(dst + (c.start[i] - base) + c.timePos[i], &table[9ull * c.upper[i]], 9);
-        });
-        return nb;
+        return fill_batch(s->cyc, b, s->cycle, o_.cycleMs, dst, pool, T);
     };
 
     auto takeFlushes = [&](bool wait) {

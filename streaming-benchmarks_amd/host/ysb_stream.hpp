@@ -100,6 +100,10 @@ public:
     void prepare();
     StreamReport run(const FlushSink& sink);
     const std::vector<std::string>& campaignIds() const { return campaigns_; }
+    // CPU check of the replay (no GPU): a cycle from the host generator, each batch of each of
+    // `cycles` rebased into a buffer and compared byte for byte with the host generator's own
+    // lines of that cycle (t0 moved by cycle * cycleMs).  A JSON summary.
+    static std::string replaySelfCheck(const StreamOptions& o, const std::vector<uint64_t>& cycles);
     ~StreamingJob();
 
 private:

@@ -46,6 +46,7 @@ struct Args {
     bool stream = false;
     StreamOptions so;
     std::string stream_csv;   // per-(campaign, window) totals of everything written
+    bool self_check = false;  // --stream-self-check: the replay's rebasing on the CPU, no GPU
 };
 
 void usage() {
@@ -86,6 +87,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--io-threads") a.io_threads = (unsigned)std::atoll(val().c_str());
         else if (k == "--io") a.io_mmap = val() != "pread";
         else if (k == "--stream") a.stream = true;
+        else if (k == "--stream-self-check") { a.stream = true; a.self_check = true; }
         else if (k == "--shards") a.so.shards = std::atoi(val().c_str());
         else if (k == "--seed") a.so.seed = std::strtoull(val().c_str(), nullptr, 10);
         else if (k == "--campaigns") a.so.campaigns = (uint32_t)std::atoll(val().c_str());
@@ -345,6 +347,10 @@ int run_stream(const Args& a) {
 int main(int argc, char** argv) {
     const Args a = parse(argc, argv);
     try {
+        if (a.self_check) {
+            std::printf("%s\n", StreamingJob::replaySelfCheck(a.so, {0, 1, 2, 7, 1000}).c_str());
+            return 0;
+        }
         if (a.stream) return run_stream(a);
         return run(a);
     } catch (const std::exception& e) {   // the job fails, as the reference's uncaught exceptions do

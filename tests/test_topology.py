@@ -191,3 +191,21 @@ def test_parallel_source_on_a_large_file(tmp_path):
     for extra in (["--batch-mb", "16"], ["--batch-mb", "9", "--batch-events", "40000"], ["--batch-mb", "256"]):
         out = last_json(run("--confPath", conf, "--dry-run", *extra))
         assert out["events"] == 250000 and out["bytes"] == os.path.getsize(ev), extra
+
+
+@pytest.mark.parametrize("rate,skew,batch_ms", [(20_000, 1, 100), (3_000, 2, 7), (50_000, 0, 100)])
+def test_stream_replay_rebasing_equals_the_generator(rate, skew, batch_ms):
+    """The streaming mode's replay (host/ysb_stream.cpp): one generated cycle of 10 s of event
+    time, cycled with every event_time moved by the cycle length by patching the nine leading
+    time digits while a batch is copied.  For cycles 0, 1, 2, 7 and 1000 every batch equals,
+    byte for byte, the generator's own lines of that cycle (t0 moved by cycle x 10 s) -- with the
+    reference's skew and late events (skew 1: late times several windows back), skew only, and
+    none; so the truth of a streaming run is the generator truth of each played cycle."""
+    exe = os.path.join(ROOT, "streaming-benchmarks_amd", "bin", "ysb_topology")
+    r = subprocess.run([exe, "--stream-self-check", "--event-rate", str(rate), "--skew", str(skew),
+                        "--batch-ms", str(batch_ms), "--batch-mb", "1"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    s = json.loads(r.stdout.strip().splitlines()[-1])
+    assert s["lines_per_cycle"] == rate * 10 and s["lines"] == 5 * s["lines_per_cycle"]
+    assert s["mismatched_batches"] == 0
+    assert s["upper_values"] >= {0: 1, 1: 7, 2: 2}[skew]
