@@ -34,17 +34,10 @@
 
 namespace ysb {
 
-#ifndef YSB_COUNT_BY_QUARTER
-#define YSB_COUNT_BY_QUARTER 1   // count kernel: 32 threads per partition slice (0: a search per record)
-#endif
-
-#ifndef YSB_PART_RING
-#define YSB_PART_RING 32         // the partition's staged records per level-2 block (one 128-B line: 72 KiB of LDS, two workgroups per CU)
-#endif
-
 constexpr int REC_TPB = 1024;
-constexpr int PART_RING = YSB_PART_RING;
-static_assert(PART_RING == 32 || PART_RING == 64, "whole 128-B lines");
+// the partition's staged records per level-2 block: one 128-B line (72 KiB of LDS, two
+// workgroups per CU; 64 measured slower, profiles/r03t_partition_ab.txt)
+constexpr int PART_RING = 32;
 constexpr int REC_WAVES = REC_TPB / 64;
 constexpr int REC_UNROLL = 8;        // records in flight per lane (loads issued together)
 constexpr u32 REC_NONE = 0xFFFFFFFFu;
@@ -258,7 +251,6 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
             r[u] = p < quads ? dr[p] : make_uint4(0u, 0u, 0u, 0u);
         }
     }
-#if YSB_COUNT_BY_QUARTER
     // TPS threads per partition slice (REC_TPB = TPS x REC_QUARTERS): thread (q, k) reads
     // records k, k + TPS, ... of run q -- coalesced lines, no search for the run
     constexpr u32 TPS = REC_TPB / REC_QUARTERS;
@@ -277,24 +269,6 @@ __global__ __launch_bounds__(REC_TPB) void rec_count_kernel(const RecParams R) {
         for (int u = 0; u < REC_UNROLL; ++u)
             if (v[u] != REC_NONE) atomicAdd(&cnt[v[u] - base_cell], 1u);
     }
-#else
-    for (u32 i0 = 0; i0 < total; i0 += REC_TPB * REC_UNROLL) {
-        u32 v[REC_UNROLL];
-#pragma unroll
-        for (int u = 0; u < REC_UNROLL; ++u) {
-            const u32 i = i0 + u * REC_TPB + tid;
-            v[u] = REC_NONE;
-            if (i < total) {
-                u32 qq = 0;
-                while (qq + 1 < (u32)REC_QUARTERS && roff[qq + 1] <= i) ++qq;
-                v[u] = R.part[rbeg[qq] + (i - roff[qq])];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < REC_UNROLL; ++u)
-            if (v[u] != REC_NONE) atomicAdd(&cnt[v[u] - base_cell], 1u);
-    }
-#endif
     __syncthreads();
     if (dense) {
 #pragma unroll

@@ -41,9 +41,6 @@ constexpr int MAX_TILES_PER_BLOCK = YSB_MAX_TILES;   // tile bounds preloaded in
 #ifndef YSB_TBL_WG_PER_CU
 #define YSB_TBL_WG_PER_CU 12
 #endif
-#ifndef YSB_TBL_BITMAP
-#define YSB_TBL_BITMAP 0     // round 3 A/B: 1 = -2 % (DESIGN.md Kernel 1, ".tbl stage 1")
-#endif
 
 // Per-input-format geometry of the scan kernel: tile capacity, prefetch registers and
 // the LDS carve (tile | slack | window counters | misc | tile bounds).
@@ -64,14 +61,8 @@ struct Geom {
     static constexpr int LCNT_BYTES = REC ? REC_BINS_MAX * REC_RING * 4 : LCNT_CAP * 4;
     static constexpr int OFF_MISC = OFF_LCNT + LCNT_BYTES;
     static constexpr int OFF_TB = OFF_MISC + 64;
-    // .tbl rows: the tile's '|' bitmap (bit i = tile byte i may be '|'), built in Phase A
-    // from the chunks in registers, so a lane reads its row's 160-bit window (6 dwords)
-    // instead of the row's 40 dwords (YSB_TBL_BITMAP; 32 B slack for windows past the tile)
-    static constexpr int OFF_BM = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
-    static constexpr bool BITMAP = TBL && !REC && YSB_TBL_BITMAP;   // (record mode: no LDS room at 12 per CU)
-    static constexpr int BM_BYTES = BITMAP ? CAP / 8 + 32 : 0;
-    static constexpr int LDS = OFF_BM + BM_BYTES;
-    static_assert(OFF_LCNT % 16 == 0 && OFF_MISC % 16 == 0 && OFF_TB % 16 == 0 && OFF_BM % 16 == 0,
+    static constexpr int LDS = OFF_TB + (MAX_TILES_PER_BLOCK + 4) * 4;
+    static_assert(OFF_LCNT % 16 == 0 && OFF_MISC % 16 == 0 && OFF_TB % 16 == 0 && LDS % 16 == 0,
                   "LDS carve must stay 16-byte aligned");
     // LDS is allocated per workgroup in 1280-byte granules (measured round 3: a .tbl geometry
     // of 13,232 B ran 12 per CU at 2/3 speed, 12,656 B at full; 163,840 / 128 = 1280)
