@@ -68,11 +68,15 @@ def parse_args(argv=None):
     ap.add_argument("--no-check", action="store_true", help="skip the generator-truth check")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[2] / .tbl extra measurements")
     ap.add_argument("--extra-steps", type=int, default=20)
-    ap.add_argument("--stream-seconds", type=int, default=70,
-                    help="extras: seconds of real-time sharded streaming (configs[4]; 70 s closes >= 5 windows); "
-                         "0 skips it")
+    ap.add_argument("--stream-seconds", type=float, default=12.0,
+                    help="extras: wall seconds of the native streaming leg (configs[4]; at the default speedup "
+                         "12 s of input is 384 s of event time: >= 30 windows close); 0 skips it")
+    ap.add_argument("--stream-event-rate", type=int, default=5_000_000,
+                    help="extras: events per second of event time in the streaming replay")
+    ap.add_argument("--stream-speedup", type=float, default=32.0,
+                    help="extras: event time per wall time of the streaming replay (5M x 32 = 160M events/s)")
     ap.add_argument("--stream-rate", type=int, default=20_000_000,
-                    help="extras: aggregate events/s of the real-time producers (configs[4] under load)")
+                    help="tools/bench_extra.py stream_sharded: aggregate events/s of the Python producers")
     ap.add_argument("--dropin-events", type=int, default=100_000_000,
                     help="extras: events through the host-staged (pinned slots, H2D) path")
     ap.add_argument("--runner-file-events", type=int, default=20_000_000,
@@ -357,8 +361,9 @@ def extras(args, device):
         "event_type, page_id), no hint: the learned-order instantiation from each batch's first line"))
     guarded(out, "tbl", lambda: extra_tbl(args, device))
     extra_layouts(args, device, out)
+    guarded(out, "alternating_producers", lambda: extra_alternating(args, device))
     if args.stream_seconds > 0:
-        guarded(out, "stream_sharded", lambda: extra_stream(args))
+        guarded(out, "stream_native", lambda: extra_stream_native(args, device))
     return out
 
 
@@ -369,9 +374,13 @@ def extra_host_staged(args, device):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_dropin
     r = {"offsets": bench_dropin.host_staged(device, args.dropin_events, raw=False),
-         "raw": bench_dropin.host_staged(device, args.dropin_events, raw=True)}
-    log("extras: host_staged %.3f / raw %.3f G events/s" % (r["offsets"]["events_per_s"] / 1e9,
-                                                           r["raw"]["events_per_s"] / 1e9))
+         "raw": bench_dropin.host_staged(device, args.dropin_events, raw=True),
+         # the same offsets leg with the DMA engine doing the H2D (YSB_F_H2D_SDMA): the path
+         # round 4 shipped, in the same process and period ("H2D")
+         "offsets_dma_engine": bench_dropin.host_staged(device, args.dropin_events, raw=False, h2d_sdma=True)}
+    log("extras: host_staged %.3f / raw %.3f / DMA-engine offsets %.3f G events/s"
+        % (r["offsets"]["events_per_s"] / 1e9, r["raw"]["events_per_s"] / 1e9,
+           r["offsets_dma_engine"]["events_per_s"] / 1e9))
     return r
 
 
@@ -497,6 +506,78 @@ def extra_layouts(args, device, out):
         guarded(out, key, one)
 
 
+def extra_alternating(args, device):
+    """Device batches whose producers alternate per launch (the generator's layout, reordered
+    keys, compact JSON -- one producer's 33.3M events per launch, in turn) on a busy compute
+    stream: each launch is decided on the previous launch's sample, the two last samples
+    disagree, so the per-tile dispatch runs (ABI 4; round 4 ran the previous producer's
+    instantiation, reordered lines through layout 0's fourth tier).  Exact vs the truth of
+    every submission."""
+    from ysb_amd import GEN_COMPACT, GEN_REORDER, GenParams, YsbContext
+    per = 33_333_334
+    gens = [GenParams(seed=42, n_campaigns=100, ads_per_campaign=10, events_per_sec=args.rate, variant=v)
+            for v in (0, GEN_REORDER, GEN_COMPACT)]
+    _, aids = gens[0].ids()
+    with YsbContext(device=device, n_campaigns=100, window_ring=1024, timing=True, max_batch_bytes=16 << 20,
+                    max_batch_events=1 << 16) as ctx:
+        ctx.load_ad_map(aids, gens[0].ad_campaign_index())
+        sets = [gen_segments(ctx, g, per, 14_285_715) for g in gens]
+        subs = [[(d_b, nb, d_o, n) for (_, n, d_b, nb, d_o) in segs] for segs in sets]
+        steps = 3 * max(1, args.extra_steps // 3)
+        for k in range(3 * max(1, args.warmup // 3)):
+            ctx.submit_device_segments(subs[k % 3])
+        ctx.sync()
+        ctx.kernel_time()
+        t0 = time.perf_counter()
+        layouts = []
+        for k in range(steps):
+            ctx.submit_device_segments(subs[k % 3])
+            layouts.append(ctx.launch_info()["layout"])
+        ctx.sync()
+        el = time.perf_counter() - t0
+        kms, launches = ctx.kernel_time()
+        pms, _, _ = ctx.path_time()
+        ctx.reset()
+        for k in range(3):
+            ctx.submit_device_segments(subs[k])
+            for (f, n, _, _, _) in sets[k]:
+                ctx.truth_accumulate(gens[k], f, n)
+        mism, truth, ring = ctx.truth_compare()
+        st = ctx.stats()
+        nbytes = sum(s[3] for segs in sets for s in segs)
+        for segs in sets:
+            free_segments(ctx, segs)
+    events = 3 * per
+    alg = (nbytes + 4 * events) / 3   # per launch
+    path = pms / max(launches, 1)
+    ach = alg / (path * 1e-3) / 1e9
+    r = {"workload": "configs[1]'s events as three producers write them (the generator's layout, reordered keys, "
+                     "compact JSON), %dM events per launch, the producer changing every launch, on a busy compute "
+                     "stream (ABI 4: the per-tile dispatch once two samples disagree)" % (per // 1_000_000),
+         "events_per_s": round(per * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
+         "avg_path_ms": round(path, 4), "alg_GBs": round(ach, 1), "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
+         "layouts_timed": {str(x): layouts.count(x) for x in sorted(set(layouts))},
+         "check": {"truth_mismatched_cells": mism, "truth_views": truth, "counted_views": ring,
+                   "deferred": st["deferred"], "parse_errors": st["parse_errors"], "join_misses": st["join_misses"]}}
+    log("extras: alternating_producers %.2f G events/s, %.3f of HBM" % (r["events_per_s"] / 1e9, r["hbm_frac"]))
+    return r
+
+
+def extra_stream_native(args, device):
+    """configs[4] natively: bin/ysb_topology --stream (tools/bench_stream.py): replay bytes
+    through the pinned double-buffered slots at the ingest ceiling, asynchronous flushes
+    through the C++ Redis writer, get-stats' per-(campaign, window) latency read back, exact
+    vs the generator truth (check-correct)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_stream
+    r = bench_stream.stream_native(device, seconds=args.stream_seconds, event_rate=args.stream_event_rate,
+                                   speedup=args.stream_speedup)
+    log("extras: stream_native %.3f G events/s, get-stats p50 / p99 %s / %s ms (closed windows %d), exact %s"
+        % (r["events_per_s"] / 1e9, r["get_stats"]["p50_ms"], r["get_stats"]["p99_ms"],
+           r["get_stats"]["closed_windows"], r["exact_vs_generator_truth"]))
+    return r
+
+
 def extra_stream(args):
     # configs[4] under load: real-time producers (16 host threads each call) writing
     # args.stream_rate events/s in all into double-buffered pinned slots, one context per
@@ -619,19 +700,31 @@ def config3_ranks(args, d):
             "ad_map_load_s": round(load_s, 2),
             "exchange": {"ms_per_step": round(x["ms"] / max(x["exchanges"], 1), 4),
                          "critical_ms_per_step": round(x["critical_ms"] / max(x["exchanges"], 1), 4),
+                         **exchange_overlap(x),
                          "bytes_per_step_per_gpu": x["bytes"] // max(x["exchanges"], 1),
                          "buckets": x["last_buckets"], "cell_bytes": x["last_width"],
                          "whole_ring_u64_bytes": x["full_ring_bytes"],
                          "note": "ms: HIP events from the plan (compute stream) to the end of the unpack (exchange "
                                  "stream): plan, all-reduce(max), read-back, pack, reduce-scatter, unpack, per step; "
                                  "critical_ms: plan to pack on the compute stream (the reduce-scatter and unpack run "
-                                 "beside the next launch)"},
+                                 "beside the next launch); rs: pack done to reduce-scatter done on the exchange stream "
+                                 "(peers' arrival included), exposed: the compute stream's wait for it at the unpack, "
+                                 "hidden = rs - exposed"},
             "check": {"checksum_blocks_mismatched": bad_blocks, "blocks": d.world,
                       "truth_mismatched_cells": sum(p["mism"] for p in per),
                       "truth_views": sum(p["truth"] for p in per), "counted_views": sum(p["ring"] for p in per),
                       "join_misses": sum(p["misses"] for p in per), "foreign_shard": sum(p["foreign"] for p in per),
                       "parse_errors": sum(p["perr"] for p in per), "out_of_ring": sum(p["oor"] for p in per),
                       "check_exchange_cell_bytes": per[0]["chk_width"]}}
+
+
+def exchange_overlap(x):
+    """Per step: the reduce-scatter's own time (rs), the part of it the compute stream waited
+    for at the unpack (exposed) and the rest, which ran beside the queued launches (hidden)."""
+    n = max(x["exchanges"], 1)
+    rs, exp = x["rs_ms"] / n, x["exposed_ms"] / n
+    return {"rs_ms_per_step": round(rs, 4), "exposed_ms_per_step": round(exp, 4),
+            "hidden_ms_per_step": round(max(rs - exp, 0.0), 4)}
 
 
 def exchange(ctx, last):
@@ -829,6 +922,7 @@ def main():
         if xinfo is not None:
             out["exchange"] = {"ms_per_step": round(xinfo["ms"] / max(xinfo["exchanges"], 1), 4),
                                "critical_ms_per_step": round(xinfo["critical_ms"] / max(xinfo["exchanges"], 1), 4),
+                               **exchange_overlap(xinfo),
                                "bytes_per_step_per_gpu": xinfo["bytes"] // max(xinfo["exchanges"], 1),
                                "buckets": xinfo["last_buckets"], "cell_bytes": xinfo["last_width"],
                                "whole_ring_u64_bytes": xinfo["full_ring_bytes"]}

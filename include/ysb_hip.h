@@ -439,8 +439,12 @@ int         ysb_group_exchange_pipelined(ysb_ctx* ctx);
  * unpack), of their part on the compute stream (critical_ms: plan to pack, plus the unpack --
  * what the launches queue behind; the reduce-scatter runs on a stream of its own beside the
  * next launch, and the unpack is enqueued on the compute stream at the next exchange or read),
- * the last exchange's bucket count and cell width (0: nothing was pending), and what one
- * whole-ring u64 exchange would move.  reset != 0 zeroes the totals after reading them. */
+ * the last exchange's bucket count and cell width (0: nothing was pending), what one
+ * whole-ring u64 exchange would move, the reduce-scatters' own time (rs_ms: pack done to
+ * reduce-scatter done, on the exchange stream, waiting for the peers included) and the part of
+ * it the compute stream stood waiting for at the unpack (exposed_ms; rs_ms - exposed_ms ran
+ * hidden beside the launches queued since -- a complete exchange exposes all of it).  reset != 0
+ * zeroes the totals after reading them.  (ABI 4 appended rs_ms and exposed_ms.) */
 typedef struct ysb_exchange_info {
     uint64_t exchanges;
     uint64_t bytes;
@@ -449,6 +453,8 @@ typedef struct ysb_exchange_info {
     uint32_t last_width;
     uint64_t full_ring_bytes;
     double   critical_ms;
+    double   rs_ms;
+    double   exposed_ms;
 } ysb_exchange_info;
 int         ysb_group_exchange_info(ysb_ctx* ctx, ysb_exchange_info* out, int reset);
 /* The plan every rank derives from the all-reduced per-bucket maxima (host function):

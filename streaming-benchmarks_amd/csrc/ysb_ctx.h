@@ -200,10 +200,10 @@ struct ysb_ctx {
     size_t unpack_entry = 0;
     u64 x_count = 0, x_bytes = 0;
     u32 x_last_slots = 0, x_last_width = 0;
-    double x_ms = 0, x_crit_ms = 0;
+    double x_ms = 0, x_crit_ms = 0, x_rs_ms = 0, x_exposed_ms = 0;
     // per exchange {start, packed (compute stream), reduce-scatter done (exchange stream),
     // unpack start, unpack end (compute stream)}
-    std::vector<std::array<hipEvent_t, 5>> xev;
+    std::vector<std::array<hipEvent_t, 6>> xev;
     size_t xev_used = 0;
     // asynchronous flushes (ysb_flush_begin / ysb_flush_end): a ring of FLUSH_SLOTS pinned row
     // buffers the compaction kernel writes straight into, each with its device-side count

@@ -277,6 +277,7 @@ int finish_unpack(ysb_ctx* c) {
     c->unpack_set = -1;
     const u32 W = c->cfg.window_ring, per = c->c_pad / (u32)c->nranks;
     const auto& ev = c->xev[c->unpack_entry];
+    HIPCHK(c, hipEventRecord(ev[5], c->s_comp));   // ev[5] -> ev[3]: the compute stream's wait
     HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_xdone[k], 0));
     HIPCHK(c, hipEventRecord(ev[3], c->s_comp));
     launch_xunpack(c->d_owned, c->d_owned8, W, per, c->d_xslots + (u64)k * W, c->unpack_R, c->d_xrecv[k],
@@ -288,7 +289,10 @@ int finish_unpack(ysb_ctx* c) {
 }
 
 // The recorded exchange timing into x_ms (plan to the end of the reduce-scatter, plus the
-// unpack) and x_crit_ms (the compute stream's share: plan to pack, plus the unpack).  Call
+// unpack), x_crit_ms (the compute stream's share: plan to pack, plus the unpack), x_rs_ms
+// (pack done to reduce-scatter done, on the exchange stream) and x_exposed_ms (how long the
+// compute stream stood at the unpack's wait for that reduce-scatter: the part of it the
+// launches queued since did not hide; a complete exchange exposes all of it).  Call
 // after finish_unpack.  wait: every entry, waiting for the last of them (an info request);
 // otherwise only the entries whose events have completed -- the rest stay pending, so the
 // host never waits behind the launches it has queued (the pipelined exchange's periodic fold).
@@ -300,14 +304,18 @@ static int collect_xev(ysb_ctx* c, bool wait) {
             std::swap(c->xev[keep++], c->xev[i]);   // pending entries keep their order
             continue;
         }
-        float ms = 0, mc = 0, mu = 0;
+        float ms = 0, mc = 0, mu = 0, mr = 0, mx = 0;
         HIPCHK(c, hipEventSynchronize(ev[2]));
         HIPCHK(c, hipEventSynchronize(ev[4]));
         HIPCHK(c, hipEventElapsedTime(&ms, ev[0], ev[2]));
         HIPCHK(c, hipEventElapsedTime(&mc, ev[0], ev[1]));
         HIPCHK(c, hipEventElapsedTime(&mu, ev[3], ev[4]));
+        HIPCHK(c, hipEventElapsedTime(&mr, ev[1], ev[2]));
+        HIPCHK(c, hipEventElapsedTime(&mx, ev[5], ev[3]));
         c->x_ms += ms + mu;
         c->x_crit_ms += mc + mu;
+        c->x_rs_ms += mr;
+        c->x_exposed_ms += mx;
     }
     c->xev_used = keep;
     return YSB_OK;
@@ -357,7 +365,7 @@ static int exchange(ysb_ctx* c, bool pipelined) {
         if (rc) return rc;
     }
     if (c->xev_used == c->xev.size()) {
-        std::array<hipEvent_t, 5> ev{};
+        std::array<hipEvent_t, 6> ev{};
         for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
         c->xev.push_back(ev);
     }
@@ -423,7 +431,8 @@ static int exchange(ysb_ctx* c, bool pipelined) {
     }
     HIPCHK(c, hipEventRecord(ev[1], c->s_comp));
     HIPCHK(c, hipEventRecord(ev[2], R ? c->s_x : c->s_comp));
-    if (!R) {   // nothing to unpack: an empty unpack interval
+    if (!R) {   // nothing to unpack: an empty unpack interval, no wait
+        HIPCHK(c, hipEventRecord(ev[5], c->s_comp));
         HIPCHK(c, hipEventRecord(ev[3], c->s_comp));
         HIPCHK(c, hipEventRecord(ev[4], c->s_comp));
     }
@@ -450,6 +459,8 @@ int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
     out->bytes = c->x_bytes;
     out->ms = c->x_ms;
     out->critical_ms = c->x_crit_ms;
+    out->rs_ms = c->x_rs_ms;
+    out->exposed_ms = c->x_exposed_ms;
     out->last_buckets = c->x_last_slots;
     out->last_width = c->x_last_width;
     out->full_ring_bytes = (u64)c->c_pad * c->cfg.window_ring * 8;
@@ -458,6 +469,8 @@ int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
         c->x_bytes = 0;
         c->x_ms = 0;
         c->x_crit_ms = 0;
+        c->x_rs_ms = 0;
+        c->x_exposed_ms = 0;
     }
     return YSB_OK;
 }

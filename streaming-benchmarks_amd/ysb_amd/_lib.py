@@ -59,7 +59,8 @@ class YsbCount(C.Structure):
 
 class YsbExchangeInfo(C.Structure):
     _fields_ = [("exchanges", C.c_uint64), ("bytes", C.c_uint64), ("ms", C.c_double), ("last_buckets", C.c_uint32),
-                ("last_width", C.c_uint32), ("full_ring_bytes", C.c_uint64), ("critical_ms", C.c_double)]
+                ("last_width", C.c_uint32), ("full_ring_bytes", C.c_uint64), ("critical_ms", C.c_double),
+                ("rs_ms", C.c_double), ("exposed_ms", C.c_double)]
 
 
 class YsbLaunchDesc(C.Structure):

@@ -316,7 +316,7 @@ class YsbContext:
 
     def exchange_info(self, reset=False):
         """Exchange accounting (ysb_group_exchange_info): exchanges, bytes, ms, last_buckets,
-        last_width, full_ring_bytes."""
+        last_width, full_ring_bytes, critical_ms, rs_ms, exposed_ms."""
         x = YsbExchangeInfo()
         self._c(lib().ysb_group_exchange_info(self._h, C.byref(x), int(reset)))
         return {n: getattr(x, n) for n, _ in YsbExchangeInfo._fields_}

@@ -56,7 +56,7 @@ int main(void) {
   P(ysb_config, flags) P(ysb_config, overflow_capacity) P(ysb_count, window_ms) P(ysb_count, count)
   P(ysb_gen_params, ad_subset) P(ysb_gen_params, n_ad_subset) P(ysb_stats, batches) P(ysb_stats, deferred)
   P(ysb_stats, foreign_shard) P(ysb_exchange_info, ms) P(ysb_exchange_info, last_width)
-  P(ysb_exchange_info, full_ring_bytes)
+  P(ysb_exchange_info, full_ring_bytes) P(ysb_exchange_info, rs_ms) P(ysb_exchange_info, exposed_ms)
   return 0;
 }
 """
@@ -80,7 +80,7 @@ def test_struct_layouts_match_ctypes(tmp_path):
     assert int(got["ysb_stats.deferred"]) == _lib.YsbStats.deferred.offset
     assert int(got["ysb_stats.foreign_shard"]) == _lib.YsbStats.foreign_shard.offset
     assert int(got["ysb_exchange_info"]) == C.sizeof(_lib.YsbExchangeInfo)
-    for f in ("ms", "last_width", "full_ring_bytes"):
+    for f in ("ms", "last_width", "full_ring_bytes", "rs_ms", "exposed_ms"):
         assert int(got["ysb_exchange_info." + f]) == getattr(_lib.YsbExchangeInfo, f).offset
 
 

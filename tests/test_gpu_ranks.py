@@ -190,6 +190,8 @@ def test_one_rank_group_range_exchange_config3_sized():
             assert 0 < x["last_buckets"] <= 128
         # rows of whole aligned 4-slot groups: each run of buckets widened by < 4 slots per end
         assert x["bytes"] % (3 * 200_000) == 0 and x["ms"] > 0
+        # complete exchanges: the compute stream waits for every reduce-scatter at its unpack
+        assert 0 < x["rs_ms"] <= x["ms"] and 0 <= x["exposed_ms"] <= x["ms"], x
         row = x["bytes"] // (3 * 200_000)
         assert row % 4 == 0 and x["last_buckets"] <= row <= x["last_buckets"] + 6
         assert x["full_ring_bytes"] == 200_000 * 128 * 8
