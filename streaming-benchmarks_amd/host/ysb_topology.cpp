@@ -8,6 +8,8 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -505,6 +507,8 @@ public:
         const int rc = fd_ < 0 ? -1 : connect(fd_, res->ai_addr, res->ai_addrlen);
         freeaddrinfo(res);
         if (rc != 0) throw std::runtime_error("redis: cannot connect to " + host + ":" + std::to_string(port));
+        const int one = 1;   // a pipeline goes out at once, not held back by Nagle's algorithm
+        setsockopt(fd_, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
     }
     ~RespClient() {
         if (fd_ >= 0) ::close(fd_);

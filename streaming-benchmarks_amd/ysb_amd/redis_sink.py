@@ -42,6 +42,7 @@ class RespClient:
 
     def __init__(self, host="127.0.0.1", port=6379, timeout=10.0):
         self.sock = socket.create_connection((host, port), timeout=timeout)
+        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self.buf = b""
 
     def close(self):

@@ -6,6 +6,7 @@ from __future__ import annotations
 import collections
 import itertools
 import socketserver
+import socket
 import threading
 
 
@@ -31,31 +32,56 @@ def _int(n):
     return b":%d\r\n" % n
 
 
-class _Handler(socketserver.StreamRequestHandler):
-    def read_cmd(self):
-        ln = self.rfile.readline()
-        if not ln:
-            return None
-        assert ln[:1] == b"*", ln
-        n = int(ln[1:])
-        args = []
-        for _ in range(n):
-            hdr = self.rfile.readline()
-            assert hdr[:1] == b"$"
-            m = int(hdr[1:])
-            args.append(self.rfile.read(m + 2)[:m].decode())
-        return args
+class _Handler(socketserver.BaseRequestHandler):
+    """RESP over one connection: every complete command in what has arrived is run, and
+    their replies go back in one send (a pipelined client gets them together; replies
+    written one by one would meet Nagle's algorithm and the client's delayed ACK)."""
 
     def handle(self):
         st = self.server.state
+        sock = self.request
+        sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        buf = b""
+        pos = 0
         while True:
-            args = self.read_cmd()
-            if args is None:
+            chunk = sock.recv(1 << 20)
+            if not chunk:
                 return
-            with st.lock:
-                st.commands += 1
-                out = self.run(st.kv, args)
-            self.wfile.write(out)
+            buf = buf[pos:] + chunk
+            pos = 0
+            out = []
+            while True:
+                cmd = self.parse(buf, pos)
+                if cmd is None:
+                    break
+                args, pos = cmd
+                with st.lock:
+                    st.commands += 1
+                    out.append(self.run(st.kv, args))
+            if out:
+                sock.sendall(b"".join(out))
+
+    @staticmethod
+    def parse(buf, pos):
+        """(args, next position) of the command at pos, or None if it is not all here."""
+        e = buf.find(b"\r\n", pos)
+        if e < 0:
+            return None
+        assert buf[pos:pos + 1] == b"*", buf[pos:pos + 40]
+        n = int(buf[pos + 1:e])
+        p = e + 2
+        args = []
+        for _ in range(n):
+            e = buf.find(b"\r\n", p)
+            if e < 0:
+                return None
+            assert buf[p:p + 1] == b"$"
+            m = int(buf[p + 1:e])
+            if e + 2 + m + 2 > len(buf):
+                return None
+            args.append(buf[e + 2:e + 2 + m].decode())
+            p = e + 2 + m + 2
+        return args, p
 
     @staticmethod
     def run(kv, args):
