@@ -1,7 +1,7 @@
 """Runs one of bench.py's extra legs by itself (profiling passes, A/B runs):
     python tools/extra_one.py config3|config3_compact|config3_reorder|tbl|stream|host_staged|native_runner|
                               reorder|reorder_fixed|reorder_flat|reorder_flat_fixed|compact|mixed|mixed_flat_fixed|
-                              mixed_blocks|mixed_blocks_flat_fixed
+                              mixed_blocks|mixed_blocks_flat_fixed|alternating|stream_native
                               [bench.py options]"""
 import json
 import os
@@ -44,5 +44,7 @@ if __name__ == "__main__":
           "reorder_fixed": lambda: layout(args, GEN_REORDER, layout_auto=False),
           "reorder_flat": lambda: layout(args, GEN_REORDER, flat_first=True),
           "reorder_flat_fixed": lambda: layout(args, GEN_REORDER, flat_first=True, layout_auto=False),
-          "compact": lambda: layout(args, GEN_COMPACT)}[leg]
+          "compact": lambda: layout(args, GEN_COMPACT),
+          "alternating": lambda: bench.extra_alternating(args, 0),
+          "stream_native": lambda: bench.extra_stream_native(args, 0)}[leg]
     print(json.dumps(fn()), flush=True)
