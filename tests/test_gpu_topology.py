@@ -57,3 +57,25 @@ def test_runner_redis_sink_check_correct(tmp_path):
         assert res and all(s == "CORRECT" for _, _, s, _ in res)
     finally:
         srv.close()
+
+
+@pytest.mark.parametrize("shards,skew", [(1, 2), (2, 1)])
+def test_native_stream_mode_exact(shards, skew):
+    """bin/ysb_topology --stream (host/ysb_stream.hpp): a short replay through the pinned
+    slots with asynchronous flushes to the Redis writer; every (campaign, window) read back
+    through Redis equals the generator truth of what the runner played (check-correct), the
+    runner's own totals agree, and the windows the final watermark passed were closed with a
+    get-stats sample per (campaign, window).  Two shards share the one GPU (each its own
+    context and slots, one watermark = the minimum); skew 1 adds the reference's late events."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import bench_stream
+    r = bench_stream.stream_native(device=0, seconds=1.5, event_rate=1_000_000, speedup=20.0, shards=shards,
+                                   slot_mb=64, skew=skew, threads=8)
+    c = r["check"]
+    assert r["exact_vs_generator_truth"], c
+    assert c["truth_mismatched_cells"] == 0 and c["counted_views"] == c["truth_views"] > 0
+    assert c["parse_errors"] == 0 and c["join_misses"] == 0 and c["overflow_dropped"] == 0
+    assert r["flushes"] >= 20 and r["windows_closed"] >= 1
+    assert r["get_stats"]["samples_closed_windows"] >= 100 * r["windows_closed"] > 0
+    assert r["runner"]["cycles"] and len(r["runner"]["cycles"]) == shards
