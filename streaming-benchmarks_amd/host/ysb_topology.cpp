@@ -415,7 +415,8 @@ void GpuAdCampaignOperator::open() {
     cfg.max_batch_events = o_.batchEvents;
     // the replay file's producer is not known here: each host batch picks its scan from its
     // first line (YSB_F_LAYOUT_AUTO; the counts do not depend on it)
-    cfg.flags = (o_.tbl ? YSB_F_FORMAT_TBL : 0u) | (o_.requireIp ? YSB_F_REQUIRE_IP : 0u) | YSB_F_LAYOUT_AUTO;
+    cfg.flags = (o_.tbl ? YSB_F_FORMAT_TBL : 0u) | (o_.requireIp ? YSB_F_REQUIRE_IP : 0u) | YSB_F_LAYOUT_AUTO |
+                YSB_F_TIMING | (o_.h2dSdma ? YSB_F_H2D_SDMA : 0u);
     if (ysb_open(&ctx_, o_.device, &cfg) != YSB_OK)
         throw std::runtime_error(std::string("ysb_open: ") + ysb_last_error(nullptr));
     // RedisJoinBolt(Map) (:443-448): the whole map on the device
@@ -441,7 +442,9 @@ void GpuAdCampaignOperator::flatMap(const char* line, uint64_t len) {
 }
 
 uint64_t GpuAdCampaignOperator::fillFromRaw(FileBasedDataSource& src) {
+    const auto t0 = std::chrono::steady_clock::now();
     const uint64_t nb = src.fillRaw(bytes_[cur_] + fillBytes_, o_.batchBytes - fillBytes_);
+    fillS_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     fillBytes_ += nb;
     rawBytes_ += nb;
     return nb;
@@ -449,8 +452,10 @@ uint64_t GpuAdCampaignOperator::fillFromRaw(FileBasedDataSource& src) {
 
 uint64_t GpuAdCampaignOperator::fillFrom(FileBasedDataSource& src) {
     uint64_t nb = 0;
+    const auto t0 = std::chrono::steady_clock::now();
     const uint64_t n = src.fill(bytes_[cur_] + fillBytes_, o_.batchBytes - fillBytes_, off_[cur_] + fillEvents_,
                                 o_.batchEvents - fillEvents_, &nb);
+    fillS_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     for (uint64_t i = 0; i < n; ++i) off_[cur_][fillEvents_ + i] += (uint32_t)fillBytes_;
     fillBytes_ += nb;
     fillEvents_ += n;
@@ -468,7 +473,13 @@ void GpuAdCampaignOperator::submit() {
     submitted_ += fillEvents_;
     fillBytes_ = fillEvents_ = 0;
     cur_ ^= 1;
+    const auto t0 = std::chrono::steady_clock::now();
     check(ysb_wait(ctx_, cur_), "ysb_wait");   // the other slot's H2D is done: refill it
+    waitS_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void GpuAdCampaignOperator::copyTime(double* ms, uint64_t* copies, uint64_t* bytes) {
+    check(ysb_copy_time(ctx_, ms, copies, bytes), "ysb_copy_time");
 }
 
 std::vector<WindowDelta> GpuAdCampaignOperator::flushWindows() {

@@ -137,6 +137,7 @@ public:
         bool tbl = false;                   // MockWindowedFlatMap's .tbl rows (:197-226)
         bool requireIp = false;             // Storm/Spark's 7-field deserializer
         bool gpuSplit = true;               // fillFromRaw + ysb_submit_raw: line starts found on the GPU
+        bool h2dSdma = false;               // YSB_F_H2D_SDMA: the slot's H2D by the DMA engine (default: a copy kernel)
     };
     GpuAdCampaignOperator(const AdCampaignMap& map, const Options& o);
     ~GpuAdCampaignOperator();
@@ -152,11 +153,17 @@ public:
     void close();                                          // RichFlatMapFunction.close
     ysb_stats stats();
     uint64_t submittedEvents() const { return submitted_; }
+    // host seconds spent filling slots (fillFrom / fillFromRaw) and waiting for a slot's H2D
+    double fillSeconds() const { return fillS_; }
+    double waitSeconds() const { return waitS_; }
+    // the slots' H2D: total ms, copies and bytes (YSB_F_TIMING, ysb_copy_time)
+    void copyTime(double* ms, uint64_t* copies, uint64_t* bytes);
 
 private:
     const AdCampaignMap& map_;
     Options o_;
     ysb_ctx* ctx_ = nullptr;
+    double fillS_ = 0, waitS_ = 0;
     uint8_t* bytes_[2] = {nullptr, nullptr};
     uint32_t* off_[2] = {nullptr, nullptr};
     int cur_ = 0;

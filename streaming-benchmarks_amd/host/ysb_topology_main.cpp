@@ -42,6 +42,7 @@ struct Args {
     long long repeat = 1;
     unsigned io_threads = 0;
     bool io_mmap = true;
+    bool h2d_sdma = false;
     // streaming mode (configs[4]): --stream plus its options (ysb_stream.hpp)
     bool stream = false;
     StreamOptions so;
@@ -54,7 +55,7 @@ void usage() {
                  "usage: ysb_topology --confPath PATH [--device N] [--sink none|csv:FILE|redis[:HOST[:PORT]]]\n"
                  "       [--format json|tbl] [--flush-ms MS] [--batch-mb MB | --batch-bytes B] [--batch-events N]\n"
                  "       [--window-ring W] [--require-ip] [--dry-run] [--print-config] [--replay-rows CSV]\n"
-                 "       [--host-split] [--repeat K] [--io-threads T] [--io mmap|pread]\n"
+                 "       [--host-split] [--repeat K] [--io-threads T] [--io mmap|pread] [--h2d-sdma]\n"
                  "   or: ysb_topology --stream [--sink none|csv:FILE|redis[:HOST[:PORT]]] [--shards N] [--device D]\n"
                  "       [--seed S] [--campaigns C] [--ads-per-campaign A] [--event-rate E] [--speedup F]\n"
                  "       [--cycle-ms MS] [--flush-ms MS] [--batch-ms MS] [--ooo-ms MS] [--seconds S]\n"
@@ -86,6 +87,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--repeat") a.repeat = std::max(1ll, std::atoll(val().c_str()));
         else if (k == "--io-threads") a.io_threads = (unsigned)std::atoll(val().c_str());
         else if (k == "--io") a.io_mmap = val() != "pread";
+        else if (k == "--h2d-sdma") a.h2d_sdma = true;
         else if (k == "--stream") a.stream = true;
         else if (k == "--stream-self-check") { a.stream = true; a.self_check = true; }
         else if (k == "--shards") a.so.shards = std::atoi(val().c_str());
@@ -163,6 +165,7 @@ int run(const Args& a) {
     o.tbl = tbl;
     o.requireIp = a.require_ip;
     o.gpuSplit = !a.host_split;
+    o.h2dSdma = a.h2d_sdma;
 
     FileBasedDataSource src(events, a.io_threads, a.io_mmap);
     const double t0 = now_s();
@@ -248,12 +251,16 @@ int run(const Args& a) {
     const double el = now_s() - t0;
     if (!csv_path.empty()) csv.write(csv_path);
     const ysb_stats s = op.stats();
+    double copy_ms = 0;
+    uint64_t copies = 0, copy_bytes = 0;
+    op.copyTime(&copy_ms, &copies, &copy_bytes);
     std::printf("{\"mode\": \"gpu\", \"events\": %llu, \"views\": %llu, \"joined\": %llu, \"join_misses\": %llu, "
                 "\"parse_errors\": %llu, \"time_errors\": %llu, \"out_of_ring\": %llu, \"overflow_dropped\": %llu, "
                 "\"batches\": %llu, \"rows_written\": %llu, \"flushes\": %llu, \"seconds\": %.3f, "
                 "\"events_per_s\": %.1f, \"stream_seconds\": %.3f, \"stream_events_per_s\": %.1f, "
                 "\"bytes\": %llu, \"stream_GBs\": %.2f, \"line_split\": \"%s\", \"repeat\": %lld, "
-                "\"format\": \"%s\", \"sink\": %s}\n",
+                "\"format\": \"%s\", \"sink\": %s, \"h2d\": \"%s\", \"copy_GBs\": %.2f, \"copy_busy_frac\": %.4f, "
+                "\"fill_s\": %.3f, \"slot_wait_s\": %.3f}\n",
                 (unsigned long long)s.events, (unsigned long long)s.views, (unsigned long long)s.joined,
                 (unsigned long long)s.join_misses, (unsigned long long)s.parse_errors,
                 (unsigned long long)s.time_errors, (unsigned long long)s.out_of_ring,
@@ -262,7 +269,9 @@ int run(const Args& a) {
                 el_stream > 0 ? (double)s.events / el_stream : 0.0, (unsigned long long)src.bytesRead(),
                 el_stream > 0 ? (double)src.bytesRead() / el_stream / 1e9 : 0.0, o.gpuSplit ? "gpu" : "host",
                 a.repeat, tbl ? "tbl" : "json",
-                json_str(a.sink).c_str());
+                json_str(a.sink).c_str(), a.h2d_sdma ? "sdma" : "kernel",
+                copy_ms > 0 ? (double)copy_bytes / (copy_ms * 1e-3) / 1e9 : 0.0,
+                el_stream > 0 ? copy_ms * 1e-3 / el_stream : 0.0, op.fillSeconds(), op.waitSeconds());
     return s.overflow_dropped ? 3 : 0;
 }
 

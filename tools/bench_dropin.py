@@ -158,7 +158,7 @@ def truth_rows(device, g, n, cids, repeat):
 
 
 def native_runner(device=0, file_events=20_000_000, repeat=5, slot_mb=256, host_split=False, workdir=None,
-                  keep=None, io="mmap"):
+                  keep=None, io="mmap", h2d_sdma=False):
     made = workdir is None
     path = workdir or tempfile.mkdtemp(prefix="ysb_replay_", dir=os.environ.get("TMPDIR") or "/tmp")
     try:
@@ -175,6 +175,8 @@ def native_runner(device=0, file_events=20_000_000, repeat=5, slot_mb=256, host_
                "csv:" + out_csv, "--batch-mb", str(slot_mb), "--repeat", str(repeat), "--io", io]
         if host_split:
             cmd += ["--host-split", "--batch-events", str((slot_mb << 20) // 200)]
+        if h2d_sdma:
+            cmd += ["--h2d-sdma"]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             raise RuntimeError("ysb_topology exited %d: %s" % (r.returncode, r.stderr[-2000:]))
@@ -208,11 +210,16 @@ def main():
     ap.add_argument("--repeat", type=int, default=5)
     ap.add_argument("--host-split", action="store_true")
     ap.add_argument("--io", default="mmap", choices=["mmap", "pread"])
+    ap.add_argument("--h2d-sdma", action="store_true", help="the slots' H2D by the DMA engine (default: a copy kernel)")
+    ap.add_argument("--workdir", default=None, help="runner: keep / reuse the replay file here")
     a = ap.parse_args()
     if a.mode == "staged":
-        out = host_staged(a.device, a.events, a.slot_mb, a.raw)
+        out = host_staged(a.device, a.events, a.slot_mb, a.raw, h2d_sdma=a.h2d_sdma)
     else:
-        out = native_runner(a.device, a.file_events, a.repeat, a.slot_mb, a.host_split, io=a.io)
+        if a.workdir:
+            os.makedirs(a.workdir, exist_ok=True)
+        out = native_runner(a.device, a.file_events, a.repeat, a.slot_mb, a.host_split, workdir=a.workdir, io=a.io,
+                            h2d_sdma=a.h2d_sdma)
     print(json.dumps(out), flush=True)
 
 
