@@ -5,12 +5,6 @@
 // definitions it uses (the LDS sources, spans, load_span, the org.json machine).
 #pragma once
 
-// A/B (round 5): flat_parse_bl2 reading each pair's key, separator and value in one LDS
-// round trip (15 aligned words) instead of two or three
-#ifndef YSB_FLAT_SPAN
-#define YSB_FLAT_SPAN 0
-#endif
-
 namespace ysb {
 
 // ---- the general path's flat tier --------------------------------------------------------
@@ -381,20 +375,7 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
         const u32 open = st == 1u ? 1u : 0u;
         kq = open ? kq : s + 1;                       // an idle lane reads inside its line
         u32 kw[4];
-#if YSB_FLAT_SPAN
-        // one LDS round trip per pair: the key, its separator and the value's 40 bytes read
-        // together as 15 aligned words from the key's first byte; the value's words are
-        // picked out after the key is named (its start lies 8..17 bytes past the first word)
-        u32 R[15];
-        const int rb = (kq + 1) >> 2;
-#pragma unroll
-        for (int j = 0; j < 15; ++j) R[j] = src.d[rb + j];
-        const u32 sh0 = (u32)((kq + 1) & 3);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) kw[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], sh0);
-#else
         load_span(src, kq + 1, kw);
-#endif
         const u32 d7 = kw[1] ^ w4('_', 'i', 'd', '"');
         const u32 dEV = kw[0] ^ w4('e', 'v', 'e', 'n');
         const u32 k2 = kw[2] & 0xFFFFFFu;
@@ -415,22 +396,7 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
         const int vq = ke + (s3 == 0u ? 3 : 2);
         u32 bad = min(s3, s2) | (id == 0u ? 1u : 0u) | (seen & id) | ((u32)(e - 1 - vq) >> 31);
         u32 w[10];
-#if YSB_FLAT_SPAN
-        {
-            // the value's first byte vq + 1 is R's byte rel (8..17: key 5 / 7 / 10 bytes,
-            // `":"` or `": "`); idle or failed lanes may point elsewhere: clamp, result unused
-            const int rel = min(max(vq + 1 - 4 * rb, 8), 19);
-            const int i0 = rel >> 2;
-            const u32 sh = (u32)(rel & 3);
-            u32 c[11];
-#pragma unroll
-            for (int j = 0; j < 11; ++j) c[j] = i0 == 2 ? R[2 + j] : i0 == 3 ? R[3 + j] : R[min(4 + j, 14)];
-#pragma unroll
-            for (int j = 0; j < 10; ++j) w[j] = __builtin_amdgcn_alignbyte(c[j + 1], c[j], sh);
-        }
-#else
         load_span(src, vq + 1, w);
-#endif
         int ve;
         u32 y;
         if (id & (K_AD | K_USER | K_PAGE)) {
@@ -445,17 +411,7 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
             }
             bad |= la == 0 ? 1u : 0u;
             ve = vq + 1 + la;
-#if YSB_FLAT_SPAN
-            // a vocabulary value (<= 16 bytes) ends inside w: the closing quote and the 3 bytes
-            // after it from w's words, no LDS round trip; a longer one by a read
-            const int yi = la >> 2;
-            const u32 ys = (u32)(la & 3);
-            const u32 lo = yi == 0 ? w[0] : yi == 1 ? w[1] : yi == 2 ? w[2] : yi == 3 ? w[3] : w[4];
-            const u32 hi = yi == 0 ? w[1] : yi == 1 ? w[2] : yi == 2 ? w[3] : yi == 3 ? w[4] : w[5];
-            y = la <= 16 ? __builtin_amdgcn_alignbyte(hi, lo, ys) : src.load4(ve);
-#else
             y = src.load4(ve);
-#endif
         }
         const u32 n3 = y ^ w4('"', ',', ' ', '"');
         const u32 n2 = (y ^ w4('"', ',', '"', 0)) & 0xFFFFFFu;
