@@ -70,12 +70,12 @@ def parse_args(argv=None):
     ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--stream-seconds", type=float, default=12.0,
                     help="extras: wall seconds of the native streaming leg (configs[4]; at the default speedup "
-                         "12 s of input is 372 s of event time: >= 30 windows close); 0 skips it")
+                         "12 s of input is 420 s of event time: >= 30 windows close); 0 skips it")
     ap.add_argument("--stream-event-rate", type=int, default=5_000_000,
                     help="extras: events per second of event time in the streaming replay")
-    ap.add_argument("--stream-speedup", type=float, default=31.0,
-                    help="extras: event time per wall time of the streaming replay (5M x 31 = 155M events/s: "
-                         "under the replay's ~158M/s host fill ceiling on a 16-core share, so it keeps up)")
+    ap.add_argument("--stream-speedup", type=float, default=35.0,
+                    help="extras: event time per wall time of the streaming replay (5M x 35 = 175M events/s: "
+                         "under the ~183M/s the replay sustains on a 16-core share, so it keeps up)")
     ap.add_argument("--stream-rate", type=int, default=20_000_000,
                     help="tools/bench_extra.py stream_sharded: aggregate events/s of the Python producers")
     ap.add_argument("--dropin-events", type=int, default=100_000_000,
@@ -389,7 +389,8 @@ def extra_native_runner(args, device, staged):
     """bin/ysb_topology (the native drop-in for `flink run ... --confPath`) over a replay file
     in the page cache, read --runner-repeat times: raw lines with the split on the GPU (the
     default) and host-split offsets, against the generator truth; vs_host_staged = its stream
-    rate / the host-staged raw path's (the H2D-bound rate)."""
+    rate / the host-staged raw path's (the H2D-bound rate).  gpu_split_dma_engine: the same
+    with the slots' H2D by the DMA engine (--h2d-sdma) instead of the copy kernel."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_dropin
     import tempfile
@@ -398,14 +399,17 @@ def extra_native_runner(args, device, staged):
         r = {"gpu_split": bench_dropin.native_runner(device, args.runner_file_events, args.runner_repeat,
                                                     workdir=path),
              "host_split": bench_dropin.native_runner(device, args.runner_file_events, args.runner_repeat,
-                                                     host_split=True, workdir=path)}
+                                                     host_split=True, workdir=path),
+             "gpu_split_dma_engine": bench_dropin.native_runner(device, args.runner_file_events, args.runner_repeat,
+                                                               workdir=path, h2d_sdma=True)}
     finally:
         import shutil
         shutil.rmtree(path, ignore_errors=True)
     if staged and "raw" in staged:
         r["vs_host_staged"] = round(r["gpu_split"]["stream_events_per_s"] / staged["raw"]["events_per_s"], 4)
-    log("extras: native_runner %.3f G events/s (host split %.3f)" % (r["gpu_split"]["stream_events_per_s"] / 1e9,
-                                                                     r["host_split"]["stream_events_per_s"] / 1e9))
+    log("extras: native_runner %.3f G events/s (host split %.3f, DMA engine %.3f)"
+        % (r["gpu_split"]["stream_events_per_s"] / 1e9, r["host_split"]["stream_events_per_s"] / 1e9,
+           r["gpu_split_dma_engine"]["stream_events_per_s"] / 1e9))
     return r
 
 

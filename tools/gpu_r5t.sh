@@ -3,7 +3,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r5t; mkdir -p $O
-timeout -k 10 400 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_raw.py tests/test_gpu_topology.py tests/test_gpu_stream.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+timeout -k 10 400 python3 -u -m pytest -q --timeout 120 --timeout-method thread tests/test_gpu_raw.py tests/test_gpu_topology.py tests/test_gpu_stream.py > $O/tests.log 2>&1 || tail -30 $O/tests.log
 tail -1 $O/tests.log
 W=/tmp/ysb_r5t_replay
 for r in 1 2; do
