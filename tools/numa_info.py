@@ -42,20 +42,47 @@ def thread_node():
     return {"cpu": cpu, "node": cpu_node(cpu)}
 
 
+def _kfd_gpu_bus(device):
+    """The PCI address of the device-th GPU in the KFD topology (nodes with SIMDs, in node
+    order: HIP's device order when no *_VISIBLE_DEVICES filter is set), or None."""
+    gpus = []
+    for d in glob.glob("/sys/class/kfd/kfd/topology/nodes/*"):
+        try:
+            props = dict(ln.split() for ln in open(os.path.join(d, "properties")) if len(ln.split()) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", 0)) > 0:
+            loc, dom = int(props.get("location_id", 0)), int(props.get("domain", 0))
+            gpus.append((int(os.path.basename(d)), "%04x:%02x:%02x.%x" % (dom, loc >> 8, (loc >> 3) & 31, loc & 7)))
+    gpus.sort()
+    return gpus[device][1] if device < len(gpus) else None
+
+
 def gpu_node(device=0):
+    """{"bus", "node"} of the GPU: the bus id from hipDeviceGetPCIBusId when this process's
+    HIP runtime sees the device, else from the KFD topology (a process whose torch bundles
+    another HIP runtime may not see it through libamdhip64), and the PCI device's numa_node."""
+    bus = None
     try:
-        hip = C.CDLL("libamdhip64.so")
+        try:
+            hip = C.CDLL("libamdhip64.so")
+        except OSError:
+            hip = C.CDLL("/opt/rocm/lib/libamdhip64.so")
+        buf = C.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) == 0:
+            bus = buf.value.decode().lower()
     except OSError:
-        hip = C.CDLL("/opt/rocm/lib/libamdhip64.so")
-    buf = C.create_string_buffer(64)
-    if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
-        return {"bus": None, "node": -1}
-    bus = buf.value.decode().lower()
+        pass
+    how = "hip"
+    if bus is None:
+        bus, how = _kfd_gpu_bus(device), "kfd"
+    if bus is None:
+        return {"bus": None, "node": -1, "from": None}
     try:
         node = int(open("/sys/bus/pci/devices/%s/numa_node" % bus).read())
     except OSError:
         node = -1
-    return {"bus": bus, "node": node}
+    return {"bus": bus, "node": node, "from": how}
 
 
 def thp_kb(addr):
