@@ -83,8 +83,9 @@ def parse_args(argv=None):
     ap.add_argument("--runner-file-events", type=int, default=20_000_000,
                     help="extras: events in the native runner's replay file")
     ap.add_argument("--runner-repeat", type=int, default=5, help="extras: times the runner reads its replay file")
-    ap.add_argument("--extras-timeout", type=int, default=300,
-                    help="N > 1: seconds the configs[2]-table leg may take before rank 0 prints the headline without it")
+    ap.add_argument("--extras-timeout", type=int, default=600,
+                    help="N > 1: seconds the extras (configs[2]-table leg, then rank 0's N-GPU native stream) may "
+                         "take before rank 0 prints the headline without them")
     ap.add_argument("--c3-events", type=int, default=100_000_000,
                     help="extras at N > 1: events per GPU of the configs[2]-table leg (1M campaigns / 10M ads)")
     ap.add_argument("--layout-fixed", action="store_true",
@@ -568,15 +569,19 @@ def extra_alternating(args, device):
     return r
 
 
-def extra_stream_native(args, device):
+def extra_stream_native(args, device, shards=1):
     """configs[4] natively: bin/ysb_topology --stream (tools/bench_stream.py): replay bytes
     through the pinned double-buffered slots at the ingest ceiling, asynchronous flushes
     through the C++ Redis writer, get-stats' per-(campaign, window) latency read back, exact
-    vs the generator truth (check-correct)."""
+    vs the generator truth (check-correct).  shards > 1 (bench.py --gpus N, rank 0 after the
+    other legs): one shard per GPU of the node (shard s on device s), one watermark = the
+    minimum over them, the same total replay rate split over the shards (the replay's host
+    threads, not the GPUs, bound it)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_stream
-    r = bench_stream.stream_native(device, seconds=args.stream_seconds, event_rate=args.stream_event_rate,
-                                   speedup=args.stream_speedup)
+    r = bench_stream.stream_native(device, seconds=args.stream_seconds,
+                                   event_rate=max(1, args.stream_event_rate // shards),
+                                   speedup=args.stream_speedup, shards=shards)
     log("extras: stream_native %.3f G events/s, get-stats p50 / p99 %s / %s ms (closed windows %d), exact %s"
         % (r["events_per_s"] / 1e9, r["get_stats"]["p50_ms"], r["get_stats"]["p99_ms"],
            r["get_stats"]["closed_windows"], r["exact_vs_generator_truth"]))
@@ -946,7 +951,8 @@ def main():
             def give_up():
                 with printed_lock:
                     if d.rank == 0 and not printed:
-                        out["extras"] = {"config3": {"error": "timed out after %d s" % args.extras_timeout}}
+                        out["extras"] = {"config3": {"error": "the N > 1 extras timed out after %d s"
+                                                                  % args.extras_timeout}}
                         print(json.dumps(out), flush=True)
                         printed.append(True)
                 # non-zero: the launcher (and CI) must see that a rank was stuck in a collective
@@ -956,6 +962,10 @@ def main():
             dog.start()
             extra = {}
             guarded(extra, "config3", lambda: config3_ranks(args, d))
+            # configs[4] across the node's GPUs: rank 0 runs the native streaming mode with one
+            # shard per rank's GPU (a process of its own; the other ranks are done with theirs)
+            if d.rank == 0 and args.stream_seconds > 0:
+                guarded(extra, "stream_native", lambda: extra_stream_native(args, 0, shards=d.world))
             dog.cancel()
 
     with printed_lock:   # (the watchdog may print the line instead, never both)
