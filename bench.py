@@ -93,6 +93,8 @@ def parse_args(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and set up torch.distributed, then stop before any GPU call")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--no-live-traffic", action="store_true",
+                    help="N = 1: take roofline.traffic from --traffic instead of two rocprofv3 --pmc child passes")
     a = ap.parse_args(argv)
     if a.events is None:
         a.events = TOTAL_EVENTS_8 // a.gpus if a.gpus >= 8 else 100_000_000
@@ -728,6 +730,54 @@ def config3_ranks(args, d):
                       "check_exchange_cell_bytes": per[0]["chk_width"]}}
 
 
+def live_traffic(args, kernel):
+    """HBM bytes per launch of the headline kernel, measured for this run's configuration by two
+    child passes of this script under `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` (one
+    counter each: the passes stay within the hardware's per-block limits), after this process's
+    timed region: per-dispatch averages of `kernel`, FETCH_SIZE x 2 (the gfx950 correction of
+    MI355X_MICROARCH.md's HBM section), KiB -> bytes.  None when rocprofv3 is absent or a pass
+    fails (the line then falls back to profiles/pmc_traffic.json)."""
+    import csv
+    import shutil
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    tmp = tempfile.mkdtemp(prefix="ysb_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    got = {}
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", counter, "--output-format", "csv", "-d", out,
+                   "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "1",
+                   "--no-cpu", "--no-check", "--no-extras", "--no-live-traffic", "--events", str(args.events),
+                   "--segment", str(args.segment), "--rate", str(args.rate)]
+            if args.per_batch:
+                cmd.append("--per-batch")
+            r = subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=200)
+            if r.returncode != 0:
+                log("live traffic: the %s pass exited %d" % (counter, r.returncode))
+                return None
+            vals = []
+            for fn in os.listdir(out):
+                if fn.endswith("counter_collection.csv"):
+                    for row in csv.DictReader(open(os.path.join(out, fn))):
+                        if row["Kernel_Name"].startswith(kernel) and row["Counter_Name"] == counter:
+                            vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None
+            got[counter] = sum(vals) / len(vals)
+    except Exception as e:   # noqa: BLE001 (the constant file is the fallback)
+        log("live traffic: %s" % e)
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    rd, wr = 2 * got["FETCH_SIZE"] * 1024, got["WRITE_SIZE"] * 1024
+    return {"hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
+            "hbm_bytes_per_launch": int(rd + wr)}
+
+
 def exchange_overlap(x):
     """Per step: the reduce-scatter's own time (rs), the part of it the compute stream waited
     for at the unpack (exposed) and the rest, which ran beside the queued launches (hidden)."""
@@ -903,6 +953,17 @@ def main():
         s0 = segs[0]
         cpu = cpu_baseline(ctx, s0[2], s0[4], s0[3], s0[1], aids, camp, args.cpu_sample, args.cpu_seconds)
 
+    traffic_source = "profiles/pmc_traffic.json (PMC passes of this configuration, tools/final_profile.sh)"
+    if d.world == 1 and not args.no_live_traffic:
+        lt = live_traffic(args, "void ysb::scan_kernel<false, false, false, %d>" % layout_run)
+        if lt:
+            traffic = lt["hbm_bytes_per_launch"]
+            traffic_source = ("measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes of this "
+                              "configuration, per-dispatch averages, FETCH_SIZE x 2 (gfx950); read %d B, write %d B"
+                              % (lt["hbm_read_bytes_per_launch"], lt["hbm_write_bytes_per_launch"]))
+    if traffic is None:
+        traffic_source = None
+
     out = None
     if d.rank == 0:
         out = {
@@ -923,6 +984,7 @@ def main():
                        else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_source,
                          "kernel": "ysb::scan_kernel<false, false, false, %d>" % layout_run,
                          "avg_launch_ms": round(avg_launch_ms, 4),
                          "alg_bytes_per_launch": int(alg_bytes_launch)},
