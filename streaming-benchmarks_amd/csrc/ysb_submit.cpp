@@ -741,10 +741,10 @@ int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) 
         c->raw_layout[slot] = hinted_layout(c, sniff_raw(c, c->h_bytes[slot], nbytes, &c->raw_learn[slot]));
     // H2D once the slot's previous kernel has run.  The split: behind the DMA engine's copy on a
     // stream of its own (the next slot's copy queues right behind this one); behind the copy
-    // kernel on the copy stream itself -- on a compute stream of its own it was measured to wait
-    // for the NEXT slot's copy kernel as well (the runner's slot refill then stalled a whole
-    // copy: 155-173 vs 211-213 M events/s, gpurun_out/r5s), in the copy stream's order it runs
-    // right after its own copy and the next copy follows it
+    // kernel on the copy stream itself, so it runs right after its own copy and the next copy
+    // follows it.  Same-box A/B of the native runner with the copy kernel (gpurun_out/r5w, r5x,
+    // four alternations each): on the copy stream 186-203 M events/s, on a stream of its own
+    // 162-181, on the compute stream 188-193 (the DMA engine 209-213)
     const bool sdma = (c->cfg.flags & YSB_F_H2D_SDMA) != 0u;
     hipStream_t ss = sdma ? c->s_split : c->s_copy;
     HIPCHK(c, hipStreamWaitEvent(c->s_copy, c->ev_kdone[slot], 0));
@@ -754,7 +754,7 @@ int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) 
     if (nbytes) HIPCHK(c, h2d(c, c->d_bytes[slot], c->hd_bytes[slot], c->h_bytes[slot], nbytes));
     if (ce) HIPCHK(c, hipEventRecord(ce[1], c->s_copy));
     HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
-    if (sdma) HIPCHK(c, hipStreamWaitEvent(ss, c->ev_h2d[slot], 0));
+    if (ss != c->s_copy) HIPCHK(c, hipStreamWaitEvent(ss, c->ev_h2d[slot], 0));
     if (nbytes) {
         // the line count goes straight to pinned memory (read at the launch)
         HIPCHK(c, launch_split_lines(c->d_bytes[slot], nbytes, c->d_split_chunk, c->d_roff[slot],
