@@ -304,3 +304,39 @@ def test_async_flushes_sum_to_the_drain_without_stopping_the_stream():
     assert {(c, w // 10000): v for (c, w), v in got.items()} == rows
     for k, v in ost.items():
         assert st[k] == v, (k, st[k], v)
+
+
+def test_async_flush_over_its_row_cap_leaves_the_rest_for_the_next():
+    """A flush holds at most 2^20 rows (ysb_flush_begin): 200k campaigns x ~7 windows of views
+    (~1.3M nonzero cells; record mode, its u8 delta ring folded in first) need two flushes --
+    the first returns 2^20 rows with more = 1 and keeps the rest on the device, the second
+    returns them with more = 0; together they equal the generator truth exactly, and nothing
+    is left for a drain."""
+    from ysb_amd.group import table_rows
+    C, W, n = 200_000, 16, 12_000_000
+    g = GenParams(seed=67, n_campaigns=C, ads_per_campaign=10, events_per_sec=n // 65)
+    _, ab = g.ids_packed()
+    with YsbContext(device=0, n_campaigns=C, window_ring=W, ring_base_bucket=g.c.t0_ms // 10000 - 8,
+                    max_batch_bytes=1 << 20, max_batch_events=1 << 12) as ctx:
+        ctx.load_ad_map_packed(ab, g.ad_campaign_index_array())
+        cap = n * g.max_line_bytes()
+        d_b, d_o = ctx.device_alloc(cap), ctx.device_alloc(4 * n + 64)
+        nb = ctx.gen_events_device(g, 0, n, d_b, cap, d_o)
+        ctx.submit_device(d_b, nb, d_o, n)
+        ctx.truth_accumulate(g, 0, n)
+        truth, lo = ctx.truth_read()
+        want = {(c, b * 10000): v for (c, b), v in table_rows(truth, lo).items()}
+        assert len(want) > (1 << 20), len(want)
+        ctx.flush_begin()
+        first, more = ctx.flush_end(wait=True)
+        assert more and len(first) == 1 << 20
+        ctx.flush_begin()
+        second, more2 = ctx.flush_end(wait=True)
+        assert not more2 and len(first) + len(second) == len(want)
+        assert not (set(first) & set(second))
+        got = dict(first)
+        got.update(second)
+        assert got == want
+        assert ctx.drain(clear=True) == {}
+        ctx.device_free(d_b)
+        ctx.device_free(d_o)
