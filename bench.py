@@ -954,7 +954,10 @@ def main():
         cpu = cpu_baseline(ctx, s0[2], s0[4], s0[3], s0[1], aids, camp, args.cpu_sample, args.cpu_seconds)
 
     traffic_source = "profiles/pmc_traffic.json (PMC passes of this configuration, tools/final_profile.sh)"
-    if d.world == 1 and not args.no_live_traffic:
+    # (not when this process runs under rocprofv3 itself: a profiler started from a profiled
+    # process would exec its program from a process whose GPU is already initialised)
+    profiled = any(k.startswith("ROCPROF_") for k in os.environ)
+    if d.world == 1 and not args.no_live_traffic and not profiled:
         lt = live_traffic(args, "void ysb::scan_kernel<false, false, false, %d>" % layout_run)
         if lt:
             traffic = lt["hbm_bytes_per_launch"]
