@@ -16,7 +16,7 @@ cp $B/rawtrace/run_kernel_stats.csv ${P}_raw_kernel_stats.csv
 tail -1 $B/rawtrace.json > ${P}_raw_dropin.json
 cp $B/mixtrace/run_kernel_stats.csv ${P}_mixed_kernel_stats.csv
 cp $B/streamtrace/run_kernel_stats.csv ${P}_stream_kernel_stats.csv
-tail -1 $B/streamtrace.json > ${P}_stream_native_trace_run.json
+tail -1 $B/streamtrace.json > ${P}_stream_native_trace_run.json   # the runner itself under the tracer
 cp $B/xtrace/run_kernel_stats.csv ${P}_exchange_kernel_stats.csv
 tail -1 $B/xcost.json > ${P}_exchange_cost.json
 { echo "# SQ counters per flat-tier dispatch (tools/sq_passes.sh over tools/extra_one.py reorder_flat_fixed, $B/sq_flat)"
