@@ -351,7 +351,13 @@ namespace ysb {
 
 // LDS layout (dynamic, 16-byte aligned carve, no static __shared__)
 // ---------------------------------------------------------------------------
-constexpr int LDS_BYTES = Geom<false>::LDS;   // the JSON geometry (Geom<true> for .tbl rows)
+constexpr int LDS_BYTES = Geom<false>::LDS;
+// layouts 2-4 (the flat tier) launch with the key table past the geometry's LDS; the JSON
+// geometries keep their workgroups per CU with it
+constexpr int FLAT_KT_LDS = KEYTAB_BYTES;
+static_assert((Geom<false>::LDS + FLAT_KT_LDS + 1279) / 1280 * 1280 * Geom<false>::WG_PER_CU <= 163840 &&
+                  (Geom<false, true>::LDS + FLAT_KT_LDS + 1279) / 1280 * 1280 * Geom<false, true>::WG_PER_CU <= 163840,
+              "the flat tier's key table must not cost a workgroup per CU");   // the JSON geometry (Geom<true> for .tbl rows)
 
 struct TileInfo {
     u64 first;
@@ -562,6 +568,12 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
     u32* lcnt = reinterpret_cast<u32*>(smem + G::OFF_LCNT);
     i64* misc64 = reinterpret_cast<i64*>(smem + G::OFF_MISC);   // [0] lbase, [1] lset, [2..5] scratch
     u32* tb = reinterpret_cast<u32*>(smem + G::OFF_TB);
+    // the flat tier's key table past the geometry's LDS (layouts 2-4 launch with KEYTAB_BYTES more)
+    u32* keytab = reinterpret_cast<u32*>(smem + G::LDS);
+    if constexpr (!TBL && LAY >= 2) {
+        if (threadIdx.x < 64) keytab[threadIdx.x] = KEYTAB.w[threadIdx.x];
+        __syncthreads();
+    }
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -666,11 +678,11 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
-            else if constexpr (LAY == 2) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb);
+            else if constexpr (LAY == 2) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb, keytab);
             else if constexpr (LAY == 3) {
                 ok1 = P.learn_cp ? learned_parse<true>(lsrc, ls, le, P, ca, cb) : learned_parse<false>(lsrc, ls, le, P, ca, cb);
                 // a line off the learned order: the flat tier (any order or spacing)
-                if (__builtin_expect(!ok1, 0)) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb);
+                if (__builtin_expect(!ok1, 0)) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb, keytab);
             }
             else if constexpr (LAY == 4) {}   // below, once the wave's mode is known
             else ok1 = vocab_stage1<LAY == 1>(lsrc, ls, le, ca);
@@ -760,7 +772,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 CanonA c2;
                 CanonB b2;
                 b2.view = false;
-                if (flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, c2, b2)) {
+                if (flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, c2, b2, keytab)) {
                     ca = c2;
                     cb = b2;
                     ok2 = true;
@@ -1246,20 +1258,20 @@ void launch_scan(const ScanParams& p, hipStream_t s) {
         // layout instantiations too (round 4), so other producers' layouts keep their fast tier
         if (p.rec_on) {
             if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<true, false, true, 1>), g, b, (Geom<false, true>::LDS), s, p);
-            else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<true, false, true, 2>), g, b, (Geom<false, true>::LDS), s, p);
-            else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<true, false, true, 3>), g, b, (Geom<false, true>::LDS), s, p);
-            else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<true, false, true, 4>), g, b, (Geom<false, true>::LDS), s, p);
+            else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<true, false, true, 2>), g, b, (Geom<false, true>::LDS + FLAT_KT_LDS), s, p);
+            else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<true, false, true, 3>), g, b, (Geom<false, true>::LDS + FLAT_KT_LDS), s, p);
+            else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<true, false, true, 4>), g, b, (Geom<false, true>::LDS + FLAT_KT_LDS), s, p);
             else hipLaunchKernelGGL((scan_kernel<true, false, true>), g, b, (Geom<false, true>::LDS), s, p);
         } else if (p.probe_serial) {
             if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<true, false, false, 1>), g, b, Geom<false>::LDS, s, p);
-            else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<true, false, false, 2>), g, b, Geom<false>::LDS, s, p);
-            else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<true, false, false, 3>), g, b, Geom<false>::LDS, s, p);
-            else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<true, false, false, 4>), g, b, Geom<false>::LDS, s, p);
+            else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<true, false, false, 2>), g, b, (Geom<false>::LDS + FLAT_KT_LDS), s, p);
+            else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<true, false, false, 3>), g, b, (Geom<false>::LDS + FLAT_KT_LDS), s, p);
+            else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<true, false, false, 4>), g, b, (Geom<false>::LDS + FLAT_KT_LDS), s, p);
             else hipLaunchKernelGGL((scan_kernel<true, false, false>), g, b, Geom<false>::LDS, s, p);
         } else if (p.layout == 1) hipLaunchKernelGGL((scan_kernel<false, false, false, 1>), g, b, Geom<false>::LDS, s, p);
-        else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<false, false, false, 2>), g, b, Geom<false>::LDS, s, p);
-        else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<false, false, false, 3>), g, b, Geom<false>::LDS, s, p);
-        else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<false, false, false, 4>), g, b, Geom<false>::LDS, s, p);
+        else if (p.layout == 2) hipLaunchKernelGGL((scan_kernel<false, false, false, 2>), g, b, (Geom<false>::LDS + FLAT_KT_LDS), s, p);
+        else if (p.layout == 3) hipLaunchKernelGGL((scan_kernel<false, false, false, 3>), g, b, (Geom<false>::LDS + FLAT_KT_LDS), s, p);
+        else if (p.layout == 4) hipLaunchKernelGGL((scan_kernel<false, false, false, 4>), g, b, (Geom<false>::LDS + FLAT_KT_LDS), s, p);
         else hipLaunchKernelGGL((scan_kernel<false, false, false>), g, b, Geom<false>::LDS, s, p);
     }
 }

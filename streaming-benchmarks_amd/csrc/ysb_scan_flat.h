@@ -7,6 +7,58 @@
 
 namespace ysb {
 
+// ---- the flat tier's key table (round 5) ---------------------------------------------------
+// DeserializeBolt's seven keys named by one LDS read instead of a compare chain (A/B: +2-3 %
+// on the flat tier and the mixed interleave, profiles/AB_LOG.md round 5).  With the key's
+// first eight bytes in kw[0], kw[1] (text, closing quote, separator), x = kw[0] ^ (kw[1] >> 8)
+// and slot = bits 17..20 of the low 32 bits of x[23:0] * KEYTAB_MUL (v_mul_u32_u24, v_bfe): a
+// perfect hash of the seven keys' texts (ad_id takes two slots: its kw[1] holds the separator's
+// first bytes, `": "` or `":"`).  Entry = {kw[0], kw[1] & m1, kw[2] & m2, meta}, meta = id |
+// kl << 8 | s1 << 16 | s2 << 24, m1 = ~0 >> s1, m2 = 0xFFFFFF >> s2: the key's text and closing
+// quote compared exactly as flat_parse_bl2's compares do; an empty slot (meta 0) names nothing.
+constexpr int KEYTAB_BYTES = 256;
+constexpr u32 KEYTAB_MUL = 8809287u;   // < 2^24 (found by search: the 8 texts land in 8 slots)
+struct KeyDef {
+    u32 w0, w1, w2, id, kl;   // w1 / w2: the bytes the key owns (text and closing quote)
+    u32 h1;                   // kw[1] as the hash sees it (with the separator's bytes)
+};
+constexpr KeyDef KEYDEFS[8] = {
+    {w4('a', 'd', '_', 'i'), w4('d', '"', 0, 0), 0u, K_AD, 5u, w4('d', '"', ':', ' ')},
+    {w4('a', 'd', '_', 'i'), w4('d', '"', 0, 0), 0u, K_AD, 5u, w4('d', '"', ':', '"')},
+    {w4('u', 's', 'e', 'r'), w4('_', 'i', 'd', '"'), 0u, K_USER, 7u, w4('_', 'i', 'd', '"')},
+    {w4('p', 'a', 'g', 'e'), w4('_', 'i', 'd', '"'), 0u, K_PAGE, 7u, w4('_', 'i', 'd', '"')},
+    {w4('a', 'd', '_', 't'), w4('y', 'p', 'e', '"'), 0u, K_ADTYPE, 7u, w4('y', 'p', 'e', '"')},
+    {w4('e', 'v', 'e', 'n'), w4('t', '_', 't', 'y'), w4('p', 'e', '"', 0), K_ETYPE, 10u, w4('t', '_', 't', 'y')},
+    {w4('e', 'v', 'e', 'n'), w4('t', '_', 't', 'i'), w4('m', 'e', '"', 0), K_ETIME, 10u, w4('t', '_', 't', 'i')},
+    {w4('i', 'p', '_', 'a'), w4('d', 'd', 'r', 'e'), w4('s', 's', '"', 0), K_IP, 10u, w4('d', 'd', 'r', 'e')},
+};
+__host__ __device__ constexpr u32 keytab_slot(u32 kw0, u32 kw1) {
+    return (u32)((unsigned long long)(((kw1 >> 8) ^ kw0) & 0xFFFFFFu) * KEYTAB_MUL) >> 17 & 15u;
+}
+struct KeyTab { u32 w[64]; };
+constexpr KeyTab make_keytab() {
+    KeyTab t{};
+    for (const KeyDef& d : KEYDEFS) {
+        const u32 s = keytab_slot(d.w0, d.h1);
+        const u32 s1 = d.kl == 5u ? 16u : 0u, s2 = d.kl == 10u ? 0u : 24u;
+        t.w[4 * s] = d.w0;
+        t.w[4 * s + 1] = d.w1;
+        t.w[4 * s + 2] = d.w2;
+        t.w[4 * s + 3] = d.id | d.kl << 8 | s1 << 16 | s2 << 24;
+    }
+    return t;
+}
+constexpr bool keytab_perfect() {   // two different keys never share a slot
+    for (int i = 0; i < 8; ++i)
+        for (int j = i + 1; j < 8; ++j)
+            if (KEYDEFS[i].id != KEYDEFS[j].id &&
+                keytab_slot(KEYDEFS[i].w0, KEYDEFS[i].h1) == keytab_slot(KEYDEFS[j].w0, KEYDEFS[j].h1))
+                return false;
+    return true;
+}
+static_assert(keytab_perfect(), "KEYTAB_MUL must separate the seven keys");
+constexpr KeyTab KEYTAB = make_keytab();
+
 // ---- the general path's flat tier --------------------------------------------------------
 // A flat object of plain double-quoted string pairs whose keys are all DeserializeBolt's
 // -- in any order, with any whitespace nextClean skips, ',' or ';' between pairs and a
@@ -350,7 +402,7 @@ __device__ __forceinline__ int bl2_vocab(u32 id, const u32 (&A)[10]) {
 // Round 4 (YSB_FLAT_BL): flat_parse_lds's common forms with no slow branch per pair -- for
 // batches whose lines carry different key orders (several producers interleaved), where
 // every per-pair branch of a per-lane walk diverges.  Per pair, for every lane at once: the
-// key named (as in flat_parse_lds), `": "` / `":"`, the value -- an id as 36 plain bytes by
+// key named (round 5: by the key table kt in LDS, KEYTAB above), `": "` / `":"`, the value -- an id as 36 plain bytes by
 // plain36's cheap test, any other value named from its vocabulary or, when it is none of
 // them, by the string scan -- and `", "` / `","` / `"}` after it; the loop runs while any
 // lane is open (a uniform exit).  Any other form (another key, a repeat, other spacing, a
@@ -363,7 +415,7 @@ __device__ __forceinline__ int bl2_vocab(u32 id, const u32 (&A)[10]) {
 // (`bad`: 0 = the pair is in the common forms), the lane state is a u32 (1 open, 2 closed,
 // 0 out: the caller's flat_parse_lds decides the line) and each decision is one compare.
 __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, u32 require, Span& ad, Span& et,
-                                               Span& tm, u32 (&adw)[9]) {
+                                               Span& tm, u32 (&adw)[9], const u32* kt) {
     // (u32)(a - b) >> 31: 1 when a < b (positions < 2^31)
     u32 st = (((src.load4(s) & 0xFFFFu) ^ w4('{', '"', 0, 0)) | ((u32)(e - 2 - s) >> 31)) == 0u ? 1u : 0u;
     int kq = s + 1;
@@ -376,18 +428,12 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
         kq = open ? kq : s + 1;                       // an idle lane reads inside its line
         u32 kw[4];
         load_span(src, kq + 1, kw);
-        const u32 d7 = kw[1] ^ w4('_', 'i', 'd', '"');
-        const u32 dEV = kw[0] ^ w4('e', 'v', 'e', 'n');
-        const u32 k2 = kw[2] & 0xFFFFFFu;
-        const u32 dAD = (kw[0] ^ w4('a', 'd', '_', 'i')) | ((kw[1] ^ w4('d', '"', 0, 0)) & 0xFFFFu);
-        const u32 dUS = (kw[0] ^ w4('u', 's', 'e', 'r')) | d7;
-        const u32 dPG = (kw[0] ^ w4('p', 'a', 'g', 'e')) | d7;
-        const u32 dAT = (kw[0] ^ w4('a', 'd', '_', 't')) | (kw[1] ^ w4('y', 'p', 'e', '"'));
-        const u32 dET = dEV | (kw[1] ^ w4('t', '_', 't', 'y')) | (k2 ^ (w4('p', 'e', '"', 0) & 0xFFFFFFu));
-        const u32 dTM = dEV | (kw[1] ^ w4('t', '_', 't', 'i')) | (k2 ^ (w4('m', 'e', '"', 0) & 0xFFFFFFu));
-        const u32 dIP = (kw[0] ^ w4('i', 'p', '_', 'a')) | (kw[1] ^ w4('d', 'd', 'r', 'e')) | (k2 ^ (w4('s', 's', '"', 0) & 0xFFFFFFu));
-        const u32 id = dAD == 0u ? K_AD : dUS == 0u ? K_USER : dPG == 0u ? K_PAGE : dAT == 0u ? K_ADTYPE
-                     : dET == 0u ? K_ETYPE : dTM == 0u ? K_ETIME : dIP == 0u ? K_IP : 0u;
+        // the key named by its slot in the key table (one LDS read; see KEYTAB above)
+        const u32 slot = (__umul24((kw[1] >> 8) ^ kw[0], KEYTAB_MUL) >> 17) & 15u;
+        const uint4 en = *reinterpret_cast<const uint4*>(kt + 4 * slot);
+        const u32 m1 = 0xFFFFFFFFu >> ((en.w >> 16) & 31u), m2 = 0xFFFFFFu >> (en.w >> 24);
+        const u32 dk = (kw[0] ^ en.x) | ((kw[1] & m1) ^ en.y) | ((kw[2] & m2) ^ en.z);
+        const u32 id = dk == 0u ? (en.w & 0xFFu) : 0u;
         const u32 k7 = id & (K_USER | K_PAGE | K_ADTYPE);
         const u32 x = id == K_AD ? __builtin_amdgcn_alignbyte(kw[2], kw[1], 2) : k7 ? kw[2] : __builtin_amdgcn_alignbyte(kw[3], kw[2], 3);
         const int ke = kq + 1 + (id == K_AD ? 5 : k7 ? 7 : 10);
@@ -488,14 +534,15 @@ __device__ __forceinline__ bool flat_parse(const S& src, int s, int e, u32 requi
 // the canonical tiers hand on (key words, event_time offset and first 20 bytes, view).
 // Other ad_id lengths go to the deferred-line kernel (its table lookup takes any key).
 template <class S, bool FAST = false>
-__device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 require, CanonA& a, CanonB& b) {
+__device__ __forceinline__ bool flat_tier(const S& src, int ls, int le, u32 require, CanonA& a, CanonB& b,
+                                          const u32* kt = nullptr) {
     Span ad{0, 0, 0}, et{0, 0, 0}, tm{0, 0, 0};
     bool okp;
     if constexpr (FAST && std::is_same<S, LdsSrc>::value) {
         u32 adw[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) adw[k] = 0u;
-        okp = flat_parse_bl2(src, ls, le, require, ad, et, tm, adw);
+        okp = flat_parse_bl2(src, ls, le, require, ad, et, tm, adw, kt);
         if (__builtin_expect(!okp, 0)) okp = flat_parse_lds(src, ls, le, require, ad, et, tm, adw);
         if (!okp || ad.e - ad.s != 36) return false;
         const bool fast_ad = adw[0] | adw[1] | adw[8];   // the id fast path kept the ad_id's words
