@@ -11,13 +11,13 @@ namespace ysb {
 // DeserializeBolt's seven keys named by one LDS read instead of a compare chain (A/B: +2-3 %
 // on the flat tier and the mixed interleave, profiles/AB_LOG.md round 5).  With the key's
 // first eight bytes in kw[0], kw[1] (text, closing quote, separator), x = kw[0] ^ (kw[1] >> 8)
-// and slot = bits 17..20 of the low 32 bits of x[23:0] * KEYTAB_MUL (v_mul_u32_u24, v_bfe): a
-// perfect hash of the seven keys' texts (ad_id takes two slots: its kw[1] holds the separator's
-// first bytes, `": "` or `":"`).  Entry = {kw[0], kw[1] & m1, kw[2] & m2, meta}, meta = id |
-// kl << 8 | s1 << 16 | s2 << 24, m1 = ~0 >> s1, m2 = 0xFFFFFF >> s2: the key's text and closing
-// quote compared exactly as flat_parse_bl2's compares do; an empty slot (meta 0) names nothing.
+// and slot = bits 20..23 of x ^ (x >> 1): a perfect hash of the seven keys' texts (found by
+// search; shifts and xors only, no quarter-rate multiply; ad_id's kw[1] holds the separator's
+// first bytes, `": "` or `":"`, and both land in its slot).  Entry = {kw[0], kw[1] & m1,
+// kw[2] & m2, meta}, meta = id | kl << 8 | s1 << 16 | s2 << 24, m1 = ~0 >> s1,
+// m2 = 0xFFFFFF >> s2: the key's text and closing quote compared exactly as the compare chain
+// did; an empty slot (meta 0) names nothing.
 constexpr int KEYTAB_BYTES = 256;
-constexpr u32 KEYTAB_MUL = 8809287u;   // < 2^24 (found by search: the 8 texts land in 8 slots)
 struct KeyDef {
     u32 w0, w1, w2, id, kl;   // w1 / w2: the bytes the key owns (text and closing quote)
     u32 h1;                   // kw[1] as the hash sees it (with the separator's bytes)
@@ -33,7 +33,8 @@ constexpr KeyDef KEYDEFS[8] = {
     {w4('i', 'p', '_', 'a'), w4('d', 'd', 'r', 'e'), w4('s', 's', '"', 0), K_IP, 10u, w4('d', 'd', 'r', 'e')},
 };
 __host__ __device__ constexpr u32 keytab_slot(u32 kw0, u32 kw1) {
-    return (u32)((unsigned long long)(((kw1 >> 8) ^ kw0) & 0xFFFFFFu) * KEYTAB_MUL) >> 17 & 15u;
+    const u32 x = kw0 ^ (kw1 >> 8);
+    return ((x ^ (x >> 1)) >> 20) & 15u;
 }
 struct KeyTab { u32 w[64]; };
 constexpr KeyTab make_keytab() {
@@ -56,7 +57,7 @@ constexpr bool keytab_perfect() {   // two different keys never share a slot
                 return false;
     return true;
 }
-static_assert(keytab_perfect(), "KEYTAB_MUL must separate the seven keys");
+static_assert(keytab_perfect(), "keytab_slot must separate the seven keys");
 constexpr KeyTab KEYTAB = make_keytab();
 
 // ---- the general path's flat tier --------------------------------------------------------
@@ -429,7 +430,7 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
         u32 kw[4];
         load_span(src, kq + 1, kw);
         // the key named by its slot in the key table (one LDS read; see KEYTAB above)
-        const u32 slot = (__umul24((kw[1] >> 8) ^ kw[0], KEYTAB_MUL) >> 17) & 15u;
+        const u32 slot = keytab_slot(kw[0], kw[1]);
         const uint4 en = *reinterpret_cast<const uint4*>(kt + 4 * slot);
         const u32 m1 = 0xFFFFFFFFu >> ((en.w >> 16) & 31u), m2 = 0xFFFFFFu >> (en.w >> 24);
         const u32 dk = (kw[0] ^ en.x) | ((kw[1] & m1) ^ en.y) | ((kw[2] & m2) ^ en.z);
