@@ -73,6 +73,26 @@ def test_bench_ranks_share_ring_base_and_sum_to_truth(world):
     assert owned == total_joined
 
 
+def test_one_rank_group_runs_bench_config3_ranks():
+    """bench.config3_ranks -- the configs[2]-table leg every N > 1 run times -- on a real
+    one-rank RCCL group: its pipelined range exchange per step, the exchange fields of its
+    line (rs / exposed / hidden per step), and its checksum check, exact."""
+    import bench
+    os.environ.pop("WORLD_SIZE", None)
+    d = bench.Dist(1)
+    d.resolve_device()
+    args = bench.parse_args(["--c3-events", "8000000", "--extra-steps", "3", "--warmup", "1"])
+    r = bench.config3_ranks(args, d)
+    ex, chk = r["exchange"], r["check"]
+    assert chk["checksum_blocks_mismatched"] == 0 and chk["truth_mismatched_cells"] == 0
+    assert chk["truth_views"] == chk["counted_views"] > 0 and chk["join_misses"] == 0
+    assert chk["foreign_shard"] == 0 and chk["parse_errors"] == 0
+    for k in ("rs_ms_per_step", "exposed_ms_per_step", "hidden_ms_per_step"):
+        assert ex[k] >= 0, (k, ex)
+    assert abs(ex["hidden_ms_per_step"] - max(ex["rs_ms_per_step"] - ex["exposed_ms_per_step"], 0.0)) <= 2e-4
+    assert r["record_mode"] and r["n_gpus"] == 1
+
+
 def test_one_rank_group_runs_bench_exchange_check():
     """A real (one-rank) RCCL group: ysb_group_init agrees on the ring, the reduce-scatter
     moves the table into the owned block, and bench.exchange_check -- the code the N-rank
