@@ -251,10 +251,10 @@ int         ysb_slot_capacity(ysb_ctx* ctx, uint64_t* max_bytes, uint64_t* max_e
  * so the caller (FileBasedDataSource.run, AdvertisingTopologyNative.java:144-165) only reads
  * the file into the pinned slot (max_batch_bytes bytes, at most max(max_batch_events,
  * max_batch_bytes / 32) lines: the device keeps 4 B per line start, not per byte).
- * Asynchronous and double-buffered like ysb_submit: H2D on the copy stream, the split on a
- * stream of its own; the batch's scan is launched once its line count is back, at the next
- * call on the context (the next submit, ysb_sync, ...), so a caller that fills the other slot
- * in between keeps the copy engine busy; ysb_wait(ctx, slot) before the slot's pinned buffer
+ * Asynchronous and double-buffered like ysb_submit: H2D on the copy stream, the split right
+ * behind it on the same stream (with YSB_F_H2D_SDMA: on a stream of its own); the batch's scan
+ * is launched once its line count is back, at the next call on the context (the next submit,
+ * ysb_sync, ...), so a caller that fills the other slot in between keeps the copies going; ysb_wait(ctx, slot) before the slot's pinned buffer
  * is rewritten.  A batch that cannot launch (more lines than the slot holds: YSB_ERR_CAPACITY,
  * or a HIP failure) is dropped, and its error is returned by the call that performs the
  * launch and by every later call that orders work after it, until ysb_reset. */
