@@ -81,3 +81,19 @@ def test_native_stream_mode_exact(shards, skew):
     # with skew 1 a late event (1e-5 of them, < 60 s late) can make an old window of one campaign
     assert 100 <= r["get_stats"]["samples_closed_windows"] <= 100 * r["windows_closed"]
     assert r["runner"]["cycles"] and len(r["runner"]["cycles"]) == shards
+
+
+def test_native_stream_mode_ring_follows_the_watermark():
+    """A 16-bucket ring under 150 s of event time: the runner moves the ring forward as the
+    watermark advances (ysb_ring_advance after taking the outstanding flushes), and every
+    count -- the buckets the ring left included -- still reaches Redis exactly."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import bench_stream
+    r = bench_stream.stream_native(device=0, seconds=2.5, event_rate=500_000, speedup=60.0, slot_mb=32, threads=8,
+                                   window_ring=16)
+    c = r["check"]
+    assert r["ring_advances"] >= 1, r["ring_advances"]
+    assert r["exact_vs_generator_truth"], c
+    assert c["truth_mismatched_cells"] == 0 and c["counted_views"] == c["truth_views"] > 0
+    assert c["overflow_dropped"] == 0 and c["parse_errors"] == 0 and c["join_misses"] == 0

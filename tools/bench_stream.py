@@ -69,7 +69,7 @@ def truth_table(device, summary):
 
 
 def stream_native(device=0, seconds=12.0, event_rate=5_000_000, speedup=32.0, shards=1, slot_mb=256,
-                  flush_ms=1000, batch_ms=100, ooo_ms=100, skew=2, threads=0, workdir=None):
+                  flush_ms=1000, batch_ms=100, ooo_ms=100, skew=2, threads=0, workdir=None, window_ring=64):
     from fake_redis import FakeRedis
     from ysb_amd import GenParams
     from ysb_amd.redis_sink import RespClient, check_correct, get_stats, new_setup
@@ -84,7 +84,7 @@ def stream_native(device=0, seconds=12.0, event_rate=5_000_000, speedup=32.0, sh
                "--totals", totals_csv, "--seconds", str(seconds), "--event-rate", str(event_rate),
                "--speedup", str(speedup), "--shards", str(shards), "--batch-mb", str(slot_mb),
                "--flush-ms", str(flush_ms), "--batch-ms", str(batch_ms), "--ooo-ms", str(ooo_ms),
-               "--skew", str(skew), "--io-threads", str(threads)]
+               "--skew", str(skew), "--io-threads", str(threads), "--window-ring", str(window_ring)]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             raise RuntimeError("ysb_topology --stream exited %d: %s" % (r.returncode, r.stderr[-2000:]))
@@ -141,6 +141,7 @@ def stream_native(device=0, seconds=12.0, event_rate=5_000_000, speedup=32.0, sh
         "copy_busy_frac": s["copy_busy_frac"], "slot_waits": s["slot_waits"], "slot_wait_ms": s["slot_wait_ms"],
         "slot_wait_max_ms": s["slot_wait_max_ms"], "max_behind_ms": s["max_behind_ms"],
         "flushes": s["flushes"], "rows_written": s["rows_written"], "redis_commands": commands,
+        "ring_advances": s["ring_advances"], "window_ring": window_ring,
         "windows_closed": s["window_close_ms"]["n"],
         "window_close_latency_event_ms": s["window_close_ms"],
         "window_close_latency_wall_ms": s["window_close_wall_ms"],
