@@ -254,10 +254,11 @@ int         ysb_slot_capacity(ysb_ctx* ctx, uint64_t* max_bytes, uint64_t* max_e
  * Asynchronous and double-buffered like ysb_submit: H2D on the copy stream, the split right
  * behind it on the same stream (with YSB_F_H2D_SDMA: on a stream of its own); the batch's scan
  * is launched once its line count is back, at the next call on the context (the next submit,
- * ysb_sync, ...), so a caller that fills the other slot in between keeps the copies going; ysb_wait(ctx, slot) before the slot's pinned buffer
- * is rewritten.  A batch that cannot launch (more lines than the slot holds: YSB_ERR_CAPACITY,
- * or a HIP failure) is dropped, and its error is returned by the call that performs the
- * launch and by every later call that orders work after it, until ysb_reset. */
+ * ysb_sync, ...), so a caller that fills the other slot in between keeps the copies going;
+ * ysb_wait(ctx, slot) before the slot's pinned buffer is rewritten.  A batch that cannot
+ * launch (more lines than the slot holds: YSB_ERR_CAPACITY, or a HIP failure) is dropped, and
+ * its error is returned by the call that performs the launch and by every later call that
+ * orders work after it, until ysb_reset. */
 int         ysb_submit_raw(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes);
 /* The same split of a device-resident batch (16-byte aligned, < 4 GiB): d_off[0..*n) <- its
  * line starts (YSB_ERR_CAPACITY, *n = the lines, if more than cap).  Synchronous. */
