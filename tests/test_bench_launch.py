@@ -66,3 +66,41 @@ def test_device_count_without_a_gpu_is_zero():
     """ysb_device_count on this CPU-only container: 0, no exception, no framework needed."""
     from ysb_amd import device_count
     assert device_count() == 0
+
+
+def test_live_traffic_reads_the_two_pmc_passes(monkeypatch, tmp_path):
+    """bench.live_traffic (roofline.traffic measured in the run): two child passes of bench.py
+    under rocprofv3, one counter each, launched with the program after `--`; per-dispatch
+    averages of the named kernel only, FETCH_SIZE x 2 (gfx950) and KiB -> bytes.  The
+    profiler is stubbed: this checks the commands and the arithmetic, not the counters."""
+    import shutil
+    import bench
+    calls = []
+
+    def fake_run(cmd, cwd=None, env=None, capture_output=None, text=None, timeout=None):
+        calls.append(cmd)
+        counter = cmd[cmd.index("--pmc") + 1]
+        out = cmd[cmd.index("-d") + 1]
+        os.makedirs(out, exist_ok=True)
+        kern = "void ysb::scan_kernel<false, false, false, 0>(ysb::ScanParams)"
+        rows = [("__amd_rocclr_fillBufferAligned", 5.0), (kern, 100.0), (kern, 300.0)]
+        with open(os.path.join(out, "run_counter_collection.csv"), "w") as f:
+            f.write('"Kernel_Name","Counter_Name","Counter_Value"\n')
+            for k, v in rows:
+                f.write('"%s","%s",%f\n' % (k, counter, v * (1 if counter == "FETCH_SIZE" else 0.5)))
+        return subprocess.CompletedProcess(cmd, 0, "", "")
+
+    monkeypatch.setattr(shutil, "which", lambda name: "/opt/rocm/bin/rocprofv3" if name == "rocprofv3" else None)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    args = bench.parse_args([])
+    r = bench.live_traffic(args, "void ysb::scan_kernel<false, false, false, 0>")
+    assert len(calls) == 2
+    for cmd, counter in zip(calls, ("FETCH_SIZE", "WRITE_SIZE")):
+        assert cmd[cmd.index("--pmc") + 1] == counter
+        assert cmd[cmd.index("--") + 1] == sys.executable and "--no-live-traffic" in cmd   # no nested profiler
+    assert r["hbm_read_bytes_per_launch"] == int(2 * 200.0 * 1024)     # mean of the kernel's dispatches
+    assert r["hbm_write_bytes_per_launch"] == int(100.0 * 1024)
+    assert r["hbm_bytes_per_launch"] == r["hbm_read_bytes_per_launch"] + r["hbm_write_bytes_per_launch"]
+    # without rocprofv3 there is no live figure (the line falls back to pmc_traffic.json)
+    monkeypatch.setattr(shutil, "which", lambda name: None)
+    assert bench.live_traffic(args, "x") is None
