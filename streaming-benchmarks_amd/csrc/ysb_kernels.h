@@ -71,18 +71,6 @@ struct Geom {
 };
 constexpr int AUX_TPB = 256;                  // threads per workgroup of the other kernels
 
-// Kernel 1m (ysb_scan_mix.h, round 5): layout 2 with LDS window counters runs as four-wave
-// workgroups that deal four tiles' lines out by producer class, two workgroups per CU.
-#ifndef YSB_MIX
-#define YSB_MIX 0
-#endif
-#ifndef YSB_MIX_WAVES
-#define YSB_MIX_WAVES 4
-#endif
-constexpr int MIX_WG_PER_CU = 8 / YSB_MIX_WAVES;
-constexpr int MIX_MAX_TILES = 512;   // tiles per static run of a four-wave workgroup (its LDS tile bounds)
-inline bool use_mix_kernel(u32 tbl, u32 layout, u32 lds_wl) { return YSB_MIX && !tbl && layout == 2 && lds_wl; }
-
 // One batch of a multi-batch launch (ysb_submit_device_segments): each keeps its own
 // u32 line offsets (so each stays under 4 GiB), and one launch scans them all -- every
 // workgroup walks its run of tiles in segment 0, then in segment 1, ..., without a

@@ -1016,8 +1016,6 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
 #endif
 }
 
-#include "ysb_scan_mix.h"
-
 // ---------------------------------------------------------------------------
 // The fork's live input format: pipe-delimited .tbl lines
 // (MockWindowedFlatMap.flatMap, flink-benchmarks/.../AdvertisingTopologyNative.java:197-226):
@@ -1250,11 +1248,6 @@ void launch_tbl_ring_autobase(const ScanParams& p, hipStream_t s) {
 void launch_scan(const ScanParams& p, hipStream_t s) {
     if (p.n == 0) return;
     const dim3 g(p.grid), b(SCAN_TPB);
-    if (use_mix_kernel(p.tbl, p.layout, p.lds_wl)) {   // Kernel 1m: p.grid counts four-wave workgroups
-        if (p.probe_serial) hipLaunchKernelGGL(mix_scan_kernel<true>, g, dim3(MIX_TPB), GeomMix::LDS, s, p);
-        else hipLaunchKernelGGL(mix_scan_kernel<false>, g, dim3(MIX_TPB), GeomMix::LDS, s, p);
-        return;
-    }
     // record mode only with HBM-resident tables (large configurations: serial probes)
     if (p.tbl) {
         if (p.rec_on) hipLaunchKernelGGL((scan_kernel<true, true, true>), g, b, (Geom<true, true>::LDS), s, p);

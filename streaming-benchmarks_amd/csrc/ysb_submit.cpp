@@ -61,9 +61,7 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
     // chunks by the workgroups that finish first.  The grid is whole rounds of resident
     // workgroups (a partial last round would idle most CUs), enough that no static run
     // exceeds MAX_TILES_PER_BLOCK tiles (the LDS copy of a run's tile bounds).
-    const bool mix = use_mix_kernel(p.tbl, p.layout, c->lds_wl);
-    const u64 resident = (u64)c->cus * (mix ? MIX_WG_PER_CU : p.tbl ? Geom<true>::WG_PER_CU : Geom<false>::WG_PER_CU);
-    const u64 max_run = mix ? MIX_MAX_TILES : MAX_TILES_PER_BLOCK;
+    const u64 resident = (u64)c->cus * (p.tbl ? Geom<true>::WG_PER_CU : Geom<false>::WG_PER_CU);
     const u32 chunk = std::min<u32>(c->dyn_chunk, MAX_TILES_PER_BLOCK);
     u64 line_base = 0, max_static = 0;
     bool any_dyn = false;
@@ -82,7 +80,7 @@ static ScanParams make_params(ysb_ctx* c, const ysb_segment* segs, u32 nseg) {
         any_dyn |= sg.n_static < sg.n_tiles;
         max_static = std::max(max_static, sg.n_static);
     }
-    const u64 rounds = std::max<u64>(1, (max_static + resident * max_run - 1) / (resident * max_run));
+    const u64 rounds = std::max<u64>(1, (max_static + resident * MAX_TILES_PER_BLOCK - 1) / (resident * MAX_TILES_PER_BLOCK));
     const u64 grid = std::max<u64>(1, std::min<u64>(max_static, rounds * resident));
     for (u32 i = 0; i < nseg; ++i) {
         ScanSeg& sg = p.seg[i];
