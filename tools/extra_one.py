@@ -1,6 +1,6 @@
 """Runs one of bench.py's extra legs by itself (profiling passes, A/B runs):
     python tools/extra_one.py config3|config3_compact|config3_reorder|tbl|stream|host_staged|native_runner|
-                              reorder|reorder_fixed|reorder_flat|reorder_flat_fixed|compact|mixed|mixed_flat_fixed|
+                              generator|reorder|reorder_fixed|reorder_flat|reorder_flat_fixed|compact|mixed|mixed_flat_fixed|
                               mixed_blocks|mixed_blocks_flat_fixed|alternating|stream_native
                               [bench.py options]"""
 import json
@@ -35,6 +35,7 @@ if __name__ == "__main__":
           "config3_reorder": lambda: bench.extra_config3(args, 0, GEN_REORDER, "reordered keys"),
           "host_staged": lambda: bench.extra_host_staged(args, 0),
           "native_runner": lambda: bench.extra_native_runner(args, 0, None),
+          "generator": lambda: layout(args, 0),
           "mixed": lambda: layout(args, GEN_MIXED),
           "mixed_blocks": lambda: layout(args, GEN_MIXED_BLOCKS),
           "mixed_blocks_flat_fixed": lambda: layout(args, GEN_MIXED_BLOCKS, flat_first=True, layout_auto=False),
