@@ -394,7 +394,6 @@ StreamReport StreamingJob::run(const FlushSink& sink) {
     int64_t nextFlush = o_.t0Ms + o_.flushMs, flushIndex = 0;
     const double stopAt = wall0 + o_.seconds;
     double firstSubmit = 0, lastSubmit = 0;
-    std::vector<std::string> patch;   // the nine leading time digits of each code, this cycle
 
     auto fill = [&](Shard* s, const ReplayCycle::Batch& b, uint8_t* dst) -> uint64_t {
         return fill_batch(s->cyc, b, s->cycle, o_.cycleMs, dst, pool, T);
