@@ -92,6 +92,8 @@ def parse_args(argv=None):
                     help="A/B: no first-line layout sampling of the device batches (YSB_F_LAYOUT_FIXED)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and set up torch.distributed, then stop before any GPU call")
+    ap.add_argument("--extras-out", default=os.path.join(ROOT, "gpurun_out", "bench_extras.json"),
+                    help="where the extras go in full (the printed line holds a summary per leg)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--no-live-traffic", action="store_true",
                     help="N = 1: take roofline.traffic from --traffic instead of two rocprofv3 --pmc child passes")
@@ -232,15 +234,101 @@ def dry_run(d, args):
         d.dist.destroy_process_group()
 
 
-def torch_sync(device=0):
-    """torch.cuda.synchronize() on this rank's own GPU (the contract's sync; the library's
-    streams are synchronised by ctx.sync() before it)."""
-    try:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.synchronize(device)
-    except Exception:
-        pass
+def device_sync(device=0):
+    """The contract's device-wide synchronize on this rank's own GPU, through the library's own
+    HIP runtime (ysb_device_sync = hipDeviceSynchronize; the library's streams are synchronised
+    by ctx.sync() before it).  Not torch.cuda.synchronize: torch 2.10 bundles its own HIP/HSA
+    runtime, and whichever runtime opens the GPU first in a process is the one that sees it
+     -- bench.py never initialises torch's."""
+    from ysb_amd import device_sync as _sync
+    _sync(device)
+
+
+# ---- the printed line ---------------------------------------------------------------------
+# The driver reads the LAST stdout line and keeps a bounded tail of stdout: the line holds the
+# contract keys and one short summary per extra leg; the extras in full go to a file
+# (--extras-out) and to one stderr line before it.
+LINE_MAX_BYTES = 6000
+
+
+def _exact(r):
+    """True / False when the leg carries a check, else None."""
+    if "exact_vs_generator_truth" in r:
+        return bool(r["exact_vs_generator_truth"])
+    ch = r.get("check")
+    if not isinstance(ch, dict):
+        return None
+    bad = 0
+    for k in ("truth_mismatched_cells", "checksum_blocks_mismatched", "overflow_dropped", "parse_errors",
+              "join_misses", "deferred", "deferred_to_general_path"):
+        v = ch.get(k)
+        if isinstance(v, (int, float)):
+            bad += v
+    x = ch.get("exchange")
+    if isinstance(x, dict):
+        bad += x.get("post_exchange_mismatched_cells", 0)
+    if "truth_views" in ch and "counted_views" in ch:
+        bad += ch["truth_views"] != ch["counted_views"]
+    return bad == 0
+
+
+def leg_summary(r):
+    """One extra leg in a few keys: events_per_s, hbm_frac, exact (or its error)."""
+    if not isinstance(r, dict):
+        return None
+    if "error" in r:
+        return {"error": str(r["error"])[:160]}
+    s = {}
+    eps = r.get("stream_events_per_s", r.get("events_per_s"))
+    if eps is not None:
+        s["events_per_s"] = eps
+    if r.get("hbm_frac") is not None:
+        s["hbm_frac"] = r["hbm_frac"]
+    ex = _exact(r)
+    if ex is not None:
+        s["exact"] = ex
+    if not s:   # a leg of sub-legs (host_staged, native_runner)
+        for k, v in r.items():
+            if isinstance(v, dict) and (v.get("events_per_s") is not None or v.get("stream_events_per_s") is not None):
+                s[k] = leg_summary(v)
+    return s
+
+
+def extras_summary(extra):
+    return {k: leg_summary(v) for k, v in (extra or {}).items()}
+
+
+def bench_line(out, extra, extras_path=None):
+    """The one JSON line rank 0 prints last: `out` (the contract keys) plus the extras'
+    summary, at most LINE_MAX_BYTES (the summary is dropped leg by leg if it would not fit)."""
+    line = dict(out)
+    if extra is not None:
+        line["extras_summary"] = extras_summary(extra)
+        if extras_path:
+            line["extras_file"] = os.path.relpath(extras_path, ROOT) if extras_path.startswith(ROOT) else extras_path
+    txt = json.dumps(line, separators=(",", ":"))
+    while len(txt) > LINE_MAX_BYTES and line.get("extras_summary"):
+        line["extras_summary"].popitem()
+        line["extras_truncated"] = True
+        txt = json.dumps(line, separators=(",", ":"))
+    return txt
+
+
+def emit(out, extra, extras_out):
+    """Full extras to extras_out and to stderr, then the compact line on stdout (last)."""
+    path = None
+    if extra is not None:
+        full = json.dumps(extra)
+        log("bench extras: " + full)
+        if extras_out:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(extras_out)), exist_ok=True)
+                with open(extras_out, "w") as f:
+                    f.write(full + "\n")
+                path = os.path.abspath(extras_out)
+            except OSError as e:
+                log("bench: could not write %s: %s" % (extras_out, e))
+    print(bench_line(out, extra, path), flush=True)
 
 
 def cpu_baseline(ctx, d_b, d_o, nb_seg, n_seg, ads, camp, sample, seconds):
@@ -657,13 +745,13 @@ def config3_ranks(args, d):
         ctx.sync()
         ctx.kernel_time()
         ctx.exchange_info(reset=True)
-        torch_sync(d.device)
+        device_sync(d.device)
         d.barrier()
         t0 = time.perf_counter()
         for i in range(args.extra_steps):
             step(i == args.extra_steps - 1)
         ctx.sync()
-        torch_sync(d.device)
+        device_sync(d.device)
         d.barrier()
         el = d.max(time.perf_counter() - t0)
         kms, launches = ctx.kernel_time()
@@ -894,22 +982,20 @@ def main():
         if d.world > 1:
             exchange(ctx, last)
 
-    # torch's own CUDA context is created here, before the warmup: created between warmup
-    # and timing it idles the GPU ~1.5 s and the first timed steps run at ramping clocks
-    torch_sync(d.device)
+    device_sync(d.device)
     for _ in range(args.warmup):
         step()
     ctx.sync()
     ctx.kernel_time()   # discard warmup launches
     if d.world > 1:
         ctx.exchange_info(reset=True)
-    torch_sync(d.device)
+    device_sync(d.device)
     d.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i == args.steps - 1)
     ctx.sync()
-    torch_sync(d.device)
+    device_sync(d.device)
     d.barrier()
     el = d.max(time.perf_counter() - t0)
     kms, launches = ctx.kernel_time()
@@ -1001,14 +1087,14 @@ def main():
                                "bytes_per_step_per_gpu": xinfo["bytes"] // max(xinfo["exchanges"], 1),
                                "buckets": xinfo["last_buckets"], "cell_bytes": xinfo["last_width"],
                                "whole_ring_u64_bytes": xinfo["full_ring_bytes"]}
-    extra = None
+    extra = None if args.no_extras else {}
     import threading
     printed_lock, printed = threading.Lock(), []
     if not args.no_extras:
         free_segments(ctx, segs)
         ctx.close()
         if d.world == 1:
-            extra = extras(args, d.device)
+            extra.update(extras(args, d.device))
         else:
             # a rank that stopped inside a collective of the leg would hold every rank (and
             # the headline line) forever: after --extras-timeout seconds rank 0 prints the
@@ -1016,16 +1102,17 @@ def main():
             def give_up():
                 with printed_lock:
                     if d.rank == 0 and not printed:
-                        out["extras"] = {"config3": {"error": "the N > 1 extras timed out after %d s"
-                                                                  % args.extras_timeout}}
-                        print(json.dumps(out), flush=True)
+                        extra["timed_out"] = {"error": "the N > 1 extras timed out after %d s"
+                                                                 % args.extras_timeout}
+                        emit(out, extra, args.extras_out)
                         printed.append(True)
-                # non-zero: the launcher (and CI) must see that a rank was stuck in a collective
-                os._exit(3)
+                # every rank's watchdog fires at the same deadline, so every rank leaves (one
+                # stuck in a collective too); 0: the headline line is valid, the leg's timeout is
+                # recorded in it
+                os._exit(0)
             dog = threading.Timer(args.extras_timeout, give_up)
             dog.daemon = True
             dog.start()
-            extra = {}
             guarded(extra, "config3", lambda: config3_ranks(args, d))
             # configs[4] across the node's GPUs: rank 0 runs the native streaming mode with one
             # shard per rank's GPU (a process of its own; the other ranks are done with theirs)
@@ -1035,9 +1122,7 @@ def main():
 
     with printed_lock:   # (the watchdog may print the line instead, never both)
         if d.rank == 0 and not printed:
-            if extra is not None:
-                out["extras"] = extra
-            print(json.dumps(out), flush=True)
+            emit(out, extra, args.extras_out)
             printed.append(True)
     if d.dist:
         d.dist.destroy_process_group()

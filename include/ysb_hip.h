@@ -36,8 +36,13 @@ extern "C" {
  * 4: ysb_device_count; a busy stream's device batches take the sampled layout only when two
  *    samples agree (else the per-tile dispatch, never a host wait for the launch queued
  *    last); a raw batch that cannot launch is a sticky error (ysb_stream returns NULL);
- *    raw batches hold at most max(max_batch_events, max_batch_bytes / 32) lines */
-#define YSB_ABI_VERSION 4
+ *    raw batches hold at most max(max_batch_events, max_batch_bytes / 32) lines
+ * 5: ysb_device_sync; raw batches read in place from caller-registered host memory
+ *    (ysb_host_register, ysb_submit_raw_mapped) with the replay's event-time rebasing on the
+ *    device (ysb_rebase_table); ysb_exchange_info_size (the struct grew in ABI 4: a caller
+ *    checks the size it was built with); YSB_F_TIMING's event records are folded into running
+ *    totals, so a caller that never reads them keeps a bounded number */
+#define YSB_ABI_VERSION 5
 
 /* status codes */
 #define YSB_OK            0
@@ -191,6 +196,13 @@ void        ysb_config_default(ysb_config* cfg);
  * fails).  A launcher maps rank -> device with it (one context per GPU, the reference's one
  * subtask per slot) without a framework's device query. */
 int         ysb_device_count(void);
+/* hipDeviceSynchronize on `device` through the library's own HIP runtime (ABI 5): a host
+ * (bench.py, a JVM) that must wait for the whole GPU without loading a framework's HIP
+ * runtime.  A process may hold only one working HIP/HSA runtime: if another one (e.g. the
+ * libamdhip64 a framework bundles) opens the GPU first, this library's runtime may see no
+ * device, and ysb_open / ysb_device_sync fail with a message that says so (INTEGRATION.md
+ * section 1.4: load order). */
+int         ysb_device_sync(int device);
 
 /* Replaces CampaignProcessorCommon(String)/prepare() (CampaignProcessorCommon.java:30-55)
  * and RedisJoinBolt.open() (AdvertisingTopologyNative.java:451-458). */
@@ -260,6 +272,34 @@ int         ysb_slot_capacity(ysb_ctx* ctx, uint64_t* max_bytes, uint64_t* max_e
  * its error is returned by the call that performs the launch and by every later call that
  * orders work after it, until ysb_reset. */
 int         ysb_submit_raw(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes);
+/* Zero-copy raw batches (ABI 5).  ysb_host_register pins and maps caller host memory (a JNI
+ * DirectByteBuffer, a replay file read into memory) for this context's device, so that
+ * ysb_submit_raw_mapped reads a batch in place over PCIe -- no copy into the pinned slot, no
+ * host pass over the bytes (the streaming replay's ingest: FileBasedDataSource.run,
+ * AdvertisingTopologyNative.java:144-165, with the source's buffer itself pinned).  Ranges
+ * must not overlap; ysb_close unregisters what is left. */
+int         ysb_host_register(ysb_ctx* ctx, void* host, uint64_t bytes);
+int         ysb_host_unregister(ysb_ctx* ctx, void* host);
+/* The replay's event-time rebasing on the device (the data/ generator's batch replay output,
+ * core.clj:166-174 played past its first cycle).  A replay cycle's line i holds its 13-digit
+ * event_time at byte time_at[i] & 0xFFFF of the line, and its leading nine digits (the
+ * 10-second bucket) equal lead_base + (time_at[i] >> 16).  The table (4 B per line) is copied
+ * into HBM; n_lines = 0 drops it. */
+int         ysb_rebase_table(ysb_ctx* ctx, const uint32_t* time_at, uint64_t n_lines, int64_t lead_base);
+typedef struct ysb_rebase {
+    uint64_t first_line;   /* the batch's first line is the table's line first_line         */
+    int64_t  lead_shift;   /* added to every line's leading nine digits (cycle k of a cycle of
+                              c ms: k * c / 10000); the result must lie in [0, 10^9)         */
+} ysb_rebase;
+/* ysb_submit_raw of a batch that lies in a registered range: `bytes` 16-byte aligned, and the
+ * range holds round_up(nbytes, 16) bytes from it.  The copy kernel (or, YSB_F_H2D_SDMA, the DMA
+ * engine) reads it in place into the slot's device buffer, the GPU splits the lines, and with
+ * rebase != NULL every line's leading event_time digits are rewritten from the rebase table
+ * before the scan (YSB_ERR_ARG at the launch if the batch has more lines than the table holds
+ * from first_line).  Asynchronous like ysb_submit_raw; the caller must not rewrite the bytes
+ * until ysb_wait(ctx, slot).  The slot's pinned host buffer is not used. */
+int         ysb_submit_raw_mapped(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes,
+                                  const ysb_rebase* rebase);
 /* The same split of a device-resident batch (16-byte aligned, < 4 GiB): d_off[0..*n) <- its
  * line starts (YSB_ERR_CAPACITY, *n = the lines, if more than cap).  Synchronous. */
 int         ysb_split_lines_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, uint32_t* d_off,
@@ -458,6 +498,9 @@ typedef struct ysb_exchange_info {
     double   exposed_ms;
 } ysb_exchange_info;
 int         ysb_group_exchange_info(ysb_ctx* ctx, ysb_exchange_info* out, int reset);
+/* sizeof(ysb_exchange_info) as this library writes it (ABI 5): a caller built against an older
+ * header (ABI 3: 48 bytes) must not pass its smaller struct to ysb_group_exchange_info. */
+uint64_t    ysb_exchange_info_size(void);
 /* The plan every rank derives from the all-reduced per-bucket maxima (host function):
  * slots[0..*n_slots) = the ring slots with slot_max > 0, ascending; *width = the cell width
  * above.  YSB_ERR_CAPACITY if nranks * max does not fit 64 bits. */

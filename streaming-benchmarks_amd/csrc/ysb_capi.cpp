@@ -4,12 +4,14 @@
 // ysb_gen_api.cpp (all over the context of ysb_ctx.h).
 #include "ysb_ctx.h"
 
+#include <unistd.h>
+
 using namespace ysb;
 
 thread_local std::string g_open_err;
 
 int fail(ysb_ctx* c, int code, const char* fmt, ...) {
-    char buf[512];
+    char buf[1024];
     va_list ap;
     va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
@@ -26,6 +28,35 @@ int ysb_abi_version(void) { return YSB_ABI_VERSION; }
 int ysb_device_count(void) {
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+// Why this process's HIP runtime sees no device: the likely cause named (Weak 6 of the round-5
+// review: torch 2.10 bundles its own libamdhip64 / libhsa-runtime64, and whichever runtime
+// opens the GPU first in a process is the one that sees it).
+static int no_device(hipError_t e) {
+    const bool kfd = access("/dev/kfd", F_OK) == 0;
+    const char* vis = getenv("HIP_VISIBLE_DEVICES");
+    if (!vis) vis = getenv("ROCR_VISIBLE_DEVICES");
+    if (kfd && !(vis && *vis == '\0'))
+        return fail(nullptr, YSB_ERR_HIP,
+                    "no HIP device available to this library's HIP runtime (hipGetDeviceCount: %s) although "
+                    "/dev/kfd exists: another HIP/HSA runtime in this process (e.g. the libamdhip64 a framework "
+                    "such as torch bundles) probably opened the GPU first -- load libysb_hip and call "
+                    "ysb_device_count / ysb_open before any other GPU runtime initialises (INTEGRATION.md 1.4)%s%s",
+                    hipGetErrorString(e), vis ? "; *_VISIBLE_DEVICES=" : "", vis ? vis : "");
+    return fail(nullptr, YSB_ERR_HIP, "no HIP device available (hipGetDeviceCount: %s%s)", hipGetErrorString(e),
+                kfd ? "" : "; no /dev/kfd: no AMD GPU driver in this environment");
+}
+
+int ysb_device_sync(int device) {
+    int ndev = 0;
+    const hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) return no_device(e);
+    if (device < 0 || device >= ndev) return fail(nullptr, YSB_ERR_ARG, "device %d out of range (%d)", device, ndev);
+    hipError_t r = hipSetDevice(device);
+    if (r == hipSuccess) r = hipDeviceSynchronize();
+    if (r != hipSuccess) return fail(nullptr, YSB_ERR_HIP, "hipDeviceSynchronize(%d): %s", device, hipGetErrorString(r));
+    return YSB_OK;
 }
 
 void ysb_config_default(ysb_config* c) {
@@ -114,6 +145,8 @@ static void destroy(ysb_ctx* c) {
     hipFree(c->d_rawn);
     hipHostFree(c->h_rawn);
     for (auto& p : c->cev) for (hipEvent_t e : p) hipEventDestroy(e);
+    hipFree(c->d_rebase);
+    for (auto& r : c->host_ranges) hipHostUnregister(reinterpret_cast<void*>(r.first));
     for (auto& f : c->fl) {
         hipHostFree(f.h_rows);
         hipHostFree(f.h_n);
@@ -150,8 +183,8 @@ int ysb_open(ysb_ctx** out, int device, const ysb_config* cfg_in) {
     if (cfg.overflow_capacity == 0 || cfg.overflow_capacity > 0xFFFFFFFFull)
         return fail(nullptr, YSB_ERR_ARG, "overflow_capacity must be in [1, 2^32)");
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
-        return fail(nullptr, YSB_ERR_HIP, "no HIP device available");
+    const hipError_t de = hipGetDeviceCount(&ndev);
+    if (de != hipSuccess || ndev == 0) return no_device(de);
     if (device < 0 || device >= ndev) return fail(nullptr, YSB_ERR_ARG, "device %d out of range (%d)", device, ndev);
 
     ysb_ctx* c = new ysb_ctx();
@@ -832,7 +865,7 @@ int ysb_kernel_time(ysb_ctx* c, double* total_ms, uint64_t* launches) {
     if (!c) return YSB_ERR_ARG;
     int rc = sync_streams(c);
     if (rc) return rc;
-    double t = 0, tp = 0;
+    double t = c->tev_ms_fold, tp = c->tev_path_fold;
     for (size_t i = 0; i < c->tev_used; ++i) {
         float ms = 0, mp = 0;
         HIPCHK(c, hipEventElapsedTime(&ms, c->tev[i][0], c->tev[i][1]));
@@ -840,11 +873,14 @@ int ysb_kernel_time(ysb_ctx* c, double* total_ms, uint64_t* launches) {
         t += ms;
         tp += mp;
     }
+    const u64 n = c->tev_folded + c->tev_used;
     if (total_ms) *total_ms = t;
-    if (launches) *launches = c->tev_used;
+    if (launches) *launches = n;
     c->path_ms_acc = tp;
-    c->path_launches_acc = c->tev_used;
+    c->path_launches_acc = n;
     c->tev_used = 0;
+    c->tev_ms_fold = c->tev_path_fold = 0;
+    c->tev_folded = 0;
     return YSB_OK;
 }
 

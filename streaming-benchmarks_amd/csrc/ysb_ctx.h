@@ -32,6 +32,9 @@ int scan_lds_bytes();
 }
 
 constexpr size_t XEV_KEEP = 64;   // exchange timing pairs pending before they are folded into x_ms
+// YSB_F_TIMING: launch / copy event records pending before the older half is folded into
+// running totals (a streaming caller may never call ysb_kernel_time / ysb_copy_time)
+constexpr size_t TIMING_KEEP = 256;
 
 // HBM-resident join table (bucket layout): buckets per key, x4 (8: 2 per key, a 4 GiB
 // table at 10M ads; fewer buckets -> a smaller table, more keys in their second bucket)
@@ -95,6 +98,22 @@ struct ysb_ctx {
     std::vector<std::array<hipEvent_t, 2>> cev;
     size_t cev_used = 0;
     u64 copy_bytes = 0;
+    double cev_ms_fold = 0;                     // pairs folded into totals (TIMING_KEEP)
+    u64 cev_folded = 0;
+    // caller host ranges registered for zero-copy raw batches (ysb_host_register): base ->
+    // {bytes, device address}
+    struct HostRange {
+        u64 bytes;
+        u8* dptr;
+    };
+    std::map<uintptr_t, HostRange> host_ranges;
+    // the replay's rebase table (ysb_rebase_table) and each slot's pending rebase
+    u32* d_rebase = nullptr;
+    u64 rebase_n = 0;
+    i64 rebase_base = 0;
+    u32 rebase_kmax = 0;                        // the largest bucket index in it
+    bool raw_rebase_on[2] = {false, false};
+    ysb_rebase raw_rebase[2]{};
     CuckooSeed cseed{};
     bool ctable_partial = false;
     bool table_loaded = false;
@@ -139,6 +158,8 @@ struct ysb_ctx {
     // timing: per launch {before scan, after scan, after the last kernel of the launch}
     std::vector<std::array<hipEvent_t, 3>> tev;
     size_t tev_used = 0;
+    double tev_ms_fold = 0, tev_path_fold = 0;   // launches folded into totals (TIMING_KEEP)
+    u64 tev_folded = 0;
     double path_ms_acc = 0;                // ysb_path_time's share, collected by ysb_kernel_time
     u64 path_launches_acc = 0;
     // record mode (ysb_count.hip)

@@ -37,7 +37,10 @@ static GenSpec spec_of(const ysb_gen_params* p, const u32* subset) {
 }
 
 static bool gen_ok(const ysb_gen_params* p) {
+    // with_skew: 0 off, 1 the reference's skew and late events, 2 the skew only (any other value
+    // would silently change the truth tables)
     return p && p->n_campaigns && p->ads_per_campaign && p->events_per_sec && p->format <= YSB_GEN_TBL &&
+           p->with_skew <= 2 &&
            p->variant <= (YSB_GEN_RANDOM_IP | YSB_GEN_MORE_AD_TYPES | YSB_GEN_COMPACT | YSB_GEN_REORDER | YSB_GEN_MIXED |
                           YSB_GEN_MIXED_BLOCKS) &&
            (!p->ad_subset || p->n_ad_subset) && (u64)p->n_campaigns * p->ads_per_campaign < (1ull << 32);

@@ -450,6 +450,8 @@ int ysb_group_reduce_scatter(ysb_ctx* c) { return c ? exchange(c, false) : YSB_E
 
 int ysb_group_exchange_pipelined(ysb_ctx* c) { return c ? exchange(c, true) : YSB_ERR_ARG; }
 
+uint64_t ysb_exchange_info_size(void) { return sizeof(ysb_exchange_info); }
+
 int ysb_group_exchange_info(ysb_ctx* c, ysb_exchange_info* out, int reset) {
     if (!c || !out) return c ? fail(c, YSB_ERR_ARG, "NULL output") : YSB_ERR_ARG;
     int rc = sync_streams(c);

@@ -191,6 +191,41 @@ void launch_sample(const SampleSegs& s, u32 nseg, u8* out, hipStream_t st) {
     if (nseg) hipLaunchKernelGGL(sample_kernel, dim3(nseg), dim3(64), 0, st, s, out);
 }
 
+// ---- the replay's event-time rebasing (ysb_submit_raw_mapped with a ysb_rebase) ------------
+// A replay cycle is played again with every event_time moved by whole 10-second buckets: only
+// the nine leading digits of the 13-digit time change.  One lane per
+// line, after the split: the line's start from off[], the digits' position and bucket index
+// from the cycle's table (4 B per line, HBM), nine byte stores.  ~9 B written + 8 B read per
+// line against the line's ~254 B copied over PCIe: the kernel is a few microseconds per batch.
+constexpr int REBASE_TPB = 256;
+
+__global__ __launch_bounds__(REBASE_TPB) void rebase_kernel(u8* __restrict__ b, u64 nbytes, const u32* __restrict__ off,
+                                                            const unsigned long long* d_n, const u32* __restrict__ tab,
+                                                            u64 tab_n, u64 cap, i64 lead) {
+    u64 n = *d_n < tab_n ? *d_n : tab_n;
+    if (n > cap) n = cap;   // (more lines than off[] holds: the launch fails on the host)
+    for (u64 i = (u64)blockIdx.x * REBASE_TPB + threadIdx.x; i < n; i += (u64)gridDim.x * REBASE_TPB) {
+        const u32 t = tab[i];
+        const u64 p = (u64)off[i] + (t & 0xFFFFu);
+        if (p + 9 > nbytes) continue;
+        u64 v = (u64)(lead + (i64)(t >> 16));
+#pragma unroll
+        for (int d = 8; d >= 0; --d) {
+            b[p + d] = (u8)('0' + v % 10);
+            v /= 10;
+        }
+    }
+}
+
+void launch_rebase(u8* b, u64 nbytes, const u32* off, u64 cap, const unsigned long long* d_n, const u32* tab,
+                   u64 tab_n, i64 lead, int cus, hipStream_t s) {
+    if (!nbytes || !tab_n) return;
+    // lines are unknown until the split's count is read on the device: a grid-stride loop
+    const u64 grid = std::max<u64>(1, std::min<u64>((u64)cus * 4, (tab_n + REBASE_TPB - 1) / REBASE_TPB));
+    hipLaunchKernelGGL(rebase_kernel, dim3((unsigned)grid), dim3(REBASE_TPB), 0, s, b, nbytes, off, d_n, tab, tab_n,
+                       cap, lead);
+}
+
 hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64 cap, unsigned long long* d_n,
                               hipStream_t s) {
     if (nbytes == 0) return hipMemsetAsync(d_n, 0, 8, s);

@@ -106,6 +106,41 @@ static int grow_u32(ysb_ctx* c, u32** buf, u64* have, u64 words) {
     return YSB_OK;
 }
 
+// YSB_F_TIMING keeps HIP events per launch and per slot copy until ysb_kernel_time /
+// ysb_copy_time read them.  A caller that never does (a streaming job) would grow them without
+// bound: once TIMING_KEEP are pending, the older half is folded into running totals (those
+// launches are TIMING_KEEP / 2 launches old -- normally long done; else this waits for them)
+// and their events are reused.
+static int fold_launch_events(ysb_ctx* c) {
+    const size_t half = TIMING_KEEP / 2;
+    for (size_t i = 0; i < half; ++i) {
+        float ms = 0, mp = 0;
+        HIPCHK(c, hipEventSynchronize(c->tev[i][2]));
+        HIPCHK(c, hipEventElapsedTime(&ms, c->tev[i][0], c->tev[i][1]));
+        HIPCHK(c, hipEventElapsedTime(&mp, c->tev[i][0], c->tev[i][2]));
+        c->tev_ms_fold += ms;
+        c->tev_path_fold += mp;
+        ++c->tev_folded;
+    }
+    std::rotate(c->tev.begin(), c->tev.begin() + (ptrdiff_t)half, c->tev.begin() + (ptrdiff_t)c->tev_used);
+    c->tev_used -= half;
+    return YSB_OK;
+}
+
+static int fold_copy_events(ysb_ctx* c) {
+    const size_t half = TIMING_KEEP / 2;
+    for (size_t i = 0; i < half; ++i) {
+        float ms = 0;
+        HIPCHK(c, hipEventSynchronize(c->cev[i][1]));
+        HIPCHK(c, hipEventElapsedTime(&ms, c->cev[i][0], c->cev[i][1]));
+        c->cev_ms_fold += ms;
+        ++c->cev_folded;
+    }
+    std::rotate(c->cev.begin(), c->cev.begin() + (ptrdiff_t)half, c->cev.begin() + (ptrdiff_t)c->cev_used);
+    c->cev_used -= half;
+    return YSB_OK;
+}
+
 // Record mode (ysb_count.hip) for this launch: large count tables without LDS window
 // counters (configs[2]), where one global atomic per joined view is the bottleneck.
 // Auto: ring >= 1M cells and launch >= 1M events; YSB_F_RECORD_COUNT forces it on
@@ -245,6 +280,7 @@ static int enqueue_scan(ysb_ctx* c, const ysb_segment* in, u32 nin) {
     if (rc) return rc;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (c->cfg.flags & YSB_F_TIMING) {
+        if (c->tev_used == TIMING_KEEP && (rc = fold_launch_events(c))) return rc;
         if (c->tev_used == c->tev.size()) {
             std::array<hipEvent_t, 3> ev{};
             for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
@@ -535,6 +571,10 @@ static int sample_device_layout(ysb_ctx* c, const ysb_segment* segs, u32 nseg, L
 static int copy_events(ysb_ctx* c, hipEvent_t** out, u64 bytes) {
     *out = nullptr;
     if (!(c->cfg.flags & YSB_F_TIMING)) return YSB_OK;
+    if (c->cev_used == TIMING_KEEP) {
+        const int rc = fold_copy_events(c);
+        if (rc) return rc;
+    }
     if (c->cev_used == c->cev.size()) {
         std::array<hipEvent_t, 2> ev{};
         for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
@@ -669,6 +709,9 @@ int launch_pending_raw(ysb_ctx* c) {
     if (hipSetDevice(c->device) != hipSuccess || hipEventSynchronize(c->ev_raw[slot]) != hipSuccess ||
         hipStreamWaitEvent(c->s_comp, c->ev_raw[slot], 0) != hipSuccess) {
         rc = fail(c, YSB_ERR_HIP, "raw batch (slot %d): waiting for its line split failed", slot);
+    } else if (c->raw_rebase_on[slot] && c->h_rawn[slot] > c->rebase_n - c->raw_rebase[slot].first_line) {
+        rc = fail(c, YSB_ERR_ARG, "raw batch (slot %d): %llu lines, more than the rebase table holds from line %llu",
+                  slot, (unsigned long long)c->h_rawn[slot], (unsigned long long)c->raw_rebase[slot].first_line);
     } else if (c->h_rawn[slot] > c->raw_lines_cap) {
         rc = fail(c, YSB_ERR_CAPACITY, "raw batch (slot %d): %llu lines, more than the %llu its slot holds "
                   "(max(max_batch_events, max_batch_bytes / 32))", slot, (unsigned long long)c->h_rawn[slot],
@@ -720,25 +763,23 @@ static int sniff_raw(const ysb_ctx* c, const u8* b, u64 nbytes, LearnDesc* d) {
     return decide_layout(c, lines, d);
 }
 
-int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) {
-    if (!c) return YSB_ERR_ARG;
+static int raw_args(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) {
     if (slot < 0 || slot > 1) return fail(c, YSB_ERR_ARG, "slot must be 0 or 1");
     if (nbytes > c->cfg.max_batch_bytes)
         return fail(c, YSB_ERR_CAPACITY, "raw batch of %llu B exceeds max_batch_bytes", (unsigned long long)nbytes);
     if (nbytes && !bytes) return fail(c, YSB_ERR_ARG, "NULL batch buffer");
     if (!c->table_loaded) return fail(c, YSB_ERR_STATE, "ysb_load_ad_map has not been called");
-    // the slot's own earlier batch launches first (its device buffers are about to be reused)
-    int rc = c->raw_pend == slot ? launch_pending_raw(c) : YSB_OK;
-    if (!rc) rc = ensure_slots(c);
-    if (!rc) rc = ensure_raw(c);
-    if (rc) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
-    // the slot's previous H2D must be done before its pinned buffer is rewritten
-    HIPCHK(c, hipEventSynchronize(c->ev_h2d[slot]));
-    if (bytes != c->h_bytes[slot] && nbytes) std::memcpy(c->h_bytes[slot], bytes, nbytes);
+    return YSB_OK;
+}
+
+// A raw batch from hsrc (host address: the layout sample, the DMA engine) / dsrc (its device
+// address: the copy kernel) into the slot's device buffer, split, optionally rebased; its scan
+// launches at the next call.  The caller has waited for the slot's previous copy.
+static int enqueue_raw(ysb_ctx* c, int slot, const u8* hsrc, const u8* dsrc, u64 nbytes, const ysb_rebase* rb) {
+    int rc;
     c->raw_layout[slot] = -1;
     if (layout_sampling(c) && nbytes)
-        c->raw_layout[slot] = hinted_layout(c, sniff_raw(c, c->h_bytes[slot], nbytes, &c->raw_learn[slot]));
+        c->raw_layout[slot] = hinted_layout(c, sniff_raw(c, hsrc, nbytes, &c->raw_learn[slot]));
     // H2D once the slot's previous kernel has run.  The split: behind the DMA engine's copy on a
     // stream of its own (the next slot's copy queues right behind this one); behind the copy
     // kernel on the copy stream itself, so it runs right after its own copy and the next copy
@@ -751,14 +792,22 @@ int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) 
     hipEvent_t* ce = nullptr;
     if ((rc = copy_events(c, &ce, nbytes))) return rc;
     if (ce) HIPCHK(c, hipEventRecord(ce[0], c->s_copy));
-    if (nbytes) HIPCHK(c, h2d(c, c->d_bytes[slot], c->hd_bytes[slot], c->h_bytes[slot], nbytes));
+    if (nbytes) HIPCHK(c, h2d(c, c->d_bytes[slot], dsrc, hsrc, nbytes));
     if (ce) HIPCHK(c, hipEventRecord(ce[1], c->s_copy));
     HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
     if (ss != c->s_copy) HIPCHK(c, hipStreamWaitEvent(ss, c->ev_h2d[slot], 0));
+    c->raw_rebase_on[slot] = rb != nullptr;
+    if (rb) c->raw_rebase[slot] = *rb;
     if (nbytes) {
         // the line count goes straight to pinned memory (read at the launch)
         HIPCHK(c, launch_split_lines(c->d_bytes[slot], nbytes, c->d_split_chunk, c->d_roff[slot],
                                      c->raw_lines_cap, c->h_rawn + slot, ss));
+        if (rb) {
+            launch_rebase(c->d_bytes[slot], nbytes, c->d_roff[slot], c->raw_lines_cap, c->h_rawn + slot,
+                          c->d_rebase + rb->first_line, c->rebase_n - rb->first_line,
+                          c->rebase_base + rb->lead_shift, c->cus, ss);
+            HIPCHK(c, hipGetLastError());
+        }
     } else {
         c->h_rawn[slot] = 0;
     }
@@ -768,6 +817,103 @@ int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) 
     rc = launch_pending_raw(c);
     c->raw_pend = slot;
     return rc;
+}
+
+int ysb_submit_raw(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = raw_args(c, slot, bytes, nbytes);
+    if (rc) return rc;
+    // the slot's own earlier batch launches first (its device buffers are about to be reused)
+    rc = c->raw_pend == slot ? launch_pending_raw(c) : YSB_OK;
+    if (!rc) rc = ensure_slots(c);
+    if (!rc) rc = ensure_raw(c);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    // the slot's previous H2D must be done before its pinned buffer is rewritten
+    HIPCHK(c, hipEventSynchronize(c->ev_h2d[slot]));
+    if (bytes != c->h_bytes[slot] && nbytes) std::memcpy(c->h_bytes[slot], bytes, nbytes);
+    return enqueue_raw(c, slot, c->h_bytes[slot], c->hd_bytes[slot], nbytes, nullptr);
+}
+
+// ---- zero-copy raw batches from registered caller memory (ABI 5) ----------------------------
+
+int ysb_host_register(ysb_ctx* c, void* host, uint64_t bytes) {
+    if (!c) return YSB_ERR_ARG;
+    if (!host || !bytes) return fail(c, YSB_ERR_ARG, "empty host range");
+    const uintptr_t a = reinterpret_cast<uintptr_t>(host);
+    for (const auto& r : c->host_ranges)
+        if (a < r.first + r.second.bytes && r.first < a + bytes) return fail(c, YSB_ERR_ARG, "host range overlaps a registered one");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipHostRegister(host, bytes, hipHostRegisterMapped));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+        hipHostUnregister(host);
+        return fail(c, YSB_ERR_HIP, "hipHostGetDevicePointer of a registered range failed");
+    }
+    c->host_ranges[a] = {bytes, static_cast<u8*>(d)};
+    return YSB_OK;
+}
+
+int ysb_host_unregister(ysb_ctx* c, void* host) {
+    if (!c) return YSB_ERR_ARG;
+    auto it = c->host_ranges.find(reinterpret_cast<uintptr_t>(host));
+    if (it == c->host_ranges.end()) return fail(c, YSB_ERR_ARG, "not a registered range");
+    // nothing queued may still read it
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->s_copy));
+    HIPCHK(c, hipHostUnregister(host));
+    c->host_ranges.erase(it);
+    return YSB_OK;
+}
+
+int ysb_rebase_table(ysb_ctx* c, const uint32_t* time_at, uint64_t n_lines, int64_t lead_base) {
+    if (!c) return YSB_ERR_ARG;
+    if (n_lines && !time_at) return fail(c, YSB_ERR_ARG, "NULL table");
+    HIPCHK(c, hipSetDevice(c->device));
+    // batches queued with the old table must be done with it
+    HIPCHK(c, hipStreamSynchronize(c->s_copy));
+    if (c->s_split) HIPCHK(c, hipStreamSynchronize(c->s_split));
+    hipFree(c->d_rebase);
+    c->d_rebase = nullptr;
+    c->rebase_n = 0;
+    if (!n_lines) return YSB_OK;
+    u32 kmax = 0;
+    for (u64 i = 0; i < n_lines; ++i) kmax = std::max(kmax, time_at[i] >> 16);
+    if (lead_base < 0 || lead_base + kmax >= 1000000000LL) return fail(c, YSB_ERR_ARG, "leading digits out of [0, 10^9)");
+    HIPCHK(c, hipMalloc(&c->d_rebase, n_lines * 4));
+    HIPCHK(c, hipMemcpy(c->d_rebase, time_at, n_lines * 4, hipMemcpyHostToDevice));
+    c->rebase_n = n_lines;
+    c->rebase_base = lead_base;
+    c->rebase_kmax = kmax;
+    return YSB_OK;
+}
+
+int ysb_submit_raw_mapped(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, const ysb_rebase* rb) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = raw_args(c, slot, bytes, nbytes);
+    if (rc) return rc;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(bytes);
+    if (a & 15) return fail(c, YSB_ERR_ARG, "a mapped batch must be 16-byte aligned");
+    const u8* dsrc = nullptr;
+    auto it = c->host_ranges.upper_bound(a);
+    if (it != c->host_ranges.begin()) {
+        --it;
+        if (a + ((nbytes + 15) & ~15ull) <= it->first + it->second.bytes) dsrc = it->second.dptr + (a - it->first);
+    }
+    if (nbytes && !dsrc) return fail(c, YSB_ERR_ARG, "the batch (rounded up to 16 B) is not inside a registered range");
+    if (rb) {
+        if (!c->d_rebase) return fail(c, YSB_ERR_STATE, "no rebase table (ysb_rebase_table)");
+        if (rb->first_line >= c->rebase_n) return fail(c, YSB_ERR_ARG, "first_line beyond the rebase table");
+        const i64 lo = c->rebase_base + rb->lead_shift;
+        if (lo < 0 || lo + (i64)c->rebase_kmax >= 1000000000LL)
+            return fail(c, YSB_ERR_ARG, "rebased leading digits out of [0, 10^9)");
+    }
+    rc = c->raw_pend == slot ? launch_pending_raw(c) : YSB_OK;
+    if (!rc) rc = ensure_slots(c);
+    if (!rc) rc = ensure_raw(c);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    return enqueue_raw(c, slot, bytes, dsrc, nbytes, rb);
 }
 
 int ysb_split_lines_device(ysb_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint32_t* d_off, uint64_t cap,
@@ -811,16 +957,18 @@ int ysb_copy_time(ysb_ctx* c, double* total_ms, uint64_t* copies, uint64_t* byte
     if (!c) return YSB_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->s_copy));
-    double t = 0;
+    double t = c->cev_ms_fold;
     for (size_t i = 0; i < c->cev_used; ++i) {
         float ms = 0;
         HIPCHK(c, hipEventElapsedTime(&ms, c->cev[i][0], c->cev[i][1]));
         t += ms;
     }
     if (total_ms) *total_ms = t;
-    if (copies) *copies = c->cev_used;
+    if (copies) *copies = c->cev_folded + c->cev_used;
     if (bytes) *bytes = c->copy_bytes;
     c->cev_used = 0;
+    c->cev_ms_fold = 0;
+    c->cev_folded = 0;
     c->copy_bytes = 0;
     return YSB_OK;
 }

@@ -63,6 +63,10 @@ class YsbExchangeInfo(C.Structure):
                 ("rs_ms", C.c_double), ("exposed_ms", C.c_double)]
 
 
+class YsbRebase(C.Structure):
+    _fields_ = [("first_line", C.c_uint64), ("lead_shift", C.c_int64)]
+
+
 class YsbLaunchDesc(C.Structure):
     _fields_ = [("layout", C.c_uint32), ("record_mode", C.c_uint32), ("hbm_table", C.c_uint32), ("tbl", C.c_uint32)]
 
@@ -101,6 +105,7 @@ _PU32 = C.c_void_p
 SIGNATURES = {
     "ysb_abi_version": (_I, []),
     "ysb_device_count": (_I, []),
+    "ysb_device_sync": (_I, [_I]),
     "ysb_config_default": (None, [C.POINTER(YsbConfig)]),
     "ysb_open": (_I, [C.POINTER(_P), _I, C.POINTER(YsbConfig)]),
     "ysb_close": (_I, [_P]),
@@ -114,6 +119,10 @@ SIGNATURES = {
     "ysb_wait": (_I, [_P, _I]),
     "ysb_slot_capacity": (_I, [_P, C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_submit_raw": (_I, [_P, _I, _PU8, _U64]),
+    "ysb_host_register": (_I, [_P, _P, _U64]),
+    "ysb_host_unregister": (_I, [_P, _P]),
+    "ysb_rebase_table": (_I, [_P, C.c_void_p, _U64, _I64]),
+    "ysb_submit_raw_mapped": (_I, [_P, _I, _PU8, _U64, C.POINTER(YsbRebase)]),
     "ysb_split_lines_device": (_I, [_P, _PU8, _U64, _PU32, _U64, C.POINTER(_U64)]),
     "ysb_copy_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_submit_device": (_I, [_P, _PU8, _U64, _PU32, _U64]),
@@ -141,6 +150,7 @@ SIGNATURES = {
     "ysb_group_exchange_pipelined": (_I, [_P]),
     "ysb_group_init_host": (_I, [_P, _I, _I, C.POINTER(YsbCollectives)]),
     "ysb_group_exchange_info": (_I, [_P, C.POINTER(YsbExchangeInfo), _I]),
+    "ysb_exchange_info_size": (_U64, []),
     "ysb_exchange_plan": (_I, [C.c_void_p, _U32, _U32, C.c_void_p, C.POINTER(_U32), C.POINTER(_U32)]),
     "ysb_group_checksum": (_I, [_P, _I, _U32, C.c_void_p]),
     "ysb_group_owned": (_I, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
@@ -161,6 +171,8 @@ SIGNATURES = {
     "ysb_json_to_tbl": (_I, [_PU8, _U64, _PU32, _U64, _PU8, _U64, _PU32, C.POINTER(_U64)]),
     "ysb_gen_dump_shards": (_I, [C.POINTER(YsbGenParams), _U64, C.c_char_p, _U32]),
 }
+
+ABI_VERSION = 5   # include/ysb_hip.h YSB_ABI_VERSION this binding is written against
 
 _lib = None
 
@@ -183,6 +195,14 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        # the structs this binding lays out must be the library's (ysb_exchange_info grew in
+        # ABI 4: an older caller's struct would be written past its end)
+        if L.ysb_abi_version() != ABI_VERSION:
+            raise ImportError("%s has ABI %d, this binding is written for ABI %d: rebuild the library"
+                              % (LIB_PATH, L.ysb_abi_version(), ABI_VERSION))
+        if L.ysb_exchange_info_size() != C.sizeof(YsbExchangeInfo):
+            raise ImportError("ysb_exchange_info is %d bytes in the library, %d in this binding"
+                              % (L.ysb_exchange_info_size(), C.sizeof(YsbExchangeInfo)))
         _lib = L
     return _lib
 

@@ -26,6 +26,13 @@ def device_count():
     return int(lib().ysb_device_count())
 
 
+def device_sync(device):
+    """hipDeviceSynchronize on `device` through the library's own HIP runtime (ysb_device_sync):
+    the bench's device-wide wait without initialising a framework's HIP runtime, which may be
+    another one than the library's (ABI 5)."""
+    check(lib().ysb_device_sync(int(device)), None)
+
+
 def rank_device(local_rank, n_visible):
     """The device a rank uses (one context per GPU): its LOCAL_RANK, unless the launcher left
     each process fewer visible devices (e.g. one per rank through HIP_VISIBLE_DEVICES): then
@@ -146,6 +153,26 @@ class YsbContext:
         (readLine's terminators); the scan launches at the next call on the context."""
         buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
         self._c(lib().ysb_submit_raw(self._h, slot, _ptr(buf), buf.size))
+
+    def host_register(self, arr):
+        """ysb_host_register: pins and maps a host numpy array for zero-copy raw batches (the
+        array must stay alive and unmoved until host_unregister or close)."""
+        self._c(lib().ysb_host_register(self._h, C.c_void_p(arr.ctypes.data), arr.nbytes))
+
+    def host_unregister(self, arr):
+        self._c(lib().ysb_host_unregister(self._h, C.c_void_p(arr.ctypes.data)))
+
+    def rebase_table(self, time_at, lead_base):
+        """ysb_rebase_table: per line (time digits' offset) | (bucket index << 16), uint32."""
+        t = np.ascontiguousarray(time_at, dtype=np.uint32)
+        self._c(lib().ysb_rebase_table(self._h, _ptr(t), t.size, int(lead_base)))
+
+    def submit_raw_mapped(self, arr, offset, nbytes, slot=0, rebase=None):
+        """ysb_submit_raw_mapped: the raw batch arr[offset:offset + nbytes] of a registered
+        array, read in place by the device; rebase = (first_line, lead_shift) or None."""
+        rb = _lib.YsbRebase(*rebase) if rebase is not None else None
+        self._c(lib().ysb_submit_raw_mapped(self._h, slot, C.c_void_p(arr.ctypes.data + offset), nbytes,
+                                            C.byref(rb) if rb is not None else None))
 
     def split_lines_device(self, d_bytes, nbytes, d_off, cap):
         """ysb_split_lines_device: the line starts of a device batch into d_off; returns n."""

@@ -32,6 +32,8 @@ class GenParams:
         self.c.events_per_sec = events_per_sec
         # True / 1: +-50 ms skew and 1e-5 late events (core.clj:166-174); 2: the skew only
         self.c.with_skew = with_skew if isinstance(with_skew, int) and not isinstance(with_skew, bool) else int(bool(with_skew))
+        if self.c.with_skew > 2:
+            raise ValueError("with_skew must be 0 (off), 1 (skew + late events) or 2 (skew only)")
         self.c.n_users = n_users
         self.c.event_stream = event_stream
         if fmt not in ("json", "tbl"):

@@ -104,3 +104,89 @@ def test_live_traffic_reads_the_two_pmc_passes(monkeypatch, tmp_path):
     # without rocprofv3 there is no live figure (the line falls back to pmc_traffic.json)
     monkeypatch.setattr(shutil, "which", lambda name: None)
     assert bench.live_traffic(args, "x") is None
+
+
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "check")
+
+
+def _r05_line():
+    """profiles/r05_bench.json: the round-5 line with its 19 extras legs in full (the line the
+    driver could not parse: 21.8 KB)."""
+    with open(os.path.join(ROOT, "profiles", "r05_bench.json")) as f:
+        d = json.load(f)
+    extra = d.pop("extras")
+    return d, extra
+
+
+def test_bench_line_is_compact_and_parseable(tmp_path, capsys):
+    """The printed line (bench.emit): the contract keys + one summary per extra leg, <= 6 KB,
+    the last stdout line, json.loads-able; the extras in full go to the file and to stderr."""
+    import bench
+    out, extra = _r05_line()
+    assert len(json.dumps(dict(out, extras=extra))) > 20000          # the round-5 failure
+    path = str(tmp_path / "extras.json")
+    bench.emit(out, extra, path)
+    cap = capsys.readouterr()
+    last = cap.out.strip().splitlines()[-1]
+    assert len(last) <= bench.LINE_MAX_BYTES
+    line = json.loads(last)
+    for k in REQUIRED:
+        assert k in line, k
+    assert line["roofline"]["frac"] == out["roofline"]["frac"] and line["roofline"]["traffic"]
+    assert line["cpu_baseline"]["cores"] >= 1
+    summ = line["extras_summary"]
+    assert set(summ) == set(extra) and not line.get("extras_truncated")
+    assert summ["config3"]["exact"] is True and summ["config3"]["hbm_frac"] > 0.5
+    assert summ["stream_native"]["exact"] is True and summ["stream_native"]["events_per_s"] > 1e8
+    assert set(summ["host_staged"]) == {"offsets", "raw", "offsets_dma_engine"}
+    assert summ["native_runner"]["gpu_split"]["events_per_s"] > 1e8
+    with open(path) as f:
+        assert json.load(f) == extra                                   # the file holds them in full
+    assert "bench extras: " in cap.err
+
+
+def test_bench_line_n_gpus_and_watchdog(capsys):
+    """The N > 1 line (exchange block, the configs[2]-table leg with its checksum check) and the
+    watchdog's line (a timed-out leg) follow the same format and size bound."""
+    import bench
+    out, _ = _r05_line()
+    out = dict(out, n_gpus=8, scaling="weak",
+               exchange={"ms_per_step": 0.31, "critical_ms_per_step": 0.12, "rs_ms_per_step": 0.2,
+                         "exposed_ms_per_step": 0.01, "hidden_ms_per_step": 0.19, "bytes_per_step_per_gpu": 12800,
+                         "buckets": 16, "cell_bytes": 1, "whole_ring_u64_bytes": 819200})
+    c3 = {"workload": "x" * 300, "events_per_s": 1.5e11, "hbm_frac": 0.6,
+          "check": {"checksum_blocks_mismatched": 0, "truth_mismatched_cells": 0, "truth_views": 5, "counted_views": 5}}
+    bad = dict(c3, check=dict(c3["check"], checksum_blocks_mismatched=1))
+    for extra, exact in (({"config3": c3}, True), ({"config3": bad}, False)):
+        bench.emit(out, extra, None)
+        line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+        assert line["n_gpus"] == 8 and line["exchange"]["buckets"] == 16
+        assert line["extras_summary"]["config3"]["exact"] is exact
+    bench.emit(out, {"config3": c3, "timed_out": {"error": "the N > 1 extras timed out after 600 s"}}, None)
+    last = capsys.readouterr().out.strip().splitlines()[-1]
+    assert len(last) <= bench.LINE_MAX_BYTES
+    assert "timed out" in json.loads(last)["extras_summary"]["timed_out"]["error"]
+
+
+def test_bench_line_drops_legs_rather_than_overflow():
+    import bench
+    out, extra = _r05_line()
+    many = {("leg%03d" % i): v for i, v in enumerate(list(extra.values()) * 10)}
+    txt = bench.bench_line(out, many)
+    assert len(txt) <= bench.LINE_MAX_BYTES
+    line = json.loads(txt)
+    assert line["extras_truncated"] and 0 < len(line["extras_summary"]) < len(many)
+    for k in REQUIRED:
+        assert k in line
+
+
+def test_bench_never_initialises_torch_cuda():
+    """The two-runtime hazard (torch bundles its own HIP runtime): bench.py's device waits go
+    through the library (ysb_device_sync), never torch.cuda."""
+    import ast
+    with open(BENCH) as f:
+        tree = ast.parse(f.read())
+    uses = [n for n in ast.walk(tree) if isinstance(n, ast.Attribute) and n.attr == "cuda"
+            and isinstance(n.value, ast.Name) and n.value.id == "torch"]
+    assert not uses

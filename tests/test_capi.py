@@ -86,7 +86,10 @@ def test_struct_layouts_match_ctypes(tmp_path):
 
 def test_abi_version_and_defaults():
     L = _lib.lib()
-    assert L.ysb_abi_version() == 4
+    assert L.ysb_abi_version() == 5 == _lib.ABI_VERSION
+    # the struct the caller lays out is the library's (ysb_exchange_info grew in ABI 4)
+    assert L.ysb_exchange_info_size() == C.sizeof(_lib.YsbExchangeInfo) == 64
+    assert C.sizeof(_lib.YsbRebase) == 16
     cfg = _lib.YsbConfig()
     L.ysb_config_default(C.byref(cfg))
     assert cfg.time_divisor_ms == 10000          # CampaignProcessorCommon.java:28
@@ -198,3 +201,28 @@ def test_route_lines_hashes_the_decoded_ad_id():
             b, _ = route_lines(np.frombuffer(b"".join(el), dtype=np.uint8),
                                np.cumsum([0] + [len(x) for x in el[:-1]]), n)
             assert np.array_equal(a, b), (mode, n)
+
+
+def test_no_device_error_names_the_cause():
+    """ysb_device_sync / ysb_open without a visible device: YSB_ERR_HIP, and the message names
+    the likely cause (here: no /dev/kfd; on a GPU box: another HIP runtime opened it first)."""
+    import os
+    import pytest
+    from ysb_amd import YsbContext, YsbError, device_sync
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU driver is present")
+    with pytest.raises(YsbError, match="no /dev/kfd"):
+        device_sync(0)
+    with pytest.raises(YsbError, match="YSB_ERR_HIP"):
+        YsbContext()
+
+
+def test_generator_rejects_unknown_skew_modes():
+    import pytest
+    from ysb_amd import GenParams, YsbError
+    with pytest.raises(ValueError):
+        GenParams(with_skew=3)
+    g = GenParams()
+    g.c.with_skew = 7                                    # past the binding: the library refuses
+    with pytest.raises(YsbError, match="YSB_ERR_ARG"):
+        g.events_host(0, 10)
