@@ -71,11 +71,15 @@ def parse_args(argv=None):
     ap.add_argument("--stream-seconds", type=float, default=12.0,
                     help="extras: wall seconds of the native streaming leg (configs[4]; at the default speedup "
                          "12 s of input is 420 s of event time: >= 30 windows close); 0 skips it")
-    ap.add_argument("--stream-event-rate", type=int, default=5_000_000,
-                    help="extras: events per second of event time in the streaming replay")
-    ap.add_argument("--stream-speedup", type=float, default=35.0,
-                    help="extras: event time per wall time of the streaming replay (5M x 35 = 175M events/s: "
-                         "under the ~183M/s the replay sustains on a 16-core share, so it keeps up)")
+    ap.add_argument("--stream-target", type=float, default=202e6,
+                    help="extras: events/s per shard (GPU) the streaming replay releases (the zero-copy feed's "
+                         "ceiling is the slot copy over PCIe, ~215M/s at 254 B per event)")
+    ap.add_argument("--stream-host-gb", type=float, default=64.0,
+                    help="extras: host memory for all shards' replay cycles (each cycle is 10 s of event time, "
+                         "at most 16 GB per shard): sets the event rate per shard, and the speedup follows "
+                         "from --stream-target")
+    ap.add_argument("--stream-replay", choices=("mapped", "mapped-raw", "copy"), default="mapped",
+                    help="extras: the streaming feed: in place from the registered cycle, or round 5's host copy")
     ap.add_argument("--stream-rate", type=int, default=20_000_000,
                     help="tools/bench_extra.py stream_sharded: aggregate events/s of the Python producers")
     ap.add_argument("--dropin-events", type=int, default=100_000_000,
@@ -284,6 +288,8 @@ def leg_summary(r):
         s["events_per_s"] = eps
     if r.get("hbm_frac") is not None:
         s["hbm_frac"] = r["hbm_frac"]
+    if r.get("vs_host_staged") is not None and eps is not None:
+        s["vs_host_staged"] = r["vs_host_staged"]
     ex = _exact(r)
     if ex is not None:
         s["exact"] = ex
@@ -456,6 +462,10 @@ def extras(args, device):
     guarded(out, "alternating_producers", lambda: extra_alternating(args, device))
     if args.stream_seconds > 0:
         guarded(out, "stream_native", lambda: extra_stream_native(args, device))
+        sn, hs = out.get("stream_native", {}), out.get("host_staged", {})
+        if "events_per_s" in sn and isinstance(hs.get("raw"), dict) and hs["raw"].get("events_per_s"):
+            # the sustained stream against the drop-in path's PCIe-bound rate in the same run
+            sn["vs_host_staged"] = round(sn["events_per_s"] / hs["raw"]["events_per_s"], 4)
     return out
 
 
@@ -659,19 +669,31 @@ def extra_alternating(args, device):
     return r
 
 
+STREAM_LINE_BYTES = 260   # a replay line (254 B) plus its share of the batches' alignment
+
+
+def stream_rates(args, shards):
+    """(event rate per shard, speedup) of the streaming replay: each shard's cycle (10 s of
+    event time) within its share of --stream-host-gb (16 GB at most), released at
+    --stream-target events/s per shard."""
+    per_gb = min(16.0, args.stream_host_gb / shards)
+    rate = int(min(args.stream_target / 35.0, per_gb * 1e9 / (10 * STREAM_LINE_BYTES)))
+    return rate, args.stream_target / rate
+
+
 def extra_stream_native(args, device, shards=1):
-    """configs[4] natively: bin/ysb_topology --stream (tools/bench_stream.py): replay bytes
-    through the pinned double-buffered slots at the ingest ceiling, asynchronous flushes
-    through the C++ Redis writer, get-stats' per-(campaign, window) latency read back, exact
-    vs the generator truth (check-correct).  shards > 1 (bench.py --gpus N, rank 0 after the
-    other legs): one shard per GPU of the node (shard s on device s), one watermark = the
-    minimum over them, the same total replay rate split over the shards (the replay's host
-    threads, not the GPUs, bound it)."""
+    """configs[4] natively: bin/ysb_topology --stream (tools/bench_stream.py): every shard's
+    replay cycle registered with its context and fed in place by a feeder thread of its own on
+    its GPU's NUMA node (the copy kernel reads the batch over PCIe, the GPU rebases the event
+    times), asynchronous flushes through the C++ Redis writer, get-stats' per-(campaign,
+    window) latency read back, exact vs the generator truth (check-correct).  shards > 1
+    (bench.py --gpus N, rank 0 after the other legs): one shard per GPU of the node (shard s on
+    device s), each at --stream-target events/s, one watermark = the minimum over them."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_stream
-    r = bench_stream.stream_native(device, seconds=args.stream_seconds,
-                                   event_rate=max(1, args.stream_event_rate // shards),
-                                   speedup=args.stream_speedup, shards=shards)
+    rate, speedup = stream_rates(args, shards)
+    r = bench_stream.stream_native(device, seconds=args.stream_seconds, event_rate=rate, speedup=speedup,
+                                   shards=shards, replay=args.stream_replay)
     log("extras: stream_native %.3f G events/s, get-stats p50 / p99 %s / %s ms (closed windows %d), exact %s"
         % (r["events_per_s"] / 1e9, r["get_stats"]["p50_ms"], r["get_stats"]["p99_ms"],
            r["get_stats"]["closed_windows"], r["exact_vs_generator_truth"]))

@@ -203,6 +203,10 @@ int         ysb_device_count(void);
  * device, and ysb_open / ysb_device_sync fail with a message that says so (INTEGRATION.md
  * section 1.4: load order). */
 int         ysb_device_sync(int device);
+/* The NUMA node of `device`'s PCI function (sysfs numa_node of hipDeviceGetPCIBusId's address;
+ * -1 when unknown), ABI 5: where a caller's registered batches and feeder threads for this GPU
+ * belong (each Flink source instance NUMA-local to the GPU its chain runs on). */
+int         ysb_device_numa_node(int device);
 
 /* Replaces CampaignProcessorCommon(String)/prepare() (CampaignProcessorCommon.java:30-55)
  * and RedisJoinBolt.open() (AdvertisingTopologyNative.java:451-458). */
@@ -300,6 +304,15 @@ typedef struct ysb_rebase {
  * until ysb_wait(ctx, slot).  The slot's pinned host buffer is not used. */
 int         ysb_submit_raw_mapped(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes,
                                   const ysb_rebase* rebase);
+/* The same for a batch whose record boundaries the source already knows (a Kafka source's
+ * messages; a replay cycle's line offsets, computed once and kept in HBM for every cycle):
+ * d_line_off holds n_events u32 offsets into `bytes` in device memory.  No line split: the copy
+ * kernel reads the bytes in place, the scan (after the rebase, with rebase != NULL: lines
+ * [first_line, first_line + n_events) of the table) is enqueued behind it on the compute stream
+ * at once.  The call first waits for the slot's previous copy (at most two in flight); the
+ * caller must not rewrite the bytes until ysb_wait(ctx, slot). */
+int         ysb_submit_mapped(ysb_ctx* ctx, int slot, const uint8_t* bytes, uint64_t nbytes,
+                              const uint32_t* d_line_off, uint64_t n_events, const ysb_rebase* rebase);
 /* The same split of a device-resident batch (16-byte aligned, < 4 GiB): d_off[0..*n) <- its
  * line starts (YSB_ERR_CAPACITY, *n = the lines, if more than cap).  Synchronous. */
 int         ysb_split_lines_device(ysb_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, uint32_t* d_off,

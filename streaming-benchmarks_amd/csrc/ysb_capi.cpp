@@ -6,6 +6,8 @@
 
 #include <unistd.h>
 
+#include <cctype>
+
 using namespace ysb;
 
 thread_local std::string g_open_err;
@@ -46,6 +48,20 @@ static int no_device(hipError_t e) {
                     hipGetErrorString(e), vis ? "; *_VISIBLE_DEVICES=" : "", vis ? vis : "");
     return fail(nullptr, YSB_ERR_HIP, "no HIP device available (hipGetDeviceCount: %s%s)", hipGetErrorString(e),
                 kfd ? "" : "; no /dev/kfd: no AMD GPU driver in this environment");
+}
+
+int ysb_device_numa_node(int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return -1;
+    for (char* p = bus; *p; ++p) *p = (char)std::tolower((unsigned char)*p);
+    char path[160];
+    std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    FILE* f = std::fopen(path, "r");
+    if (!f) return -1;
+    int node = -1;
+    if (std::fscanf(f, "%d", &node) != 1) node = -1;
+    std::fclose(f);
+    return node;
 }
 
 int ysb_device_sync(int device) {

@@ -222,14 +222,14 @@ void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_
 // split_chunks(nbytes) u32 of scratch.  Asynchronous on s.
 u64 split_chunks(u64 nbytes);
 // the slots' host -> device copy by a kernel (ysb_split.hip): src a device-visible pinned host pointer
-void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t s);
+void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t s, bool prio = false);
 hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64 cap, unsigned long long* d_n,
                               hipStream_t s);
 // The replay's event-time rebasing (ysb_split.hip, ysb_submit_raw_mapped): for the first
 // min(*d_n, tab_n, cap) lines of a split raw batch (starts off[0..cap)), the nine digits at line
 // start + (tab[i] & 0xFFFF) <- lead + (tab[i] >> 16), zero-padded; writes stay inside [0, nbytes).
-void launch_rebase(u8* b, u64 nbytes, const u32* off, u64 cap, const unsigned long long* d_n, const u32* tab,
-                   u64 tab_n, i64 lead, int cus, hipStream_t s);
+void launch_rebase(u8* b, u64 nbytes, const u32* off, u64 cap, const unsigned long long* d_n, u64 n_val,
+                   const u32* tab, u64 tab_n, i64 lead, int cus, hipStream_t s);   // d_n NULL: n_val lines
 // Layout sampling of device launches: sampled lines (spread over the launch's segments),
 // copied on the device (in stream order after the batch's producer) into pinned host memory,
 // SAMPLE_STRIDE bytes per line: u32 {line start, sampled length, valid, 0}, then

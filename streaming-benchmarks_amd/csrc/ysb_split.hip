@@ -40,8 +40,10 @@ constexpr int H2D_TPB = 256, H2D_UNROLL = 4;
 
 typedef u32 h2d_v4 __attribute__((ext_vector_type(4)));
 
+template <bool PRIO>
 __global__ __launch_bounds__(H2D_TPB) void h2d_copy_kernel(const h2d_v4* __restrict__ src, h2d_v4* __restrict__ dst,
                                                            u64 vecs) {
+    if (PRIO) __builtin_amdgcn_s_setprio(3);   // issue ahead of a concurrent scan's waves on the SIMD
     const u64 stride = (u64)gridDim.x * H2D_TPB;
     u64 i = (u64)blockIdx.x * H2D_TPB + threadIdx.x;
     for (; i + (H2D_UNROLL - 1) * stride < vecs; i += H2D_UNROLL * stride) {
@@ -55,13 +57,17 @@ __global__ __launch_bounds__(H2D_TPB) void h2d_copy_kernel(const h2d_v4* __restr
 }
 
 // bytes rounded up to whole 16-byte vectors: both buffers have >= 64 bytes of slack
-void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t s) {
+void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t s, bool prio) {
     const u64 vecs = (bytes + 15) / 16;
     if (!vecs) return;
     // one workgroup per CU (4 waves): ~4 MiB in flight, far above PCIe's bandwidth x latency
     const u64 grid = std::max<u64>(1, std::min<u64>((u64)cus, (vecs + H2D_TPB - 1) / H2D_TPB));
-    hipLaunchKernelGGL(h2d_copy_kernel, dim3((unsigned)grid), dim3(H2D_TPB), 0, s, static_cast<const h2d_v4*>(src),
-                       static_cast<h2d_v4*>(dst), vecs);
+    if (prio)
+        hipLaunchKernelGGL(h2d_copy_kernel<true>, dim3((unsigned)grid), dim3(H2D_TPB), 0, s,
+                           static_cast<const h2d_v4*>(src), static_cast<h2d_v4*>(dst), vecs);
+    else
+        hipLaunchKernelGGL(h2d_copy_kernel<false>, dim3((unsigned)grid), dim3(H2D_TPB), 0, s,
+                           static_cast<const h2d_v4*>(src), static_cast<h2d_v4*>(dst), vecs);
 }
 
 u64 split_chunks(u64 nbytes) { return (nbytes + SPLIT_CHUNK - 1) / SPLIT_CHUNK; }
@@ -200,9 +206,10 @@ void launch_sample(const SampleSegs& s, u32 nseg, u8* out, hipStream_t st) {
 constexpr int REBASE_TPB = 256;
 
 __global__ __launch_bounds__(REBASE_TPB) void rebase_kernel(u8* __restrict__ b, u64 nbytes, const u32* __restrict__ off,
-                                                            const unsigned long long* d_n, const u32* __restrict__ tab,
-                                                            u64 tab_n, u64 cap, i64 lead) {
-    u64 n = *d_n < tab_n ? *d_n : tab_n;
+                                                            const unsigned long long* d_n, u64 n_val,
+                                                            const u32* __restrict__ tab, u64 tab_n, u64 cap, i64 lead) {
+    const u64 nl = d_n ? *d_n : n_val;
+    u64 n = nl < tab_n ? nl : tab_n;
     if (n > cap) n = cap;   // (more lines than off[] holds: the launch fails on the host)
     for (u64 i = (u64)blockIdx.x * REBASE_TPB + threadIdx.x; i < n; i += (u64)gridDim.x * REBASE_TPB) {
         const u32 t = tab[i];
@@ -217,13 +224,15 @@ __global__ __launch_bounds__(REBASE_TPB) void rebase_kernel(u8* __restrict__ b, 
     }
 }
 
-void launch_rebase(u8* b, u64 nbytes, const u32* off, u64 cap, const unsigned long long* d_n, const u32* tab,
-                   u64 tab_n, i64 lead, int cus, hipStream_t s) {
+void launch_rebase(u8* b, u64 nbytes, const u32* off, u64 cap, const unsigned long long* d_n, u64 n_val,
+                   const u32* tab, u64 tab_n, i64 lead, int cus, hipStream_t s) {
     if (!nbytes || !tab_n) return;
-    // lines are unknown until the split's count is read on the device: a grid-stride loop
-    const u64 grid = std::max<u64>(1, std::min<u64>((u64)cus * 4, (tab_n + REBASE_TPB - 1) / REBASE_TPB));
-    hipLaunchKernelGGL(rebase_kernel, dim3((unsigned)grid), dim3(REBASE_TPB), 0, s, b, nbytes, off, d_n, tab, tab_n,
-                       cap, lead);
+    // (a raw batch's lines are unknown until the split's count is read on the device: a
+    // grid-stride loop either way)
+    const u64 lines = d_n ? tab_n : std::min(n_val, tab_n);
+    const u64 grid = std::max<u64>(1, std::min<u64>((u64)cus * 4, (lines + REBASE_TPB - 1) / REBASE_TPB));
+    hipLaunchKernelGGL(rebase_kernel, dim3((unsigned)grid), dim3(REBASE_TPB), 0, s, b, nbytes, off, d_n, n_val, tab,
+                       tab_n, cap, lead);
 }
 
 hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64 cap, unsigned long long* d_n,

@@ -106,6 +106,14 @@ static int grow_u32(ysb_ctx* c, u32** buf, u64* have, u64 words) {
     return YSB_OK;
 }
 
+// s waits for e -- unless e has completed already: the slot copies' wait for the slot's last
+// scan is normally long satisfied, and a cross-queue barrier packet costs the copy queue time
+// between copies even when it has nothing to wait for.
+static hipError_t wait_unless_done(hipStream_t s, hipEvent_t e) {
+    if (hipEventQuery(e) == hipSuccess) return hipSuccess;
+    return hipStreamWaitEvent(s, e, 0);
+}
+
 // YSB_F_TIMING keeps HIP events per launch and per slot copy until ysb_kernel_time /
 // ysb_copy_time read them.  A caller that never does (a streaming job) would grow them without
 // bound: once TIMING_KEEP are pending, the older half is folded into running totals (those
@@ -604,7 +612,7 @@ static int ensure_slots(ysb_ctx* c) {
 // YSB_F_H2D_SDMA.
 static hipError_t h2d(ysb_ctx* c, void* dst, const void* dsrc, const void* hsrc, u64 bytes) {
     if (c->cfg.flags & YSB_F_H2D_SDMA) return hipMemcpyAsync(dst, hsrc, bytes, hipMemcpyHostToDevice, c->s_copy);
-    launch_h2d_copy(dst, dsrc, bytes, c->cus, c->s_copy);
+    launch_h2d_copy(dst, dsrc, bytes, c->cus * c->h2d_wg, c->s_copy, c->h2d_prio);
     return hipGetLastError();
 }
 
@@ -634,7 +642,7 @@ int ysb_submit(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, cons
     if (bytes != c->h_bytes[slot] && nbytes) std::memcpy(c->h_bytes[slot], bytes, nbytes);
     if (line_off != c->h_off[slot] && n) std::memcpy(c->h_off[slot], line_off, n * 4);
     // ... and the slot's previous kernel must be done before its device buffers are
-    HIPCHK(c, hipStreamWaitEvent(c->s_copy, c->ev_kdone[slot], 0));
+    HIPCHK(c, wait_unless_done(c->s_copy, c->ev_kdone[slot]));
     hipEvent_t* ce = nullptr;
     if ((rc = copy_events(c, &ce, nbytes + n * 4))) return rc;
     if (ce) HIPCHK(c, hipEventRecord(ce[0], c->s_copy));
@@ -684,6 +692,9 @@ static int ensure_raw(ysb_ctx* c) {
         if (!c->ev_raw[s]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_raw[s], hipEventDisableTiming));
     }
     if (!c->s_split) HIPCHK(c, hipStreamCreateWithFlags(&c->s_split, hipStreamNonBlocking));
+    if (const char* e = getenv("YSB_SPLIT_STREAM")) c->split_place = std::atoi(e);
+    if (const char* e = getenv("YSB_H2D_WG")) c->h2d_wg = std::max(1, std::atoi(e));
+    if (const char* e = getenv("YSB_H2D_PRIO")) c->h2d_prio = std::atoi(e) != 0;
     const u64 words = split_chunks(c->cfg.max_batch_bytes) + 1;
     if (c->split_chunk_words < words) {
         hipFree(c->d_split_chunk);
@@ -787,8 +798,9 @@ static int enqueue_raw(ysb_ctx* c, int slot, const u8* hsrc, const u8* dsrc, u64
     // four alternations each): on the copy stream 186-203 M events/s, on a stream of its own
     // 162-181, on the compute stream 188-193 (the DMA engine 209-213)
     const bool sdma = (c->cfg.flags & YSB_F_H2D_SDMA) != 0u;
-    hipStream_t ss = sdma ? c->s_split : c->s_copy;
-    HIPCHK(c, hipStreamWaitEvent(c->s_copy, c->ev_kdone[slot], 0));
+    // (YSB_SPLIT_STREAM, A/B only: 1 a stream of its own, 2 the compute stream)
+    hipStream_t ss = sdma || c->split_place == 1 ? c->s_split : c->split_place == 2 ? c->s_comp : c->s_copy;
+    HIPCHK(c, wait_unless_done(c->s_copy, c->ev_kdone[slot]));
     hipEvent_t* ce = nullptr;
     if ((rc = copy_events(c, &ce, nbytes))) return rc;
     if (ce) HIPCHK(c, hipEventRecord(ce[0], c->s_copy));
@@ -803,7 +815,7 @@ static int enqueue_raw(ysb_ctx* c, int slot, const u8* hsrc, const u8* dsrc, u64
         HIPCHK(c, launch_split_lines(c->d_bytes[slot], nbytes, c->d_split_chunk, c->d_roff[slot],
                                      c->raw_lines_cap, c->h_rawn + slot, ss));
         if (rb) {
-            launch_rebase(c->d_bytes[slot], nbytes, c->d_roff[slot], c->raw_lines_cap, c->h_rawn + slot,
+            launch_rebase(c->d_bytes[slot], nbytes, c->d_roff[slot], c->raw_lines_cap, c->h_rawn + slot, 0,
                           c->d_rebase + rb->first_line, c->rebase_n - rb->first_line,
                           c->rebase_base + rb->lead_shift, c->cus, ss);
             HIPCHK(c, hipGetLastError());
@@ -914,6 +926,64 @@ int ysb_submit_raw_mapped(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t n
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     return enqueue_raw(c, slot, bytes, dsrc, nbytes, rb);
+}
+
+// A mapped batch whose line offsets are already in HBM: nothing waits for a line count, so the
+// copy queue holds copies only (a raw batch's split and rebase between copies cost the copy
+// queue ~4 % of its time: DESIGN.md section 11) and the scan is enqueued at once behind the
+// copy on the compute stream.
+int ysb_submit_mapped(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, const uint32_t* d_line_off,
+                      uint64_t n, const ysb_rebase* rb) {
+    if (!c) return YSB_ERR_ARG;
+    int rc = raw_args(c, slot, bytes, nbytes);
+    if (rc) return rc;
+    if (n > 0x7FFFFFFFull) return fail(c, YSB_ERR_CAPACITY, "at most 2^31-1 events per batch");
+    if (n && !d_line_off) return fail(c, YSB_ERR_ARG, "NULL line offsets");
+    const uintptr_t a = reinterpret_cast<uintptr_t>(bytes);
+    if (a & 15) return fail(c, YSB_ERR_ARG, "a mapped batch must be 16-byte aligned");
+    const u8* dsrc = nullptr;
+    auto it = c->host_ranges.upper_bound(a);
+    if (it != c->host_ranges.begin()) {
+        --it;
+        if (a + ((nbytes + 15) & ~15ull) <= it->first + it->second.bytes) dsrc = it->second.dptr + (a - it->first);
+    }
+    if (nbytes && !dsrc) return fail(c, YSB_ERR_ARG, "the batch (rounded up to 16 B) is not inside a registered range");
+    if (rb) {
+        if (!c->d_rebase) return fail(c, YSB_ERR_STATE, "no rebase table (ysb_rebase_table)");
+        if (rb->first_line > c->rebase_n || n > c->rebase_n - rb->first_line)
+            return fail(c, YSB_ERR_ARG, "the batch's lines run past the rebase table");
+        const i64 lo = c->rebase_base + rb->lead_shift;
+        if (lo < 0 || lo + (i64)c->rebase_kmax >= 1000000000LL)
+            return fail(c, YSB_ERR_ARG, "rebased leading digits out of [0, 10^9)");
+    }
+    if (!n) return YSB_OK;
+    rc = launch_pending_raw(c);   // batches launch in submission order
+    if (!rc) rc = ensure_slots(c);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    // at most two copies in flight: the slot's previous one must be done (its device buffer is
+    // then only still read by its scan, which the copy waits for on the device)
+    HIPCHK(c, hipEventSynchronize(c->ev_h2d[slot]));
+    if (layout_sampling(c)) c->submit_layout = hinted_layout(c, sniff_raw(c, bytes, nbytes, &c->submit_learn));
+    HIPCHK(c, wait_unless_done(c->s_copy, c->ev_kdone[slot]));
+    hipEvent_t* ce = nullptr;
+    if ((rc = copy_events(c, &ce, nbytes))) return rc;
+    if (ce) HIPCHK(c, hipEventRecord(ce[0], c->s_copy));
+    HIPCHK(c, h2d(c, c->d_bytes[slot], dsrc, bytes, nbytes));
+    if (ce) HIPCHK(c, hipEventRecord(ce[1], c->s_copy));
+    HIPCHK(c, hipEventRecord(c->ev_h2d[slot], c->s_copy));
+    HIPCHK(c, hipStreamWaitEvent(c->s_comp, c->ev_h2d[slot], 0));
+    if (rb) {
+        launch_rebase(c->d_bytes[slot], nbytes, d_line_off, n, nullptr, n, c->d_rebase + rb->first_line,
+                      c->rebase_n - rb->first_line, c->rebase_base + rb->lead_shift, c->cus, c->s_comp);
+        HIPCHK(c, hipGetLastError());
+    }
+    const ysb_segment sg{c->d_bytes[slot], nbytes, d_line_off, n};
+    rc = enqueue_scan(c, &sg, 1);
+    c->submit_layout = -1;
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_kdone[slot], c->s_comp));
+    return YSB_OK;
 }
 
 int ysb_split_lines_device(ysb_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint32_t* d_off, uint64_t cap,

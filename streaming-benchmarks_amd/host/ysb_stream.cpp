@@ -1,7 +1,13 @@
 // ysb_stream.cpp -- implementation of ysb_stream.hpp (the runner's streaming mode).
 #include "ysb_stream.hpp"
 
+#include <pthread.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <time.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -24,50 +30,127 @@ double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-constexpr int64_t BUCKET_MS = 10000;      // CampaignProcessorCommon.java:28 (time_divisor)
-constexpr uint64_t GEN_PIECE = 8u << 20;  // events per device generator call
+double thread_cpu_s() {
+    timespec ts{};
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+constexpr int64_t BUCKET_MS = 10000;       // CampaignProcessorCommon.java:28 (time_divisor)
+constexpr uint64_t GEN_PIECE = 2u << 20;   // events per generator call
+constexpr uint64_t BATCH_ALIGN = 64;       // each batch's first byte (ysb_submit_raw_mapped: >= 16)
+constexpr int64_t LEAD_SLACK = 16;         // buckets below t0's a line may fall in (skew, late events)
 const char ET_KEY[] = "\"event_time\"";
 
 void check_ctx(int rc, ysb_ctx* c, const char* what) {
     if (rc != YSB_OK) throw std::runtime_error(std::string(what) + ": " + ysb_last_error(c));
 }
 
+unsigned default_threads(const StreamOptions& o) {
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    return o.threads ? o.threads : std::max(1u, hw / (unsigned)std::max(1, o.shards));
+}
+
+// Pins the calling thread to `cpus` (threads it creates inherit the mask); false if it could not.
+bool pin_to(const std::vector<int>& cpus) {
+    if (cpus.empty()) return false;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int c : cpus) CPU_SET(c, &set);
+    return pthread_setaffinity_np(pthread_self(), sizeof set, &set) == 0;
+}
+
 }  // namespace
 
-// One cycle of the replay: the generator's lines over cycleMs of event time, each line's 13
-// time digits located, and the slot-sized batches it is released in.
+int gpuNumaNode(int device) { return ysb_device_numa_node(device); }
+
+std::vector<int> nodeCpus(int node) {
+    std::vector<int> out;
+    if (node < 0) return out;
+    FILE* f = std::fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+    if (!f) return out;
+    char buf[4096] = {0};
+    const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
+    for (char* p = buf; *p;) {   // "0-23,96-119"
+        char* e = nullptr;
+        const long a = std::strtol(p, &e, 10);
+        if (e == p) break;
+        long b = a;
+        if (*e == '-') {
+            p = e + 1;
+            b = std::strtol(p, &e, 10);
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET((int)c, &allowed)) out.push_back((int)c);
+        p = *e == ',' ? e + 1 : e;
+        if (*p == '\n') break;
+    }
+    return out;
+}
+
+// One cycle of the replay: the generator's lines over cycleMs of event time, laid out batch by
+// batch in one anonymous mapping (each batch 64-byte aligned, the lines of a batch back to
+// back), each line's event_time digits located, and the batches the cycle is released in.
 struct ReplayCycle {
-    std::vector<uint8_t> bytes;
-    std::vector<uint64_t> start;     // n + 1 line starts
-    std::vector<uint16_t> timePos;   // the 13 time digits' offset within the line
-    std::vector<uint16_t> upper;     // their leading 9 digits, minus upperMin
+    uint8_t* bytes = nullptr;
+    uint64_t reserved = 0;           // bytes mapped (virtual)
+    uint64_t used = 0;               // bytes written, slack included (what is registered)
+    std::vector<uint64_t> start;     // n line starts in `bytes`
+    // per line: offset of its 13 time digits within the line | (leading nine digits - upperMin) << 16
+    std::vector<uint32_t> timeAt;
     int64_t upperMin = 0;
     uint32_t nUpper = 0;
     struct Batch {
         uint64_t a, b;               // lines [a, b)
+        uint64_t off, nbytes;        // its bytes: [off, off + nbytes) of `bytes`
         int64_t releaseMs;           // nominal emission time of line b - 1 (cycle 0)
         int64_t maxTimeMs;           // the largest event_time in it (cycle 0)
     };
     std::vector<Batch> batches;
-    uint64_t lines() const { return start.size() - 1; }
+    uint64_t lines() const { return start.size(); }
+    ReplayCycle() = default;
+    ReplayCycle(const ReplayCycle&) = delete;
+    ReplayCycle& operator=(const ReplayCycle&) = delete;
+    ~ReplayCycle() {
+        if (bytes) munmap(bytes, reserved);
+    }
 };
 
 struct StreamingJob::Shard {
-    int index = 0, device = 0;
+    int index = 0, device = 0, node = -1;
+    std::vector<int> cpus;
+    bool pinned = false;
     ysb_ctx* ctx = nullptr;
     uint8_t* slot[2] = {nullptr, nullptr};
     ysb_gen_params gen{};
     std::vector<uint32_t> subset;
     ReplayCycle cyc;
-    // progress
+    bool registered = false;
+    uint32_t* d_lineOff = nullptr;   // (mapped) every line's offset within its batch, in HBM
+    double prepareS = 0, registerS = 0;
+    // feeder state (the feeder thread's own)
     uint64_t cycle = 0, next = 0;    // the next batch: cyc.batches[next] of cycle `cycle`
     int cur = 0;
     int64_t maxTime = INT64_MIN;
     uint64_t events = 0, batches = 0;
-    std::deque<int64_t> flushes;     // indices of this shard's outstanding asynchronous flushes
+    std::deque<std::pair<int64_t, int64_t>> flushes;   // outstanding: (flush index, watermark at its begin)
+    int64_t flushBegun = 0;
     int64_t ringLo = 0;
+    uint64_t ringAdvances = 0, slowSubmits = 0;
+    double submitMs = 0, slowMs = 0, slowMaxMs = 0, maxBehindMs = 0, cpuS = 0;
+    double firstSubmit = 0, lastSubmit = 0, doneAt = 0;
+    std::atomic<bool> synced{false};
+    std::thread th;
+    std::string error;
     ~Shard() {
-        if (ctx) ysb_close(ctx);
+        if (th.joinable()) th.join();
+        if (ctx && d_lineOff) ysb_device_free(ctx, d_lineOff);
+        if (ctx) ysb_close(ctx);   // (unregisters the cycle before it is unmapped)
     }
 };
 
@@ -75,6 +158,7 @@ StreamingJob::StreamingJob(const StreamOptions& o) : o_(o) {
     if (o_.cycleMs <= 0 || o_.cycleMs % BUCKET_MS) throw std::runtime_error("the replay cycle must be a multiple of 10 000 ms");
     if (o_.t0Ms % BUCKET_MS) throw std::runtime_error("t0 must be a multiple of 10 000 ms");
     if (o_.shards < 1 || o_.eventRate < 1 || o_.speedup <= 0) throw std::runtime_error("bad stream options");
+    if (o_.skew < 0 || o_.skew > 2) throw std::runtime_error("skew must be 0 (off), 1 (skew + late events) or 2 (skew only)");
 }
 
 StreamingJob::~StreamingJob() {
@@ -82,98 +166,127 @@ StreamingJob::~StreamingJob() {
 }
 
 // The shard's replay cycle: generated on its GPU (ysb_gen_events_device, the data/ generator)
-// in pieces and copied to host memory -- or, ctx NULL (the CPU self-check), by the host
-// generator -- then indexed.
-static void build_cycle(ysb_ctx* ctx, const ysb_gen_params& g, const StreamOptions& o,
-                        ReplayCycle& c, WorkerPool& pool) {
+// in pieces -- or, ctx NULL (the CPU checks), by the host generator -- and laid out batch by
+// batch: batches close at batchMs of nominal emission time or a slot's bytes, whichever comes
+// first; each starts 64-byte aligned.  The pages are written by the calling thread (first touch:
+// on its NUMA node).
+static void build_cycle(ysb_ctx* ctx, const ysb_gen_params& g, const StreamOptions& o, ReplayCycle& c,
+                        WorkerPool& pool) {
     const uint64_t n = (uint64_t)(o.eventRate * (double)o.cycleMs / 1000.0);
     if (n == 0) throw std::runtime_error("empty replay cycle");
     const uint64_t maxLine = ysb_gen_max_line_bytes(&g);
-    c.bytes.reserve(n * 256);
-    c.start.assign(n + 1, 0);
-    void *d_b = nullptr, *d_o = nullptr;
+    c.reserved = n * (maxLine + BATCH_ALIGN) + (1u << 20);
+    void* m = mmap(nullptr, c.reserved, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) throw std::runtime_error("replay cycle: mmap failed");
+    c.bytes = static_cast<uint8_t*>(m);
+    madvise(c.bytes, c.reserved, MADV_HUGEPAGE);
+    c.start.assign(n, 0);
+    c.timeAt.assign(n, 0);
+    const int64_t base = g.t0_ms / BUCKET_MS - LEAD_SLACK;
+    c.upperMin = base;
+    auto nominal = [&](uint64_t i) { return g.t0_ms + (int64_t)((i * 1000ull) / g.events_per_sec); };
     const uint64_t piece = std::min<uint64_t>(n, GEN_PIECE);
-    std::vector<uint8_t> hbuf;
+    void *d_b = nullptr, *d_o = nullptr;
     if (ctx) {
         check_ctx(ysb_device_alloc(ctx, piece * maxLine + 64, &d_b), ctx, "ysb_device_alloc");
         check_ctx(ysb_device_alloc(ctx, piece * 4 + 64, &d_o), ctx, "ysb_device_alloc");
-    } else {
-        hbuf.resize(piece * maxLine + 64);
     }
-    std::vector<uint32_t> off(piece);
+    std::vector<uint8_t> hbuf(piece * maxLine + 64);
+    std::vector<uint32_t> off(piece + 1);
+    std::vector<std::string> err(pool.size());
+    std::vector<uint32_t> kmax(pool.size(), 0);
+    uint64_t pos = 0;                 // write position in c.bytes
+    bool open = false;
+    ReplayCycle::Batch cur{};
+    int64_t lim = 0;
+    auto close_batch = [&](uint64_t b) {
+        cur.b = b;
+        cur.nbytes = pos - cur.off;
+        cur.releaseMs = nominal(b - 1);
+        c.batches.push_back(cur);
+        open = false;
+    };
     for (uint64_t first = 0; first < n; first += piece) {
-        const uint64_t m = std::min(piece, n - first);
+        const uint64_t mcount = std::min(piece, n - first);
         uint64_t nb = 0;
-        const uint64_t base = c.bytes.size();
         if (ctx) {
-            check_ctx(ysb_gen_events_device(ctx, &g, first, m, (uint8_t*)d_b, piece * maxLine, (uint32_t*)d_o, &nb), ctx,
-                      "ysb_gen_events_device");
-            c.bytes.resize(base + nb);
-            check_ctx(ysb_memcpy_d2h(ctx, c.bytes.data() + base, d_b, nb), ctx, "ysb_memcpy_d2h");
-            check_ctx(ysb_memcpy_d2h(ctx, off.data(), d_o, m * 4), ctx, "ysb_memcpy_d2h");
-        } else {
-            if (ysb_gen_events_host_mt(&g, first, m, hbuf.data(), hbuf.size(), off.data(), &nb, pool.size()) != YSB_OK)
-                throw std::runtime_error(std::string("ysb_gen_events_host_mt: ") + ysb_last_error(nullptr));
-            c.bytes.insert(c.bytes.end(), hbuf.begin(), hbuf.begin() + (ptrdiff_t)nb);
+            check_ctx(ysb_gen_events_device(ctx, &g, first, mcount, (uint8_t*)d_b, piece * maxLine, (uint32_t*)d_o, &nb),
+                      ctx, "ysb_gen_events_device");
+            check_ctx(ysb_memcpy_d2h(ctx, hbuf.data(), d_b, nb), ctx, "ysb_memcpy_d2h");
+            check_ctx(ysb_memcpy_d2h(ctx, off.data(), d_o, mcount * 4), ctx, "ysb_memcpy_d2h");
+        } else if (ysb_gen_events_host_mt(&g, first, mcount, hbuf.data(), hbuf.size(), off.data(), &nb, pool.size()) != YSB_OK) {
+            throw std::runtime_error(std::string("ysb_gen_events_host_mt: ") + ysb_last_error(nullptr));
         }
-        for (uint64_t i = 0; i < m; ++i) c.start[first + i] = base + off[i];
+        off[mcount] = (uint32_t)nb;
+        // the layout: sequential (batch boundaries depend on the lines before), positions only
+        for (uint64_t j = 0; j < mcount; ++j) {
+            const uint64_t i = first + j, len = off[j + 1] - off[j];
+            if (open && (nominal(i) >= lim || pos + len - cur.off > o.slotBytes)) close_batch(i);
+            if (!open) {
+                pos = (pos + BATCH_ALIGN - 1) / BATCH_ALIGN * BATCH_ALIGN;
+                cur = ReplayCycle::Batch{i, i, pos, 0, 0, INT64_MIN};
+                lim = nominal(i) + o.batchMs;
+                open = true;
+                if (len > o.slotBytes) throw std::runtime_error("a replay line is longer than the slot");
+            }
+            c.start[i] = pos;
+            pos += len;
+        }
+        // the bytes and the time index: in parallel
+        pool.run(pool.size(), [&](unsigned t) {
+            const uint64_t ja = mcount * t / pool.size(), jb = mcount * (t + 1) / pool.size();
+            uint32_t km = 0;
+            for (uint64_t j = ja; j < jb && err[t].empty(); ++j) {
+                const uint64_t i = first + j, len = off[j + 1] - off[j];
+                const uint8_t* l = hbuf.data() + off[j];
+                std::memcpy(c.bytes + c.start[i], l, len);
+                const void* k = memmem(l, len, ET_KEY, sizeof ET_KEY - 1);
+                uint64_t p = k ? (uint64_t)((const uint8_t*)k - l) + sizeof ET_KEY - 1 : len;
+                while (p < len && (l[p] == ' ' || l[p] == ':')) ++p;
+                if (p < len && l[p] == '"') ++p;
+                if (p + 13 >= len || l[p + 13] != '"' || p > 0xFFFF) { err[t] = "line " + std::to_string(i) + ": no 13-digit event_time"; break; }
+                int64_t v = 0;
+                for (int d = 0; d < 13; ++d) {
+                    if (l[p + d] < '0' || l[p + d] > '9') { err[t] = "line " + std::to_string(i) + ": event_time"; break; }
+                    v = v * 10 + (l[p + d] - '0');
+                }
+                const int64_t kk = v / BUCKET_MS - base;
+                if (kk < 0 || kk > 0xFFFF) { err[t] = "line " + std::to_string(i) + ": event_time out of the cycle's range"; break; }
+                c.timeAt[i] = (uint32_t)p | ((uint32_t)kk << 16);
+                km = std::max(km, (uint32_t)kk);
+            }
+            kmax[t] = std::max(kmax[t], km);
+        });
+        for (const auto& e : err)
+            if (!e.empty()) throw std::runtime_error("replay cycle: " + e);
     }
-    c.start[n] = c.bytes.size();
+    if (open) close_batch(n);
+    c.used = pos + BATCH_ALIGN;       // slack: a batch's copy reads up to 15 bytes past its end
+    c.nUpper = 1 + *std::max_element(kmax.begin(), kmax.end());
+    // each batch's largest event_time (cycle 0): from the index, in parallel over batches
+    pool.run(pool.size(), [&](unsigned t) {
+        for (size_t k = t; k < c.batches.size(); k += pool.size()) {
+            ReplayCycle::Batch& b = c.batches[k];
+            int64_t mx = INT64_MIN;
+            for (uint64_t i = b.a; i < b.b; ++i) {
+                const uint8_t* d = c.bytes + c.start[i] + (c.timeAt[i] & 0xFFFFu);
+                int64_t v = 0;
+                for (int q = 0; q < 13; ++q) v = v * 10 + (d[q] - '0');
+                mx = std::max(mx, v);
+            }
+            b.maxTimeMs = mx;
+        }
+    });
     if (ctx) {
         ysb_device_free(ctx, d_b);
         ysb_device_free(ctx, d_o);
     }
-    // each line's 13 time digits: their offset and the leading nine as a number
-    c.timePos.assign(n, 0);
-    std::vector<int64_t> up(n), tm(n);
-    std::vector<std::string> err(pool.size());
-    pool.run(pool.size(), [&](unsigned t) {
-        const uint64_t a = n * t / pool.size(), b = n * (t + 1) / pool.size();
-        for (uint64_t i = a; i < b && err[t].empty(); ++i) {
-            const uint8_t* l = c.bytes.data() + c.start[i];
-            const uint64_t len = c.start[i + 1] - c.start[i];
-            const void* k = memmem(l, len, ET_KEY, sizeof ET_KEY - 1);
-            uint64_t p = k ? (uint64_t)((const uint8_t*)k - l) + sizeof ET_KEY - 1 : len;
-            while (p < len && (l[p] == ' ' || l[p] == ':')) ++p;
-            if (p < len && l[p] == '"') ++p;
-            if (p + 13 >= len || l[p + 13] != '"') { err[t] = "line " + std::to_string(i) + ": no 13-digit event_time"; break; }
-            int64_t v = 0;
-            for (int d = 0; d < 13; ++d) {
-                if (l[p + d] < '0' || l[p + d] > '9') { err[t] = "line " + std::to_string(i) + ": event_time"; break; }
-                v = v * 10 + (l[p + d] - '0');
-            }
-            c.timePos[i] = (uint16_t)p;
-            up[i] = v / BUCKET_MS;
-            tm[i] = v;
-        }
-    });
-    for (const auto& e : err)
-        if (!e.empty()) throw std::runtime_error("replay cycle: " + e);
-    c.upperMin = *std::min_element(up.begin(), up.end());
-    const int64_t umax = *std::max_element(up.begin(), up.end());
-    if (umax - c.upperMin >= 65535) throw std::runtime_error("replay cycle spans too many windows");
-    c.nUpper = (uint32_t)(umax - c.upperMin + 1);
-    c.upper.resize(n);
-    for (uint64_t i = 0; i < n; ++i) c.upper[i] = (uint16_t)(up[i] - c.upperMin);
-    // batches: at most a slot's bytes and batchMs of nominal emission time each
-    auto nominal = [&](uint64_t i) { return g.t0_ms + (int64_t)((i * 1000ull) / g.events_per_sec); };
-    for (uint64_t a = 0; a < n;) {
-        uint64_t b = a;
-        int64_t mx = INT64_MIN;
-        const int64_t lim = nominal(a) + o.batchMs;
-        while (b < n && c.start[b + 1] - c.start[a] <= o.slotBytes && (b == a || nominal(b) < lim)) {
-            mx = std::max(mx, tm[b]);
-            ++b;
-        }
-        if (b == a) throw std::runtime_error("a replay line is longer than the slot");
-        c.batches.push_back({a, b, nominal(b - 1), mx});
-        a = b;
-    }
 }
 
-// Batch b of cycle `cycle` into dst: its lines copied in parallel pieces, every event_time moved
-// by cycle * cycleMs -- the nine leading digits replaced from a per-cycle table of the few
-// values they take (the four trailing digits do not change: cycleMs is a multiple of 10 000).
+// The host restatement of the device rebase (ysb_split.hip rebase_kernel): batch b of cycle
+// `cycle` copied into dst with every line's nine leading event_time digits moved by
+// cycle * cycleMs / 10 000 buckets (the four trailing digits do not change).  Round 5's fill and
+// the CPU checks.
 static uint64_t fill_batch(const ReplayCycle& c, const ReplayCycle::Batch& b, uint64_t cycle, int64_t cycleMs,
                            uint8_t* dst, WorkerPool& pool, unsigned T) {
     const int64_t shift = (int64_t)cycle * (cycleMs / BUCKET_MS);
@@ -185,21 +298,20 @@ static uint64_t fill_batch(const ReplayCycle& c, const ReplayCycle::Batch& b, ui
             v /= 10;
         }
     }
-    const uint64_t base = c.start[b.a], nb = c.start[b.b] - base;
     const uint64_t lines = b.b - b.a;
-    const unsigned tn = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(std::min(T, pool.size()), nb >> 22));
+    const unsigned tn = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(std::min(T, pool.size()), b.nbytes >> 22));
     pool.run(tn, [&](unsigned t) {
         const uint64_t la = b.a + lines * t / tn, lb = b.a + lines * (t + 1) / tn;
-        const uint64_t pa = c.start[la], pb = c.start[lb];
-        std::memcpy(dst + (pa - base), c.bytes.data() + pa, pb - pa);
+        const uint64_t pa = c.start[la], pb = lb < b.b ? c.start[lb] : b.off + b.nbytes;
+        std::memcpy(dst + (pa - b.off), c.bytes + pa, pb - pa);
         if (shift)
             for (uint64_t i = la; i < lb; ++i)
-                std::memcpy(dst + (c.start[i] - base) + c.timePos[i], &table[9ull * c.upper[i]], 9);
+                std::memcpy(dst + (c.start[i] - b.off) + (c.timeAt[i] & 0xFFFFu), &table[9ull * (c.timeAt[i] >> 16)], 9);
     });
-    return nb;
+    return b.nbytes;
 }
 
-std::string StreamingJob::replaySelfCheck(const StreamOptions& o, const std::vector<uint64_t>& cycles) {
+static ysb_gen_params shard_gen(const StreamOptions& o, uint32_t stream) {
     ysb_gen_params g;
     ysb_gen_default(&g);
     g.seed = o.seed;
@@ -208,14 +320,19 @@ std::string StreamingJob::replaySelfCheck(const StreamOptions& o, const std::vec
     g.t0_ms = o.t0Ms;
     g.events_per_sec = (uint64_t)o.eventRate;
     g.with_skew = (uint32_t)o.skew;
-    g.event_stream = 1;
+    g.event_stream = stream;
+    return g;
+}
+
+std::string StreamingJob::replaySelfCheck(const StreamOptions& o, const std::vector<uint64_t>& cycles) {
+    const ysb_gen_params g = shard_gen(o, 1);
     const unsigned T = o.threads ? o.threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     WorkerPool pool(T);
     ReplayCycle c;
     build_cycle(nullptr, g, o, c, pool);
     std::vector<uint8_t> buf(o.slotBytes + 64), ref(o.slotBytes + 64);
     std::vector<uint32_t> off(c.lines() + 1);
-    uint64_t lines = 0, bad = 0, batches = 0;
+    uint64_t lines = 0, bad = 0, batches = 0, misaligned = 0;
     for (uint64_t cy : cycles) {
         ysb_gen_params gc = g;
         gc.t0_ms = o.t0Ms + (int64_t)cy * o.cycleMs;   // the generator's own lines of that cycle
@@ -225,31 +342,93 @@ std::string StreamingJob::replaySelfCheck(const StreamOptions& o, const std::vec
             if (ysb_gen_events_host(&gc, b.a, b.b - b.a, ref.data(), ref.size(), off.data(), &rb) != YSB_OK)
                 throw std::runtime_error("ysb_gen_events_host failed");
             if (rb != nb || std::memcmp(buf.data(), ref.data(), nb) != 0) ++bad;
+            misaligned += (b.off % BATCH_ALIGN) != 0;
             lines += b.b - b.a;
             ++batches;
         }
     }
-    char o2[256];
+    char o2[320];
     std::snprintf(o2, sizeof o2, "{\"mode\": \"stream-self-check\", \"lines_per_cycle\": %llu, \"batches\": %llu, "
-                  "\"lines\": %llu, \"mismatched_batches\": %llu, \"upper_values\": %u}",
+                  "\"lines\": %llu, \"mismatched_batches\": %llu, \"misaligned_batches\": %llu, \"upper_values\": %u}",
                   (unsigned long long)c.lines(), (unsigned long long)batches, (unsigned long long)lines,
-                  (unsigned long long)bad, c.nUpper);
+                  (unsigned long long)bad, (unsigned long long)misaligned, c.nUpper);
     return o2;
 }
 
+std::string StreamingJob::feedCheck(const StreamOptions& o, double seconds) {
+    // every shard: its own cycle (its own event stream), built and fed on a thread of its own
+    const int S = o.shards;
+    std::vector<std::unique_ptr<ReplayCycle>> cyc(S);
+    std::vector<std::thread> th;
+    std::vector<std::string> err(S);
+    for (int s = 0; s < S; ++s)
+        th.emplace_back([&, s] {
+            try {
+                WorkerPool pool(default_threads(o));
+                cyc[s].reset(new ReplayCycle());
+                build_cycle(nullptr, shard_gen(o, 1 + (uint32_t)s), o, *cyc[s], pool);
+            } catch (const std::exception& e) {
+                err[s] = e.what();
+            }
+        });
+    for (auto& t : th) t.join();
+    th.clear();
+    for (const auto& e : err)
+        if (!e.empty()) throw std::runtime_error(e);
+    // every feeder fills its own slot buffer as fast as it can (one thread each)
+    std::vector<uint64_t> ev(S, 0);
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false};
+    std::vector<double> el(S, 0);
+    for (int s = 0; s < S; ++s)
+        th.emplace_back([&, s] {
+            const ReplayCycle& c = *cyc[s];
+            std::vector<uint8_t> slot(o.slotBytes + 64);
+            WorkerPool pool(1);
+            ++ready;
+            while (!go.load()) std::this_thread::yield();
+            const double t0 = now_s();
+            uint64_t cycle = 0, next = 0, events = 0;
+            while (now_s() - t0 < seconds) {
+                const ReplayCycle::Batch& b = c.batches[next];
+                fill_batch(c, b, cycle, o.cycleMs, slot.data(), pool, 1);
+                events += b.b - b.a;
+                if (++next == c.batches.size()) {
+                    next = 0;
+                    ++cycle;
+                }
+            }
+            el[s] = now_s() - t0;
+            ev[s] = events;
+        });
+    while (ready.load() < S) std::this_thread::yield();
+    go = true;
+    for (auto& t : th) t.join();
+    uint64_t total = 0;
+    double mx = 0;
+    for (int s = 0; s < S; ++s) {
+        total += ev[s];
+        mx = std::max(mx, el[s]);
+    }
+    const double rate = mx > 0 ? (double)total / mx : 0;
+    const double lineBytes = (double)(cyc[0]->used) / (double)cyc[0]->lines();
+    char out[512];
+    std::snprintf(out, sizeof out, "{\"mode\": \"stream-feed-check\", \"shards\": %d, \"seconds\": %.2f, "
+                  "\"lines_per_cycle\": %llu, \"batches_per_cycle\": %zu, \"copy_events_per_s\": %.1f, "
+                  "\"copy_GBs\": %.2f, \"hardware_threads\": %u}",
+                  S, seconds, (unsigned long long)cyc[0]->lines(), cyc[0]->batches.size(), rate,
+                  rate * lineBytes / 1e9, std::thread::hardware_concurrency());
+    return out;
+}
+
 void StreamingJob::prepare() {
-    ysb_gen_params g;
-    ysb_gen_default(&g);
-    g.seed = o_.seed;
-    g.n_campaigns = o_.campaigns;
-    g.ads_per_campaign = o_.adsPerCampaign;
+    ysb_gen_params g = shard_gen(o_, 0);
     std::vector<char> cid(36ull * o_.campaigns), aid(36ull * o_.campaigns * o_.adsPerCampaign);
     if (ysb_gen_ids(&g, cid.data(), aid.data()) != YSB_OK) throw std::runtime_error("ysb_gen_ids failed");
     const uint64_t A = (uint64_t)o_.campaigns * o_.adsPerCampaign;
     for (uint32_t c = 0; c < o_.campaigns; ++c) campaigns_.emplace_back(&cid[36ull * c], 36);
     for (uint64_t a = 0; a < A; ++a) ads_.emplace_back(&aid[36 * a], 36);
     const int ndev = std::max(1, ysb_device_count());
-    WorkerPool pool(o_.threads ? o_.threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
     std::vector<const char*> keys(A);
     std::vector<uint32_t> camp(A);
     for (uint64_t a = 0; a < A; ++a) {
@@ -261,33 +440,68 @@ void StreamingJob::prepare() {
         shards_.push_back(sh);
         sh->index = s;
         sh->device = (o_.device + s) % ndev;
-        ysb_config cfg;
-        ysb_config_default(&cfg);
-        cfg.n_campaigns = o_.campaigns;
-        cfg.window_ring = o_.windowRing;
-        cfg.max_batch_bytes = o_.slotBytes;
-        cfg.max_batch_events = o_.slotBytes / 64;
-        cfg.ring_base_bucket = o_.t0Ms / BUCKET_MS - 8;
-        cfg.flags = o_.timing ? YSB_F_TIMING : 0u;
-        if (ysb_open(&sh->ctx, sh->device, &cfg) != YSB_OK)
-            throw std::runtime_error(std::string("ysb_open: ") + ysb_last_error(nullptr));
-        sh->ringLo = cfg.ring_base_bucket;
-        check_ctx(ysb_load_ad_map(sh->ctx, keys.data(), nullptr, camp.data(), A), sh->ctx, "ysb_load_ad_map");
-        for (int k = 0; k < 2; ++k) check_ctx(ysb_slot_buffers(sh->ctx, k, &sh->slot[k], nullptr), sh->ctx, "ysb_slot_buffers");
-        // the shard's own event stream over its ad_id shard (ysb_ad_shard), as bench.py's ranks
-        sh->gen = g;
-        sh->gen.t0_ms = o_.t0Ms;
-        sh->gen.events_per_sec = (uint64_t)o_.eventRate;
-        sh->gen.with_skew = (uint32_t)o_.skew;
-        sh->gen.event_stream = 1 + (uint32_t)s;
-        if (o_.shards > 1) {
-            for (uint64_t a = 0; a < A; ++a)
-                if (ysb_ad_shard(ads_[a].data(), 36, (uint32_t)o_.shards) == (uint32_t)s) sh->subset.push_back((uint32_t)a);
-            sh->gen.ad_subset = sh->subset.data();
-            sh->gen.n_ad_subset = (uint32_t)sh->subset.size();
-        }
-        build_cycle(sh->ctx, sh->gen, o_, sh->cyc, pool);
+        sh->node = gpuNumaNode(sh->device);
+        if (o_.pinNuma) sh->cpus = nodeCpus(sh->node);
     }
+    // every shard prepared on a thread of its own, on its GPU's NUMA node: the context, the
+    // cycle (generated on its GPU, its pages first touched there), registered with the context
+    std::vector<std::thread> th;
+    for (Shard* sh : shards_)
+        th.emplace_back([&, sh] {
+            try {
+                const double t0 = now_s();
+                sh->pinned = pin_to(sh->cpus);
+                WorkerPool pool(default_threads(o_));
+                ysb_config cfg;
+                ysb_config_default(&cfg);
+                cfg.n_campaigns = o_.campaigns;
+                cfg.window_ring = o_.windowRing;
+                cfg.max_batch_bytes = o_.slotBytes;
+                cfg.max_batch_events = o_.slotBytes / 64;
+                cfg.ring_base_bucket = o_.t0Ms / BUCKET_MS - 8;
+                cfg.flags = o_.timing ? YSB_F_TIMING : 0u;
+                if (ysb_open(&sh->ctx, sh->device, &cfg) != YSB_OK)
+                    throw std::runtime_error(std::string("ysb_open: ") + ysb_last_error(nullptr));
+                sh->ringLo = cfg.ring_base_bucket;
+                check_ctx(ysb_load_ad_map(sh->ctx, keys.data(), nullptr, camp.data(), A), sh->ctx, "ysb_load_ad_map");
+                for (int k = 0; k < 2; ++k)
+                    check_ctx(ysb_slot_buffers(sh->ctx, k, &sh->slot[k], nullptr), sh->ctx, "ysb_slot_buffers");
+                // the shard's own event stream over its ad_id shard (ysb_ad_shard), as bench.py's ranks
+                sh->gen = shard_gen(o_, 1 + (uint32_t)sh->index);
+                if (o_.shards > 1) {
+                    for (uint64_t a = 0; a < A; ++a)
+                        if (ysb_ad_shard(ads_[a].data(), 36, (uint32_t)o_.shards) == (uint32_t)sh->index)
+                            sh->subset.push_back((uint32_t)a);
+                    sh->gen.ad_subset = sh->subset.data();
+                    sh->gen.n_ad_subset = (uint32_t)sh->subset.size();
+                }
+                build_cycle(sh->ctx, sh->gen, o_, sh->cyc, pool);
+                const double t1 = now_s();
+                if (o_.replay != StreamOptions::COPY) {
+                    check_ctx(ysb_host_register(sh->ctx, sh->cyc.bytes, (sh->cyc.used + 4095) / 4096 * 4096), sh->ctx,
+                              "ysb_host_register");
+                    sh->registered = true;
+                    check_ctx(ysb_rebase_table(sh->ctx, sh->cyc.timeAt.data(), sh->cyc.lines(), sh->cyc.upperMin),
+                              sh->ctx, "ysb_rebase_table");
+                }
+                if (o_.replay == StreamOptions::MAPPED) {   // the line offsets, once for every cycle
+                    std::vector<uint32_t> lo(sh->cyc.lines());
+                    for (const auto& b : sh->cyc.batches)
+                        for (uint64_t i = b.a; i < b.b; ++i) lo[i] = (uint32_t)(sh->cyc.start[i] - b.off);
+                    void* d = nullptr;
+                    check_ctx(ysb_device_alloc(sh->ctx, lo.size() * 4 + 64, &d), sh->ctx, "ysb_device_alloc");
+                    sh->d_lineOff = static_cast<uint32_t*>(d);
+                    check_ctx(ysb_memcpy_h2d(sh->ctx, d, lo.data(), lo.size() * 4), sh->ctx, "ysb_memcpy_h2d");
+                }
+                sh->registerS = now_s() - t1;
+                sh->prepareS = now_s() - t0;
+            } catch (const std::exception& e) {
+                sh->error = e.what();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (Shard* sh : shards_)
+        if (!sh->error.empty()) throw std::runtime_error("shard " + std::to_string(sh->index) + ": " + sh->error);
 }
 
 namespace {
@@ -374,154 +588,235 @@ private:
     }
 };
 
+// The shards' flushes merged by index: a flush goes to the sink once every shard delivered it,
+// in index order, its watermark the minimum of the shards' (each taken at that shard's begin).
+class FlushMerger {
+public:
+    FlushMerger(SinkThread& st, int shards) : st_(st), shards_(shards) {}
+    void deliver(int64_t index, int64_t watermark, std::vector<WindowDelta>&& rows) {
+        std::lock_guard<std::mutex> g(m_);
+        Pending& p = pend_[index];
+        if (p.left < 0) {
+            p.left = shards_;
+            p.f.index = index;
+            p.f.watermarkMs = INT64_MAX;
+        }
+        p.f.watermarkMs = std::min(p.f.watermarkMs, watermark);
+        for (auto& r : rows) p.f.rows.push_back(std::move(r));
+        --p.left;
+        while (!pend_.empty() && pend_.begin()->first == next_ && pend_.begin()->second.left == 0) {
+            st_.push(std::move(pend_.begin()->second.f));
+            pend_.erase(pend_.begin());
+            ++next_;
+        }
+    }
+    bool empty() {
+        std::lock_guard<std::mutex> g(m_);
+        return pend_.empty();
+    }
+
+private:
+    struct Pending {
+        int left = -1;
+        FlushRows f;
+    };
+    SinkThread& st_;
+    const int shards_;
+    std::mutex m_;
+    std::map<int64_t, Pending> pend_;
+    int64_t next_ = 0;
+};
+
 }  // namespace
 
 StreamReport StreamingJob::run(const FlushSink& sink) {
     StreamReport rep;
-    const unsigned T = o_.threads ? o_.threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    WorkerPool pool(T);
-    const double wall0 = now_s() + 0.05;   // the replay clock starts 50 ms from now (warm threads)
+    const unsigned T = default_threads(o_);
+    const double wall0 = now_s() + 0.1;   // the replay clock starts 100 ms from now (feeders started)
     auto clock = [&]() -> int64_t { return o_.t0Ms + (int64_t)((now_s() - wall0) * 1000.0 * o_.speedup); };
     auto wallOf = [&](int64_t eventMs) { return wall0 + (double)(eventMs - o_.t0Ms) / (1000.0 * o_.speedup); };
     SinkThread st(sink, clock);
+    FlushMerger merger(st, (int)shards_.size());
     rep.linesPerCycle = shards_[0]->cyc.lines();
-    for (Shard* s : shards_) {
-        ysb_copy_time(s->ctx, nullptr, nullptr, nullptr);   // reset the copy timing
-        check_ctx(ysb_wait(s->ctx, 0), s->ctx, "ysb_wait");
-    }
-    std::deque<FlushRows> pending;   // begun on every shard, not yet taken from all
-    std::deque<int> pendingLeft;
-    int64_t nextFlush = o_.t0Ms + o_.flushMs, flushIndex = 0;
     const double stopAt = wall0 + o_.seconds;
-    double firstSubmit = 0, lastSubmit = 0;
+    std::atomic<int64_t> flushReq{0};
+    std::atomic<bool> stop{false}, final{false}, failed{false};
 
-    auto fill = [&](Shard* s, const ReplayCycle::Batch& b, uint8_t* dst) -> uint64_t {
-        return fill_batch(s->cyc, b, s->cycle, o_.cycleMs, dst, pool, T);
-    };
-
-    auto takeFlushes = [&](bool wait) {
-        for (Shard* s : shards_) {
-            while (!s->flushes.empty()) {
-                uint64_t n = 0;
-                int more = 0;
-                int rc = ysb_flush_end(s->ctx, wait ? 1 : 0, nullptr, 0, &n, &more);
-                if (rc == YSB_PENDING) break;
-                check_ctx(rc, s->ctx, "ysb_flush_end");
-                std::vector<ysb_count> rows(std::max<uint64_t>(n, 1));
-                check_ctx(ysb_flush_end(s->ctx, 1, rows.data(), n, &n, &more), s->ctx, "ysb_flush_end");
-                const int64_t idx = s->flushes.front();
-                s->flushes.pop_front();
-                const size_t at = (size_t)(idx - pending.front().index);
-                for (uint64_t i = 0; i < n; ++i)
-                    pending[at].rows.push_back({campaigns_[rows[i].campaign], rows[i].window_ms, rows[i].count});
-                --pendingLeft[at];
+    // ---- one feeder per shard: it owns the shard's context ------------------------------
+    auto feed = [&](Shard* s) {
+        const double cpu0 = thread_cpu_s();
+        try {
+            pin_to(s->cpus);
+            WorkerPool pool(o_.replay == StreamOptions::COPY ? T : 1u);
+            ysb_copy_time(s->ctx, nullptr, nullptr, nullptr);   // reset the copy timing
+            check_ctx(ysb_wait(s->ctx, 0), s->ctx, "ysb_wait");
+            auto takeFlushes = [&](bool wait) {
+                while (!s->flushes.empty()) {
+                    uint64_t n = 0;
+                    int more = 0;
+                    int rc = ysb_flush_end(s->ctx, wait ? 1 : 0, nullptr, 0, &n, &more);
+                    if (rc == YSB_PENDING) break;
+                    check_ctx(rc, s->ctx, "ysb_flush_end");
+                    std::vector<ysb_count> rows(std::max<uint64_t>(n, 1));
+                    check_ctx(ysb_flush_end(s->ctx, 1, rows.data(), n, &n, &more), s->ctx, "ysb_flush_end");
+                    std::vector<WindowDelta> d;
+                    d.reserve(n);
+                    for (uint64_t i = 0; i < n; ++i) d.push_back({campaigns_[rows[i].campaign], rows[i].window_ms, rows[i].count});
+                    merger.deliver(s->flushes.front().first, s->flushes.front().second, std::move(d));
+                    s->flushes.pop_front();
+                }
+            };
+            auto beginFlushes = [&]() {
+                const int64_t want = flushReq.load();
+                while (s->flushBegun < want) {
+                    if (s->flushes.size() == 4) takeFlushes(true);   // at most 4 outstanding: the oldest first
+                    check_ctx(ysb_flush_begin(s->ctx, INT64_MIN, INT64_MAX), s->ctx, "ysb_flush_begin");
+                    s->flushes.push_back({s->flushBegun++, s->maxTime == INT64_MIN ? INT64_MIN : s->maxTime - o_.oooMs});
+                }
+            };
+            // the ring follows this shard's watermark: when the newest bucket nears the ring's
+            // end, a synchronous move (rare) -- only when it moves the base
+            auto followRing = [&]() {
+                if (s->maxTime == INT64_MIN) return;
+                if (s->maxTime / BUCKET_MS + 8 < s->ringLo + (int64_t)o_.windowRing) return;
+                const int64_t lo = (s->maxTime - o_.oooMs) / BUCKET_MS - 8;
+                if (lo <= s->ringLo) return;
+                takeFlushes(true);
+                check_ctx(ysb_ring_advance(s->ctx, lo), s->ctx, "ysb_ring_advance");
+                s->ringLo = lo;
+                ++s->ringAdvances;
+            };
+            while (!stop.load()) {
+                const double w = now_s();
+                bool any = false;
+                const ReplayCycle::Batch& b = s->cyc.batches[s->next];
+                const double due = wallOf(b.releaseMs + (int64_t)s->cycle * o_.cycleMs);
+                if (w >= due && w < stopAt) {
+                    s->maxBehindMs = std::max(s->maxBehindMs, (w - due) * 1e3);
+                    const double t0 = now_s();
+                    const ysb_rebase rb{b.a, (int64_t)s->cycle * (o_.cycleMs / BUCKET_MS)};
+                    if (o_.replay == StreamOptions::MAPPED) {
+                        check_ctx(ysb_submit_mapped(s->ctx, s->cur, s->cyc.bytes + b.off, b.nbytes, s->d_lineOff + b.a,
+                                                    b.b - b.a, &rb), s->ctx, "ysb_submit_mapped");
+                    } else if (o_.replay == StreamOptions::MAPPED_RAW) {
+                        check_ctx(ysb_submit_raw_mapped(s->ctx, s->cur, s->cyc.bytes + b.off, b.nbytes, &rb), s->ctx,
+                                  "ysb_submit_raw_mapped");
+                    } else {
+                        check_ctx(ysb_wait(s->ctx, s->cur), s->ctx, "ysb_wait");   // the slot's last copy is done
+                        const uint64_t nb = fill_batch(s->cyc, b, s->cycle, o_.cycleMs, s->slot[s->cur], pool, T);
+                        check_ctx(ysb_submit_raw(s->ctx, s->cur, s->slot[s->cur], nb), s->ctx, "ysb_submit_raw");
+                    }
+                    const double t1 = now_s(), dt = (t1 - t0) * 1e3;
+                    s->submitMs += dt;
+                    if (dt > 1.0) {
+                        ++s->slowSubmits;
+                        s->slowMs += dt;
+                        s->slowMaxMs = std::max(s->slowMaxMs, dt);
+                    }
+                    if (!s->firstSubmit) s->firstSubmit = t0;
+                    s->lastSubmit = t1;
+                    s->maxTime = std::max(s->maxTime, b.maxTimeMs + (int64_t)s->cycle * o_.cycleMs);
+                    s->events += b.b - b.a;
+                    ++s->batches;
+                    s->cur ^= 1;
+                    if (++s->next == s->cyc.batches.size()) {
+                        s->next = 0;
+                        ++s->cycle;
+                    }
+                    any = true;
+                }
+                beginFlushes();
+                takeFlushes(false);
+                followRing();
+                if (!any) {
+                    // sleep until the next batch is due (at most 200 us: flushes to begin / take)
+                    const double nd = wallOf(s->cyc.batches[s->next].releaseMs + (int64_t)s->cycle * o_.cycleMs) - now_s();
+                    if (nd > 20e-6) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)std::min(200.0, nd * 1e6 - 10)));
+                }
             }
-        }
-        while (!pending.empty() && pendingLeft.front() == 0) {
-            st.push(std::move(pending.front()));
-            pending.pop_front();
-            pendingLeft.pop_front();
-        }
-    };
-
-    auto watermark = [&]() {
-        int64_t wm = INT64_MAX;
-        for (Shard* s : shards_) wm = std::min(wm, s->maxTime == INT64_MIN ? INT64_MIN : s->maxTime - o_.oooMs);
-        return wm;
-    };
-
-    auto beginFlush = [&]() {
-        FlushRows f;
-        f.index = flushIndex++;
-        f.watermarkMs = watermark();
-        for (Shard* s : shards_) {
-            if (s->flushes.size() == 4) {   // at most 4 outstanding: take the oldest first
+            // end of input: every batch counted, then the final flushes the coordinator asks for
+            check_ctx(ysb_sync(s->ctx), s->ctx, "ysb_sync");
+            s->doneAt = now_s();
+            s->synced = true;
+            while (!final.load() && !failed.load()) std::this_thread::sleep_for(std::chrono::microseconds(100));
+            if (!failed.load()) {
+                beginFlushes();
                 takeFlushes(true);
             }
-            check_ctx(ysb_flush_begin(s->ctx, INT64_MIN, INT64_MAX), s->ctx, "ysb_flush_begin");
-            s->flushes.push_back(f.index);
+        } catch (const std::exception& e) {
+            s->error = e.what();
+            failed = true;
+            s->synced = true;
         }
-        pending.push_back(std::move(f));
-        pendingLeft.push_back((int)shards_.size());
+        s->cpuS = thread_cpu_s() - cpu0;
     };
+    for (Shard* s : shards_) s->th = std::thread(feed, s);
 
-    // the ring follows the watermark: when it nears the ring's end, a synchronous move (rare)
-    auto followRing = [&](Shard* s) {
-        const int64_t wmB = s->maxTime / BUCKET_MS;
-        if (wmB + 8 < s->ringLo + (int64_t)o_.windowRing) return;
-        takeFlushes(true);
-        const int64_t lo = std::max(s->ringLo, watermark() / BUCKET_MS - 8);
-        check_ctx(ysb_ring_advance(s->ctx, lo), s->ctx, "ysb_ring_advance");
-        s->ringLo = lo;
-        ++rep.ringAdvances;
-    };
-
-    while (true) {
-        const double w = now_s();
-        bool any = false, running = w < stopAt;
-        for (Shard* s : shards_) {
-            if (!running) break;
-            const ReplayCycle::Batch& b = s->cyc.batches[s->next];
-            const int64_t rel = b.releaseMs + (int64_t)s->cycle * o_.cycleMs;
-            const double due = wallOf(rel);
-            if (w < due) continue;
-            rep.maxBehindMs = std::max(rep.maxBehindMs, (w - due) * 1e3);
-            const uint64_t nb = fill(s, b, s->slot[s->cur]);
-            check_ctx(ysb_submit_raw(s->ctx, s->cur, s->slot[s->cur], nb), s->ctx, "ysb_submit_raw");
-            if (!firstSubmit) firstSubmit = now_s();
-            lastSubmit = now_s();
-            s->maxTime = std::max(s->maxTime, b.maxTimeMs + (int64_t)s->cycle * o_.cycleMs);
-            s->events += b.b - b.a;
-            ++s->batches;
-            s->cur ^= 1;
-            const double t0 = now_s();
-            check_ctx(ysb_wait(s->ctx, s->cur), s->ctx, "ysb_wait");   // the other slot's copy: refill it
-            const double wt = (now_s() - t0) * 1e3;
-            if (wt > 0.1) {
-                ++rep.slotWaits;
-                rep.slotWaitMs += wt;
-                rep.slotWaitMaxMs = std::max(rep.slotWaitMaxMs, wt);
-            }
-            if (++s->next == s->cyc.batches.size()) {
-                s->next = 0;
-                ++s->cycle;
-            }
-            followRing(s);
-            any = true;
-        }
-        if (clock() >= nextFlush && running) {
-            beginFlush();
+    // ---- the flusher's clock (CampaignProcessorCommon.java:45: every flushMs) ----------------
+    int64_t nextFlush = o_.t0Ms + o_.flushMs;
+    while (now_s() < stopAt && !failed.load()) {
+        if (clock() >= nextFlush) {
+            ++flushReq;
             nextFlush += o_.flushMs;
-            any = true;
         }
-        takeFlushes(false);
-        if (!running) break;
-        if (!any) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
-    // end of input: every batch counted, the last flush, then a drain for anything outside the
-    // ring (the side list); the watermark stays where the input stopped
-    for (Shard* s : shards_) check_ctx(ysb_sync(s->ctx), s->ctx, "ysb_sync");
-    beginFlush();
-    takeFlushes(true);
+    stop = true;
+    for (Shard* s : shards_)
+        while (!s->synced.load()) std::this_thread::sleep_for(std::chrono::microseconds(100));
+    ++flushReq;   // the last flush: everything submitted
+    final = true;
+    for (Shard* s : shards_) s->th.join();
+    for (Shard* s : shards_)
+        if (!s->error.empty()) throw std::runtime_error("shard " + std::to_string(s->index) + ": " + s->error);
+    if (!merger.empty()) throw std::runtime_error("a flush was not delivered by every shard");
+
+    // a drain for anything outside the ring (the side list); the watermark stays where the input stopped
     FlushRows last;
-    last.index = flushIndex++;
-    last.watermarkMs = watermark();
+    last.index = flushReq.load();
+    last.watermarkMs = INT64_MAX;
     for (Shard* s : shards_) {
+        last.watermarkMs = std::min(last.watermarkMs, s->maxTime == INT64_MIN ? INT64_MIN : s->maxTime - o_.oooMs);
         uint64_t n = 0;
         check_ctx(ysb_drain(s->ctx, INT64_MIN, INT64_MAX, 0, nullptr, 0, &n), s->ctx, "ysb_drain");
         std::vector<ysb_count> rows(std::max<uint64_t>(n, 1));
         check_ctx(ysb_drain(s->ctx, INT64_MIN, INT64_MAX, 1, rows.data(), n, &n), s->ctx, "ysb_drain");
         for (uint64_t i = 0; i < n; ++i) last.rows.push_back({campaigns_[rows[i].campaign], rows[i].window_ms, rows[i].count});
     }
+    const int64_t finalWm = last.watermarkMs;
     st.push(std::move(last));
     st.finish();
 
-    rep.wallSeconds = lastSubmit - firstSubmit;
+    double first = 0, lastSubmit = 0, done = 0;
     for (Shard* s : shards_) {
+        ShardReport sr;
+        sr.device = s->device;
+        sr.numaNode = s->node;
+        sr.pinned = s->pinned;
+        sr.events = s->events;
+        sr.batches = s->batches;
+        sr.cycles = s->cycle;
+        sr.partialLines = s->next ? s->cyc.batches[s->next].a : 0;
+        sr.submitMs = s->submitMs;
+        sr.feederCpuS = s->cpuS;
+        sr.maxBehindMs = s->maxBehindMs;
+        sr.ringAdvances = s->ringAdvances;
+        sr.replayGB = (double)s->cyc.used / 1e9;
+        sr.prepareS = s->prepareS;
+        sr.registerS = s->registerS;
+        rep.shards.push_back(sr);
         rep.events += s->events;
         rep.batches += s->batches;
         rep.cycles.push_back(s->cycle);
-        rep.partialLines.push_back(s->next ? s->cyc.batches[s->next].a : 0);
+        rep.partialLines.push_back(sr.partialLines);
+        rep.slotWaits += s->slowSubmits;
+        rep.slotWaitMs += s->slowMs;
+        rep.slotWaitMaxMs = std::max(rep.slotWaitMaxMs, s->slowMaxMs);
+        rep.maxBehindMs = std::max(rep.maxBehindMs, s->maxBehindMs);
+        rep.ringAdvances += s->ringAdvances;
+        if (s->firstSubmit && (!first || s->firstSubmit < first)) first = s->firstSubmit;
+        lastSubmit = std::max(lastSubmit, s->lastSubmit);
+        done = std::max(done, s->doneAt);
         double ms = 0;
         uint64_t copies = 0, bytes = 0;
         check_ctx(ysb_copy_time(s->ctx, &ms, &copies, &bytes), s->ctx, "ysb_copy_time");
@@ -533,9 +828,10 @@ StreamReport StreamingJob::run(const FlushSink& sink) {
         rep.parseErrors += x.parse_errors;
         rep.joinMisses += x.join_misses;
     }
-    // (the last batch's events count over the interval up to its submit: close enough at
-    // hundreds of batches; the report also carries the wall time)
+    // every submitted event counted, from the first submit to the last shard's ysb_sync
+    rep.wallSeconds = first ? done - first : 0;
     rep.eventsPerSecond = rep.wallSeconds > 0 ? (double)rep.events / rep.wallSeconds : 0;
+    rep.submitEventsPerSecond = lastSubmit > first ? (double)rep.events / (lastSubmit - first) : 0;
     rep.targetEventsPerSecond = o_.eventRate * o_.speedup * (double)shards_.size();
     rep.copyGBs = rep.copyMs > 0 ? (double)rep.copyBytes / (rep.copyMs * 1e-3) / 1e9 : 0;
     rep.copyBusyFrac = rep.wallSeconds > 0 ? rep.copyMs * 1e-3 / rep.wallSeconds / (double)shards_.size() : 0;
@@ -544,7 +840,7 @@ StreamReport StreamingJob::run(const FlushSink& sink) {
     rep.closeReplayMs = st.closeMs;
     rep.cwReplayMs = st.cwMs;
     rep.openAtEnd = st.seen.size() - st.closed.size();
-    rep.finalWatermarkMs = watermark();
+    rep.finalWatermarkMs = finalWm;
     return rep;
 }
 

@@ -5,29 +5,42 @@
 // and get-stats (data/src/setup/core.clj:130-149) reads time_updated - window_ms back as
 // the latency of each window.
 //
-// Here a StreamingJob drives one context per shard (GPU), each fed through its pinned
-// double-buffered slots (ysb_submit_raw) from a replay of pre-generated event lines, with
+// A StreamingJob drives one context per shard (GPU).  Like the reference, where every parallel
+// source instance feeds its own operator chain (AdvertisingTopologyNative.java:97-99,114-119),
+// every shard has a feeder thread of its own, pinned to its GPU's NUMA node, that owns the
+// shard's context: it releases the shard's batches on the replay clock, begins and takes the
+// shard's flushes, and moves the shard's ring.  The main thread only runs the flusher's clock,
+// merges the shards' flushes and hands them to the sink thread.
+//
 //   * event time   the replay's: the data/ generator's lines over one cycle of event time,
-//                  cycled with every event_time moved by the cycle length (only the nine
-//                  leading digits of a 13-digit time change: patched while the lines are
-//                  copied into the slot); the lines of a cycle are released no earlier than
-//                  their nominal emission time on the replay clock, which runs `speedup`
-//                  times faster than the wall clock (a recorded stream played fast: every
-//                  time relation of the reference -- 10 s windows, the 1 s flusher, the
-//                  +-50 ms skew, the 100 ms buffer timeout -- holds in event time);
-//   * watermark    the largest event_time submitted minus the out-of-orderness bound, the
-//                  minimum over the shards (Flink's watermark at a keyed operator);
-//   * flushes      every flushMs of event time, ysb_flush_begin on every shard (no drain of
-//                  the stream), the rows taken by ysb_flush_end without waiting and written by
-//                  a sink thread (Redis in the reference's schema, time_updated from the replay
-//                  clock; and/or the CSV totals);
+//                  cycled with every event_time moved by the cycle length; the lines of a cycle
+//                  are released no earlier than their nominal emission time on the replay clock,
+//                  which runs `speedup` times faster than the wall clock (a recorded stream
+//                  played fast: every time relation of the reference -- 10 s windows, the 1 s
+//                  flusher, the +-50 ms skew, the 100 ms buffer timeout -- holds in event time);
+//   * ingest       (mapped, the default) the cycle sits in host memory laid out batch by batch
+//                  (each batch 64-byte aligned), registered with the shard's context once
+//                  (ysb_host_register), its line offsets in HBM (computed once: every cycle
+//                  reuses them, as a Kafka source knows its message boundaries); a batch is
+//                  handed over in place (ysb_submit_mapped): the GPU's copy kernel reads it over
+//                  PCIe and the nine leading event_time digits are rewritten on the GPU for the
+//                  cycle being played (ysb_rebase_table) -- no host pass over the bytes, and
+//                  nothing but copies on the copy queue.  (mapped-raw: the same with the line
+//                  split on the GPU, ysb_submit_raw_mapped; copy, round 5's path: the feeder
+//                  copies the batch into the pinned slot and patches the digits itself.)
+//   * watermark    per shard the largest event_time submitted minus the out-of-orderness bound;
+//                  a merged flush's watermark is the minimum over the shards at their begins
+//                  (Flink's watermark at a keyed operator);
+//   * flushes      every flushMs of event time each shard begins a flush (ysb_flush_begin, no
+//                  drain of the stream) and takes it when ready (ysb_flush_end without waiting);
+//                  the merged flush is written by a sink thread (Redis in the reference's schema,
+//                  time_updated from the replay clock; and/or the CSV totals);
 //   * windows      a window is closed by the first flush whose watermark has passed its end;
 //                  its close latency is that flush's write time minus the window end, and each
 //                  (campaign, window)'s time_updated - window_ms at that point is the sample
-//                  get-stats reports (no event of a closed window can arrive later: skew +-50 ms
-//                  under a 100 ms bound, and the late-by events are off unless asked for);
-//   * the ring     follows the watermark (ysb_ring_advance, synchronous, rare: W - 16 buckets
-//                  of event time apart), the buckets it leaves reported by a drain.
+//                  get-stats reports;
+//   * the ring     each shard's follows its own watermark (ysb_ring_advance, synchronous, rare:
+//                  W - 16 buckets of event time apart), the buckets it leaves reported by a drain.
 #pragma once
 
 #include <cstdint>
@@ -55,9 +68,15 @@ struct StreamOptions {
     double seconds = 12;              // wall seconds of input
     uint64_t slotBytes = 256ull << 20;
     uint32_t windowRing = 64;
-    unsigned threads = 0;             // copy threads (0: min(16, hardware))
+    unsigned threads = 0;             // host threads per shard for preparing (and, copy mode, filling) (0: 16 / shards)
     int64_t t0Ms = 1700000000000LL;   // nominal time of event 0 (a multiple of 10 000)
-    bool timing = true;               // YSB_F_TIMING: the slots' copy time
+    bool timing = true;               // YSB_F_TIMING: the slots' copy time (folded by the library)
+    // ingest: MAPPED in place from the registered cycle, its line offsets kept in HBM
+    // (ysb_submit_mapped); MAPPED_RAW in place with the line split on the GPU
+    // (ysb_submit_raw_mapped); COPY round 5's host copy into the pinned slot (ysb_submit_raw)
+    enum Replay { MAPPED = 0, MAPPED_RAW = 1, COPY = 2 };
+    int replay = MAPPED;
+    bool pinNuma = true;              // feeder threads (and the cycle's pages) on the GPU's NUMA node
 };
 
 // One flush as the sink sees it: every shard's deltas, the watermark at its begin and the
@@ -68,18 +87,32 @@ struct FlushRows {
     std::vector<WindowDelta> rows;
 };
 
+struct ShardReport {
+    int device = 0, numaNode = -1;
+    bool pinned = false;              // the feeder ran on its GPU's node's CPUs
+    uint64_t events = 0, batches = 0, cycles = 0, partialLines = 0;
+    double submitMs = 0;              // wall time inside the submit calls (incl. the wait for the line count)
+    double feederCpuS = 0;            // the feeder thread's CPU time
+    double maxBehindMs = 0;           // how late (wall ms) a batch was released after its time
+    uint64_t ringAdvances = 0;
+    double replayGB = 0, prepareS = 0, registerS = 0;
+};
+
 struct StreamReport {
     uint64_t events = 0, batches = 0, flushes = 0, rowsWritten = 0;
-    double wallSeconds = 0, eventsPerSecond = 0, targetEventsPerSecond = 0;
+    // wall time from the first submit to the last batch counted (every shard's ysb_sync) and
+    // events / that; the submit-side rate (first to last submit) separately
+    double wallSeconds = 0, eventsPerSecond = 0, submitEventsPerSecond = 0, targetEventsPerSecond = 0;
     double copyMs = 0, copyGBs = 0, copyBusyFrac = 0;
     uint64_t copyBytes = 0;
-    uint64_t slotWaits = 0;           // submits that waited > 0.1 ms for the other slot's copy
+    uint64_t slotWaits = 0;           // submits that took > 1 ms (the copy queue was full)
     double slotWaitMs = 0, slotWaitMaxMs = 0;
-    double maxBehindMs = 0;           // how late (wall ms) a batch was released after its time
+    double maxBehindMs = 0;
     uint64_t ringAdvances = 0;
     std::vector<uint64_t> cycles;     // per shard: whole replay cycles submitted ...
     std::vector<uint64_t> partialLines;   // ... and the lines of the next one
     uint64_t linesPerCycle = 0;
+    std::vector<ShardReport> shards;
     // windows closed by the watermark: close latency (write time - window end)
     std::vector<double> closeReplayMs;
     // per (campaign, window) of those windows: time_updated - window_ms at the close (get-stats)
@@ -95,15 +128,22 @@ using FlushSink = std::function<void(const FlushRows&, int64_t nowMs)>;
 class StreamingJob {
 public:
     explicit StreamingJob(const StreamOptions& o);
-    // Generates the replay cycles (one per shard) and opens the contexts.  The campaign and ad
-    // ids are the generator's (ysb_gen_ids): campaignIds()[i] is campaign index i's UUID.
+    // Opens the contexts and generates the replay cycles (one per shard, each on its own
+    // thread on its GPU's NUMA node).  The campaign and ad ids are the generator's
+    // (ysb_gen_ids): campaignIds()[i] is campaign index i's UUID.
     void prepare();
     StreamReport run(const FlushSink& sink);
     const std::vector<std::string>& campaignIds() const { return campaigns_; }
     // CPU check of the replay (no GPU): a cycle from the host generator, each batch of each of
-    // `cycles` rebased into a buffer and compared byte for byte with the host generator's own
-    // lines of that cycle (t0 moved by cycle * cycleMs).  A JSON summary.
+    // `cycles` rebased into a buffer (the host restatement of the device rebase) and compared
+    // byte for byte with the host generator's own lines of that cycle (t0 moved by cycle *
+    // cycleMs).  A JSON summary.
     static std::string replaySelfCheck(const StreamOptions& o, const std::vector<uint64_t>& cycles);
+    // CPU measurement of the copy feeders (no GPU): `shards` host cycles, each shard's feeder on
+    // a thread of its own filling its slot buffer as fast as it can for `seconds` (round 5's fill:
+    // memcpy + digit patch).  A JSON summary with the aggregate events/s.  (The mapped feeder has
+    // no per-byte host work: its cost per batch is the submit call, measured by the GPU run.)
+    static std::string feedCheck(const StreamOptions& o, double seconds);
     ~StreamingJob();
 
 private:
@@ -112,6 +152,11 @@ private:
     std::vector<std::string> campaigns_, ads_;
     std::vector<Shard*> shards_;
 };
+
+// The NUMA node of a GPU (its PCI device's numa_node; -1 unknown) and the CPUs of a node this
+// process may run on (empty: none / unknown).
+int gpuNumaNode(int device);
+std::vector<int> nodeCpus(int node);
 
 }  // namespace topology
 }  // namespace ysb

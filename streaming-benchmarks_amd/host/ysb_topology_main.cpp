@@ -48,6 +48,8 @@ struct Args {
     StreamOptions so;
     std::string stream_csv;   // per-(campaign, window) totals of everything written
     bool self_check = false;  // --stream-self-check: the replay's rebasing on the CPU, no GPU
+    bool feed_check = false;  // --stream-feed-check: the feeders' host rate on the CPU, no GPU
+    double feed_seconds = 2;
 };
 
 void usage() {
@@ -59,7 +61,9 @@ void usage() {
                  "   or: ysb_topology --stream [--sink none|csv:FILE|redis[:HOST[:PORT]]] [--shards N] [--device D]\n"
                  "       [--seed S] [--campaigns C] [--ads-per-campaign A] [--event-rate E] [--speedup F]\n"
                  "       [--cycle-ms MS] [--flush-ms MS] [--batch-ms MS] [--ooo-ms MS] [--seconds S]\n"
-                 "       [--batch-mb MB] [--window-ring W] [--skew 0|1|2] [--io-threads T] [--totals CSV]\n");
+                 "       [--batch-mb MB] [--window-ring W] [--skew 0|1|2] [--io-threads T] [--totals CSV]\n"
+                 "       [--replay mapped|mapped-raw|copy] [--no-numa] [--no-timing]\n"
+                 "   or: ysb_topology --stream-self-check | --stream-feed-check [--shards N] [--feed-seconds S] ...\n");
 }
 
 Args parse(int argc, char** argv) {
@@ -102,6 +106,16 @@ Args parse(int argc, char** argv) {
         else if (k == "--seconds") a.so.seconds = std::atof(val().c_str());
         else if (k == "--skew") a.so.skew = std::atoi(val().c_str());
         else if (k == "--totals") a.stream_csv = val();
+        else if (k == "--stream-feed-check") { a.stream = true; a.feed_check = true; }
+        else if (k == "--feed-seconds") a.feed_seconds = std::atof(val().c_str());
+        else if (k == "--no-numa") a.so.pinNuma = false;
+        else if (k == "--no-timing") a.so.timing = false;
+        else if (k == "--replay") {
+            const std::string m = val();
+            if (m != "mapped" && m != "mapped-raw" && m != "copy") { usage(); std::exit(2); }
+            a.so.replay = m == "mapped" ? StreamOptions::MAPPED : m == "mapped-raw" ? StreamOptions::MAPPED_RAW
+                                                                                    : StreamOptions::COPY;
+        }
         else { usage(); std::exit(2); }
     }
     if (a.stream) {   // the generator's ids and events: no config file needed
@@ -326,7 +340,21 @@ int run_stream(const Args& a) {
     }
     cyc += "]";
     part += "]";
-    std::printf("{\"mode\": \"stream\", \"shards\": %d, \"events\": %llu, \"batches\": %llu, \"wall_s\": %.3f, "
+    std::string per = "[";
+    for (size_t i = 0; i < r.shards.size(); ++i) {
+        const ShardReport& s = r.shards[i];
+        char b[512];
+        std::snprintf(b, sizeof b, "%s{\"device\": %d, \"numa_node\": %d, \"feeder_pinned\": %s, \"events\": %llu, "
+                      "\"batches\": %llu, \"submit_ms\": %.1f, \"feeder_cpu_s\": %.3f, \"max_behind_ms\": %.2f, "
+                      "\"ring_advances\": %llu, \"replay_GB\": %.2f, \"prepare_s\": %.2f, \"register_s\": %.2f}",
+                      i ? ", " : "", s.device, s.numaNode, s.pinned ? "true" : "false", (unsigned long long)s.events,
+                      (unsigned long long)s.batches, s.submitMs, s.feederCpuS, s.maxBehindMs,
+                      (unsigned long long)s.ringAdvances, s.replayGB, s.prepareS, s.registerS);
+        per += b;
+    }
+    per += "]";
+    std::printf("{\"mode\": \"stream\", \"replay\": \"%s\", \"shards\": %d, \"events\": %llu, \"batches\": %llu, "
+                "\"wall_s\": %.3f, \"submit_events_per_s\": %.1f, \"per_shard\": %s, "
                 "\"events_per_s\": %.1f, \"target_events_per_s\": %.1f, \"copy_GBs\": %.2f, \"copy_busy_frac\": %.4f, "
                 "\"slot_waits\": %llu, \"slot_wait_ms\": %.2f, \"slot_wait_max_ms\": %.3f, \"max_behind_ms\": %.2f, "
                 "\"flushes\": %llu, \"rows_written\": %llu, \"ring_advances\": %llu, "
@@ -337,7 +365,9 @@ int run_stream(const Args& a) {
                 "\"t0_ms\": %lld, \"lines_per_cycle\": %llu, \"cycles\": %s, \"partial_lines\": %s, "
                 "\"overflow_dropped\": %llu, \"parse_errors\": %llu, \"join_misses\": %llu, \"prepare_s\": %.2f, "
                 "\"sink\": %s}\n",
-                a.so.shards, (unsigned long long)r.events, (unsigned long long)r.batches, r.wallSeconds, r.eventsPerSecond,
+                a.so.replay == StreamOptions::MAPPED ? "mapped" : a.so.replay == StreamOptions::MAPPED_RAW ? "mapped-raw" : "copy",
+                a.so.shards, (unsigned long long)r.events, (unsigned long long)r.batches,
+                r.wallSeconds, r.submitEventsPerSecond, per.c_str(), r.eventsPerSecond,
                 r.targetEventsPerSecond, r.copyGBs, r.copyBusyFrac, (unsigned long long)r.slotWaits, r.slotWaitMs,
                 r.slotWaitMaxMs, r.maxBehindMs, (unsigned long long)r.flushes, (unsigned long long)r.rowsWritten,
                 (unsigned long long)r.ringAdvances, dist(r.closeReplayMs, 1.0).c_str(), dist(r.closeReplayMs, f).c_str(),
@@ -358,6 +388,10 @@ int main(int argc, char** argv) {
     try {
         if (a.self_check) {
             std::printf("%s\n", StreamingJob::replaySelfCheck(a.so, {0, 1, 2, 7, 1000}).c_str());
+            return 0;
+        }
+        if (a.feed_check) {
+            std::printf("%s\n", StreamingJob::feedCheck(a.so, a.feed_seconds).c_str());
             return 0;
         }
         if (a.stream) return run_stream(a);

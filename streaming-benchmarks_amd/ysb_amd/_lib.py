@@ -106,6 +106,7 @@ SIGNATURES = {
     "ysb_abi_version": (_I, []),
     "ysb_device_count": (_I, []),
     "ysb_device_sync": (_I, [_I]),
+    "ysb_device_numa_node": (_I, [_I]),
     "ysb_config_default": (None, [C.POINTER(YsbConfig)]),
     "ysb_open": (_I, [C.POINTER(_P), _I, C.POINTER(YsbConfig)]),
     "ysb_close": (_I, [_P]),
@@ -123,6 +124,7 @@ SIGNATURES = {
     "ysb_host_unregister": (_I, [_P, _P]),
     "ysb_rebase_table": (_I, [_P, C.c_void_p, _U64, _I64]),
     "ysb_submit_raw_mapped": (_I, [_P, _I, _PU8, _U64, C.POINTER(YsbRebase)]),
+    "ysb_submit_mapped": (_I, [_P, _I, _PU8, _U64, _PU32, _U64, C.POINTER(YsbRebase)]),
     "ysb_split_lines_device": (_I, [_P, _PU8, _U64, _PU32, _U64, C.POINTER(_U64)]),
     "ysb_copy_time": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_U64), C.POINTER(_U64)]),
     "ysb_submit_device": (_I, [_P, _PU8, _U64, _PU32, _U64]),

@@ -174,6 +174,13 @@ class YsbContext:
         self._c(lib().ysb_submit_raw_mapped(self._h, slot, C.c_void_p(arr.ctypes.data + offset), nbytes,
                                             C.byref(rb) if rb is not None else None))
 
+    def submit_mapped(self, arr, offset, nbytes, d_off, n, slot=0, rebase=None):
+        """ysb_submit_mapped: arr[offset:offset + nbytes] of a registered array with its n line
+        offsets already in device memory (d_off); rebase = (first_line, lead_shift) or None."""
+        rb = _lib.YsbRebase(*rebase) if rebase is not None else None
+        self._c(lib().ysb_submit_mapped(self._h, slot, C.c_void_p(arr.ctypes.data + offset), nbytes,
+                                        C.c_void_p(d_off), n, C.byref(rb) if rb is not None else None))
+
     def split_lines_device(self, d_bytes, nbytes, d_off, cap):
         """ysb_split_lines_device: the line starts of a device batch into d_off; returns n."""
         n = C.c_uint64()

@@ -115,6 +115,38 @@ def test_rebase_moves_every_event_by_whole_buckets(shift):
     assert bytes(buf[parts[0][0]:parts[0][0] + parts[0][1]]) == bytes(data[:parts[0][1]])
 
 
+@pytest.mark.parametrize("shift", [None, 5])
+def test_mapped_batches_with_device_offsets(shift):
+    """ysb_submit_mapped: the same batches with their line offsets already in HBM (no split):
+    counts equal the raw-mapped path's and the generator truth, rebased or not."""
+    g = GenParams(events_per_sec=100_000, with_skew=2)
+    data, off = g.events_host(0, 150_000)
+    tab, base = time_table(data, off)
+    buf, parts = layout_batches(data, off, 6)
+    # every line's offset within its batch (what the replay runner keeps in HBM per cycle)
+    lo = np.empty(off.size, dtype=np.uint32)
+    for (p, nb, a, n) in parts:
+        lo[a:a + n] = off[a:a + n] - off[a]
+    with ctx_for(g) as ctx:
+        ctx.host_register(buf)
+        ctx.rebase_table(tab, base)
+        d_lo = ctx.device_alloc(lo.nbytes + 64)
+        ctx.h2d(d_lo, lo)
+        for i, (p, nb, a, n) in enumerate(parts):
+            ctx.submit_mapped(buf, p, nb, d_lo + 4 * a, n, slot=i % 2,
+                              rebase=None if shift is None else (a, shift))
+        ctx.sync()
+        st = ctx.stats()
+        assert st["events"] == off.size and st["parse_errors"] == 0 and st["deferred"] == 0
+        gs = GenParams(events_per_sec=100_000, with_skew=2, t0_ms=T0 + (shift or 0) * 10_000)
+        ctx.truth_accumulate(gs, 0, off.size)
+        mism, truth, ring = ctx.truth_compare()
+        assert mism == 0 and truth == ring and truth > 0
+        with pytest.raises(YsbError, match="YSB_ERR_ARG"):   # lines past the rebase table
+            ctx.submit_mapped(buf, parts[-1][0], parts[-1][1], d_lo, off.size, rebase=(1, 0))
+        ctx.device_free(d_lo)
+
+
 def test_mapped_argument_errors():
     g = GenParams(events_per_sec=100_000)
     data, off = g.events_host(0, 2000)

@@ -208,4 +208,18 @@ def test_stream_replay_rebasing_equals_the_generator(rate, skew, batch_ms):
     s = json.loads(r.stdout.strip().splitlines()[-1])
     assert s["lines_per_cycle"] == rate * 10 and s["lines"] == 5 * s["lines_per_cycle"]
     assert s["mismatched_batches"] == 0
+    assert s["misaligned_batches"] == 0      # every batch 64-byte aligned (ysb_submit_raw_mapped)
     assert s["upper_values"] >= {0: 1, 1: 7, 2: 2}[skew]
+
+
+def test_stream_feed_check_runs_one_feeder_per_shard():
+    """--stream-feed-check (CPU, no GPU): each shard's feeder on a thread of its own, filling its
+    slot (round 5's copy path: memcpy + time-digit patch) -- the aggregate rate is reported per
+    shard count; the numbers for DESIGN.md come from a quiet machine, here only the contract."""
+    exe = os.path.join(ROOT, "streaming-benchmarks_amd", "bin", "ysb_topology")
+    for shards in (1, 2):
+        r = subprocess.run([exe, "--stream-feed-check", "--shards", str(shards), "--event-rate", "20000",
+                            "--feed-seconds", "0.3", "--batch-mb", "4"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["shards"] == shards and s["lines_per_cycle"] == 200_000 and s["copy_events_per_s"] > 0

@@ -69,7 +69,8 @@ def truth_table(device, summary):
 
 
 def stream_native(device=0, seconds=12.0, event_rate=5_000_000, speedup=32.0, shards=1, slot_mb=256,
-                  flush_ms=1000, batch_ms=100, ooo_ms=100, skew=2, threads=0, workdir=None, window_ring=64):
+                  flush_ms=1000, batch_ms=100, ooo_ms=100, skew=2, threads=0, workdir=None, window_ring=64,
+                  replay="mapped"):
     from fake_redis import FakeRedis
     from ysb_amd import GenParams
     from ysb_amd.redis_sink import RespClient, check_correct, get_stats, new_setup
@@ -84,7 +85,8 @@ def stream_native(device=0, seconds=12.0, event_rate=5_000_000, speedup=32.0, sh
                "--totals", totals_csv, "--seconds", str(seconds), "--event-rate", str(event_rate),
                "--speedup", str(speedup), "--shards", str(shards), "--batch-mb", str(slot_mb),
                "--flush-ms", str(flush_ms), "--batch-ms", str(batch_ms), "--ooo-ms", str(ooo_ms),
-               "--skew", str(skew), "--io-threads", str(threads), "--window-ring", str(window_ring)]
+               "--skew", str(skew), "--io-threads", str(threads), "--window-ring", str(window_ring),
+               "--replay", replay]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             raise RuntimeError("ysb_topology --stream exited %d: %s" % (r.returncode, r.stderr[-2000:]))
@@ -127,16 +129,24 @@ def stream_native(device=0, seconds=12.0, event_rate=5_000_000, speedup=32.0, sh
         srv.close()
     f = 1.0 / s["speedup"]
     out = {
-        "config": "configs[4] natively (bin/ysb_topology --stream, host/ysb_stream.hpp): %d shard(s), the data/ "
-                  "generator's lines replayed from host memory through the pinned double-buffered slots "
-                  "(ysb_submit_raw, the H2D by the copy kernel), event time %.0fx the wall clock (%.1fM events per "
-                  "event-second per shard), skew %s, watermark = max event_time - %d ms, asynchronous flush every "
-                  "%d event-ms (ysb_flush_begin/end) through the C++ Redis writer to an in-process RESP server"
-                  % (s["shards"], s["speedup"], s["event_rate"] / 1e6,
+        "config": "configs[4] natively (bin/ysb_topology --stream, host/ysb_stream.hpp): %d shard(s), one feeder "
+                  "thread per shard on its GPU's NUMA node, the data/ generator's lines replayed from host memory %s, "
+                  "event time %.0fx the wall clock (%.2fM events per event-second per shard), skew %s, watermark = "
+                  "max event_time - %d ms, asynchronous flush every %d event-ms (ysb_flush_begin/end) through the "
+                  "C++ Redis writer to an in-process RESP server"
+                  % (s["shards"], {"mapped": "in place (ysb_submit_mapped: the registered cycle read by the copy kernel, "
+                                           "its line offsets kept in HBM, the time digits rebased on the GPU)",
+                                 "mapped-raw": "in place with the line split on the GPU (ysb_submit_raw_mapped, the time "
+                                               "digits rebased on the GPU)"}.get(
+                         s.get("replay"), "through the pinned double-buffered slots (host copy + time patch, ysb_submit_raw)"),
+                     s["speedup"], s["event_rate"] / 1e6,
                      "+-50 ms, no late events" if s["skew"] == 2 else ("+-50 ms and 1e-5 late < 60 s" if s["skew"] else "off"),
                      s["ooo_ms"], s["flush_ms"]),
+        "replay": s.get("replay"),
         "events": s["events"], "events_per_s": s["events_per_s"], "target_events_per_s": s["target_events_per_s"],
+        "submit_events_per_s": s.get("submit_events_per_s"),
         "per_gpu_events_per_s": round(s["events_per_s"] / s["shards"], 1),
+        "per_shard": s.get("per_shard"),
         "wall_s": s["wall_s"], "batches": s["batches"], "copy_GBs": s["copy_GBs"],
         "copy_busy_frac": s["copy_busy_frac"], "slot_waits": s["slot_waits"], "slot_wait_ms": s["slot_wait_ms"],
         "slot_wait_max_ms": s["slot_wait_max_ms"], "max_behind_ms": s["max_behind_ms"],
@@ -178,9 +188,10 @@ def main():
     ap.add_argument("--batch-ms", type=int, default=100)
     ap.add_argument("--skew", type=int, default=2)
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--replay", choices=("mapped", "mapped-raw", "copy"), default="mapped")
     a = ap.parse_args()
     print(json.dumps(stream_native(a.device, a.seconds, a.event_rate, a.speedup, a.shards, a.slot_mb, a.flush_ms,
-                                   a.batch_ms, skew=a.skew, threads=a.threads)), flush=True)
+                                   a.batch_ms, skew=a.skew, threads=a.threads, replay=a.replay)), flush=True)
 
 
 if __name__ == "__main__":
