@@ -37,9 +37,10 @@ extern "C" {
  *    samples agree (else the per-tile dispatch, never a host wait for the launch queued
  *    last); a raw batch that cannot launch is a sticky error (ysb_stream returns NULL);
  *    raw batches hold at most max(max_batch_events, max_batch_bytes / 32) lines
- * 5: ysb_device_sync; raw batches read in place from caller-registered host memory
- *    (ysb_host_register, ysb_submit_raw_mapped) with the replay's event-time rebasing on the
- *    device (ysb_rebase_table); ysb_exchange_info_size (the struct grew in ABI 4: a caller
+ * 5: ysb_device_sync, ysb_device_numa_node; batches read in place from caller-registered host
+ *    memory (ysb_host_register; raw lines: ysb_submit_raw_mapped; offsets in device memory:
+ *    ysb_submit_mapped) with the replay's event-time rebasing on the device
+ *    (ysb_rebase_table); ysb_exchange_info_size (the struct grew in ABI 4: a caller
  *    checks the size it was built with); YSB_F_TIMING's event records are folded into running
  *    totals, so a caller that never reads them keeps a bounded number */
 #define YSB_ABI_VERSION 5
@@ -201,7 +202,7 @@ int         ysb_device_count(void);
  * runtime.  A process may hold only one working HIP/HSA runtime: if another one (e.g. the
  * libamdhip64 a framework bundles) opens the GPU first, this library's runtime may see no
  * device, and ysb_open / ysb_device_sync fail with a message that says so (INTEGRATION.md
- * section 1.4: load order). */
+ * section 1.4a: load order). */
 int         ysb_device_sync(int device);
 /* The NUMA node of `device`'s PCI function (sysfs numa_node of hipDeviceGetPCIBusId's address;
  * -1 when unknown), ABI 5: where a caller's registered batches and feeder threads for this GPU

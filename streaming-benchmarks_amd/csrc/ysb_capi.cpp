@@ -44,7 +44,7 @@ static int no_device(hipError_t e) {
                     "no HIP device available to this library's HIP runtime (hipGetDeviceCount: %s) although "
                     "/dev/kfd exists: another HIP/HSA runtime in this process (e.g. the libamdhip64 a framework "
                     "such as torch bundles) probably opened the GPU first -- load libysb_hip and call "
-                    "ysb_device_count / ysb_open before any other GPU runtime initialises (INTEGRATION.md 1.4)%s%s",
+                    "ysb_device_count / ysb_open before any other GPU runtime initialises (INTEGRATION.md 1.4a)%s%s",
                     hipGetErrorString(e), vis ? "; *_VISIBLE_DEVICES=" : "", vis ? vis : "");
     return fail(nullptr, YSB_ERR_HIP, "no HIP device available (hipGetDeviceCount: %s%s)", hipGetErrorString(e),
                 kfd ? "" : "; no /dev/kfd: no AMD GPU driver in this environment");
