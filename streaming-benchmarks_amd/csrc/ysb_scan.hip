@@ -50,12 +50,16 @@
 #ifndef YSB_DIAG_NO_FLUSH
 #define YSB_DIAG_NO_FLUSH 0    // LDS window counters never flushed to the ring
 #endif
+#ifndef YSB_DIAG_FLAT_IDX
+#define YSB_DIAG_FLAT_IDX 0    // layout 2: the structural index's classification only (round 6)
+#endif
 
 namespace ysb {
 
 constexpr bool DIAG_A_ONLY = YSB_DIAG_A_ONLY, DIAG_NO_PROBE = YSB_DIAG_NO_PROBE,
                DIAG_NO_PROBE2 = YSB_DIAG_NO_PROBE2, DIAG_NO_COUNT = YSB_DIAG_NO_COUNT,
-               DIAG_NO_REC = YSB_DIAG_NO_REC, DIAG_NO_FLUSH = YSB_DIAG_NO_FLUSH;
+               DIAG_NO_REC = YSB_DIAG_NO_REC, DIAG_NO_FLUSH = YSB_DIAG_NO_FLUSH,
+               DIAG_FLAT_IDX = YSB_DIAG_FLAT_IDX;
 
 // Key ids (bit masks) of the fields DeserializeBolt reads.
 enum : u32 {
@@ -678,6 +682,10 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
             ls = (int)(my_off - cur.s0 + cur.delta);
             le = (int)(my_end - cur.s0 + cur.delta);
             if constexpr (TBL) ok1 = tbl_stage1(lsrc, ls, le, ca);
+            else if constexpr (LAY == 2 && DIAG_FLAT_IDX) {
+                const u32 x = flat_index_only(lsrc, ls, le);   // timing diagnostic: nothing counted
+                if (x == 0x9E3779B9u) tl.miss += 1;
+            }
             else if constexpr (LAY == 2) ok1 = flat_tier<LdsSrc, true>(lsrc, ls, le, P.require_mask, ca, cb, keytab);
             else if constexpr (LAY == 3) {
                 ok1 = P.learn_cp ? learned_parse<true>(lsrc, ls, le, P, ca, cb) : learned_parse<false>(lsrc, ls, le, P, ca, cb);
@@ -779,7 +787,7 @@ __global__ __launch_bounds__(SCAN_TPB) __attribute__((amdgpu_waves_per_eu((Geom<
                 }
             }
         }
-        dfr = li < cur.count && !ok2;   // bad offsets, other layouts, escapes, over-size tiles
+        dfr = li < cur.count && !ok2 && !(DIAG_FLAT_IDX && LAY == 2);   // bad offsets, other layouts, escapes, over-size tiles
         pend = ok2 && cb.view;                                             // EventFilterBolt
         // RedisJoinBolt's lookup (36-byte keys), views only (a third of the lanes:
         // scattered loads cost address-unit time per lane), issued before the time parse

@@ -484,6 +484,42 @@ __device__ __forceinline__ bool flat_parse_bl2(const LdsSrc& src, int s, int e, 
     return true;
 }
 
+// YSB_DIAG_FLAT_IDX (a timing diagnostic, round 6; never used for results): the first half of
+// the wave-cooperative structural index the round-5 review asked for, on the lane's own line --
+// every 16-B chunk of [s, e) read from LDS (one ds_read_b128) and classified (quote bytes
+// exactly, backslash and control bytes), the quote positions extracted in order by bit scans,
+// as the owner lane's walk would consume them -- with nothing named or parsed after it.  Its
+// cost is a lower bound of the index design's; the caller counts nothing.  A checksum keeps
+// the work alive.
+__device__ __forceinline__ u32 flat_index_only(const LdsSrc& src, int s, int e) {
+    u32 acc = 0, nq = 0, bad = 0;
+    int q = s & ~15;
+#pragma unroll 1
+    for (; q < e; q += 16) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src.d + (q >> 2));
+        const u32 w[4] = {v.x, v.y, v.z, v.w};
+        u32 qm = 0, bm = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32 x = w[k] ^ 0x22222222u;
+            const u32 z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);   // quote bytes, exact
+            const u32 b = zero_bytes(w[k] ^ 0x5C5C5C5Cu) | zero_bytes(w[k] & 0xE0E0E0E0u);
+            qm |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
+            bm |= (((b >> 7) & 1u) | ((b >> 14) & 2u) | ((b >> 21) & 4u) | ((b >> 28) & 8u)) << (4 * k);
+        }
+        const u32 lo = q < s ? 0xFFFFu << (s - q) : 0xFFFFu;
+        const u32 hi = q + 16 > e - 1 ? (1u << (e - 1 - q)) - 1u : 0xFFFFu;   // (the line's '\n' is no byte of it)
+        qm &= lo & hi;
+        bad |= bm & lo & hi;
+        while (qm) {   // the owner's walk takes the quotes in order
+            acc = acc * 31u + (u32)(q + __builtin_ctz(qm));
+            ++nq;
+            qm &= qm - 1u;
+        }
+    }
+    return acc ^ (nq << 24) ^ bad;
+}
+
 // FAST (the flat-first instantiation only): the whitespace skips' first step outside their
 // loops, and the id values (ad / user / page) checked as 36-byte UUIDs in one step before
 // the string scan -- the same decisions, fewer divergent loop trips.
