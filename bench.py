@@ -94,6 +94,10 @@ def parse_args(argv=None):
                     help="extras at N > 1: events per GPU of the configs[2]-table leg (1M campaigns / 10M ads)")
     ap.add_argument("--layout-fixed", action="store_true",
                     help="A/B: no first-line layout sampling of the device batches (YSB_F_LAYOUT_FIXED)")
+    ap.add_argument("--rehearse-host-collectives", action="store_true",
+                    help="N > 1 on a box with fewer GPUs: the ranks share the visible GPUs and exchange over gloo "
+                         "on host memory (ysb_group_init_host) instead of RCCL -- a rehearsal of the N-rank flow, "
+                         "not a measurement")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and set up torch.distributed, then stop before any GPU call")
     ap.add_argument("--extras-out", default=os.path.join(ROOT, "gpurun_out", "bench_extras.json"),
@@ -754,8 +758,7 @@ def config3_ranks(args, d):
             ctx.close()
         raise RuntimeError("; ".join(errs))
     try:
-        uid = d.bcast_bytes(YsbContext.group_unique_id() if d.rank == 0 else None)
-        ctx.group_init(d.rank, d.world, uid)
+        group_init(ctx, d, args)
         load_s = time.perf_counter() - t
         sub = [(d_b, nb, d_o, n) for (_, n, d_b, nb, d_o) in segs]
 
@@ -888,6 +891,19 @@ def live_traffic(args, kernel):
             "hbm_bytes_per_launch": int(rd + wr)}
 
 
+def group_init(ctx, d, args):
+    """The keyBy exchange's group: RCCL over the node's GPUs (ysb_group_init), or -- the
+    --rehearse-host-collectives rehearsal of the N-rank flow on a box with fewer GPUs, where
+    RCCL refuses two ranks on one device -- the same exchange over the ranks' gloo
+    collectives on host memory (ysb_group_init_host)."""
+    if args.rehearse_host_collectives:
+        ctx.group_init_host(d.rank, d.world, d.dist)
+        return
+    from ysb_amd import YsbContext
+    uid = d.bcast_bytes(YsbContext.group_unique_id() if d.rank == 0 else None)
+    ctx.group_init(d.rank, d.world, uid)
+
+
 def exchange_overlap(x):
     """Per step: the reduce-scatter's own time (rs), the part of it the compute stream waited
     for at the unpack (exposed) and the rest, which ran beside the queued launches (hidden)."""
@@ -981,8 +997,7 @@ def main():
     # join table; the post-exchange check proves nothing is missed
     ctx.load_ad_map(aids, camp, shard=(d.rank, d.world) if d.world > 1 else None)
     if d.world > 1:
-        uid = d.bcast_bytes(YsbContext.group_unique_id() if d.rank == 0 else None)
-        ctx.group_init(d.rank, d.world, uid)
+        group_init(ctx, d, args)
 
     # ---- resident input: generated straight into HBM ----------------------------------
     t_gen = time.perf_counter()
@@ -1091,7 +1106,10 @@ def main():
                        "event_time_rate_per_s": args.rate, "batches_per_step": len(segs),
                        "launches_per_step": launches_per_step,
                        "json_bytes_per_event": round(total_bytes / args.events, 3),
-                       "parallelism": "ad_id-hash shards x%d, RCCL reduce-scatter" % d.world if d.world > 1
+                       "parallelism": ("ad_id-hash shards x%d, %s" % (d.world, "REHEARSAL: gloo host collectives, ranks "
+                                                                     "sharing the box's GPUs (not a measurement)"
+                                                                     if args.rehearse_host_collectives else
+                                                                     "RCCL reduce-scatter")) if d.world > 1
                        else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
