@@ -116,6 +116,7 @@ struct ysb_ctx {
     int split_place = 0;                        // raw split on: 0 the copy stream, 1 s_split, 2 s_comp (A/B)
     int h2d_wg = 1;                             // copy-kernel workgroups per CU (A/B)
     bool h2d_prio = false;                      // copy kernel at raised wave priority (A/B)
+    int h2d_grid = 0;                           // copy-kernel workgroups (A/B; 0: one per CU)
     ysb_rebase raw_rebase[2]{};
     CuckooSeed cseed{};
     bool ctable_partial = false;

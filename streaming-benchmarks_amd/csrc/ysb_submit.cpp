@@ -612,7 +612,7 @@ static int ensure_slots(ysb_ctx* c) {
 // YSB_F_H2D_SDMA.
 static hipError_t h2d(ysb_ctx* c, void* dst, const void* dsrc, const void* hsrc, u64 bytes) {
     if (c->cfg.flags & YSB_F_H2D_SDMA) return hipMemcpyAsync(dst, hsrc, bytes, hipMemcpyHostToDevice, c->s_copy);
-    launch_h2d_copy(dst, dsrc, bytes, c->cus * c->h2d_wg, c->s_copy, c->h2d_prio);
+    launch_h2d_copy(dst, dsrc, bytes, c->h2d_grid ? c->h2d_grid : c->cus * c->h2d_wg, c->s_copy, c->h2d_prio);
     return hipGetLastError();
 }
 
@@ -695,6 +695,7 @@ static int ensure_raw(ysb_ctx* c) {
     if (const char* e = getenv("YSB_SPLIT_STREAM")) c->split_place = std::atoi(e);
     if (const char* e = getenv("YSB_H2D_WG")) c->h2d_wg = std::max(1, std::atoi(e));
     if (const char* e = getenv("YSB_H2D_PRIO")) c->h2d_prio = std::atoi(e) != 0;
+    if (const char* e = getenv("YSB_H2D_GRID")) c->h2d_grid = std::max(0, std::atoi(e));
     const u64 words = split_chunks(c->cfg.max_batch_bytes) + 1;
     if (c->split_chunk_words < words) {
         hipFree(c->d_split_chunk);
