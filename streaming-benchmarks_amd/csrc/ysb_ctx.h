@@ -113,10 +113,10 @@ struct ysb_ctx {
     i64 rebase_base = 0;
     u32 rebase_kmax = 0;                        // the largest bucket index in it
     bool raw_rebase_on[2] = {false, false};
-    int split_place = 0;                        // raw split on: 0 the copy stream, 1 s_split, 2 s_comp (A/B)
+    int split_place = 1;                        // raw split on: 1 s_split (default), 0 the copy stream, 2 s_comp (A/B)
     int h2d_wg = 1;                             // copy-kernel workgroups per CU (A/B)
     bool h2d_prio = false;                      // copy kernel at raised wave priority (A/B)
-    int h2d_grid = 0;                           // copy-kernel workgroups (A/B; 0: one per CU)
+    int h2d_grid = 32;                          // copy-kernel workgroups (0: one per CU; YSB_H2D_GRID A/B)
     ysb_rebase raw_rebase[2]{};
     CuckooSeed cseed{};
     bool ctable_partial = false;

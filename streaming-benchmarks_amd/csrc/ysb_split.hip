@@ -60,7 +60,9 @@ __global__ __launch_bounds__(H2D_TPB) void h2d_copy_kernel(const h2d_v4* __restr
 void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t s, bool prio) {
     const u64 vecs = (bytes + 15) / 16;
     if (!vecs) return;
-    // one workgroup per CU (4 waves): ~4 MiB in flight, far above PCIe's bandwidth x latency
+    // `cus` workgroups: the caller's choice (32: 512 KiB in flight, well above PCIe's bandwidth
+    // x latency, and few enough slow PCIe requests that HBM work beside the copy is not starved;
+    // ysb_submit.cpp enqueue_raw)
     const u64 grid = std::max<u64>(1, std::min<u64>((u64)cus, (vecs + H2D_TPB - 1) / H2D_TPB));
     if (prio)
         hipLaunchKernelGGL(h2d_copy_kernel<true>, dim3((unsigned)grid), dim3(H2D_TPB), 0, s,

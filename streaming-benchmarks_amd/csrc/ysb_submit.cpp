@@ -792,14 +792,16 @@ static int enqueue_raw(ysb_ctx* c, int slot, const u8* hsrc, const u8* dsrc, u64
     c->raw_layout[slot] = -1;
     if (layout_sampling(c) && nbytes)
         c->raw_layout[slot] = hinted_layout(c, sniff_raw(c, hsrc, nbytes, &c->raw_learn[slot]));
-    // H2D once the slot's previous kernel has run.  The split: behind the DMA engine's copy on a
-    // stream of its own (the next slot's copy queues right behind this one); behind the copy
-    // kernel on the copy stream itself, so it runs right after its own copy and the next copy
-    // follows it.  Same-box A/B of the native runner with the copy kernel (gpurun_out/r5w, r5x,
-    // four alternations each): on the copy stream 186-203 M events/s, on a stream of its own
-    // 162-181, on the compute stream 188-193 (the DMA engine 209-213)
+    // H2D once the slot's previous kernel has run.  The split on a stream of its own behind its
+    // copy, so the next slot's copy queues right behind this one.  Round 5 kept it on the copy
+    // stream: beside a copy kernel of one workgroup per CU the split was starved (its 32 us
+    // count took 2.7 ms, and the slot's scan waited behind it).  The copy kernel's grid is now 32
+    // workgroups (h2d_grid): still far more bytes in flight than PCIe's bandwidth x latency, and
+    // the HBM work beside it (split, scan) no longer queues behind its slow requests.  Same-box
+    // A/B (gpurun_out/r6r, r6s): raw host-staged 210 -> 214-218 M events/s, the raw streaming
+    // replay 197 -> 206-209 (copy queue busy 0.958 -> 0.986).  (YSB_SPLIT_STREAM: 0 the copy
+    // stream, 2 the compute stream -- A/B only.)
     const bool sdma = (c->cfg.flags & YSB_F_H2D_SDMA) != 0u;
-    // (YSB_SPLIT_STREAM, A/B only: 1 a stream of its own, 2 the compute stream)
     hipStream_t ss = sdma || c->split_place == 1 ? c->s_split : c->split_place == 2 ? c->s_comp : c->s_copy;
     HIPCHK(c, wait_unless_done(c->s_copy, c->ev_kdone[slot]));
     hipEvent_t* ce = nullptr;
