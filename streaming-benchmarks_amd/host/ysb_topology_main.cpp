@@ -385,6 +385,11 @@ int run_stream(const Args& a) {
 
 int main(int argc, char** argv) {
     const Args a = parse(argc, argv);
+    if (ysb_abi_version() != YSB_ABI_VERSION || ysb_exchange_info_size() != sizeof(ysb_exchange_info)) {
+        std::fprintf(stderr, "ysb_topology: libysb_hip.so has ABI %d, this runner was built for ABI %d: rebuild\n",
+                     ysb_abi_version(), YSB_ABI_VERSION);
+        return 2;
+    }
     try {
         if (a.self_check) {
             std::printf("%s\n", StreamingJob::replaySelfCheck(a.so, {0, 1, 2, 7, 1000}).c_str());
