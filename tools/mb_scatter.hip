@@ -114,6 +114,25 @@ __global__ __launch_bounds__(64) void k(const unsigned char* __restrict__ buf, u
 #pragma unroll
             for (int q = 0; q < 8; ++q) acc += v[q].x ^ v[q].w;
         }
+        if (MODE >= 14 && MODE <= 17 && act) {   // 48-B probes of one 64-B slot, other cache policies
+            const uint4* p = probe_tab + 4 * (h & probe_mask);
+            uint4 a, b, c;
+            if constexpr (MODE == 14) {   // nontemporal (global_load ... nt)
+                typedef u32 v4u __attribute__((ext_vector_type(4)));
+                const v4u* pv = reinterpret_cast<const v4u*>(p);
+                const v4u x = __builtin_nontemporal_load(pv), y = __builtin_nontemporal_load(pv + 1),
+                          z = __builtin_nontemporal_load(pv + 2);
+                a = make_uint4(x[0], x[1], x[2], x[3]); b = make_uint4(y[0], y[1], y[2], y[3]); c = make_uint4(z[0], z[1], z[2], z[3]);
+            } else {                      // buffer loads with cache-policy bits sc0 / sc1 / sc0|sc1
+                constexpr int AUX = MODE == 15 ? 1 : MODE == 16 ? 2 : 3;
+                const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(p), 0, 64, 0x00020000);
+                const auto x = __builtin_amdgcn_raw_buffer_load_b128(rb, 0, 0, AUX);
+                const auto y = __builtin_amdgcn_raw_buffer_load_b128(rb, 16, 0, AUX);
+                const auto z = __builtin_amdgcn_raw_buffer_load_b128(rb, 32, 0, AUX);
+                a = make_uint4(x[0], x[1], x[2], x[3]); b = make_uint4(y[0], y[1], y[2], y[3]); c = make_uint4(z[0], z[1], z[2], z[3]);
+            }
+            acc += a.x ^ b.y ^ c.z;
+        }
         if (MODE == 12 && act) {   // 64-B probe: 4 x 16 B of one 64-B slot
             const uint4* p = probe_tab + 4 * (h & probe_mask);
             const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
@@ -184,7 +203,8 @@ int main(int argc, char** argv) {
                            "u64 atomics, 16 MiB", "48-B probes, same tile", "48-B probes, next tile",
                            "48-B probes as one 63-lane load", "32-B probes (2 loads)",
                            "128-B bucket probes (8 loads)", "48-B probes + 1/13 dependent 2nd",
-                           "64-B probes (4 loads)"};
+                           "64-B probes (4 loads)", "(table sweep)", "48-B probes, nontemporal",
+                           "48-B probes, buffer sc0", "48-B probes, buffer sc1", "48-B probes, buffer sc0|sc1"};
     int only = argc > 1 ? atoi(argv[1]) : -1;
     if (only == 13) {   // 128-B bucket probes beside the stream vs table size (Infinity Cache residency)
         for (u64 mib : {64ull, 128ull, 192ull, 224ull, 256ull, 320ull, 512ull, 1024ull, 4096ull}) {
@@ -219,9 +239,11 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    for (int mode = 0; mode < 13; ++mode) {
+    for (int mode = 0; mode < 18; ++mode) {
+        if (mode == 13) continue;   // (13: the table-size sweep above)
         if (only >= 0 && mode != only && !(only == 100 && (mode == 0 || mode == 6 || mode == 8 || mode == 9)) &&
-            !(only == 101 && (mode == 0 || mode == 6 || mode >= 10))) continue;
+            !(only == 101 && (mode == 0 || mode == 6 || mode >= 10)) &&
+            !(only == 102 && (mode == 0 || mode == 6 || mode == 10 || mode == 12 || mode >= 14))) continue;
         float best = 1e9;
         for (int rep = 0; rep < 6; ++rep) {
             hipEventRecord(a);
@@ -230,7 +252,8 @@ int main(int argc, char** argv) {
                 case 0: L(0); break; case 1: L(1); break; case 2: L(2); break; case 3: L(3); break;
                 case 4: L(4); break; case 5: L(5); break; case 6: L(6); break; case 7: L(7); break;
                 case 8: L(8); break; case 9: L(9); break; case 10: L(10); break; case 11: L(11); break;
-                case 12: L(12); break;
+                case 12: L(12); break; case 14: L(14); break; case 15: L(15); break; case 16: L(16); break;
+                case 17: L(17); break;
             }
             hipEventRecord(b);
             hipEventSynchronize(b);
