@@ -495,7 +495,9 @@ def extra_native_runner(args, device, staged):
     in the page cache, read --runner-repeat times: raw lines with the split on the GPU (the
     default) and host-split offsets, against the generator truth; vs_host_staged = its stream
     rate / the host-staged raw path's (the H2D-bound rate).  gpu_split_dma_engine: the same
-    with the slots' H2D by the DMA engine (--h2d-sdma) instead of the copy kernel."""
+    with the slots' H2D by the DMA engine (--h2d-sdma) instead of the copy kernel.
+    gpu_split_mapped: --io mapped, the file's page-cache mapping registered and every batch read
+    in place by the copy kernel (no host copy into a pinned slot)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_dropin
     import tempfile
@@ -506,15 +508,17 @@ def extra_native_runner(args, device, staged):
              "host_split": bench_dropin.native_runner(device, args.runner_file_events, args.runner_repeat,
                                                      host_split=True, workdir=path),
              "gpu_split_dma_engine": bench_dropin.native_runner(device, args.runner_file_events, args.runner_repeat,
-                                                               workdir=path, h2d_sdma=True)}
+                                                               workdir=path, h2d_sdma=True),
+             "gpu_split_mapped": bench_dropin.native_runner(device, args.runner_file_events, args.runner_repeat,
+                                                           workdir=path, io="mapped")}
     finally:
         import shutil
         shutil.rmtree(path, ignore_errors=True)
     if staged and "raw" in staged:
         r["vs_host_staged"] = round(r["gpu_split"]["stream_events_per_s"] / staged["raw"]["events_per_s"], 4)
-    log("extras: native_runner %.3f G events/s (host split %.3f, DMA engine %.3f)"
+    log("extras: native_runner %.3f G events/s (host split %.3f, DMA engine %.3f, mapped %.3f)"
         % (r["gpu_split"]["stream_events_per_s"] / 1e9, r["host_split"]["stream_events_per_s"] / 1e9,
-           r["gpu_split_dma_engine"]["stream_events_per_s"] / 1e9))
+           r["gpu_split_dma_engine"]["stream_events_per_s"] / 1e9, r["gpu_split_mapped"]["stream_events_per_s"] / 1e9))
     return r
 
 

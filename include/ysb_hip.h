@@ -296,8 +296,10 @@ typedef struct ysb_rebase {
     int64_t  lead_shift;   /* added to every line's leading nine digits (cycle k of a cycle of
                               c ms: k * c / 10000); the result must lie in [0, 10^9)         */
 } ysb_rebase;
-/* ysb_submit_raw of a batch that lies in a registered range: `bytes` 16-byte aligned, and the
- * range holds round_up(nbytes, 16) bytes from it.  The copy kernel (or, YSB_F_H2D_SDMA, the DMA
+/* ysb_submit_raw of a batch that lies in a registered range: at any byte address (a file
+ * mapping's batch starts where the previous one's last line ended), the range holding the batch
+ * widened to 16-byte boundaries on both sides (the copy reads whole 16-byte vectors).  The copy
+ * kernel (or, YSB_F_H2D_SDMA, the DMA
  * engine) reads it in place into the slot's device buffer, the GPU splits the lines, and with
  * rebase != NULL every line's leading event_time digits are rewritten from the rebase table
  * before the scan (YSB_ERR_ARG at the launch if the batch has more lines than the table holds

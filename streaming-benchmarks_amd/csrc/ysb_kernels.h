@@ -223,6 +223,9 @@ void launch_checksum(const unsigned long long* table, u32 rows, u32 W, i64 ring_
 u64 split_chunks(u64 nbytes);
 // the slots' host -> device copy by a kernel (ysb_split.hip): src a device-visible pinned host pointer
 void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t s, bool prio = false);
+// the same from a device-visible host address at any byte alignment (reads up to 31 bytes
+// past src + bytes, from the 16-byte boundary below src)
+void launch_h2d_copy_unaligned(void* dst, const void* src, u64 bytes, int wgs, hipStream_t s);
 hipError_t launch_split_lines(const u8* b, u64 nbytes, u32* chunk, u32* off, u64 cap, unsigned long long* d_n,
                               hipStream_t s);
 // The replay's event-time rebasing (ysb_split.hip, ysb_submit_raw_mapped): for the first

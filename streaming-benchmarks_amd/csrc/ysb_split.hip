@@ -72,6 +72,86 @@ void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t
                            static_cast<const h2d_v4*>(src), static_cast<h2d_v4*>(dst), vecs);
 }
 
+// The same from a source at any byte address (a file mapping's batch starts where the previous
+// batch's last line ended): output vector i = bytes [16 i + sh, 16 i + sh + 16) of the 16-byte
+// aligned `src`, whose first nsrc vectors are read (to the 16-byte boundary at or above the
+// batch's end, never further: the same bound the aligned copy keeps).  A wave copies H2D_UNROLL
+// x 64 consecutive vectors per step (4 KB, all loads in flight at once; waves a grid stride
+// apart): each lane loads one source vector, the next one is its right neighbour's (a lane
+// shuffle) or, at lane 63, the next slice's lane 0's (a lane read); only the step's very last
+// vector needs a load of its own (+1/256 of the loads: a one-per-lane-63 extra load, measured
+// first, cost ~6 % of the PCIe rate, profiles/AB_LOG.md).
+// bytes [4 Q + r, 4 Q + r + 16) of the 32 bytes a:b (Q = shift / 4 a template argument: the
+// word selection costs nothing, the byte shift is one v_alignbyte per word)
+template <int Q>
+__device__ __forceinline__ h2d_v4 shift_bytes(const h2d_v4& a, const h2d_v4& b, u32 r) {
+    const u32 w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    h2d_v4 o;
+    o.x = __builtin_amdgcn_alignbyte(w[Q + 1], w[Q + 0], r);
+    o.y = __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], r);
+    o.z = __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], r);
+    o.w = __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], r);
+    return o;
+}
+
+__device__ __forceinline__ h2d_v4 lane_down(const h2d_v4& v) {
+    return h2d_v4{(u32)__shfl_down((int)v.x, 1), (u32)__shfl_down((int)v.y, 1), (u32)__shfl_down((int)v.z, 1),
+                  (u32)__shfl_down((int)v.w, 1)};
+}
+
+__device__ __forceinline__ h2d_v4 lane0(const h2d_v4& v) {
+    return h2d_v4{(u32)__builtin_amdgcn_readlane((int)v.x, 0), (u32)__builtin_amdgcn_readlane((int)v.y, 0),
+                  (u32)__builtin_amdgcn_readlane((int)v.z, 0), (u32)__builtin_amdgcn_readlane((int)v.w, 0)};
+}
+
+template <int Q>
+__global__ __launch_bounds__(H2D_TPB) void h2d_copy_unaligned_kernel(const h2d_v4* __restrict__ src,
+                                                                     h2d_v4* __restrict__ dst, u64 vecs, u64 nsrc,
+                                                                     u32 r) {
+    constexpr u64 STEP = 64 * H2D_UNROLL;   // vectors a wave copies per step
+    const u32 lane = threadIdx.x & 63u;
+    const u64 waves = (u64)gridDim.x * (H2D_TPB / 64);
+    const u64 wave = (u64)blockIdx.x * (H2D_TPB / 64) + (threadIdx.x >> 6);
+    for (u64 b = wave * STEP; b < vecs; b += waves * STEP) {   // wave-uniform
+        h2d_v4 a[H2D_UNROLL], tail = h2d_v4{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < H2D_UNROLL; ++u) {
+            const u64 i = b + u * 64 + lane;
+            a[u] = i < nsrc ? __builtin_nontemporal_load(src + i) : h2d_v4{0, 0, 0, 0};
+        }
+        if (lane == 63u && b + STEP < nsrc) tail = __builtin_nontemporal_load(src + b + STEP);
+#pragma unroll
+        for (int u = 0; u < H2D_UNROLL; ++u) {
+            const u64 i = b + u * 64 + lane;
+            // both cross-lane reads in every lane (a ?: evaluates one operand only: the
+            // shuffle must not run under lane != 63, or lane 62 reads an inactive lane's 0)
+            const h2d_v4 down = lane_down(a[u]);
+            const h2d_v4 nx = u + 1 < H2D_UNROLL ? lane0(a[u + 1 < H2D_UNROLL ? u + 1 : u]) : tail;
+            h2d_v4 n = down;
+            if (lane == 63u) n = nx;
+            if (i < vecs) __builtin_nontemporal_store(shift_bytes<Q>(a[u], n, r), dst + i);
+        }
+    }
+}
+
+void launch_h2d_copy_unaligned(void* dst, const void* src, u64 bytes, int wgs, hipStream_t s) {
+    const u64 vecs = (bytes + 15) / 16;
+    if (!vecs) return;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+    const u64 nsrc = ((a & 15) + bytes + 15) / 16;
+    const u64 per_wg = (u64)(H2D_TPB / 64) * 64 * H2D_UNROLL;
+    const u64 grid = std::max<u64>(1, std::min<u64>((u64)wgs, (vecs + per_wg - 1) / per_wg));
+    const h2d_v4* s16 = reinterpret_cast<const h2d_v4*>(a & ~(uintptr_t)15);
+    h2d_v4* d16 = static_cast<h2d_v4*>(dst);
+    const u32 r = (u32)(a & 3);
+    switch ((a >> 2) & 3) {
+    case 0: hipLaunchKernelGGL(h2d_copy_unaligned_kernel<0>, dim3((unsigned)grid), dim3(H2D_TPB), 0, s, s16, d16, vecs, nsrc, r); break;
+    case 1: hipLaunchKernelGGL(h2d_copy_unaligned_kernel<1>, dim3((unsigned)grid), dim3(H2D_TPB), 0, s, s16, d16, vecs, nsrc, r); break;
+    case 2: hipLaunchKernelGGL(h2d_copy_unaligned_kernel<2>, dim3((unsigned)grid), dim3(H2D_TPB), 0, s, s16, d16, vecs, nsrc, r); break;
+    default: hipLaunchKernelGGL(h2d_copy_unaligned_kernel<3>, dim3((unsigned)grid), dim3(H2D_TPB), 0, s, s16, d16, vecs, nsrc, r); break;
+    }
+}
+
 u64 split_chunks(u64 nbytes) { return (nbytes + SPLIT_CHUNK - 1) / SPLIT_CHUNK; }
 
 // high bit of every zero byte of x (exact, no carries between bytes)

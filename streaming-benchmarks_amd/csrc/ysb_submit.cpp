@@ -612,7 +612,9 @@ static int ensure_slots(ysb_ctx* c) {
 // YSB_F_H2D_SDMA.
 static hipError_t h2d(ysb_ctx* c, void* dst, const void* dsrc, const void* hsrc, u64 bytes) {
     if (c->cfg.flags & YSB_F_H2D_SDMA) return hipMemcpyAsync(dst, hsrc, bytes, hipMemcpyHostToDevice, c->s_copy);
-    launch_h2d_copy(dst, dsrc, bytes, c->h2d_grid ? c->h2d_grid : c->cus * c->h2d_wg, c->s_copy, c->h2d_prio);
+    const int wgs = c->h2d_grid ? c->h2d_grid : c->cus * c->h2d_wg;
+    if (reinterpret_cast<uintptr_t>(dsrc) & 15) launch_h2d_copy_unaligned(dst, dsrc, bytes, wgs, c->s_copy);
+    else launch_h2d_copy(dst, dsrc, bytes, wgs, c->s_copy, c->h2d_prio);
     return hipGetLastError();
 }
 
@@ -865,6 +867,10 @@ int ysb_host_register(ysb_ctx* c, void* host, uint64_t bytes) {
         hipHostUnregister(host);
         return fail(c, YSB_ERR_HIP, "hipHostGetDevicePointer of a registered range failed");
     }
+    if ((reinterpret_cast<uintptr_t>(d) ^ a) & 15) {   // the copy's 16-byte widening assumes it
+        hipHostUnregister(host);
+        return fail(c, YSB_ERR_HIP, "the device alias of a registered range is not 16-byte congruent to it");
+    }
     c->host_ranges[a] = {bytes, static_cast<u8*>(d)};
     return YSB_OK;
 }
@@ -903,19 +909,26 @@ int ysb_rebase_table(ysb_ctx* c, const uint32_t* time_at, uint64_t n_lines, int6
     return YSB_OK;
 }
 
+// The device alias of a mapped batch, or NULL when the batch widened to 16-byte boundaries on
+// both sides (what the copy reads: launch_h2d_copy / launch_h2d_copy_unaligned) is not inside
+// one registered range.
+static const u8* mapped_src(const ysb_ctx* c, const uint8_t* bytes, u64 nbytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(bytes);
+    auto it = c->host_ranges.upper_bound(a);
+    if (it == c->host_ranges.begin()) return nullptr;
+    --it;
+    const uintptr_t lo = a & ~uintptr_t(15), hi = (a + nbytes + 15) & ~uintptr_t(15);
+    if (lo < it->first || hi > it->first + it->second.bytes) return nullptr;
+    return it->second.dptr + (a - it->first);
+}
+
 int ysb_submit_raw_mapped(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbytes, const ysb_rebase* rb) {
     if (!c) return YSB_ERR_ARG;
     int rc = raw_args(c, slot, bytes, nbytes);
     if (rc) return rc;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(bytes);
-    if (a & 15) return fail(c, YSB_ERR_ARG, "a mapped batch must be 16-byte aligned");
-    const u8* dsrc = nullptr;
-    auto it = c->host_ranges.upper_bound(a);
-    if (it != c->host_ranges.begin()) {
-        --it;
-        if (a + ((nbytes + 15) & ~15ull) <= it->first + it->second.bytes) dsrc = it->second.dptr + (a - it->first);
-    }
-    if (nbytes && !dsrc) return fail(c, YSB_ERR_ARG, "the batch (rounded up to 16 B) is not inside a registered range");
+    const u8* dsrc = mapped_src(c, bytes, nbytes);
+    if (nbytes && !dsrc)
+        return fail(c, YSB_ERR_ARG, "the batch (widened to 16-byte boundaries) is not inside a registered range");
     if (rb) {
         if (!c->d_rebase) return fail(c, YSB_ERR_STATE, "no rebase table (ysb_rebase_table)");
         if (rb->first_line >= c->rebase_n) return fail(c, YSB_ERR_ARG, "first_line beyond the rebase table");
@@ -942,15 +955,9 @@ int ysb_submit_mapped(ysb_ctx* c, int slot, const uint8_t* bytes, uint64_t nbyte
     if (rc) return rc;
     if (n > 0x7FFFFFFFull) return fail(c, YSB_ERR_CAPACITY, "at most 2^31-1 events per batch");
     if (n && !d_line_off) return fail(c, YSB_ERR_ARG, "NULL line offsets");
-    const uintptr_t a = reinterpret_cast<uintptr_t>(bytes);
-    if (a & 15) return fail(c, YSB_ERR_ARG, "a mapped batch must be 16-byte aligned");
-    const u8* dsrc = nullptr;
-    auto it = c->host_ranges.upper_bound(a);
-    if (it != c->host_ranges.begin()) {
-        --it;
-        if (a + ((nbytes + 15) & ~15ull) <= it->first + it->second.bytes) dsrc = it->second.dptr + (a - it->first);
-    }
-    if (nbytes && !dsrc) return fail(c, YSB_ERR_ARG, "the batch (rounded up to 16 B) is not inside a registered range");
+    const u8* dsrc = mapped_src(c, bytes, nbytes);
+    if (nbytes && !dsrc)
+        return fail(c, YSB_ERR_ARG, "the batch (widened to 16-byte boundaries) is not inside a registered range");
     if (rb) {
         if (!c->d_rebase) return fail(c, YSB_ERR_STATE, "no rebase table (ysb_rebase_table)");
         if (rb->first_line > c->rebase_n || n > c->rebase_n - rb->first_line)

@@ -346,6 +346,27 @@ uint64_t FileBasedDataSource::fillRaw(uint8_t* buf, uint64_t cap) {
     return end;
 }
 
+uint64_t FileBasedDataSource::mappingBytes() const {
+    const uint64_t page = (uint64_t)::sysconf(_SC_PAGESIZE);
+    return map_ ? (size_ + page - 1) / page * page : 0;
+}
+
+uint64_t FileBasedDataSource::nextMapped(uint64_t cap, const uint8_t** p) {
+    if (!map_) throw std::runtime_error("nextMapped needs the file mapped (--io mmap)");
+    *p = map_ + pos_;
+    if (!cap || pos_ >= size_) return 0;
+    const uint64_t have = std::min(cap, size_ - pos_);
+    uint64_t end = have;
+    if (pos_ + have < size_) {   // not the file's last bytes: up to the last complete line
+        const uint64_t tail = std::min<uint64_t>(have, 1u << 16);
+        const bool anyCr = std::memchr(map_ + pos_ + have - tail, '\r', tail) != nullptr;
+        end = completeEnd(map_ + pos_, have, anyCr);
+    }
+    pos_ += end;
+    bytes_ += end;
+    return end;
+}
+
 uint64_t FileBasedDataSource::fill(uint8_t* buf, uint64_t cap, uint32_t* off, uint64_t maxLines, uint64_t* nbytes) {
     *nbytes = 0;
     if (!maxLines || !cap) return 0;
@@ -460,6 +481,28 @@ uint64_t GpuAdCampaignOperator::fillFrom(FileBasedDataSource& src) {
     fillBytes_ += nb;
     fillEvents_ += n;
     return n;
+}
+
+void GpuAdCampaignOperator::registerSource(FileBasedDataSource& src) {
+    if (!src.mapping()) throw std::runtime_error("--io mapped needs the events file mapped");
+    check(ysb_host_register(ctx_, const_cast<uint8_t*>(src.mapping()), src.mappingBytes()), "ysb_host_register");
+}
+
+// FileBasedDataSource.run's batch without the copy into a slot: the lines stay in the page
+// cache, the copy kernel reads them over PCIe into the slot's device buffer (any byte alignment:
+// launch_h2d_copy_unaligned) and the GPU splits them.
+uint64_t GpuAdCampaignOperator::submitMapped(FileBasedDataSource& src) {
+    const uint8_t* p = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t nb = src.nextMapped(o_.batchBytes, &p);
+    fillS_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!nb) return 0;
+    check(ysb_submit_raw_mapped(ctx_, cur_, p, nb, nullptr), "ysb_submit_raw_mapped");
+    cur_ ^= 1;
+    const auto t1 = std::chrono::steady_clock::now();
+    check(ysb_wait(ctx_, cur_), "ysb_wait");   // at most two batches in flight
+    waitS_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    return nb;
 }
 
 void GpuAdCampaignOperator::submit() {

@@ -99,6 +99,13 @@ public:
     // The same without the line split: buf receives whole lines, the return value is their
     // bytes (0 = end of file); the GPU finds the line starts (ysb_submit_raw).
     uint64_t fillRaw(uint8_t* buf, uint64_t cap);
+    // Zero-copy (mmap mode only): the next whole lines, at most cap bytes, where they lie in the
+    // mapping -- *p points into it, the return value is their bytes (0 = end of file).  The
+    // GPU reads them in place (ysb_submit_raw_mapped) once the mapping is registered.
+    uint64_t nextMapped(uint64_t cap, const uint8_t** p);
+    // The mapping (NULL without mmap) and its registrable length (whole pages).
+    const uint8_t* mapping() const { return map_; }
+    uint64_t mappingBytes() const;
     // Back to the file's start (a replay source read again).
     void rewind();
     uint64_t linesRead() const { return lines_; }
@@ -138,6 +145,7 @@ public:
         bool requireIp = false;             // Storm/Spark's 7-field deserializer
         bool gpuSplit = true;               // fillFromRaw + ysb_submit_raw: line starts found on the GPU
         bool h2dSdma = false;               // YSB_F_H2D_SDMA: the slot's H2D by the DMA engine (default: a copy kernel)
+        bool mappedIo = false;              // the source's mapping registered, batches read in place (--io mapped)
     };
     GpuAdCampaignOperator(const AdCampaignMap& map, const Options& o);
     ~GpuAdCampaignOperator();
@@ -148,6 +156,8 @@ public:
     void flatMap(const char* line, uint64_t len);          // one record
     uint64_t fillFrom(FileBasedDataSource& src);           // a slot's worth of records, zero-copy
     uint64_t fillFromRaw(FileBasedDataSource& src);        // the same as raw lines (bytes returned)
+    void registerSource(FileBasedDataSource& src);         // pin + map the source's mapping (mappedIo)
+    uint64_t submitMapped(FileBasedDataSource& src);       // the next whole lines, read in place: bytes
     void submit();                                         // hand the open slot to the GPU
     std::vector<WindowDelta> flushWindows();               // CampaignProcessorCommon.flushWindows (:91-98)
     void close();                                          // RichFlatMapFunction.close

@@ -42,6 +42,10 @@ struct Args {
     long long repeat = 1;
     unsigned io_threads = 0;
     bool io_mmap = true;
+    // --io mapped: the mapping registered, batches read in place by the GPU; auto (the default):
+    // that whenever the GPU splits the lines and the slots' copy is the copy kernel's, with
+    // slot copies out of the mapping if the registration is refused
+    std::string io = "auto";
     bool h2d_sdma = false;
     // streaming mode (configs[4]): --stream plus its options (ysb_stream.hpp)
     bool stream = false;
@@ -57,7 +61,8 @@ void usage() {
                  "usage: ysb_topology --confPath PATH [--device N] [--sink none|csv:FILE|redis[:HOST[:PORT]]]\n"
                  "       [--format json|tbl] [--flush-ms MS] [--batch-mb MB | --batch-bytes B] [--batch-events N]\n"
                  "       [--window-ring W] [--require-ip] [--dry-run] [--print-config] [--replay-rows CSV]\n"
-                 "       [--host-split] [--repeat K] [--io-threads T] [--io mmap|pread] [--h2d-sdma]\n"
+                 "       [--host-split] [--repeat K] [--io-threads T] [--io auto|mapped|mmap|pread]\n"
+                 "       [--h2d-sdma]\n"
                  "   or: ysb_topology --stream [--sink none|csv:FILE|redis[:HOST[:PORT]]] [--shards N] [--device D]\n"
                  "       [--seed S] [--campaigns C] [--ads-per-campaign A] [--event-rate E] [--speedup F]\n"
                  "       [--cycle-ms MS] [--flush-ms MS] [--batch-ms MS] [--ooo-ms MS] [--seconds S]\n"
@@ -90,7 +95,12 @@ Args parse(int argc, char** argv) {
         else if (k == "--host-split") a.host_split = true;
         else if (k == "--repeat") a.repeat = std::max(1ll, std::atoll(val().c_str()));
         else if (k == "--io-threads") a.io_threads = (unsigned)std::atoll(val().c_str());
-        else if (k == "--io") a.io_mmap = val() != "pread";
+        else if (k == "--io") {
+            const std::string m = val();
+            if (m != "mmap" && m != "pread" && m != "mapped" && m != "auto") { usage(); std::exit(2); }
+            a.io_mmap = m != "pread";
+            a.io = m;
+        }
         else if (k == "--h2d-sdma") a.h2d_sdma = true;
         else if (k == "--stream") a.stream = true;
         else if (k == "--stream-self-check") { a.stream = true; a.self_check = true; }
@@ -180,9 +190,29 @@ int run(const Args& a) {
     o.requireIp = a.require_ip;
     o.gpuSplit = !a.host_split;
     o.h2dSdma = a.h2d_sdma;
+    o.mappedIo = a.io == "mapped" || (a.io == "auto" && o.gpuSplit && !o.h2dSdma);
+    if (a.io == "mapped" && !o.gpuSplit) {
+        std::fprintf(stderr, "--io mapped reads raw lines in place: not with --host-split\n");
+        return 2;
+    }
 
     FileBasedDataSource src(events, a.io_threads, a.io_mmap);
     const double t0 = now_s();
+    if (a.dry && a.io == "mapped") {   // the mapped source's ranges alone: whole lines, every byte once
+        uint64_t nb, bytes = 0, batches = 0, cut = 0;
+        const uint8_t* p = nullptr;
+        while ((nb = src.nextMapped(o.batchBytes, &p)) > 0) {
+            if (p != src.mapping() + bytes) throw std::runtime_error("mapped ranges not back to back");
+            const uint8_t last = p[nb - 1];
+            if (last != '\n' && last != '\r') ++cut;   // only the file's last line may lack its terminator
+            bytes += nb;
+            ++batches;
+        }
+        std::printf("{\"mode\": \"dry-run\", \"io\": \"mapped\", \"bytes\": %llu, \"batches\": %llu, "
+                    "\"unterminated\": %llu}\n",
+                    (unsigned long long)bytes, (unsigned long long)batches, (unsigned long long)cut);
+        return 0;
+    }
     if (a.dry) {   // host half only: map + source, no device
         std::vector<uint8_t> buf(o.batchBytes);
         std::vector<uint32_t> off(o.batchEvents);
@@ -238,6 +268,17 @@ int run(const Args& a) {
 
     GpuAdCampaignOperator op(map, o);
     op.open();
+    if (o.mappedIo && a.io == "auto" && !src.mapping()) o.mappedIo = false;   // nothing mapped (empty file)
+    if (o.mappedIo) {
+        try {
+            op.registerSource(src);
+        } catch (const std::exception& e) {
+            if (a.io == "mapped") throw;
+            std::fprintf(stderr, "note: the events file's mapping cannot be read in place (%s): slot copies\n",
+                         e.what());
+            o.mappedIo = false;
+        }
+    }
     const double t_open = now_s();   // the stream itself: from the first read to close
     uint64_t rows = 0, flushes = 0;
     auto flush = [&]() {
@@ -250,8 +291,8 @@ int run(const Args& a) {
     double last_flush = now_s();
     for (long long rep = 0; rep < a.repeat; ++rep) {
         if (rep) src.rewind();
-        while ((o.gpuSplit ? op.fillFromRaw(src) : op.fillFrom(src)) > 0) {
-            op.submit();
+        while (o.mappedIo ? op.submitMapped(src) > 0 : (o.gpuSplit ? op.fillFromRaw(src) : op.fillFrom(src)) > 0) {
+            if (!o.mappedIo) op.submit();
             if (a.flush_ms > 0 && (now_s() - last_flush) * 1000.0 >= (double)a.flush_ms) {
                 flush();
                 last_flush = now_s();
@@ -283,7 +324,7 @@ int run(const Args& a) {
                 el_stream > 0 ? (double)s.events / el_stream : 0.0, (unsigned long long)src.bytesRead(),
                 el_stream > 0 ? (double)src.bytesRead() / el_stream / 1e9 : 0.0, o.gpuSplit ? "gpu" : "host",
                 a.repeat, tbl ? "tbl" : "json",
-                json_str(a.sink).c_str(), a.h2d_sdma ? "sdma" : "kernel",
+                json_str(a.sink).c_str(), a.h2d_sdma ? "sdma" : o.mappedIo ? "mapped" : "kernel",
                 copy_ms > 0 ? (double)copy_bytes / (copy_ms * 1e-3) / 1e9 : 0.0,
                 el_stream > 0 ? copy_ms * 1e-3 / el_stream : 0.0, op.fillSeconds(), op.waitSeconds());
     return s.overflow_dropped ? 3 : 0;

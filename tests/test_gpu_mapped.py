@@ -159,7 +159,7 @@ def test_mapped_argument_errors():
         with pytest.raises(YsbError, match="YSB_ERR_ARG"):
             ctx.host_register(buf[16:])                          # overlaps
         with pytest.raises(YsbError, match="YSB_ERR_ARG"):
-            ctx.submit_raw_mapped(buf, 8, 64)                    # not 16-byte aligned
+            ctx.submit_raw_mapped(buf, buf.size - 8, 16)         # past the range's end
         with pytest.raises(YsbError, match="YSB_ERR_ARG"):
             ctx.submit_raw_mapped(buf, 0, buf.size + 64)         # past the registered range
         with pytest.raises(YsbError, match="YSB_ERR_STATE"):
@@ -171,6 +171,90 @@ def test_mapped_argument_errors():
         ctx.submit_raw_mapped(buf, 0, parts[0][1], rebase=(0, 1))
         with pytest.raises(YsbError, match="rebase table"):
             ctx.sync()                                           # the launch fails, sticky until reset
+
+
+def test_unaligned_batches_back_to_back():
+    """A file mapping's batches (the native runner's mapped FileBasedDataSource): cut at line
+    boundaries and submitted where they lie, back to back at every byte alignment -- the copy
+    kernel's shifted path (launch_h2d_copy_unaligned).  Counts equal the copied batches' and
+    the generator truth; no line broke."""
+    g = GenParams(events_per_sec=100_000, with_skew=2)
+    data, off = g.events_host(0, 60_000)
+    ends = np.append(off[1:], len(data)).astype(np.int64)
+    rng = np.random.default_rng(7)
+    cuts = np.unique(np.concatenate([[0, off.size], rng.integers(1, off.size, 40), np.arange(1, 40)]))
+    for lead in (0, 3, 8, 15):   # the whole file's start alignment
+        buf = aligned(len(data) + 32)
+        buf[lead:lead + len(data)] = data
+        with ctx_for(g) as a, ctx_for(g) as b:
+            a.host_register(buf)
+            shifts = set()
+            for i, (x, y) in enumerate(zip(cuts[:-1], cuts[1:])):
+                p, nb = lead + int(off[x]), int(ends[y - 1] - off[x])
+                shifts.add(p % 16)
+                a.submit_raw_mapped(buf, p, nb, slot=i % 2)
+                b.submit_raw(buf[p:p + nb], slot=i % 2)
+            a.sync()
+            b.sync()
+            assert len(shifts) == 16
+            got = a.drain()
+            assert got == b.drain() and sum(got.values()) > 0
+            st = a.stats()
+            assert st["events"] == off.size and st["parse_errors"] == 0 and st["deferred"] == 0
+            a.truth_accumulate(g, 0, off.size)
+            mism, truth, ring = a.truth_compare()
+            assert mism == 0 and truth == ring
+            a.host_unregister(buf)
+
+
+def test_unaligned_mapped_with_device_offsets_and_rebase():
+    """ysb_submit_mapped of unaligned batches, rebased: the shifted copy feeds the rebase and
+    the scan the same bytes as an aligned one."""
+    g = GenParams(events_per_sec=100_000, with_skew=2)
+    data, off = g.events_host(0, 50_000)
+    tab, base = time_table(data, off)
+    ends = np.append(off[1:], len(data)).astype(np.int64)
+    cuts = [0, 1, 2, 3, 777, 5000, 12345, 30001, 49999, off.size]
+    lo = np.empty(off.size, dtype=np.uint32)
+    for x, y in zip(cuts[:-1], cuts[1:]):
+        lo[x:y] = off[x:y] - off[x]
+    buf = aligned(len(data) + 32)
+    buf[5:5 + len(data)] = data
+    with ctx_for(g) as ctx:
+        ctx.host_register(buf)
+        ctx.rebase_table(tab, base)
+        d_lo = ctx.device_alloc(lo.nbytes + 64)
+        ctx.h2d(d_lo, lo)
+        for i, (x, y) in enumerate(zip(cuts[:-1], cuts[1:])):
+            ctx.submit_mapped(buf, 5 + int(off[x]), int(ends[y - 1] - off[x]), d_lo + 4 * x, y - x,
+                              slot=i % 2, rebase=(x, 3))
+        ctx.sync()
+        st = ctx.stats()
+        assert st["events"] == off.size and st["parse_errors"] == 0 and st["deferred"] == 0
+        gs = GenParams(events_per_sec=100_000, with_skew=2, t0_ms=T0 + 30_000)
+        ctx.truth_accumulate(gs, 0, off.size)
+        mism, truth, ring = ctx.truth_compare()
+        assert mism == 0 and truth == ring and truth > 0
+        ctx.device_free(d_lo)
+
+
+def test_mapped_range_is_checked_at_16_byte_boundaries():
+    """The copy reads whole 16-byte vectors: a batch whose widened span leaves the registered
+    range is refused even when its own bytes are inside."""
+    g = GenParams(events_per_sec=100_000)
+    data, off = g.events_host(0, 100)
+    buf = aligned(len(data) + 64)
+    buf[8:8 + len(data)] = data
+    view = buf[8:8 + len(data)]                                    # starts 8 bytes past a boundary
+    with ctx_for(g) as ctx:
+        ctx.host_register(view)
+        with pytest.raises(YsbError, match="registered range"):
+            ctx.submit_raw_mapped(view, 0, len(data))
+        ctx.host_unregister(view)
+        ctx.host_register(buf)
+        ctx.submit_raw_mapped(buf, 8, len(data))
+        ctx.sync()
+        assert ctx.stats()["events"] == off.size and ctx.stats()["parse_errors"] == 0
 
 
 def test_timing_records_are_folded():

@@ -31,13 +31,17 @@ def read_csv(path):
     ("gen_s7.tbl", "gen_s7.ad_to_campaign.csv", "gen_s7_tbl", ["--batch-bytes", "8192"]),
     ("edge_tbl.tbl", "gen_s7.ad_to_campaign.txt", "edge_tbl", []),
 ])
-def test_runner_csv_sink_matches_golden(tmp_path, events, admap, stem, extra):
+@pytest.mark.parametrize("io", ["mmap", "mapped"])
+def test_runner_csv_sink_matches_golden(tmp_path, events, admap, stem, extra, io):
+    """io = mapped: the file's mapping registered, every batch read in place at whatever byte
+    alignment its first line has (ysb_submit_raw_mapped, launch_h2d_copy_unaligned)."""
     conf = write_conf(tmp_path, gd.path(events), gd.path(admap))
     out_csv = tmp_path / "windows.csv"
-    r = subprocess.run([EXE, "--confPath", conf, "--sink", "csv:%s" % out_csv, "--flush-ms", "0"] + extra,
+    r = subprocess.run([EXE, "--confPath", conf, "--sink", "csv:%s" % out_csv, "--flush-ms", "0", "--io", io] + extra,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     out = last_json(r)
+    assert out["h2d"] == ("mapped" if io == "mapped" else "kernel")
     exp_rows, exp_st = gd.expected(stem)
     assert read_csv(out_csv) == exp_rows
     for k, v in exp_st.items():

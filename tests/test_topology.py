@@ -98,6 +98,27 @@ def test_readline_lone_cr_and_mixed_terminators(tmp_path, batch):
     assert out["events"] == want and out["bytes"] == len(data)
 
 
+@pytest.mark.parametrize("batch", ["300", "523", "777", "4096", "268435456"])
+def test_mapped_source_ranges_are_whole_lines(tmp_path, batch):
+    """--io mapped hands the GPU ranges of the file mapping itself (nextMapped): back to back,
+    every byte once, each ending at a readLine terminator -- never between '\r' and '\n' --
+    except the file's unterminated last line."""
+    raw, _ = gd.events("gen_s7")
+    lines = raw.split(b"\n")[:-1][:60]
+    seps = [b"\n", b"\r\n", b"\r", b"\r\r", b"\n\n", b"\r\n\r"]
+    data = b"".join(ln + seps[i % len(seps)] for i, ln in enumerate(lines)) + b"x\ry"
+    ev = tmp_path / "mixed.jsonl"
+    ev.write_bytes(data)
+    conf = write_conf(tmp_path, str(ev), gd.path("gen_s7.ad_to_campaign.txt"))
+    out = last_json(run("--confPath", conf, "--dry-run", "--io", "mapped", "--batch-bytes", batch))
+    assert out["io"] == "mapped" and out["bytes"] == len(data) and out["unterminated"] == 1
+    assert out["batches"] == (1 if int(batch) > len(data) else out["batches"]) and out["batches"] >= 1
+    if int(batch) < len(data):
+        assert out["batches"] >= len(data) // int(batch)
+    r = run("--confPath", conf, "--io", "mapped", "--host-split", ok=False)
+    assert r.returncode == 2 and "--host-split" in r.stderr
+
+
 def test_print_config(tmp_path):
     conf = write_conf(tmp_path, "/x/events.tbl", gd.path("gen_s7.ad_to_campaign.csv"))
     r = run("--confPath", conf, "--print-config", "--dry-run", ok=False)
