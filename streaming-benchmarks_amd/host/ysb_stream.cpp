@@ -15,6 +15,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <set>
 #include <stdexcept>
 #include <thread>
@@ -628,6 +629,66 @@ private:
 };
 
 }  // namespace
+
+std::string StreamingJob::mergeCheck(int shards, int flushes, uint64_t seed) {
+    if (shards < 1 || flushes < 1) throw std::runtime_error("mergeCheck: shards and flushes must be >= 1");
+    const int64_t W0 = 1700000000000LL, STEP = 2500;
+    std::vector<std::vector<int64_t>> wm(shards, std::vector<int64_t>(flushes));
+    std::mt19937_64 rng(seed);
+    for (int s = 0; s < shards; ++s)
+        for (int i = 0; i < flushes; ++i) wm[s][i] = W0 + i * STEP - (int64_t)(rng() % 3001);
+    std::vector<FlushRows> got;
+    std::mutex gm;
+    int64_t fake_now = W0;
+    std::set<int64_t> closed;
+    {
+        SinkThread st([&](const FlushRows& f, int64_t) {
+            std::lock_guard<std::mutex> g(gm);
+            got.push_back(f);
+        }, [&]() { return fake_now; });
+        FlushMerger merger(st, shards);
+        std::vector<std::thread> th;
+        for (int s = 0; s < shards; ++s)
+            th.emplace_back([&, s]() {
+                std::mt19937_64 r(seed * 977 + (uint64_t)s);
+                for (int i = 0; i < flushes; ++i) {
+                    std::this_thread::sleep_for(std::chrono::microseconds(r() % 300));
+                    const int64_t w = (W0 + i * STEP) / BUCKET_MS * BUCKET_MS;
+                    std::vector<WindowDelta> rows{{"c" + std::to_string(s), w, (uint64_t)(s + 1)}};
+                    merger.deliver(i, wm[s][i], std::move(rows));
+                }
+            });
+        for (auto& t : th) t.join();
+        st.finish();
+        closed = st.closed;
+    }
+    // the expectation: in index order, min watermark, every shard's row; windows closed by the
+    // first flush (at or after the one that first shows them) whose watermark passes their end
+    bool inOrder = (int)got.size() == flushes, wmMin = true, rowsOk = true;
+    std::set<int64_t> seen, want;
+    for (int i = 0; i < (int)got.size(); ++i) {
+        const FlushRows& f = got[i];
+        inOrder = inOrder && f.index == i;
+        int64_t m = INT64_MAX;
+        for (int s = 0; s < shards; ++s) m = std::min(m, wm[s][std::min<int64_t>(f.index, flushes - 1)]);
+        wmMin = wmMin && f.watermarkMs == m;
+        std::set<std::string> cs;
+        for (const WindowDelta& d : f.rows) cs.insert(d.campaign);
+        rowsOk = rowsOk && (int)f.rows.size() == shards && (int)cs.size() == shards;
+        for (const WindowDelta& d : f.rows) seen.insert(d.windowMs);
+        for (int64_t w : seen)
+            if (w + BUCKET_MS <= f.watermarkMs) want.insert(w);
+    }
+    const bool ok = inOrder && wmMin && rowsOk && closed == want && !want.empty();
+    char b[320];
+    std::snprintf(b, sizeof b,
+                  "{\"mode\": \"stream-merge-check\", \"shards\": %d, \"flushes\": %d, \"delivered\": %zu, "
+                  "\"in_order\": %s, \"watermark_min\": %s, \"rows\": %s, \"closed\": %zu, \"closed_expected\": %zu, "
+                  "\"ok\": %s}",
+                  shards, flushes, got.size(), inOrder ? "true" : "false", wmMin ? "true" : "false",
+                  rowsOk ? "true" : "false", closed.size(), want.size(), ok ? "true" : "false");
+    return b;
+}
 
 StreamReport StreamingJob::run(const FlushSink& sink) {
     StreamReport rep;

@@ -144,6 +144,12 @@ public:
     // memcpy + digit patch).  A JSON summary with the aggregate events/s.  (The mapped feeder has
     // no per-byte host work: its cost per batch is the submit call, measured by the GPU run.)
     static std::string feedCheck(const StreamOptions& o, double seconds);
+    // CPU check of the shards' flush merge (no GPU): `shards` threads deliver `flushes` flushes
+    // each, at random moments, with jittered watermarks and one delta row per flush, through the
+    // runner's own merger and sink thread.  Checks: the sink sees every index once, in order,
+    // with every shard's rows and the minimum of the shards' watermarks; the windows it closes
+    // are exactly those the merged watermarks pass.  A JSON summary ("ok": true|false).
+    static std::string mergeCheck(int shards, int flushes, uint64_t seed);
     ~StreamingJob();
 
 private:

@@ -53,6 +53,8 @@ struct Args {
     std::string stream_csv;   // per-(campaign, window) totals of everything written
     bool self_check = false;  // --stream-self-check: the replay's rebasing on the CPU, no GPU
     bool feed_check = false;  // --stream-feed-check: the feeders' host rate on the CPU, no GPU
+    bool merge_check = false; // --stream-merge-check: the shards' flush merge on the CPU, no GPU
+    int merge_flushes = 400;
     double feed_seconds = 2;
 };
 
@@ -68,7 +70,8 @@ void usage() {
                  "       [--cycle-ms MS] [--flush-ms MS] [--batch-ms MS] [--ooo-ms MS] [--seconds S]\n"
                  "       [--batch-mb MB] [--window-ring W] [--skew 0|1|2] [--io-threads T] [--totals CSV]\n"
                  "       [--replay mapped|mapped-raw|copy] [--no-numa] [--no-timing]\n"
-                 "   or: ysb_topology --stream-self-check | --stream-feed-check [--shards N] [--feed-seconds S] ...\n");
+                 "   or: ysb_topology --stream-self-check | --stream-feed-check [--shards N] [--feed-seconds S] ...\n"
+                 "   or: ysb_topology --stream-merge-check [--shards N] [--merge-flushes F] [--seed S]\n");
 }
 
 Args parse(int argc, char** argv) {
@@ -118,6 +121,8 @@ Args parse(int argc, char** argv) {
         else if (k == "--totals") a.stream_csv = val();
         else if (k == "--stream-feed-check") { a.stream = true; a.feed_check = true; }
         else if (k == "--feed-seconds") a.feed_seconds = std::atof(val().c_str());
+        else if (k == "--stream-merge-check") { a.stream = true; a.merge_check = true; }
+        else if (k == "--merge-flushes") a.merge_flushes = std::atoi(val().c_str());
         else if (k == "--no-numa") a.so.pinNuma = false;
         else if (k == "--no-timing") a.so.timing = false;
         else if (k == "--replay") {
@@ -439,6 +444,11 @@ int main(int argc, char** argv) {
         if (a.feed_check) {
             std::printf("%s\n", StreamingJob::feedCheck(a.so, a.feed_seconds).c_str());
             return 0;
+        }
+        if (a.merge_check) {
+            const std::string r = StreamingJob::mergeCheck(a.so.shards, a.merge_flushes, a.so.seed);
+            std::printf("%s\n", r.c_str());
+            return r.find("\"ok\": true") != std::string::npos ? 0 : 1;
         }
         if (a.stream) return run_stream(a);
         return run(a);

@@ -119,6 +119,19 @@ def test_mapped_source_ranges_are_whole_lines(tmp_path, batch):
     assert r.returncode == 2 and "--host-split" in r.stderr
 
 
+@pytest.mark.parametrize("shards,seed", [(1, 1), (2, 2), (3, 3), (8, 4)])
+def test_stream_shards_flush_merge(shards, seed):
+    """--stream-merge-check (CPU, no GPU): the per-shard feeders' flushes, delivered by one
+    thread per shard at random moments with jittered watermarks, go through the runner's own
+    merger and sink thread: every index once and in order, every shard's rows, the minimum
+    watermark (Flink's at a keyed operator), and exactly the windows those watermarks pass
+    closed (host/ysb_stream.cpp FlushMerger, SinkThread; CampaignProcessorCommon.java:35-55)."""
+    r = run("--stream-merge-check", "--shards", str(shards), "--merge-flushes", "250", "--seed", str(seed))
+    out = last_json(r)
+    assert out["ok"] and out["in_order"] and out["watermark_min"] and out["rows"]
+    assert out["delivered"] == 250 and out["closed"] == out["closed_expected"] > 50
+
+
 def test_print_config(tmp_path):
     conf = write_conf(tmp_path, "/x/events.tbl", gd.path("gen_s7.ad_to_campaign.csv"))
     r = run("--confPath", conf, "--print-config", "--dry-run", ok=False)
