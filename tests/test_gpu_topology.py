@@ -48,6 +48,37 @@ def test_runner_csv_sink_matches_golden(tmp_path, events, admap, stem, extra, io
         assert out[k] == v, k
 
 
+@pytest.mark.parametrize("batch", ["300", "523", "4096", "268435456"])
+def test_runner_mapped_io_readline_terminators(tmp_path, batch):
+    """--io mapped over a file whose lines end in "\\n", "\\r\\n", a lone "\\r", blank lines
+    and an unterminated last line, cut into tiny batches at every byte alignment: the windows
+    and stats equal the oracle's over readLine's records (oracle/dostats.split_lines, run) and
+    the slot-copy path's."""
+    from oracle import dostats
+    raw, _ = gd.events("gen_s7")
+    lines = raw.split(b"\n")[:-1][:600]
+    seps = [b"\n", b"\r\n", b"\r", b"\r\r", b"\n\n", b"\r\n\r", b"\n"]
+    data = b"".join(ln + seps[i % len(seps)] for i, ln in enumerate(lines)) + lines[0][:-3]
+    ev = tmp_path / "mixed.jsonl"
+    ev.write_bytes(data)
+    admap = gd.path("gen_s7.ad_to_campaign.txt")
+    conf = write_conf(tmp_path, str(ev), admap)
+    with open(admap, "rb") as f:
+        want = dostats.run(dostats.split_lines(data)[0], dostats.load_ad_map_json_lines(f.read()))
+    idx = gd.campaign_index()
+    want_rows = {(idx[c], b): n for (c, b), n in want.counts.items()}
+    outs = {}
+    for io in ("mapped", "mmap"):
+        out_csv = tmp_path / ("w_%s.csv" % io)
+        r = subprocess.run([EXE, "--confPath", conf, "--sink", "csv:%s" % out_csv, "--flush-ms", "0", "--io", io,
+                            "--batch-bytes", batch], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        outs[io] = last_json(r)
+        assert read_csv(out_csv) == want_rows, io
+        assert outs[io]["events"] == want.events and outs[io]["parse_errors"] == want.parse_errors, io
+    assert outs["mapped"]["h2d"] == "mapped" and outs["mmap"]["h2d"] == "kernel"
+
+
 def test_runner_redis_sink_check_correct(tmp_path):
     conf = write_conf(tmp_path, gd.path("gen_s7.jsonl"), gd.path("gen_s7.ad_to_campaign.txt"))
     srv = FakeRedis()
