@@ -209,7 +209,7 @@ def main():
     ap.add_argument("--file-events", type=int, default=20_000_000)
     ap.add_argument("--repeat", type=int, default=5)
     ap.add_argument("--host-split", action="store_true")
-    ap.add_argument("--io", default="mmap", choices=["mmap", "pread", "mapped"])
+    ap.add_argument("--io", default="mmap", choices=["auto", "mapped", "mmap", "pread"])
     ap.add_argument("--h2d-sdma", action="store_true", help="the slots' H2D by the DMA engine (default: a copy kernel)")
     ap.add_argument("--workdir", default=None, help="runner: keep / reuse the replay file here")
     a = ap.parse_args()
