@@ -75,12 +75,14 @@ void launch_h2d_copy(void* dst, const void* src, u64 bytes, int cus, hipStream_t
 // The same from a source at any byte address (a file mapping's batch starts where the previous
 // batch's last line ended): output vector i = bytes [16 i + sh, 16 i + sh + 16) of the 16-byte
 // aligned `src`, whose first nsrc vectors are read (to the 16-byte boundary at or above the
-// batch's end, never further: the same bound the aligned copy keeps).  A wave copies H2D_UNROLL
-// x 64 consecutive vectors per step (4 KB, all loads in flight at once; waves a grid stride
-// apart): each lane loads one source vector, the next one is its right neighbour's (a lane
-// shuffle) or, at lane 63, the next slice's lane 0's (a lane read); only the step's very last
-// vector needs a load of its own (+1/256 of the loads: a one-per-lane-63 extra load, measured
-// first, cost ~6 % of the PCIe rate, profiles/AB_LOG.md).
+// batch's end, never further: the same bound the aligned copy keeps).  Each wave copies one
+// contiguous run of steps of H2D_UNROLL x 64 vectors (4 KB).  A lane loads one source vector;
+// the next one is its right neighbour's (a lane shuffle) or, at lane 63, the next slice's lane
+// 0's (a lane read), and the next step's loads are issued before the current step's shifts
+// and stores: the step's last vector comes from them (no extra load) and the loop's own
+// instructions overlap the PCIe round trip.  Measured against two simpler forms (a grid
+// stride of steps with one extra load per step: -2 %; one extra load per wave slice and the
+// word shift picked at run time: -10 %), profiles/AB_LOG.md round 6.
 // bytes [4 Q + r, 4 Q + r + 16) of the 32 bytes a:b (Q = shift / 4 a template argument: the
 // word selection costs nothing, the byte shift is one v_alignbyte per word)
 template <int Q>
@@ -106,31 +108,42 @@ __device__ __forceinline__ h2d_v4 lane0(const h2d_v4& v) {
 
 template <int Q>
 __global__ __launch_bounds__(H2D_TPB) void h2d_copy_unaligned_kernel(const h2d_v4* __restrict__ src,
-                                                                     h2d_v4* __restrict__ dst, u64 vecs, u64 nsrc,
-                                                                     u32 r) {
-    constexpr u64 STEP = 64 * H2D_UNROLL;   // vectors a wave copies per step
+                                                                          h2d_v4* __restrict__ dst, u64 vecs,
+                                                                          u64 nsrc, u32 r) {
+    constexpr u64 STEP = 64 * H2D_UNROLL;
     const u32 lane = threadIdx.x & 63u;
     const u64 waves = (u64)gridDim.x * (H2D_TPB / 64);
     const u64 wave = (u64)blockIdx.x * (H2D_TPB / 64) + (threadIdx.x >> 6);
-    for (u64 b = wave * STEP; b < vecs; b += waves * STEP) {   // wave-uniform
-        h2d_v4 a[H2D_UNROLL], tail = h2d_v4{0, 0, 0, 0};
+    const u64 steps = (vecs + STEP - 1) / STEP;
+    const u64 s0 = steps * wave / waves, s1 = steps * (wave + 1) / waves;   // wave-uniform
+    if (s0 >= s1) return;
+    auto load = [&](u64 i) { return i < nsrc ? __builtin_nontemporal_load(src + i) : h2d_v4{0, 0, 0, 0}; };
+    h2d_v4 cur[H2D_UNROLL], nxt[H2D_UNROLL];
 #pragma unroll
-        for (int u = 0; u < H2D_UNROLL; ++u) {
-            const u64 i = b + u * 64 + lane;
-            a[u] = i < nsrc ? __builtin_nontemporal_load(src + i) : h2d_v4{0, 0, 0, 0};
+    for (int u = 0; u < H2D_UNROLL; ++u) cur[u] = load(s0 * STEP + u * 64 + lane);
+    for (u64 st = s0; st < s1; ++st) {
+        const u64 b = st * STEP;
+        if (st + 1 < s1) {
+#pragma unroll
+            for (int u = 0; u < H2D_UNROLL; ++u) nxt[u] = load(b + STEP + u * 64 + lane);
+        } else {   // the run's end: only the vector after it
+            nxt[0] = load(b + STEP + lane);
+#pragma unroll
+            for (int u = 1; u < H2D_UNROLL; ++u) nxt[u] = h2d_v4{0, 0, 0, 0};
         }
-        if (lane == 63u && b + STEP < nsrc) tail = __builtin_nontemporal_load(src + b + STEP);
 #pragma unroll
         for (int u = 0; u < H2D_UNROLL; ++u) {
             const u64 i = b + u * 64 + lane;
-            // both cross-lane reads in every lane (a ?: evaluates one operand only: the
-            // shuffle must not run under lane != 63, or lane 62 reads an inactive lane's 0)
-            const h2d_v4 down = lane_down(a[u]);
-            const h2d_v4 nx = u + 1 < H2D_UNROLL ? lane0(a[u + 1 < H2D_UNROLL ? u + 1 : u]) : tail;
+            // both cross-lane reads in every lane (a ?: evaluates one operand only: a shuffle
+            // under lane != 63 would give lane 62 an inactive lane's 0)
+            const h2d_v4 down = lane_down(cur[u]);
+            const h2d_v4 nx = lane0(u + 1 < H2D_UNROLL ? cur[u + 1 < H2D_UNROLL ? u + 1 : u] : nxt[0]);
             h2d_v4 n = down;
             if (lane == 63u) n = nx;
-            if (i < vecs) __builtin_nontemporal_store(shift_bytes<Q>(a[u], n, r), dst + i);
+            if (i < vecs) __builtin_nontemporal_store(shift_bytes<Q>(cur[u], n, r), dst + i);
         }
+#pragma unroll
+        for (int u = 0; u < H2D_UNROLL; ++u) cur[u] = nxt[u];
     }
 }
 
