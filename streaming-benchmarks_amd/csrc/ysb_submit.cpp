@@ -608,7 +608,8 @@ static int ensure_slots(ysb_ctx* c) {
 }
 
 // A slot's host -> device copy on the copy stream: by the CUs from the pinned slot's device
-// address (launch_h2d_copy, the default: ysb_split.hip says why), or by the DMA engine with
+// address (launch_h2d_copy, the default: ysb_split.hip says why; a mapped batch that does not
+// start on a 16-byte boundary by launch_h2d_copy_unaligned), or by the DMA engine with
 // YSB_F_H2D_SDMA.
 static hipError_t h2d(ysb_ctx* c, void* dst, const void* dsrc, const void* hsrc, u64 bytes) {
     if (c->cfg.flags & YSB_F_H2D_SDMA) return hipMemcpyAsync(dst, hsrc, bytes, hipMemcpyHostToDevice, c->s_copy);
