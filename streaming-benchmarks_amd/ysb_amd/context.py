@@ -154,10 +154,12 @@ class YsbContext:
         buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
         self._c(lib().ysb_submit_raw(self._h, slot, _ptr(buf), buf.size))
 
-    def host_register(self, arr):
+    def host_register(self, arr, nbytes=None):
         """ysb_host_register: pins and maps a host numpy array for zero-copy raw batches (the
-        array must stay alive and unmoved until host_unregister or close)."""
-        self._c(lib().ysb_host_register(self._h, C.c_void_p(arr.ctypes.data), arr.nbytes))
+        array must stay alive and unmoved until host_unregister or close).  nbytes: the length
+        to register from arr's start when it is not arr.nbytes (a file mapping's whole pages)."""
+        self._c(lib().ysb_host_register(self._h, C.c_void_p(arr.ctypes.data),
+                                        arr.nbytes if nbytes is None else int(nbytes)))
 
     def host_unregister(self, arr):
         self._c(lib().ysb_host_unregister(self._h, C.c_void_p(arr.ctypes.data)))

@@ -257,6 +257,33 @@ def test_mapped_range_is_checked_at_16_byte_boundaries():
         assert ctx.stats()["events"] == off.size and ctx.stats()["parse_errors"] == 0
 
 
+@pytest.mark.parametrize("cap", [777, 64 << 10, 256 << 20])
+def test_file_source_in_place_equals_oracle(tmp_path, cap):
+    """ysb_amd.FileBasedDataSource.run: a file with every readLine terminator, its mapping
+    registered and every batch submitted in place (any byte alignment): the counts and stats
+    equal the oracle's over readLine's records (oracle/dostats), and the generator's own file
+    equals its truth."""
+    import golden_data as gd
+    from oracle import dostats
+    from ysb_amd import FileBasedDataSource
+    raw, _ = gd.events("gen_s7")
+    lines = raw.split(b"\n")[:-1]
+    seps = [b"\n", b"\r\n", b"\r", b"\r\r", b"\n\n", b"\r\n\r", b"\n"]
+    data = b"".join(ln + seps[i % len(seps)] for i, ln in enumerate(lines)) + lines[1][:-2]
+    ev = tmp_path / "mixed.jsonl"
+    ev.write_bytes(data)
+    want = dostats.run(dostats.split_lines(data)[0], gd.ad_map())
+    cidx = gd.campaign_index()
+    with YsbContext(n_campaigns=len(cidx), max_batch_bytes=max(cap, 4096)) as ctx:
+        ctx.load_ad_map(*gd.ad_arrays())
+        with FileBasedDataSource(str(ev)) as src:
+            assert src.run(ctx, cap) == len(data) and src.batches >= 1
+        st = ctx.stats()
+        assert st["events"] == want.events and st["parse_errors"] == want.parse_errors
+        got = {(c, w // 10000): n for (c, w), n in ctx.drain().items()}
+        assert got == {(cidx[c], b): n for (c, b), n in want.counts.items()}
+
+
 def test_timing_records_are_folded():
     """YSB_F_TIMING with many launches and no kernel_time call in between (a streaming job):
     the records are folded into totals (TIMING_KEEP = 256 pending at most), every launch and
