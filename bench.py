@@ -71,7 +71,7 @@ def parse_args(argv=None):
     ap.add_argument("--stream-seconds", type=float, default=12.0,
                     help="extras: wall seconds of the native streaming leg (configs[4]; at the default speedup "
                          "12 s of input is 420 s of event time: >= 30 windows close); 0 skips it")
-    ap.add_argument("--stream-target", type=float, default=202e6,
+    ap.add_argument("--stream-target", type=float, default=210e6,
                     help="extras: events/s per shard (GPU) the streaming replay releases (the zero-copy feed's "
                          "ceiling is the slot copy over PCIe, ~215M/s at 254 B per event)")
     ap.add_argument("--stream-host-gb", type=float, default=64.0,
